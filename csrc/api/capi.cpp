@@ -1,0 +1,89 @@
+// Flat C API over the engine for the Python package (ctypes) and other FFI users.
+// Every entry point catches C++ exceptions and returns a negative status; the last error
+// message is retrievable with sa_last_error().
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "sa/capi.h"
+#include "sa/engine.h"
+
+namespace {
+thread_local std::string g_err;
+template <typename F>
+int guarded(F&& f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    SA_LOGE("%s", e.what());
+    return -1;
+  } catch (...) {
+    g_err = "unknown error";
+    return -1;
+  }
+}
+}  // namespace
+
+extern "C" {
+
+const char* sa_version(void) { return SA_VERSION_STRING; }
+const char* sa_last_error(void) { return g_err.c_str(); }
+
+void* sa_engine_create(const char* model, const char* weights, int height, int width, int batch,
+                       int iters, int device, int use_graph, unsigned long long seed) {
+  sa::StereoEngine* out = nullptr;
+  int rc = guarded([&] {
+    sa::EngineConfig cfg;
+    cfg.model = model ? model : "";
+    cfg.weights = weights ? weights : "";
+    cfg.height = height;
+    cfg.width = width;
+    cfg.batch = batch;
+    cfg.iters = iters;
+    cfg.device = device;
+    cfg.use_graph = use_graph != 0;
+    cfg.seed = seed;
+    out = sa::StereoEngine::create(cfg).release();
+  });
+  return rc == 0 ? out : nullptr;
+}
+
+void sa_engine_destroy(void* e) { delete static_cast<sa::StereoEngine*>(e); }
+
+int sa_engine_set_q(void* e, const float* q16) {
+  return guarded([&] { static_cast<sa::StereoEngine*>(e)->set_Q(q16); });
+}
+
+int sa_engine_set_rectify_maps(void* e, const float* ml, const float* mr) {
+  return guarded([&] { static_cast<sa::StereoEngine*>(e)->set_rectify_maps(ml, mr); });
+}
+
+int sa_engine_run_device(void* e, const void* left, const void* right, float* disp, float* cloud,
+                         int rectify, void* stream, void* rect_left, void* rect_right) {
+  return guarded([&] {
+    static_cast<sa::StereoEngine*>(e)->run_device((const uint8_t*)left, (const uint8_t*)right, disp,
+                                                  cloud, rectify != 0, (hipStream_t)stream,
+                                                  (uint8_t*)rect_left, (uint8_t*)rect_right);
+  });
+}
+
+int sa_engine_run_host(void* e, void* left, void* right, float* disp, float* cloud, int rectify) {
+  return guarded([&] {
+    static_cast<sa::StereoEngine*>(e)->run_host((uint8_t*)left, (uint8_t*)right, disp, cloud,
+                                                rectify != 0);
+  });
+}
+
+long long sa_engine_device_bytes(void* e) {
+  return (long long)static_cast<sa::StereoEngine*>(e)->device_bytes();
+}
+
+const float* sa_engine_aux_output(void* e, int* n) {
+  return static_cast<sa::StereoEngine*>(e)->aux_output(n);
+}
+
+void* sa_engine_stream(void* e) { return (void*)static_cast<sa::StereoEngine*>(e)->stream(); }
+
+}  // extern "C"

@@ -1,0 +1,27 @@
+// Flat C API of libstereo_amd.so (engine lifecycle + per-frame execution).  Kernel-level
+// entry points are declared in sa/kernels.h.
+#pragma once
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SA_VERSION_STRING "stereoalgorithms_amd 0.1.0 (gfx950)"
+
+const char* sa_version(void);
+const char* sa_last_error(void);
+void* sa_engine_create(const char* model, const char* weights, int height, int width, int batch,
+                       int iters, int device, int use_graph, unsigned long long seed);
+void sa_engine_destroy(void* engine);
+int sa_engine_set_q(void* engine, const float* q16);
+int sa_engine_set_rectify_maps(void* engine, const float* map_left, const float* map_right);
+int sa_engine_run_device(void* engine, const void* left, const void* right, float* disp,
+                         float* cloud, int rectify, void* stream, void* rect_left, void* rect_right);
+int sa_engine_run_host(void* engine, void* left, void* right, float* disp, float* cloud,
+                       int rectify);
+long long sa_engine_device_bytes(void* engine);
+const float* sa_engine_aux_output(void* engine, int* n);
+void* sa_engine_stream(void* engine);
+
+#ifdef __cplusplus
+}
+#endif

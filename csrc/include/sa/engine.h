@@ -1,0 +1,117 @@
+// StereoEngine: one model instance on one GPU, one HIP stream, static memory plan, whole-frame
+// hipGraph.  Replaces the reference's per-model TensorRT wrappers (RAFTStereo/src/TRTRAFTStereo.cpp,
+// HitNet/src/HitNet.cpp, CREStereo/src/TRTCREStereo.cpp, FastACVNet_plus/src/TRTFastACVNet_plus.cpp)
+// with a single base class; per-model subclasses only describe the network.
+//
+// Per frame:  [remap (optional rectification)] -> model forward (incl. its fused preprocess)
+//             -> reprojection (disparity -> XYZRGB with Q)  — all inside one captured graph.
+#pragma once
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "sa/runtime.h"
+
+namespace sa {
+
+struct EngineConfig {
+  std::string model;       // preset name (e.g. "raftstereo-realtime"); empty = from weights metadata
+  std::string weights;     // .safetensors path; empty = deterministic random init (seed)
+  int height = 480, width = 640, batch = 1;
+  int iters = -1;          // override iteration count (RAFT / CREStereo); -1 = preset default
+  int device = 0;
+  bool use_graph = true;
+  uint64_t seed = 0;
+};
+
+// Deterministic random-init helpers: in "random" mode missing weights are synthesised with the
+// PyTorch default conv init (U(-1/sqrt(fan_in), +1/sqrt(fan_in))) and identity BatchNorm.
+struct WeightSource {
+  WeightStore* ws = nullptr;
+  bool random = false;
+  uint64_t seed = 0;
+  void conv(const std::string& name, int cout, int cin, int kh, int kw, bool bias = true);
+  void bn(const std::string& name, int c);
+  void linear(const std::string& name, int out, int in, bool bias = true);
+  void ln(const std::string& name, int c);
+  void param(const std::string& name, std::vector<int64_t> shape, float lo, float hi);
+};
+
+struct StageTimes {
+  float total_ms = 0;  // device time of the captured frame
+};
+
+class StereoEngine {
+ public:
+  virtual ~StereoEngine();
+  static std::unique_ptr<StereoEngine> create(const EngineConfig& cfg);
+
+  const EngineConfig& config() const { return cfg_; }
+  virtual const char* name() const = 0;
+  // Output the network produces before sign correction (RAFT flow is negative disparity).
+  int H() const { return cfg_.height; }
+  int W() const { return cfg_.width; }
+  int B() const { return cfg_.batch; }
+
+  // Q (4x4, row-major) for reprojection; rectification maps [2][H][W][2] (left, right).
+  void set_Q(const float* q16);
+  void set_rectify_maps(const float* maps_left, const float* maps_right);
+  bool has_rectify() const { return rect_maps_ != nullptr; }
+
+  // Device-side frame: u8 BGR [B][H][W][3] device pointers in, fp32 disparity [B][H][W] and
+  // optional XYZRGB cloud [B][H][W][6] out (device pointers).  Runs on `stream` (the caller's) —
+  // the engine's graph is launched there.  rectified_* (optional) receive the remapped inputs.
+  void run_device(const uint8_t* left, const uint8_t* right, float* disp, float* cloud,
+                  bool rectify, hipStream_t stream, uint8_t* rect_left = nullptr,
+                  uint8_t* rect_right = nullptr);
+  // Host-side frame = the reference's timed region (RAFTStereo/src/TRTRAFTStereo.cpp:119-146):
+  // pinned staging, H2D, graph, D2H of disparity and point cloud, synchronise.
+  void run_host(uint8_t* left, uint8_t* right, float* disp, float* cloud, bool rectify);
+
+  hipStream_t stream() const { return stream_; }
+  size_t device_bytes() const { return arena_.bytes(); }
+  // low-resolution flow / auxiliary output (RAFT "diff" = coords1 - coords0), may be null
+  virtual const float* aux_output(int* n) const {
+    *n = 0;
+    return nullptr;
+  }
+  long frames_run() const { return launches_per_frame_; }
+
+ protected:
+  explicit StereoEngine(const EngineConfig& cfg);
+  void init();  // allocs io buffers, calls build(), warms up, captures
+  // subclass hooks
+  virtual void build(WeightSource& src) = 0;
+  // consume in_left_/in_right_ (device u8 BGR, already rectified if requested), write disp_
+  // (positive disparity, fp32 [B][H][W]).
+  virtual void forward(hipStream_t s) = 0;
+
+  void frame(hipStream_t s, bool rectify);  // the captured body
+  void launch_frame(hipStream_t s, bool rectify);
+
+  EngineConfig cfg_;
+  DeviceArena arena_;
+  hipStream_t stream_ = nullptr;
+  std::unique_ptr<WeightStore> store_;
+  uint8_t* in_left_ = nullptr;   // model input (rectified or raw copy)
+  uint8_t* in_right_ = nullptr;
+  uint8_t* raw_left_ = nullptr;  // pre-rectification staging
+  uint8_t* raw_right_ = nullptr;
+  float* disp_ = nullptr;
+  float* cloud_ = nullptr;
+  float* rect_maps_ = nullptr;  // [2][H][W][2]
+  float Q_[16];
+  bool have_Q_ = false;
+  GraphExec graph_[2];  // [no rectify, rectify]
+  uint8_t* pin_in_ = nullptr;
+  float* pin_out_ = nullptr;
+  long launches_per_frame_ = 0;
+};
+
+// model factories (models/*.cpp)
+std::unique_ptr<StereoEngine> make_raft_stereo(const EngineConfig& cfg);
+std::unique_ptr<StereoEngine> make_crestereo(const EngineConfig& cfg);
+std::unique_ptr<StereoEngine> make_hitnet(const EngineConfig& cfg);
+std::unique_ptr<StereoEngine> make_fast_acvnet(const EngineConfig& cfg);
+
+}  // namespace sa

@@ -1,0 +1,132 @@
+// Launch-argument structs and host launchers for every hand-written CDNA4 kernel.
+// The structs are plain C so that the Python ctypes layer (stereoalgorithms_amd/_native.py)
+// can mirror them field-for-field for numerics tests against PyTorch.
+//
+// Layout conventions (all kernels):
+//   * activations are NHWC, fp16, with an explicit per-pixel stride in ELEMENTS so that a
+//     tensor can be a channel slice of a wider buffer (concat-free producers/consumers);
+//   * channel counts/offsets/strides used by vectorised paths are multiples of 8 (16 B);
+//   * weights for convolutions are pre-packed fp16 [Cout_pad][Kpad], K ordered (kh, kw, ci).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum SaAct { SA_ACT_NONE = 0, SA_ACT_RELU = 1, SA_ACT_LEAKY = 2, SA_ACT_TANH = 3, SA_ACT_SIGMOID = 4 };
+
+enum SaEpi {
+  SA_EPI_STORE = 0,     // y = act(acc*scale + bias) [; y = act2(y + res)] -> fp16
+  SA_EPI_GRU_ZR = 1,    // z = sig(acc+b+cz) -> aux ; r = sig(acc+b+cr) -> rh = r*h
+  SA_EPI_GRU_Q = 2,     // q = tanh(acc+b+cq) ; h = (1-z)h + zq  (in place on h)
+  SA_EPI_FLOW_ACC = 3,  // fp32 out[m*out_stride] += acc(ch0)*scale + bias  (RAFT coords1 += delta)
+  SA_EPI_STORE_F32 = 4  // y = act(acc*scale + bias) -> fp32
+};
+
+typedef struct {
+  const void* ptr;  // fp16 data, already offset to this source's first channel
+  int32_t channels; // multiple of 8
+  int32_t stride;   // elements between consecutive pixels
+} SaConvSrc;
+
+typedef struct {
+  SaConvSrc src[4];
+  int32_t nsrc;
+  int32_t N, H, W, Cin;  // Cin = sum(src[i].channels)
+  int32_t KH, KW, sh, sw, ph, pw, dh, dw;
+  int32_t Ho, Wo;
+  const void* weight;  // fp16 [Cout_pad][Kpad]
+  const float* bias;   // [Cout] or NULL
+  int32_t Cout, Kpad;
+  void* out;
+  int32_t out_stride;
+  int32_t epi, act, act2;
+  float alpha;  // leaky slope
+  float scale;  // multiplies acc before bias
+  const void* res;  // residual fp16 (SA_EPI_STORE)
+  int32_t res_stride;
+  const void* ctx;  // GRU context biases fp16: ZR reads [cz | cr], Q reads cq
+  int32_t ctx_stride;
+  void* aux;  // GRU z buffer fp16
+  int32_t aux_stride;
+  void* hbuf;  // GRU hidden state fp16
+  int32_t h_stride;
+  void* rh;  // GRU r*h output fp16 (ZR)
+  int32_t rh_stride;
+  double* stats;  // optional per-(n, cout) {sum, sumsq} of the stored value (instance norm)
+  int32_t tile_cfg;  // -1 = auto
+  int32_t _pad;
+} SaConvArgs;
+
+int sa_conv2d(const SaConvArgs* a, hipStream_t stream);
+
+// ---- normalisation / elementwise ------------------------------------------------------------
+// Instance-norm apply (biased var, eps): y = act(norm(x)); if res: y = act2(resnorm(res) + y)
+typedef struct {
+  const void* x; int32_t x_stride;
+  const double* stats;      // [N][C][2] sums of x
+  const void* res; int32_t res_stride;
+  const double* res_stats;  // NULL -> residual used raw
+  void* out; int32_t out_stride;
+  int32_t N, HW, C;
+  int32_t act, act2;
+  float eps, alpha;
+} SaNormArgs;
+int sa_instnorm_apply(const SaNormArgs* a, hipStream_t stream);
+
+// F.avg_pool2d(x, 3, stride=2, padding=1) (count_include_pad) on NHWC fp16
+int sa_avgpool3s2(const void* x, int x_stride, void* out, int out_stride, int N, int H, int W,
+                  int C, hipStream_t stream);
+// F.avg_pool2d(x, k, stride=k) (k = 2, 4, ...)
+int sa_avgpool_k(const void* x, int x_stride, void* out, int out_stride, int N, int H, int W,
+                 int C, int k, hipStream_t stream);
+// F.interpolate(x, (Ho, Wo), mode='bilinear', align_corners) on NHWC fp16, optional scale
+int sa_interp_bilinear(const void* x, int x_stride, void* out, int out_stride, int N, int H,
+                       int W, int C, int Ho, int Wo, int align_corners, float mul,
+                       hipStream_t stream);
+
+// ---- RAFT-Stereo correlation ----------------------------------------------------------------
+// corr[b,h,w1,w2] = <f1[b,h,w1,:], f2[b,h,w2,:]>/sqrt(C), plus avg-pool pyramid along w2.
+// pyr points to levels laid out back to back: level l is [B*H][W1][W2_l] fp32.
+int sa_corr1d_pyramid(const void* f1, const void* f2, int stride, int B, int H, int W1, int W2,
+                      int C, int levels, float* pyr, hipStream_t stream);
+// Lookup: for each pixel, levels x (2r+1) bilinear taps along w2 at coords/2^l + dx.
+// flow = fp32 x-flow [B*H*W1]; coords_x = w1 + flow.  Writes fp16 corr features (out, C_out
+// channels, zero padded), and optionally flow features [flow_x, 0, ...] into flow_out slots.
+int sa_corr1d_lookup(const float* pyr, const float* flow, int B, int H, int W1, int W2,
+                     int levels, int radius, void* out, int out_stride, int out_channels,
+                     void* flow_out, int flow_stride, int flow_channels, void* flow_out2,
+                     int flow_stride2, hipStream_t stream);
+
+// ---- upsampling -----------------------------------------------------------------------------
+// RAFT convex upsampling: mask [B*H*W][9*f*f] fp16 (softmax over the 9), flow fp32 [B*H*W]
+// (x component).  Writes full-res fp32 output = sign * (f * flow) combination.
+int sa_convex_upsample(const void* mask, int mask_stride, const float* flow, int B, int H, int W,
+                       int factor, float sign, float* out, hipStream_t stream);
+
+// ---- pre / post processing ------------------------------------------------------------------
+enum SaNormMode {
+  SA_PRE_RAW = 0,        // RGB 0..255 (RAFT/CREStereo reference inputs)
+  SA_PRE_UNIT = 1,       // RGB / 255 (HITNet)
+  SA_PRE_IMAGENET = 2,   // (RGB/255 - mean)/std (Fast-ACVNet+)
+  SA_PRE_SIGNED = 3      // 2*(RGB/255) - 1 (RAFT / CREStereo in-network normalisation)
+};
+// u8 BGR [B][H][W][3] -> fp16 NHWC, channels [c_off, c_off+3) of a stride-`out_stride` pixel,
+// remaining channels up to `zero_to` zero-filled.
+int sa_preprocess(const uint8_t* bgr, int B, int H, int W, int mode, void* out, int out_stride,
+                  int c_off, int zero_to, hipStream_t stream);
+// Bilinear remap (cv::remap INTER_LINEAR, BORDER_CONSTANT 0) of u8 BGR with float maps
+// [H][W][2]; B images share `maps` index b % nmaps.
+int sa_remap_bgr(const uint8_t* src, int B, int Hs, int Ws, const float* maps, int nmaps,
+                 int H, int W, uint8_t* dst, hipStream_t stream);
+// disparity -> XYZRGB point cloud (cv::reprojectImageTo3D with the full 4x4 Q) + signed copy
+// of the disparity.  disp_in has `disp_stride` floats per pixel (channel 0 used).
+int sa_reproject(const float* disp_in, int disp_stride, float sign, const uint8_t* left_bgr,
+                 int B, int H, int W, const float* Q16, float* disp_out, float* cloud,
+                 hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,169 @@
+// Engine runtime: device arena (static memory plan), NHWC tensor views, host weight store
+// (safetensors), packed convolution layers, hipGraph capture.
+//
+// The reference's runtime is TensorRT (engine build / deserialize / enqueue:
+// common/ONNX2TRT.cpp:43-128, RAFTStereo/src/TRTRAFTStereo.cpp:48-113).  Here the model graph is
+// our own C++ code: every activation is carved from one arena at init (shapes are static), all
+// launches go to one stream and the whole frame is captured into a hipGraph once.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "sa/common.h"
+#include "sa/kernels.h"
+
+namespace sa {
+
+// ------------------------------------------------------------------ device arena
+class DeviceArena {
+ public:
+  DeviceArena() = default;
+  ~DeviceArena();
+  DeviceArena(const DeviceArena&) = delete;
+  DeviceArena& operator=(const DeviceArena&) = delete;
+  // Allocations are individually hipMalloc'd (so ASan-like tooling sees bounds) and freed
+  // together; sizes are rounded to 256 B.
+  void* alloc(size_t bytes);
+  size_t bytes() const { return total_; }
+  void release();
+
+ private:
+  std::vector<void*> ptrs_;
+  size_t total_ = 0;
+};
+
+// ------------------------------------------------------------------ tensors
+enum class DT { F16 = 0, F32 = 1, U8 = 2 };
+inline size_t dt_size(DT d) { return d == DT::F16 ? 2 : (d == DT::F32 ? 4 : 1); }
+
+// NHWC view.  `stride` = elements between consecutive pixels (>= c); ptr points at channel 0 of
+// this view (so a channel slice is a pointer offset).
+struct Tensor {
+  void* ptr = nullptr;
+  int n = 0, h = 0, w = 0, c = 0, stride = 0;
+  DT dt = DT::F16;
+  long pixels() const { return (long)n * h * w; }
+  size_t nbytes() const { return (size_t)pixels() * stride * dt_size(dt); }
+  Tensor slice_c(int off, int cnt) const {
+    Tensor t = *this;
+    t.ptr = (char*)ptr + (size_t)off * dt_size(dt);
+    t.c = cnt;
+    return t;
+  }
+  Tensor slice_n(int off, int cnt) const {
+    Tensor t = *this;
+    t.ptr = (char*)ptr + (size_t)off * h * w * stride * dt_size(dt);
+    t.n = cnt;
+    return t;
+  }
+  template <typename T>
+  T* as() const { return reinterpret_cast<T*>(ptr); }
+};
+
+Tensor make_tensor(DeviceArena& a, int n, int h, int w, int c, DT dt = DT::F16, int stride = -1);
+
+// ------------------------------------------------------------------ host weights
+struct HostTensor {
+  std::vector<int64_t> shape;
+  std::vector<float> data;  // converted to fp32 on load
+  int64_t numel() const {
+    int64_t n = 1;
+    for (auto s : shape) n *= s;
+    return n;
+  }
+};
+
+class WeightStore {
+ public:
+  // safetensors file (F32 / F16 / BF16 tensors).  `__metadata__` entries are kept as strings.
+  static std::unique_ptr<WeightStore> load_safetensors(const std::string& path);
+  bool has(const std::string& name) const { return t_.count(name) > 0; }
+  const HostTensor& get(const std::string& name) const;
+  std::string meta(const std::string& key, const std::string& dflt = "") const;
+  void put(const std::string& name, HostTensor t) { t_[name] = std::move(t); }
+  void set_meta(const std::string& k, const std::string& v) { meta_[k] = v; }
+  const std::map<std::string, HostTensor>& all() const { return t_; }
+
+ private:
+  std::map<std::string, HostTensor> t_;
+  std::map<std::string, std::string> meta_;
+};
+
+// ------------------------------------------------------------------ conv layers
+// Describes how the conv's (padded) input channels map to the checkpoint's input channels:
+// a list of {real, padded} segments concatenated along channels.
+struct ChanSeg {
+  int real, padded;
+};
+
+struct ConvSpec {
+  int kh = 3, kw = 3, sh = 1, sw = 1, ph = -1, pw = -1, dh = 1, dw = 1;
+};
+
+class ConvLayer {
+ public:
+  ConvLayer() = default;
+  // weight: [Cout][Cin][KH][KW] from `ws`, bias optional; optional BatchNorm fold with prefix
+  // `bn` (weight, bias, running_mean, running_var); `scale` multiplies weights and bias.
+  // Several checkpoint convs may be stacked along Cout (`wnames`).
+  void build(DeviceArena& arena, const WeightStore& ws, const std::vector<std::string>& wnames,
+             const std::vector<ChanSeg>& in_segs, ConvSpec spec,
+             const std::vector<std::string>& bn_names = {}, float scale = 1.f, float bn_eps = 1e-5f);
+  // Build from explicit host arrays (used by the native random-init path and tests).
+  void build_raw(DeviceArena& arena, const std::vector<float>& w, const std::vector<float>& b,
+                 int cout, int cin, const std::vector<ChanSeg>& in_segs, ConvSpec spec);
+
+  int cout() const { return cout_; }
+  int cin_padded() const { return cin_pad_; }
+  int out_h(int h) const { return (h + 2 * spec_.ph - spec_.dh * (spec_.kh - 1) - 1) / spec_.sh + 1; }
+  int out_w(int w) const { return (w + 2 * spec_.pw - spec_.dw * (spec_.kw - 1) - 1) / spec_.sw + 1; }
+
+  // Fill launch args for inputs (channel-concatenated sources) -> output view.
+  SaConvArgs args(const std::vector<Tensor>& srcs, const Tensor& out) const;
+  void run(hipStream_t s, const std::vector<Tensor>& srcs, const Tensor& out, int act = SA_ACT_NONE,
+           const Tensor* res = nullptr, int act2 = SA_ACT_NONE, double* stats = nullptr,
+           float alpha = 0.01f) const;
+  void launch(hipStream_t s, SaConvArgs& a) const;
+
+ private:
+  void upload(DeviceArena& arena, const std::vector<float>& w, const std::vector<float>& b, int cout,
+              int cin, const std::vector<ChanSeg>& segs);
+  ConvSpec spec_;
+  int cout_ = 0, cin_pad_ = 0, kpad_ = 0;
+  void* wdev_ = nullptr;
+  float* bdev_ = nullptr;
+};
+
+// ------------------------------------------------------------------ graph capture
+class GraphExec {
+ public:
+  ~GraphExec() { reset(); }
+  template <typename F>
+  void capture(hipStream_t s, F&& fn) {
+    reset();
+    HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    try {
+      fn();
+    } catch (...) {
+      hipGraph_t g;
+      (void)hipStreamEndCapture(s, &g);
+      if (g) (void)hipGraphDestroy(g);
+      throw;
+    }
+    HIP_CHECK(hipStreamEndCapture(s, &graph_));
+    HIP_CHECK(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
+  }
+  void launch(hipStream_t s) const { HIP_CHECK(hipGraphLaunch(exec_, s)); }
+  bool ready() const { return exec_ != nullptr; }
+  void reset();
+
+ private:
+  hipGraph_t graph_ = nullptr;
+  hipGraphExec_t exec_ = nullptr;
+};
+
+}  // namespace sa

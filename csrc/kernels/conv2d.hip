@@ -1,0 +1,371 @@
+// Implicit-GEMM 2-D convolution on CDNA4 matrix cores (gfx950).
+//
+// GEMM view: M = N*Ho*Wo output pixels (rows), N = Cout, K = KH*KW*Cin (ordered kh, kw, ci).
+// A (im2col) is gathered on the fly from NHWC fp16 activations — up to four channel-concatenated
+// sources, so torch.cat([h, x...]) in ConvGRU / motion encoder never materialises.  B is the
+// pre-packed fp16 weight [Cout_pad][Kpad].  Tiles: BMxBNx32 staged through LDS with register
+// double buffering, v_mfma_f32_16x16x32_f16 with fp32 accumulation, 256-thread workgroups
+// (4 wave64), XOR-swizzled 64-B LDS rows so the ds_read_b128 fragment reads are conflict-free
+// for the 4x16-lane read groups of gfx950.
+//
+// Epilogues are fused: bias/scale/activation, residual+activation, ConvGRU gate math
+// (z/r sigmoid, r*h, q tanh + state update), RAFT coordinate update, and per-channel
+// instance-norm statistics.  This replaces the TensorRT-fused convolutions that the reference
+// hides inside its engines (RAFTStereo/src/TRTRAFTStereo.cpp:137; upstream network layers per
+// SURVEY.md §2.2 M1/M2).
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include "sa/kernels.h"
+
+namespace {
+
+typedef _Float16 f16;
+typedef f16 half8 __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float act_apply(float v, int act, float alpha) {
+  switch (act) {
+    case SA_ACT_RELU: return v > 0.f ? v : 0.f;
+    case SA_ACT_LEAKY: return v > 0.f ? v : v * alpha;
+    case SA_ACT_TANH: {
+      float e = __expf(-2.f * fabsf(v));
+      float t = (1.f - e) / (1.f + e);
+      return v < 0.f ? -t : t;
+    }
+    case SA_ACT_SIGMOID: return 1.f / (1.f + __expf(-v));
+    default: return v;
+  }
+}
+
+__device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + __expf(-v)); }
+__device__ __forceinline__ float tanhf_(float v) { return act_apply(v, SA_ACT_TANH, 0.f); }
+
+__device__ __forceinline__ void load8(const f16* p, float* v) {
+  half8 h = *reinterpret_cast<const half8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (float)h[j];
+}
+__device__ __forceinline__ void store8(f16* p, const float* v) {
+  half8 h;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) h[j] = (f16)v[j];
+  *reinterpret_cast<half8*>(p) = h;
+}
+
+template <int BM, int BN, int WM, int WN>
+struct ConvCfg {
+  static constexpr int BK = 32;
+  static constexpr int TM = BM / WM, TN = BN / WN;
+  static constexpr int FM = TM / 16, FN = TN / 16;
+  static constexpr int A_CH = BM * 4, B_CH = BN * 4;  // 16-byte chunks per stage
+  static constexpr int A_PT = (A_CH + 255) / 256, B_PT = (B_CH + 255) / 256;
+  static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  static constexpr int STAGE_BYTES = 2 * (A_BYTES + B_BYTES);
+  static constexpr int CST = BN + 4;  // fp32 C-tile row stride
+  static constexpr int C_BYTES = BM * CST * 4;
+  static constexpr int SMEM = STAGE_BYTES > C_BYTES ? STAGE_BYTES : C_BYTES;
+  static_assert(WM * WN == 4, "4 waves per workgroup");
+  static_assert(TM % 16 == 0 && TN % 16 == 0, "wave tile must be 16-aligned");
+};
+
+// swizzled byte offset of (row, 16B-chunk) inside a [rows][32 halfs] stage buffer
+__device__ __forceinline__ int swz(int row, int c) { return row * 64 + ((c ^ (((row >> 3) & 1) * 3)) << 4); }
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
+  using C = ConvCfg<BM, BN, WM, WN>;
+  __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  const int HWo = p.Ho * p.Wo;
+  const int M = p.N * HWo;
+  const int m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int nk = p.Kpad / C::BK;
+  const int taps = p.KH * p.KW;
+
+  // ---------------- per-thread A-row precompute ----------------
+  const int cth = tid & 3;  // chunk index this thread loads (constant over k)
+  int a_ih0[C::A_PT], a_iw0[C::A_PT], a_nb[C::A_PT];
+  bool a_ok[C::A_PT];
+#pragma unroll
+  for (int i = 0; i < C::A_PT; ++i) {
+    int q = tid + 256 * i;
+    int row = q >> 2;
+    int m = m0 + row;
+    bool ok = (q < C::A_CH) && (m < M);
+    int mm = ok ? m : 0;
+    int n = mm / HWo;
+    int r = mm - n * HWo;
+    int oh = r / p.Wo, ow = r - oh * p.Wo;
+    a_ih0[i] = oh * p.sh - p.ph;
+    a_iw0[i] = ow * p.sw - p.pw;
+    a_nb[i] = n * p.H;
+    a_ok[i] = ok;
+  }
+  // k-position tracking for this thread's chunk
+  int k_tap, k_ci;
+  {
+    int kc = cth * 8;
+    k_tap = kc / p.Cin;
+    k_ci = kc - k_tap * p.Cin;
+  }
+  // source channel boundaries
+  int sb1 = p.src[0].channels;
+  int sb2 = sb1 + (p.nsrc > 1 ? p.src[1].channels : 0);
+  int sb3 = sb2 + (p.nsrc > 2 ? p.src[2].channels : 0);
+
+  const f16* wptr = reinterpret_cast<const f16*>(p.weight);
+
+  half8 ra[C::A_PT], rb[C::B_PT];
+  const half8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
+
+  auto load_tile = [&](int kt) {
+    // A: im2col gather
+    int kh = k_tap / p.KW, kw = k_tap - (k_tap / p.KW) * p.KW;
+    bool kok = k_tap < taps;
+    int s = (k_ci >= sb1) + (k_ci >= sb2) + (k_ci >= sb3);
+    int cbase = s == 0 ? 0 : (s == 1 ? sb1 : (s == 2 ? sb2 : sb3));
+    const f16* sptr = reinterpret_cast<const f16*>(p.src[s].ptr) + (k_ci - cbase);
+    int sstride = p.src[s].stride;
+#pragma unroll
+    for (int i = 0; i < C::A_PT; ++i) {
+      int ih = a_ih0[i] + kh * p.dh;
+      int iw = a_iw0[i] + kw * p.dw;
+      bool ok = a_ok[i] && kok && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+      if (ok) {
+        size_t pix = (size_t)(a_nb[i] + ih) * p.W + iw;
+        ra[i] = *reinterpret_cast<const half8*>(sptr + pix * sstride);
+      } else {
+        ra[i] = zero8;
+      }
+    }
+    // B: packed weights, always in bounds (Cout padded to a multiple of 128)
+#pragma unroll
+    for (int i = 0; i < C::B_PT; ++i) {
+      int q = tid + 256 * i;
+      if (q < C::B_CH) {
+        int row = q >> 2;
+        rb[i] = *reinterpret_cast<const half8*>(wptr + (size_t)(n0 + row) * p.Kpad + kt * C::BK +
+                                                 (q & 3) * 8);
+      }
+    }
+    // advance k position by BK for the next tile
+    k_ci += C::BK;
+    while (k_ci >= p.Cin) {
+      k_ci -= p.Cin;
+      ++k_tap;
+    }
+  };
+
+  auto store_tile = [&](int buf) {
+    char* sa = smem + buf * (C::A_BYTES + C::B_BYTES);
+    char* sb = sa + C::A_BYTES;
+#pragma unroll
+    for (int i = 0; i < C::A_PT; ++i) {
+      int q = tid + 256 * i;
+      if (q < C::A_CH) *reinterpret_cast<half8*>(sa + swz(q >> 2, q & 3)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < C::B_PT; ++i) {
+      int q = tid + 256 * i;
+      if (q < C::B_CH) *reinterpret_cast<half8*>(sb + swz(q >> 2, q & 3)) = rb[i];
+    }
+  };
+
+  floatx4 acc[C::FM][C::FN];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets (row = lane&15, chunk = lane>>4, swizzled)
+  const int frow = lane & 15;
+  const int foff = frow * 64 + (((lane >> 4) ^ (((frow >> 3) & 1) * 3)) << 4);
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_tile(kt + 1);
+    const char* sa = smem + cur * (C::A_BYTES + C::B_BYTES);
+    const char* sb = sa + C::A_BYTES;
+    half8 af[C::FM], bf[C::FN];
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+      af[i] = *reinterpret_cast<const half8*>(sa + (wm * C::TM + i * 16) * 64 + foff);
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j)
+      bf[j] = *reinterpret_cast<const half8*>(sb + (wn * C::TN + j * 16) * 64 + foff);
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    if (kt + 1 < nk) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---------------- epilogue: stage C through LDS ----------------
+  float* ct = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int row = wm * C::TM + i * 16 + (lane >> 4) * 4 + r;
+        int col = wn * C::TN + j * 16 + (lane & 15);
+        ct[row * C::CST + col] = acc[i][j][r];
+      }
+  __syncthreads();
+
+  constexpr int CPR = BN / 8;  // 8-channel chunks per row
+  constexpr int RPI = 256 / CPR;  // rows per pass
+  const int cc = tid % CPR;
+  const int co = n0 + cc * 8;
+  const bool do_stats = p.stats != nullptr;
+  float ssum[8], ssq[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ssum[j] = ssq[j] = 0.f;
+  int cur_img = -1;
+  const int nvalid = p.Cout - co;  // channels valid in this chunk (may be <=0 or <8)
+
+  auto flush_stats = [&](int img) {
+    if (img < 0) return;
+    for (int j = 0; j < 8 && j < nvalid; ++j) {
+      double* sp = p.stats + ((size_t)img * p.Cout + co + j) * 2;
+      atomicAdd(sp, (double)ssum[j]);
+      atomicAdd(sp + 1, (double)ssq[j]);
+      ssum[j] = ssq[j] = 0.f;
+    }
+  };
+
+  float bias8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bias8[j] = (p.bias && j < nvalid) ? p.bias[co + j] : 0.f;
+
+  if (nvalid > 0) {
+    for (int row = tid / CPR; row < BM; row += RPI) {
+      const int m = m0 + row;
+      if (m >= M) break;
+      float v[8];
+      const float* cp = ct + row * C::CST + cc * 8;
+      floatx4 c0 = *reinterpret_cast<const floatx4*>(cp);
+      floatx4 c1 = *reinterpret_cast<const floatx4*>(cp + 4);
+      v[0] = c0[0]; v[1] = c0[1]; v[2] = c0[2]; v[3] = c0[3];
+      v[4] = c1[0]; v[5] = c1[1]; v[6] = c1[2]; v[7] = c1[3];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = v[j] * p.scale + bias8[j];
+      const bool full = nvalid >= 8;
+
+      if (p.epi == SA_EPI_STORE || p.epi == SA_EPI_STORE_F32) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], p.act, p.alpha);
+        if (p.res) {
+          const f16* rp = reinterpret_cast<const f16*>(p.res) + (size_t)m * p.res_stride + co;
+          float r8[8];
+          if (full) load8(rp, r8);
+          else for (int j = 0; j < 8; ++j) r8[j] = j < nvalid ? (float)rp[j] : 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j] + r8[j], p.act2, p.alpha);
+        }
+        if (p.epi == SA_EPI_STORE) {
+          f16* op = reinterpret_cast<f16*>(p.out) + (size_t)m * p.out_stride + co;
+          if (full) store8(op, v);
+          else for (int j = 0; j < nvalid; ++j) op[j] = (f16)v[j];
+        } else {
+          float* op = reinterpret_cast<float*>(p.out) + (size_t)m * p.out_stride + co;
+          for (int j = 0; j < 8 && j < nvalid; ++j) op[j] = v[j];
+        }
+        if (do_stats) {
+          int img = m / HWo;
+          if (img != cur_img) {
+            flush_stats(cur_img);
+            cur_img = img;
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            ssum[j] += v[j];
+            ssq[j] += v[j] * v[j];
+          }
+        }
+      } else if (p.epi == SA_EPI_GRU_ZR) {
+        const int Hd = p.Cout >> 1;
+        const f16* cptr = reinterpret_cast<const f16*>(p.ctx) + (size_t)m * p.ctx_stride + co;
+        float c8[8];
+        load8(cptr, c8);
+        if (co < Hd) {
+          float z[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) z[j] = sigmoidf_(v[j] + c8[j]);
+          store8(reinterpret_cast<f16*>(p.aux) + (size_t)m * p.aux_stride + co, z);
+        } else {
+          const int ch = co - Hd;
+          float h8[8], rh[8];
+          load8(reinterpret_cast<const f16*>(p.hbuf) + (size_t)m * p.h_stride + ch, h8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) rh[j] = sigmoidf_(v[j] + c8[j]) * h8[j];
+          store8(reinterpret_cast<f16*>(p.rh) + (size_t)m * p.rh_stride + ch, rh);
+        }
+      } else if (p.epi == SA_EPI_GRU_Q) {
+        float c8[8], z8[8], h8[8];
+        load8(reinterpret_cast<const f16*>(p.ctx) + (size_t)m * p.ctx_stride + co, c8);
+        load8(reinterpret_cast<const f16*>(p.aux) + (size_t)m * p.aux_stride + co, z8);
+        f16* hp = reinterpret_cast<f16*>(p.hbuf) + (size_t)m * p.h_stride + co;
+        load8(hp, h8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float q = tanhf_(v[j] + c8[j]);
+          h8[j] = (1.f - z8[j]) * h8[j] + z8[j] * q;
+        }
+        store8(hp, h8);
+      } else if (p.epi == SA_EPI_FLOW_ACC) {
+        if (co == 0) {
+          float* fp = reinterpret_cast<float*>(p.out) + (size_t)m * p.out_stride;
+          *fp += v[0];
+        }
+      }
+    }
+  }
+  if (do_stats) flush_stats(cur_img);
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
+  const int M = a->N * a->Ho * a->Wo;
+  dim3 grid((M + BM - 1) / BM, (a->Cout + BN - 1) / BN);
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN>), grid, dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
+  if (a->Kpad % 32 != 0 || a->Cin % 8 != 0 || a->nsrc < 1 || a->nsrc > 4) return -2;
+  int cfg = a->tile_cfg;
+  if (cfg < 0) {
+    const int M = a->N * a->Ho * a->Wo;
+    if (a->Cout <= 16) cfg = 2;
+    else if (a->Cout <= 64) cfg = 1;
+    else {
+      // prefer the 128x128 tile only when it still fills the chip
+      long tiles128 = (long)((M + 127) / 128) * ((a->Cout + 127) / 128);
+      cfg = tiles128 >= 512 ? 0 : 1;
+    }
+  }
+  switch (cfg) {
+    case 0: return launch_cfg<128, 128, 2, 2>(a, stream);
+    case 1: return launch_cfg<128, 64, 2, 2>(a, stream);
+    case 2: return launch_cfg<256, 16, 4, 1>(a, stream);
+    case 3: return launch_cfg<64, 64, 2, 2>(a, stream);
+    default: return -3;
+  }
+}

@@ -1,0 +1,220 @@
+// Memory-bound NHWC fp16 kernels: instance-norm apply (+residual), 3x3/s2 and kxk average
+// pooling, bilinear resize.  Every thread moves 8 channels (16 B) per access (CDNA4 guide,
+// Guideline 13) and the kernels read/write channel slices of wider buffers so that
+// torch.cat-style concatenations in the upstream networks are free.
+//
+// Upstream ops mirrored: nn.InstanceNorm2d (RAFT-Stereo fnet, CREStereo fnet),
+// pool2x = F.avg_pool2d(x, 3, 2, 1) and interp = F.interpolate(bilinear, align_corners=True)
+// between the multi-level ConvGRUs of RAFT-Stereo.
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include "sa/kernels.h"
+
+namespace {
+typedef _Float16 f16;
+typedef f16 half8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float act_apply(float v, int act, float alpha) {
+  switch (act) {
+    case SA_ACT_RELU: return v > 0.f ? v : 0.f;
+    case SA_ACT_LEAKY: return v > 0.f ? v : v * alpha;
+    case SA_ACT_TANH: return tanhf(v);
+    case SA_ACT_SIGMOID: return 1.f / (1.f + __expf(-v));
+    default: return v;
+  }
+}
+
+__device__ __forceinline__ void ld8(const f16* p, float* v) {
+  half8 h = *reinterpret_cast<const half8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (float)h[j];
+}
+__device__ __forceinline__ void st8(f16* p, const float* v) {
+  half8 h;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) h[j] = (f16)v[j];
+  *reinterpret_cast<half8*>(p) = h;
+}
+
+__global__ void instnorm_apply_kernel(const SaNormArgs a) {
+  const int C8 = a.C >> 3;
+  const long total = (long)a.N * a.HW * C8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % C8);
+    const long pix = i / C8;
+    const int n = (int)(pix / a.HW);
+    const int c = c8 * 8;
+    float v[8];
+    ld8(reinterpret_cast<const f16*>(a.x) + pix * a.x_stride + c, v);
+    const double inv = 1.0 / (double)a.HW;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const double* s = a.stats + ((long)n * a.C + c + j) * 2;
+      double mean = s[0] * inv;
+      double var = s[1] * inv - mean * mean;
+      float rstd = rsqrtf((float)(var > 0.0 ? var : 0.0) + a.eps);
+      v[j] = act_apply((v[j] - (float)mean) * rstd, a.act, a.alpha);
+    }
+    if (a.res) {
+      float r[8];
+      ld8(reinterpret_cast<const f16*>(a.res) + pix * a.res_stride + c, r);
+      if (a.res_stats) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const double* s = a.res_stats + ((long)n * a.C + c + j) * 2;
+          double mean = s[0] * inv;
+          double var = s[1] * inv - mean * mean;
+          float rstd = rsqrtf((float)(var > 0.0 ? var : 0.0) + a.eps);
+          r[j] = (r[j] - (float)mean) * rstd;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j] + r[j], a.act2, a.alpha);
+    }
+    st8(reinterpret_cast<f16*>(a.out) + pix * a.out_stride + c, v);
+  }
+}
+
+__global__ void avgpool3s2_kernel(const f16* __restrict__ x, int xs, f16* __restrict__ out, int os,
+                                  int N, int H, int W, int C, int Ho, int Wo) {
+  const int C8 = C >> 3;
+  const long total = (long)N * Ho * Wo * C8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C8) * 8;
+    long p = i / C8;
+    const int ow = (int)(p % Wo);
+    p /= Wo;
+    const int oh = (int)(p % Ho);
+    const int n = (int)(p / Ho);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int dy = -1; dy <= 1; ++dy) {
+      int ih = oh * 2 + dy;
+      if (ih < 0 || ih >= H) continue;
+      for (int dx = -1; dx <= 1; ++dx) {
+        int iw = ow * 2 + dx;
+        if (iw < 0 || iw >= W) continue;
+        float v[8];
+        ld8(x + ((long)(n * H + ih) * W + iw) * xs + c, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += v[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] *= (1.f / 9.f);
+    st8(out + ((long)(n * Ho + oh) * Wo + ow) * os + c, acc);
+  }
+}
+
+__global__ void avgpoolk_kernel(const f16* __restrict__ x, int xs, f16* __restrict__ out, int os,
+                                int N, int H, int W, int C, int Ho, int Wo, int k) {
+  const int C8 = C >> 3;
+  const long total = (long)N * Ho * Wo * C8;
+  const float inv = 1.f / (float)(k * k);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C8) * 8;
+    long p = i / C8;
+    const int ow = (int)(p % Wo);
+    p /= Wo;
+    const int oh = (int)(p % Ho);
+    const int n = (int)(p / Ho);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int dy = 0; dy < k; ++dy)
+      for (int dx = 0; dx < k; ++dx) {
+        float v[8];
+        ld8(x + ((long)(n * H + oh * k + dy) * W + ow * k + dx) * xs + c, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += v[j];
+      }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] *= inv;
+    st8(out + ((long)(n * Ho + oh) * Wo + ow) * os + c, acc);
+  }
+}
+
+__device__ __forceinline__ float src_index(int dst, int in_size, int out_size, int ac) {
+  if (ac) return out_size > 1 ? (float)dst * (float)(in_size - 1) / (float)(out_size - 1) : 0.f;
+  float s = ((float)dst + 0.5f) * (float)in_size / (float)out_size - 0.5f;
+  return s < 0.f ? 0.f : s;
+}
+
+__global__ void interp_kernel(const f16* __restrict__ x, int xs, f16* __restrict__ out, int os,
+                              int N, int H, int W, int C, int Ho, int Wo, int ac, float mul) {
+  const int C8 = C >> 3;
+  const long total = (long)N * Ho * Wo * C8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C8) * 8;
+    long p = i / C8;
+    const int ow = (int)(p % Wo);
+    p /= Wo;
+    const int oh = (int)(p % Ho);
+    const int n = (int)(p / Ho);
+    float sy = src_index(oh, H, Ho, ac), sx = src_index(ow, W, Wo, ac);
+    int y0 = (int)floorf(sy), x0 = (int)floorf(sx);
+    y0 = y0 > H - 1 ? H - 1 : y0;
+    x0 = x0 > W - 1 ? W - 1 : x0;
+    int y1 = y0 + 1 < H ? y0 + 1 : H - 1;
+    int x1 = x0 + 1 < W ? x0 + 1 : W - 1;
+    float ly = sy - y0, lx = sx - x0;
+    float v00[8], v01[8], v10[8], v11[8];
+    ld8(x + ((long)(n * H + y0) * W + x0) * xs + c, v00);
+    ld8(x + ((long)(n * H + y0) * W + x1) * xs + c, v01);
+    ld8(x + ((long)(n * H + y1) * W + x0) * xs + c, v10);
+    ld8(x + ((long)(n * H + y1) * W + x1) * xs + c, v11);
+    float r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      r[j] = mul * ((1.f - ly) * ((1.f - lx) * v00[j] + lx * v01[j]) +
+                    ly * ((1.f - lx) * v10[j] + lx * v11[j]));
+    st8(out + ((long)(n * Ho + oh) * Wo + ow) * os + c, r);
+  }
+}
+
+inline int grid_for(long work) {
+  long g = (work + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+extern "C" int sa_instnorm_apply(const SaNormArgs* a, hipStream_t stream) {
+  if (a->C % 8) return -2;
+  long work = (long)a->N * a->HW * (a->C / 8);
+  hipLaunchKernelGGL(instnorm_apply_kernel, dim3(grid_for(work)), dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_avgpool3s2(const void* x, int xs, void* out, int os, int N, int H, int W, int C,
+                             hipStream_t stream) {
+  if (C % 8) return -2;
+  int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  long work = (long)N * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(avgpool3s2_kernel, dim3(grid_for(work)), dim3(256), 0, stream,
+                     (const f16*)x, xs, (f16*)out, os, N, H, W, C, Ho, Wo);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_avgpool_k(const void* x, int xs, void* out, int os, int N, int H, int W, int C,
+                            int k, hipStream_t stream) {
+  if (C % 8) return -2;
+  int Ho = H / k, Wo = W / k;
+  long work = (long)N * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(avgpoolk_kernel, dim3(grid_for(work)), dim3(256), 0, stream, (const f16*)x,
+                     xs, (f16*)out, os, N, H, W, C, Ho, Wo, k);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_interp_bilinear(const void* x, int xs, void* out, int os, int N, int H, int W,
+                                  int C, int Ho, int Wo, int ac, float mul, hipStream_t stream) {
+  if (C % 8) return -2;
+  long work = (long)N * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(interp_kernel, dim3(grid_for(work)), dim3(256), 0, stream, (const f16*)x, xs,
+                     (f16*)out, os, N, H, W, C, Ho, Wo, ac, mul);
+  return (int)hipGetLastError();
+}

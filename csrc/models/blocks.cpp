@@ -1,0 +1,96 @@
+#include "blocks.h"
+
+namespace sa {
+
+Norm parse_norm(const std::string& s) {
+  if (s == "batch") return Norm::Batch;
+  if (s == "instance") return Norm::Instance;
+  if (s == "none" || s.empty()) return Norm::None;
+  throw Error("unsupported norm " + s);
+}
+
+void instnorm(hipStream_t s, const Tensor& x, const double* stats, const Tensor& out, int act,
+              const Tensor* res, const double* res_stats, int act2) {
+  SaNormArgs a{};
+  a.x = x.ptr;
+  a.x_stride = x.stride;
+  a.stats = stats;
+  a.res = res ? res->ptr : nullptr;
+  a.res_stride = res ? res->stride : 0;
+  a.res_stats = res_stats;
+  a.out = out.ptr;
+  a.out_stride = out.stride;
+  a.N = x.n;
+  a.HW = x.h * x.w;
+  a.C = x.c;
+  a.act = act;
+  a.act2 = act2;
+  a.eps = 1e-5f;
+  a.alpha = 0.01f;
+  int rc = sa_instnorm_apply(&a, s);
+  SA_REQUIRE(rc == 0, "instnorm failed");
+  SA_LAUNCH_CHECK(s);
+}
+
+void ResBlock::build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std::string& p,
+                     int in_planes, int planes, int stride, Norm nrm, int N, int H, int W) {
+  norm = nrm;
+  has_down = !(stride == 1 && in_planes == planes);
+  src.conv(p + ".conv1", planes, in_planes, 3, 3);
+  src.conv(p + ".conv2", planes, planes, 3, 3);
+  if (has_down) src.conv(p + ".downsample.0", planes, in_planes, 1, 1);
+  const bool bn = norm == Norm::Batch;
+  if (bn) {
+    src.bn(p + ".norm1", planes);
+    src.bn(p + ".norm2", planes);
+    if (has_down) src.bn(p + ".norm3", planes);
+  }
+  const WeightStore& ws = *src.ws;
+  ConvSpec s3;
+  s3.sh = s3.sw = stride;
+  c1.build(a, ws, {p + ".conv1"}, {{in_planes, in_planes}}, s3, bn ? std::vector<std::string>{p + ".norm1"} : std::vector<std::string>{});
+  ConvSpec s1;
+  c2.build(a, ws, {p + ".conv2"}, {{planes, planes}}, s1, bn ? std::vector<std::string>{p + ".norm2"} : std::vector<std::string>{});
+  if (has_down) {
+    ConvSpec sd;
+    sd.sh = sd.sw = stride;
+    sd.ph = sd.pw = 0;
+    down.build(a, ws, {p + ".downsample.0"}, {{in_planes, in_planes}}, sd,
+               bn ? std::vector<std::string>{p + ".norm3"} : std::vector<std::string>{});
+  }
+  const int Ho = c1.out_h(H), Wo = c1.out_w(W);
+  if (norm == Norm::Instance) {
+    y1 = make_tensor(a, N, Ho, Wo, planes);
+    y2 = make_tensor(a, N, Ho, Wo, planes);
+    st1 = sp.take(N, planes);
+    st2 = sp.take(N, planes);
+    if (has_down) std_ = sp.take(N, planes);
+  }
+  a1 = make_tensor(a, N, Ho, Wo, planes);
+  if (has_down) yd = make_tensor(a, N, Ho, Wo, planes);
+  out = make_tensor(a, N, Ho, Wo, planes);
+}
+
+void ResBlock::run(hipStream_t s, const StatsPool& sp, const Tensor& x) const {
+  if (norm == Norm::Instance) {
+    c1.run(s, {x}, y1, SA_ACT_NONE, nullptr, SA_ACT_NONE, sp.resolve(st1));
+    instnorm(s, y1, sp.resolve(st1), a1, SA_ACT_RELU);
+    c2.run(s, {a1}, y2, SA_ACT_NONE, nullptr, SA_ACT_NONE, sp.resolve(st2));
+    if (has_down) {
+      down.run(s, {x}, yd, SA_ACT_NONE, nullptr, SA_ACT_NONE, sp.resolve(std_));
+      instnorm(s, y2, sp.resolve(st2), out, SA_ACT_RELU, &yd, sp.resolve(std_), SA_ACT_RELU);
+    } else {
+      instnorm(s, y2, sp.resolve(st2), out, SA_ACT_RELU, &x, nullptr, SA_ACT_RELU);
+    }
+  } else {
+    c1.run(s, {x}, a1, SA_ACT_RELU);
+    if (has_down) {
+      down.run(s, {x}, yd, SA_ACT_NONE);
+      c2.run(s, {a1}, out, SA_ACT_RELU, &yd, SA_ACT_RELU);
+    } else {
+      c2.run(s, {a1}, out, SA_ACT_RELU, &x, SA_ACT_RELU);
+    }
+  }
+}
+
+}  // namespace sa

@@ -1,0 +1,58 @@
+// Reusable network blocks built on ConvLayer: residual blocks with batch (folded) / instance /
+// no normalisation, and the instance-norm statistics pool.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "sa/engine.h"
+
+namespace sa {
+
+enum class Norm { None, Batch, Instance };
+Norm parse_norm(const std::string& s);
+
+// Per-forward statistics buffers (double {sum, sumsq} per (n, c)), zeroed by one memset.
+class StatsPool {
+ public:
+  double* take(int n, int c) {
+    size_t need = (size_t)n * c * 2;
+    reserve_.push_back(need);
+    offs_.push_back(total_);
+    total_ += need;
+    return reinterpret_cast<double*>((size_t)offs_.size());  // placeholder resolved in finalize
+  }
+  void finalize(DeviceArena& a) {
+    base_ = (double*)a.alloc(std::max<size_t>(total_, 1) * sizeof(double));
+  }
+  double* resolve(double* handle) const {
+    if (!handle) return nullptr;
+    size_t idx = (size_t)handle - 1;
+    return base_ + offs_[idx];
+  }
+  void zero(hipStream_t s) const { HIP_CHECK(hipMemsetAsync(base_, 0, std::max<size_t>(total_, 1) * sizeof(double), s)); }
+
+ private:
+  std::vector<size_t> reserve_, offs_;
+  size_t total_ = 0;
+  double* base_ = nullptr;
+};
+
+// ResidualBlock of RAFT-Stereo / CREStereo extractors (upstream core/extractor.py):
+//   y = relu(norm1(conv1(x))); y = relu(norm2(conv2(y))); x' = downsample(x) if needed;
+//   out = relu(x' + y)
+struct ResBlock {
+  ConvLayer c1, c2, down;
+  bool has_down = false;
+  Norm norm = Norm::None;
+  Tensor y1, a1, y2, yd, out;
+  double *st1 = nullptr, *st2 = nullptr, *std_ = nullptr;  // StatsPool handles
+  void build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std::string& prefix, int in_planes,
+             int planes, int stride, Norm norm, int N, int H, int W);
+  void run(hipStream_t s, const StatsPool& sp, const Tensor& x) const;
+};
+
+// norm apply helper
+void instnorm(hipStream_t s, const Tensor& x, const double* stats, const Tensor& out, int act,
+              const Tensor* res = nullptr, const double* res_stats = nullptr, int act2 = SA_ACT_NONE);
+
+}  // namespace sa

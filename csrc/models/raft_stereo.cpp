@@ -1,0 +1,459 @@
+// RAFT-Stereo (sceneflow and realtime presets) as a native op graph.
+//
+// Reference pins: I/O contract of RAFTStereo/src/TRTRAFTStereo.cpp:13-20
+// (inputs left/right [1,3,480,640] RGB 0..255, output flow_up [1,1,H,W] = negative disparity,
+// optional low-res flow "diff"), export flags at README_en.md:88-101.  The network itself follows
+// upstream RAFT-Stereo (core/raft_stereo.py, extractor.py, update.py, corr.py) with weight names
+// identical to the upstream state_dict, so converted checkpoints load unchanged.
+//
+// Per frame (B stereo pairs):
+//   preprocess (2x/255-1, fp16 NHWC)            1 launch
+//   feature / context encoders                  ~40-60 launches (instance-norm stats fused in conv)
+//   corr pyramid (MFMA, pooled levels fused)    1 launch
+//   iters x [lookup, motion encoder x5, ConvGRU(zr+q fused gates) per level, flow head (+coords
+//            update fused)]; mask head + convex upsample on the last iteration only
+//   reprojection (base class)
+// The entire frame is one hipGraph.
+#include <cmath>
+
+#include "blocks.h"
+
+namespace sa {
+namespace {
+
+struct RaftCfg {
+  int n_downsample = 2;
+  int n_gru = 3;
+  bool slow_fast = false;
+  bool shared = false;
+  int iters = 32;
+  int hidden = 128;
+  int levels = 4;
+  int radius = 4;
+  Norm context_norm = Norm::Batch;
+};
+
+RaftCfg preset(const std::string& name) {
+  RaftCfg c;
+  if (name == "raftstereo-sceneflow" || name == "raftstereo") {
+    // upstream defaults (train_stereo.py / demo.py): n_downsample 2, 3 GRUs, 32 valid iters
+  } else if (name == "raftstereo-realtime") {
+    // README_en.md:95-101: --shared_backbone --n_downsample 3 --n_gru_layers 2 --slow_fast_gru
+    // --valid_iters 7 --mixed_precision
+    c.n_downsample = 3;
+    c.n_gru = 2;
+    c.slow_fast = true;
+    c.shared = true;
+    c.iters = 7;
+  } else {
+    throw Error("unknown RAFT-Stereo preset " + name);
+  }
+  return c;
+}
+
+int conv_out(int x, int k, int s, int p) { return (x + 2 * p - k) / s + 1; }
+
+class RaftStereo : public StereoEngine {
+ public:
+  explicit RaftStereo(const EngineConfig& cfg) : StereoEngine(cfg), rc_(preset(cfg.model)) {
+    if (cfg.iters > 0) rc_.iters = cfg.iters;
+  }
+  const char* name() const override { return "RAFTStereo"; }
+  const float* aux_output(int* n) const override {
+    *n = B() * lh_[0] * lw_[0];
+    return flow_;
+  }
+
+ protected:
+  void build(WeightSource& src) override;
+  void forward(hipStream_t s) override;
+
+ private:
+  struct Encoder {  // BasicEncoder / MultiBasicEncoder trunk (conv1 + layer1..3)
+    ConvLayer conv1;
+    Norm norm;
+    Tensor c1y, c1a;
+    double* c1st = nullptr;
+    std::vector<ResBlock> layers;  // layer1..3 (2 blocks each)
+  };
+  void build_trunk(Encoder& e, WeightSource& src, const std::string& p, Norm norm, int N);
+  void run_trunk(hipStream_t s, const Encoder& e, const Tensor& img) const;
+  void gru(hipStream_t s, int lvl, const std::vector<Tensor>& x) const;
+
+  RaftCfg rc_;
+  StatsPool sp_;
+  Tensor img_;  // [2B][H][W][8] preprocessed
+  Encoder fnet_, cnet_;
+  ConvLayer fconv2_;          // fnet.conv2 (1x1 128->256) (non-shared)
+  ResBlock shared_rb_;        // conv2.0 (shared backbone)
+  ConvLayer shared_conv_;     // conv2.1
+  std::vector<ResBlock> layer4_, layer5_;
+  // context heads [level][net/ctx]
+  ResBlock head_rb_[3][2];
+  ConvLayer head_conv_[3][2];
+  ConvLayer zqr_[3];
+  Tensor fmap_;              // [2B][h0][w0][256]
+  Tensor net_[3], ctxh_[3], czrq_[3];
+  // update block
+  ConvLayer convc1_, convc2_, convf1_, convf2_, mconv_;
+  ConvLayer gzr_[3], gq_[3];
+  ConvLayer fh1_, fh1mask_, fh2_, mask2_;
+  Tensor corr_feat_, flow_feat_, cor1_, flo1_, corflo_, motion_;
+  Tensor z_[3], rh_[3];
+  Tensor pool_[2], interp_[2];  // pool_[i] = pool2x(net[i]) at level i+1; interp_[i] = interp(net[i+1]) at level i
+  Tensor fh_, mask_;
+  float* pyr_ = nullptr;
+  float* flow_ = nullptr;
+  int lh_[3], lw_[3];
+};
+
+void RaftStereo::build_trunk(Encoder& e, WeightSource& src, const std::string& p, Norm norm, int N) {
+  DeviceArena& a = arena_;
+  e.norm = norm;
+  const int s1 = 1 + (rc_.n_downsample > 2);
+  src.conv(p + ".conv1", 64, 3, 7, 7);
+  if (norm == Norm::Batch) src.bn(p + ".norm1", 64);
+  ConvSpec sp7;
+  sp7.sh = sp7.sw = s1;
+  e.conv1.build(a, *src.ws, {p + ".conv1"}, {{3, 8}}, sp7,
+                norm == Norm::Batch ? std::vector<std::string>{p + ".norm1"} : std::vector<std::string>{});
+  int h = conv_out(H(), 7, s1, 3), w = conv_out(W(), 7, s1, 3);
+  if (norm == Norm::Instance) {
+    e.c1y = make_tensor(a, N, h, w, 64);
+    e.c1st = sp_.take(N, 64);
+  }
+  e.c1a = make_tensor(a, N, h, w, 64);
+  const int dims[3] = {64, 96, 128};
+  const int strides[3] = {1, 1 + (rc_.n_downsample > 1), 1 + (rc_.n_downsample > 0)};
+  int inp = 64;
+  e.layers.resize(6);
+  for (int l = 0; l < 3; ++l) {
+    for (int b = 0; b < 2; ++b) {
+      ResBlock& rb = e.layers[l * 2 + b];
+      int st = b == 0 ? strides[l] : 1;
+      rb.build(a, src, sp_, p + ".layer" + std::to_string(l + 1) + "." + std::to_string(b), inp,
+               dims[l], st, norm, N, h, w);
+      h = rb.out.h;
+      w = rb.out.w;
+      inp = dims[l];
+    }
+  }
+}
+
+void RaftStereo::run_trunk(hipStream_t s, const Encoder& e, const Tensor& img) const {
+  if (e.norm == Norm::Instance) {
+    e.conv1.run(s, {img}, e.c1y, SA_ACT_NONE, nullptr, SA_ACT_NONE, sp_.resolve(e.c1st));
+    instnorm(s, e.c1y, sp_.resolve(e.c1st), e.c1a, SA_ACT_RELU);
+  } else {
+    e.conv1.run(s, {img}, e.c1a, SA_ACT_RELU);
+  }
+  const Tensor* x = &e.c1a;
+  for (const auto& rb : e.layers) {
+    rb.run(s, sp_, *x);
+    x = &rb.out;
+  }
+}
+
+void RaftStereo::build(WeightSource& src) {
+  DeviceArena& a = arena_;
+  const int Bn = B();
+  const int hd = rc_.hidden;
+  img_ = make_tensor(a, 2 * Bn, H(), W(), 8);
+
+  // ---------------- encoders ----------------
+  build_trunk(cnet_, src, "cnet", rc_.context_norm, rc_.shared ? 2 * Bn : Bn);
+  lh_[0] = cnet_.layers.back().out.h;
+  lw_[0] = cnet_.layers.back().out.w;
+  if (!rc_.shared) {
+    build_trunk(fnet_, src, "fnet", Norm::Instance, 2 * Bn);
+    src.conv("fnet.conv2", 256, 128, 1, 1);
+    ConvSpec s1;
+    fconv2_.build(a, *src.ws, {"fnet.conv2"}, {{128, 128}}, s1);
+  } else {
+    shared_rb_.build(a, src, sp_, "conv2.0", 128, 128, 1, Norm::Instance, 2 * Bn, lh_[0], lw_[0]);
+    src.conv("conv2.1", 256, 128, 3, 3);
+    ConvSpec s3;
+    shared_conv_.build(a, *src.ws, {"conv2.1"}, {{128, 128}}, s3);
+  }
+  fmap_ = make_tensor(a, 2 * Bn, lh_[0], lw_[0], 256);
+
+  // context levels 2,3 (layer4/5 always exist in MultiBasicEncoder)
+  layer4_.resize(2);
+  layer5_.resize(2);
+  {
+    int h = lh_[0], w = lw_[0];
+    for (int b = 0; b < 2; ++b) {
+      layer4_[b].build(a, src, sp_, "cnet.layer4." + std::to_string(b), 128, 128, b == 0 ? 2 : 1,
+                       rc_.context_norm, Bn, h, w);
+      h = layer4_[b].out.h;
+      w = layer4_[b].out.w;
+    }
+    lh_[1] = h;
+    lw_[1] = w;
+    for (int b = 0; b < 2; ++b) {
+      layer5_[b].build(a, src, sp_, "cnet.layer5." + std::to_string(b), 128, 128, b == 0 ? 2 : 1,
+                       rc_.context_norm, Bn, h, w);
+      h = layer5_[b].out.h;
+      w = layer5_[b].out.w;
+    }
+    lh_[2] = h;
+    lw_[2] = w;
+  }
+  const char* lvl_names[3] = {"outputs08", "outputs16", "outputs32"};
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 2; ++j) {
+      std::string p = std::string("cnet.") + lvl_names[i] + "." + std::to_string(j);
+      ConvSpec s3;
+      if (i < 2) {
+        head_rb_[i][j].build(a, src, sp_, p + ".0", 128, 128, 1, rc_.context_norm, Bn, lh_[i], lw_[i]);
+        src.conv(p + ".1", hd, 128, 3, 3);
+        head_conv_[i][j].build(a, *src.ws, {p + ".1"}, {{128, 128}}, s3);
+      } else {
+        src.conv(p, hd, 128, 3, 3);
+        head_conv_[i][j].build(a, *src.ws, {p}, {{128, 128}}, s3);
+      }
+    }
+  }
+  for (int i = 0; i < rc_.n_gru; ++i) {
+    net_[i] = make_tensor(a, Bn, lh_[i], lw_[i], hd);
+    ctxh_[i] = make_tensor(a, Bn, lh_[i], lw_[i], hd);
+    czrq_[i] = make_tensor(a, Bn, lh_[i], lw_[i], 3 * hd);
+    std::string p = "context_zqr_convs." + std::to_string(i);
+    src.conv(p, 3 * hd, hd, 3, 3);
+    ConvSpec s3;
+    zqr_[i].build(a, *src.ws, {p}, {{hd, hd}}, s3);
+  }
+
+  // ---------------- correlation ----------------
+  {
+    long tot = 0;
+    int wl = lw_[0];
+    for (int l = 0; l < rc_.levels; ++l) {
+      tot += (long)Bn * lh_[0] * lw_[0] * wl;
+      wl >>= 1;
+    }
+    pyr_ = (float*)a.alloc(tot * 4);
+  }
+  flow_ = (float*)a.alloc((size_t)Bn * lh_[0] * lw_[0] * 4);
+
+  // ---------------- update block ----------------
+  const int cor_planes = rc_.levels * (2 * rc_.radius + 1);
+  const int corp = round_up(cor_planes, 8);
+  const std::string u = "update_block.";
+  src.conv(u + "encoder.convc1", 64, cor_planes, 1, 1);
+  src.conv(u + "encoder.convc2", 64, 64, 3, 3);
+  src.conv(u + "encoder.convf1", 64, 2, 7, 7);
+  src.conv(u + "encoder.convf2", 64, 64, 3, 3);
+  src.conv(u + "encoder.conv", 128 - 2, 128, 3, 3);
+  const WeightStore& ws = *src.ws;
+  ConvSpec s3, s1, s7;
+  s1.kh = s1.kw = 1;
+  convc1_.build(a, ws, {u + "encoder.convc1"}, {{cor_planes, corp}}, s1);
+  convc2_.build(a, ws, {u + "encoder.convc2"}, {{64, 64}}, s3);
+  convf1_.build(a, ws, {u + "encoder.convf1"}, {{2, 8}}, s7);
+  convf2_.build(a, ws, {u + "encoder.convf2"}, {{64, 64}}, s3);
+  mconv_.build(a, ws, {u + "encoder.conv"}, {{128, 128}}, s3);
+
+  const char* gnames[3] = {"gru08", "gru16", "gru32"};
+  for (int i = 0; i < rc_.n_gru; ++i) {
+    int xin;
+    if (i == 0) xin = 128 + (rc_.n_gru > 1 ? hd : 0);
+    else if (i == 1) xin = hd + (rc_.n_gru == 3 ? hd : 0);
+    else xin = hd;
+    std::string p = u + gnames[i];
+    src.conv(p + ".convz", hd, hd + xin, 3, 3);
+    src.conv(p + ".convr", hd, hd + xin, 3, 3);
+    src.conv(p + ".convq", hd, hd + xin, 3, 3);
+    std::vector<ChanSeg> segs = {{hd, hd}};
+    for (int k = 0; k < xin / 128; ++k) segs.push_back({128, 128});
+    gzr_[i].build(a, ws, {p + ".convz", p + ".convr"}, segs, s3);
+    gq_[i].build(a, ws, {p + ".convq"}, segs, s3);
+    z_[i] = make_tensor(a, Bn, lh_[i], lw_[i], hd);
+    rh_[i] = make_tensor(a, Bn, lh_[i], lw_[i], hd);
+  }
+  const int f = 1 << rc_.n_downsample;
+  src.conv(u + "flow_head.conv1", 256, hd, 3, 3);
+  src.conv(u + "flow_head.conv2", 2, 256, 3, 3);
+  src.conv(u + "mask.0", 256, hd, 3, 3);
+  src.conv(u + "mask.2", f * f * 9, 256, 1, 1);
+  fh1_.build(a, ws, {u + "flow_head.conv1"}, {{hd, hd}}, s3);
+  fh1mask_.build(a, ws, {u + "flow_head.conv1", u + "mask.0"}, {{hd, hd}}, s3);
+  {
+    // only the x component of delta_flow is used (upstream zeroes delta_flow[:,1])
+    const HostTensor& w2 = ws.get(u + "flow_head.conv2.weight");
+    const HostTensor& b2 = ws.get(u + "flow_head.conv2.bias");
+    std::vector<float> wx(w2.data.begin(), w2.data.begin() + 256 * 9);
+    std::vector<float> bx = {b2.data[0]};
+    fh2_.build_raw(a, wx, bx, 1, 256, {{256, 256}}, s3);
+  }
+  mask2_.build(a, ws, {u + "mask.2"}, {{256, 256}}, s1, {}, 0.25f);
+
+  const int h0 = lh_[0], w0 = lw_[0];
+  corr_feat_ = make_tensor(a, Bn, h0, w0, corp);
+  flow_feat_ = make_tensor(a, Bn, h0, w0, 8);
+  cor1_ = make_tensor(a, Bn, h0, w0, 64);
+  flo1_ = make_tensor(a, Bn, h0, w0, 64);
+  corflo_ = make_tensor(a, Bn, h0, w0, 128);
+  motion_ = make_tensor(a, Bn, h0, w0, 128);
+  fh_ = make_tensor(a, Bn, h0, w0, 512);
+  mask_ = make_tensor(a, Bn, h0, w0, round_up(f * f * 9, 8));
+  for (int i = 0; i + 1 < rc_.n_gru; ++i) {
+    pool_[i] = make_tensor(a, Bn, lh_[i + 1], lw_[i + 1], hd);
+    interp_[i] = make_tensor(a, Bn, lh_[i], lw_[i], hd);
+  }
+  sp_.finalize(a);
+}
+
+void RaftStereo::gru(hipStream_t s, int i, const std::vector<Tensor>& x) const {
+  std::vector<Tensor> srcs = {net_[i]};
+  srcs.insert(srcs.end(), x.begin(), x.end());
+  SaConvArgs za = gzr_[i].args(srcs, z_[i]);
+  za.epi = SA_EPI_GRU_ZR;
+  za.ctx = czrq_[i].ptr;
+  za.ctx_stride = czrq_[i].stride;
+  za.aux = z_[i].ptr;
+  za.aux_stride = z_[i].stride;
+  za.hbuf = net_[i].ptr;
+  za.h_stride = net_[i].stride;
+  za.rh = rh_[i].ptr;
+  za.rh_stride = rh_[i].stride;
+  gzr_[i].launch(s, za);
+  srcs[0] = rh_[i];
+  SaConvArgs qa = gq_[i].args(srcs, net_[i]);
+  qa.epi = SA_EPI_GRU_Q;
+  qa.ctx = czrq_[i].slice_c(2 * rc_.hidden, rc_.hidden).ptr;
+  qa.ctx_stride = czrq_[i].stride;
+  qa.aux = z_[i].ptr;
+  qa.aux_stride = z_[i].stride;
+  qa.hbuf = net_[i].ptr;
+  qa.h_stride = net_[i].stride;
+  gq_[i].launch(s, qa);
+}
+
+static void check(int rc, const char* what) { SA_REQUIRE(rc == 0, "%s failed (rc=%d)", what, rc); }
+
+void RaftStereo::forward(hipStream_t s) {
+  const int Bn = B();
+  const int hd = rc_.hidden;
+  sp_.zero(s);
+  // preprocess: left images -> img[0:B], right -> img[B:2B], 2*(x/255)-1, RGB, 8-ch padded
+  check(sa_preprocess(in_left_, Bn, H(), W(), SA_PRE_SIGNED, img_.ptr, 8, 0, 8, s), "preprocess");
+  check(sa_preprocess(in_right_, Bn, H(), W(), SA_PRE_SIGNED, img_.slice_n(Bn, Bn).ptr, 8, 0, 8, s), "preprocess");
+
+  // encoders
+  if (rc_.shared) {
+    run_trunk(s, cnet_, img_);
+    const Tensor& v = cnet_.layers.back().out;
+    shared_rb_.run(s, sp_, v);
+    shared_conv_.run(s, {shared_rb_.out}, fmap_);
+  } else {
+    run_trunk(s, cnet_, img_.slice_n(0, Bn));
+    run_trunk(s, fnet_, img_);
+    fconv2_.run(s, {fnet_.layers.back().out}, fmap_);
+  }
+  Tensor x = cnet_.layers.back().out.slice_n(0, Bn);
+  Tensor lvl_in[3];
+  lvl_in[0] = x;
+  if (rc_.n_gru >= 2) {
+    layer4_[0].run(s, sp_, x);
+    layer4_[1].run(s, sp_, layer4_[0].out);
+    lvl_in[1] = layer4_[1].out;
+  }
+  if (rc_.n_gru >= 3) {
+    layer5_[0].run(s, sp_, lvl_in[1]);
+    layer5_[1].run(s, sp_, layer5_[0].out);
+    lvl_in[2] = layer5_[1].out;
+  }
+  for (int i = 0; i < rc_.n_gru; ++i) {
+    Tensor hin[2] = {lvl_in[i], lvl_in[i]};
+    if (i < 2) {
+      head_rb_[i][0].run(s, sp_, lvl_in[i]);
+      head_rb_[i][1].run(s, sp_, lvl_in[i]);
+      hin[0] = head_rb_[i][0].out;
+      hin[1] = head_rb_[i][1].out;
+    }
+    head_conv_[i][0].run(s, {hin[0]}, net_[i], SA_ACT_TANH);
+    head_conv_[i][1].run(s, {hin[1]}, ctxh_[i], SA_ACT_RELU);
+    zqr_[i].run(s, {ctxh_[i]}, czrq_[i]);
+  }
+
+  // correlation pyramid
+  const int h0 = lh_[0], w0 = lw_[0];
+  check(sa_corr1d_pyramid(fmap_.ptr, fmap_.slice_n(Bn, Bn).ptr, 256, Bn, h0, w0, w0, 256,
+                          rc_.levels, pyr_, s),
+        "corr pyramid");
+  HIP_CHECK(hipMemsetAsync(flow_, 0, (size_t)Bn * h0 * w0 * 4, s));
+
+  auto pool = [&](int i) {  // pool_[i] = pool2x(net[i])
+    check(sa_avgpool3s2(net_[i].ptr, net_[i].stride, pool_[i].ptr, pool_[i].stride, Bn, lh_[i],
+                        lw_[i], hd, s),
+          "pool2x");
+  };
+  auto interp = [&](int i) {  // interp_[i] = interp(net[i+1], net[i])
+    check(sa_interp_bilinear(net_[i + 1].ptr, net_[i + 1].stride, interp_[i].ptr, interp_[i].stride,
+                             Bn, lh_[i + 1], lw_[i + 1], hd, lh_[i], lw_[i], 1, 1.f, s),
+          "interp");
+  };
+  auto gru32 = [&]() {
+    pool(1);
+    gru(s, 2, {pool_[1]});
+  };
+  auto gru16 = [&]() {
+    pool(0);
+    if (rc_.n_gru == 3) {
+      interp(1);
+      gru(s, 1, {pool_[0], interp_[1]});
+    } else {
+      gru(s, 1, {pool_[0]});
+    }
+  };
+
+  const int f = 1 << rc_.n_downsample;
+  for (int it = 0; it < rc_.iters; ++it) {
+    const bool last = it == rc_.iters - 1;
+    check(sa_corr1d_lookup(pyr_, flow_, Bn, h0, w0, w0, rc_.levels, rc_.radius, corr_feat_.ptr,
+                           corr_feat_.stride, corr_feat_.c, flow_feat_.ptr, flow_feat_.stride, 8,
+                           motion_.slice_c(126, 2).ptr, motion_.stride, s),
+          "corr lookup");
+    if (rc_.n_gru == 3 && rc_.slow_fast) gru32();
+    if (rc_.n_gru >= 2 && rc_.slow_fast) {
+      if (rc_.n_gru == 3) gru32();
+      gru16();
+    }
+    // motion encoder
+    convc1_.run(s, {corr_feat_}, cor1_, SA_ACT_RELU);
+    convc2_.run(s, {cor1_}, corflo_.slice_c(0, 64), SA_ACT_RELU);
+    convf1_.run(s, {flow_feat_}, flo1_, SA_ACT_RELU);
+    convf2_.run(s, {flo1_}, corflo_.slice_c(64, 64), SA_ACT_RELU);
+    mconv_.run(s, {corflo_}, motion_.slice_c(0, 126), SA_ACT_RELU);
+    if (rc_.n_gru == 3) gru32();
+    if (rc_.n_gru >= 2) gru16();
+    if (rc_.n_gru > 1) {
+      interp(0);
+      gru(s, 0, {motion_, interp_[0]});
+    } else {
+      gru(s, 0, {motion_});
+    }
+    // flow head (+ mask head on the last iteration), coords1 += delta (x only)
+    if (last) fh1mask_.run(s, {net_[0]}, fh_, SA_ACT_RELU);
+    else fh1_.run(s, {net_[0]}, fh_.slice_c(0, 256), SA_ACT_RELU);
+    {
+      SaConvArgs fa = fh2_.args({fh_.slice_c(0, 256)}, Tensor{flow_, Bn, h0, w0, 1, 1, DT::F32});
+      fa.epi = SA_EPI_FLOW_ACC;
+      fh2_.launch(s, fa);
+    }
+    if (last) mask2_.run(s, {fh_.slice_c(256, 256)}, mask_);
+  }
+  // convex upsampling; disparity = -flow_up
+  check(sa_convex_upsample(mask_.ptr, mask_.stride, flow_, Bn, h0, w0, f, -1.f, disp_, s),
+        "convex upsample");
+  (void)hd;
+}
+
+}  // namespace
+
+std::unique_ptr<StereoEngine> make_raft_stereo(const EngineConfig& cfg) {
+  return std::unique_ptr<StereoEngine>(new RaftStereo(cfg));
+}
+
+}  // namespace sa

@@ -1,0 +1,20 @@
+// Model families whose native graphs are not wired yet fail loudly at creation.
+#include "sa/engine.h"
+
+namespace sa {
+#ifndef SA_HAVE_CRESTEREO
+std::unique_ptr<StereoEngine> make_crestereo(const EngineConfig& cfg) {
+  throw Error("CREStereo native engine not built (preset " + cfg.model + ")");
+}
+#endif
+#ifndef SA_HAVE_HITNET
+std::unique_ptr<StereoEngine> make_hitnet(const EngineConfig& cfg) {
+  throw Error("HITNet native engine not built (preset " + cfg.model + ")");
+}
+#endif
+#ifndef SA_HAVE_FASTACV
+std::unique_ptr<StereoEngine> make_fast_acvnet(const EngineConfig& cfg) {
+  throw Error("Fast-ACVNet+ native engine not built (preset " + cfg.model + ")");
+}
+#endif
+}  // namespace sa

@@ -1,0 +1,216 @@
+// StereoEngine base: io buffers, rectification + reprojection around the model forward,
+// graph capture, host-side timed path.
+#include "sa/engine.h"
+
+#include <cmath>
+#include <cstring>
+
+namespace sa {
+
+// ------------------------------------------------------------------ deterministic init
+static uint64_t fnv1a(const std::string& s, uint64_t seed) {
+  uint64_t h = 1469598103934665603ull ^ (seed * 0x9E3779B97F4A7C15ull);
+  for (unsigned char c : s) {
+    h ^= c;
+    h *= 1099511628211ull;
+  }
+  return h;
+}
+
+struct SplitMix {
+  uint64_t x;
+  uint64_t next() {
+    uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  }
+  float uniform(float lo, float hi) { return lo + (hi - lo) * (float)((next() >> 40) * (1.0 / 16777216.0)); }
+};
+
+void WeightSource::param(const std::string& name, std::vector<int64_t> shape, float lo, float hi) {
+  if (ws->has(name)) {
+    const auto& t = ws->get(name);
+    SA_REQUIRE(t.shape == shape, "weight %s has unexpected shape", name.c_str());
+    return;
+  }
+  SA_REQUIRE(random, "missing weight %s", name.c_str());
+  HostTensor t;
+  t.shape = shape;
+  t.data.resize(t.numel());
+  SplitMix rng{fnv1a(name, seed)};
+  for (auto& v : t.data) v = lo == hi ? lo : rng.uniform(lo, hi);
+  ws->put(name, std::move(t));
+}
+
+void WeightSource::conv(const std::string& name, int cout, int cin, int kh, int kw, bool bias) {
+  float bound = 1.f / std::sqrt((float)(cin * kh * kw));
+  param(name + ".weight", {cout, cin, kh, kw}, -bound, bound);
+  if (bias) param(name + ".bias", {cout}, -bound, bound);
+}
+
+void WeightSource::bn(const std::string& name, int c) {
+  param(name + ".weight", {c}, 1.f, 1.f);
+  param(name + ".bias", {c}, 0.f, 0.f);
+  param(name + ".running_mean", {c}, 0.f, 0.f);
+  param(name + ".running_var", {c}, 1.f, 1.f);
+}
+
+void WeightSource::linear(const std::string& name, int out, int in, bool bias) {
+  float bound = 1.f / std::sqrt((float)in);
+  param(name + ".weight", {out, in}, -bound, bound);
+  if (bias) param(name + ".bias", {out}, -bound, bound);
+}
+
+void WeightSource::ln(const std::string& name, int c) {
+  param(name + ".weight", {c}, 1.f, 1.f);
+  param(name + ".bias", {c}, 0.f, 0.f);
+}
+
+// ------------------------------------------------------------------ engine
+StereoEngine::StereoEngine(const EngineConfig& cfg) : cfg_(cfg) {
+  for (int i = 0; i < 16; ++i) Q_[i] = 0.f;
+}
+
+StereoEngine::~StereoEngine() {
+  graph_[0].reset();
+  graph_[1].reset();
+  if (pin_in_) (void)hipHostFree(pin_in_);
+  if (pin_out_) (void)hipHostFree(pin_out_);
+  if (stream_) (void)hipStreamDestroy(stream_);
+  arena_.release();
+}
+
+std::unique_ptr<StereoEngine> StereoEngine::create(const EngineConfig& cfg_in) {
+  EngineConfig cfg = cfg_in;
+  HIP_CHECK(hipSetDevice(cfg.device));
+  std::unique_ptr<WeightStore> store;
+  if (!cfg.weights.empty()) {
+    store = WeightStore::load_safetensors(cfg.weights);
+    if (cfg.model.empty()) cfg.model = store->meta("model");
+  } else {
+    store = std::make_unique<WeightStore>();
+  }
+  SA_REQUIRE(!cfg.model.empty(), "no model preset given and none in weights metadata");
+  std::unique_ptr<StereoEngine> e;
+  const std::string& m = cfg.model;
+  if (m.rfind("raftstereo", 0) == 0) e = make_raft_stereo(cfg);
+  else if (m.rfind("crestereo", 0) == 0) e = make_crestereo(cfg);
+  else if (m.rfind("hitnet", 0) == 0) e = make_hitnet(cfg);
+  else if (m.rfind("fastacvnet", 0) == 0) e = make_fast_acvnet(cfg);
+  else throw Error("unknown model preset: " + m);
+  e->store_ = std::move(store);
+  e->init();
+  return e;
+}
+
+void StereoEngine::init() {
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  const size_t img = (size_t)B() * H() * W() * 3;
+  in_left_ = (uint8_t*)arena_.alloc(img);
+  in_right_ = (uint8_t*)arena_.alloc(img);
+  raw_left_ = (uint8_t*)arena_.alloc(img);
+  raw_right_ = (uint8_t*)arena_.alloc(img);
+  disp_ = (float*)arena_.alloc((size_t)B() * H() * W() * 4);
+  cloud_ = (float*)arena_.alloc((size_t)B() * H() * W() * 6 * 4);
+  HIP_CHECK(hipHostMalloc((void**)&pin_in_, 2 * img, hipHostMallocDefault));
+  HIP_CHECK(hipHostMalloc((void**)&pin_out_, (size_t)B() * H() * W() * 7 * 4 + 2 * img, hipHostMallocDefault));
+  WeightSource src{store_.get(), cfg_.weights.empty(), cfg_.seed};
+  build(src);
+  store_.reset();  // host copies no longer needed
+  HIP_CHECK(hipDeviceSynchronize());
+  SA_LOGI("%s: built, %.1f MiB device memory", name(), arena_.bytes() / 1048576.0);
+}
+
+void StereoEngine::set_Q(const float* q16) {
+  std::memcpy(Q_, q16, sizeof(Q_));
+  have_Q_ = true;
+  graph_[0].reset();  // Q is baked into the reprojection launch
+  graph_[1].reset();
+}
+
+void StereoEngine::set_rectify_maps(const float* ml, const float* mr) {
+  const size_t n = (size_t)H() * W() * 2;
+  if (!rect_maps_) rect_maps_ = (float*)arena_.alloc(2 * n * 4);
+  HIP_CHECK(hipMemcpy(rect_maps_, ml, n * 4, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(rect_maps_ + n, mr, n * 4, hipMemcpyHostToDevice));
+}
+
+void StereoEngine::frame(hipStream_t s, bool rectify) {
+  if (rectify) {
+    SA_REQUIRE(rect_maps_ != nullptr, "rectification requested but no maps set");
+    // left images use map 0, right images map 1 (maps laid out [2][H][W][2])
+    int rc = sa_remap_bgr(raw_left_, B(), H(), W(), rect_maps_, 1, H(), W(), in_left_, s);
+    SA_REQUIRE(rc == 0, "remap failed");
+    rc = sa_remap_bgr(raw_right_, B(), H(), W(), rect_maps_ + (size_t)H() * W() * 2, 1, H(), W(), in_right_, s);
+    SA_REQUIRE(rc == 0, "remap failed");
+  }
+  forward(s);
+  if (have_Q_) {
+    int rc = sa_reproject(disp_, 1, 1.f, in_left_, B(), H(), W(), Q_, nullptr, cloud_, s);
+    SA_REQUIRE(rc == 0, "reproject failed");
+  }
+  SA_LAUNCH_CHECK(s);
+}
+
+void StereoEngine::launch_frame(hipStream_t s, bool rectify) {
+  GraphExec& g = graph_[rectify ? 1 : 0];
+  if (cfg_.use_graph) {
+    // capture on the engine's own (non-blocking) stream — capture cannot use the legacy null
+    // stream torch hands out by default — then replay on the caller's stream.
+    if (!g.ready()) g.capture(stream_, [&] { frame(stream_, rectify); });
+    g.launch(s);
+  } else {
+    frame(s, rectify);
+  }
+  launches_per_frame_++;
+}
+
+void StereoEngine::run_device(const uint8_t* left, const uint8_t* right, float* disp, float* cloud,
+                              bool rectify, hipStream_t s, uint8_t* rect_left, uint8_t* rect_right) {
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  const size_t img = (size_t)B() * H() * W() * 3;
+  uint8_t* dl = rectify ? raw_left_ : in_left_;
+  uint8_t* dr = rectify ? raw_right_ : in_right_;
+  HIP_CHECK(hipMemcpyAsync(dl, left, img, hipMemcpyDeviceToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(dr, right, img, hipMemcpyDeviceToDevice, s));
+  launch_frame(s, rectify);
+  const size_t n = (size_t)B() * H() * W();
+  if (disp) HIP_CHECK(hipMemcpyAsync(disp, disp_, n * 4, hipMemcpyDeviceToDevice, s));
+  if (cloud && have_Q_) HIP_CHECK(hipMemcpyAsync(cloud, cloud_, n * 24, hipMemcpyDeviceToDevice, s));
+  if (rectify && rect_left) HIP_CHECK(hipMemcpyAsync(rect_left, in_left_, img, hipMemcpyDeviceToDevice, s));
+  if (rectify && rect_right) HIP_CHECK(hipMemcpyAsync(rect_right, in_right_, img, hipMemcpyDeviceToDevice, s));
+}
+
+void StereoEngine::run_host(uint8_t* left, uint8_t* right, float* disp, float* cloud, bool rectify) {
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  hipStream_t s = stream_;
+  const size_t img = (size_t)B() * H() * W() * 3;
+  const size_t n = (size_t)B() * H() * W();
+  std::memcpy(pin_in_, left, img);
+  std::memcpy(pin_in_ + img, right, img);
+  uint8_t* dl = rectify ? raw_left_ : in_left_;
+  uint8_t* dr = rectify ? raw_right_ : in_right_;
+  HIP_CHECK(hipMemcpyAsync(dl, pin_in_, img, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(dr, pin_in_ + img, img, hipMemcpyHostToDevice, s));
+  launch_frame(s, rectify);
+  float* pd = pin_out_;
+  float* pc = pin_out_ + n;
+  uint8_t* pr = reinterpret_cast<uint8_t*>(pin_out_ + 7 * n);
+  if (disp) HIP_CHECK(hipMemcpyAsync(pd, disp_, n * 4, hipMemcpyDeviceToHost, s));
+  if (cloud && have_Q_) HIP_CHECK(hipMemcpyAsync(pc, cloud_, n * 24, hipMemcpyDeviceToHost, s));
+  if (rectify) {
+    HIP_CHECK(hipMemcpyAsync(pr, in_left_, img, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(pr + img, in_right_, img, hipMemcpyDeviceToHost, s));
+  }
+  HIP_CHECK(hipStreamSynchronize(s));
+  if (disp) std::memcpy(disp, pd, n * 4);
+  if (cloud && have_Q_) std::memcpy(cloud, pc, n * 24);
+  if (rectify) {  // reference semantics: inputs are overwritten with their rectified versions
+    std::memcpy(left, pr, img);
+    std::memcpy(right, pr + img, img);
+  }
+}
+
+}  // namespace sa

@@ -1,0 +1,107 @@
+"""Native build driver: compiles csrc/ into in-tree shared libraries.
+
+* ``libstereo_amd.so``  — HIP kernels (gfx950) + engine runtime + models + C API (hipcc)
+* ``libstereo_host.so`` — CPU-only geometry / calibration / image I/O (g++), loadable without a GPU
+
+Incremental (object timestamps vs. sources and headers), parallel.  Used by
+``__graft_entry__.build()`` and ``python -m stereoalgorithms_amd._build``.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "csrc"
+LIBDIR = Path(__file__).resolve().parent / "lib"
+OBJDIR = ROOT / "build" / "obj"
+ARCH = os.environ.get("SA_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CXX = os.environ.get("CXX_HOST", "g++")
+
+HOST_DIRS = ("geometry", "io")  # CPU-only sources -> libstereo_host.so
+DEVICE_DIRS = ("kernels", "runtime", "models", "api")
+
+COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC / 'include'}", "-Wall", "-Wno-unused-function"]
+
+
+def _headers_mtime() -> float:
+    hs = list((CSRC / "include").rglob("*.h")) + list(CSRC.rglob("*.h"))
+    return max((h.stat().st_mtime for h in hs), default=0.0)
+
+
+def _sources(dirs):
+    out = []
+    for d in dirs:
+        out += sorted((CSRC / d).rglob("*.hip")) + sorted((CSRC / d).rglob("*.cpp"))
+    return out
+
+
+def _compile(src: Path, obj: Path, host_only: bool, hmt: float, verbose: bool) -> str | None:
+    if obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, hmt):
+        return None
+    obj.parent.mkdir(parents=True, exist_ok=True)
+    if host_only:
+        cmd = [CXX, *COMMON_FLAGS, "-c", str(src), "-o", str(obj)]
+    else:
+        cmd = [HIPCC, f"--offload-arch={ARCH}", *COMMON_FLAGS, "-c", str(src), "-o", str(obj)]
+        if src.suffix == ".hip":
+            cmd[1:1] = ["-x", "hip"]
+        cmd += [f"-I{CSRC / 'models'}", "-munsafe-fp-atomics"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {src}\n{r.stdout}\n{r.stderr}")
+    return str(src.relative_to(ROOT))
+
+
+def _link(objs, out: Path, host_only: bool, extra=()):
+    newest = max(o.stat().st_mtime for o in objs)
+    if out.exists() and out.stat().st_mtime >= newest:
+        return False
+    out.parent.mkdir(parents=True, exist_ok=True)
+    if host_only:
+        cmd = [CXX, "-shared", "-o", str(out), *map(str, objs), *extra]
+    else:
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", str(out), *map(str, objs), *extra]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed: {out}\n{r.stdout}\n{r.stderr}")
+    return True
+
+
+def build(jobs: int | None = None, verbose: bool = False) -> dict:
+    jobs = jobs or min(16, os.cpu_count() or 4)
+    hmt = _headers_mtime()
+    host_src = _sources(HOST_DIRS)
+    dev_src = _sources(DEVICE_DIRS)
+    tasks = []
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        for s in host_src:
+            tasks.append(ex.submit(_compile, s, OBJDIR / "host" / (s.stem + s.suffix + ".o"), True, hmt, verbose))
+        for s in dev_src:
+            tasks.append(ex.submit(_compile, s, OBJDIR / "dev" / (s.stem + s.suffix + ".o"), False, hmt, verbose))
+        built = [t.result() for t in tasks]
+    built = [b for b in built if b]
+    host_lib = LIBDIR / "libstereo_host.so"
+    dev_lib = LIBDIR / "libstereo_amd.so"
+    host_objs = [OBJDIR / "host" / (s.stem + s.suffix + ".o") for s in host_src]
+    dev_objs = [OBJDIR / "dev" / (s.stem + s.suffix + ".o") for s in dev_src]
+    if host_objs:
+        _link(host_objs, host_lib, True, extra=["-ljpeg", "-lpng16"] if _has_img_libs() else [])
+    _link(dev_objs, dev_lib, False, extra=[f"-L{LIBDIR}", "-lstereo_host", "-Wl,-rpath,$ORIGIN"] if host_objs else [])
+    return {"compiled": built, "libs": [str(host_lib), str(dev_lib)]}
+
+
+def _has_img_libs() -> bool:
+    libdir = Path("/usr/lib/x86_64-linux-gnu")
+    return (libdir / "libjpeg.so").exists() and (libdir / "libpng16.so").exists()
+
+
+if __name__ == "__main__":
+    info = build(verbose="-v" in sys.argv)
+    print(f"compiled {len(info['compiled'])} files -> {info['libs']}")

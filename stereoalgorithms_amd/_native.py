@@ -1,0 +1,166 @@
+"""ctypes bindings for the in-tree native libraries.
+
+``libstereo_amd.so`` (HIP kernels + engine) is loaded after ``torch`` so that it binds to the HIP
+runtime torch already mapped (same SONAME, one runtime per process).  On a machine with a GPU a
+missing library is a hard error — there is no silent eager fallback for any op.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+LIBDIR = Path(__file__).resolve().parent / "lib"
+
+_dev = None
+_host = None
+
+
+class NativeMissing(RuntimeError):
+    pass
+
+
+def _load(name: str):
+    path = LIBDIR / name
+    if not path.exists():
+        raise NativeMissing(
+            f"{path} not built — run `python -m stereoalgorithms_amd._build` (or __graft_entry__.build())")
+    return C.CDLL(str(path), mode=C.RTLD_GLOBAL)
+
+
+def dev():
+    """libstereo_amd.so (requires torch imported first so the HIP runtime is shared)."""
+    global _dev
+    if _dev is None:
+        import torch  # noqa: F401  (bind to torch's HIP runtime)
+        _dev = _load("libstereo_amd.so")
+        _declare_dev(_dev)
+    return _dev
+
+
+def host():
+    """libstereo_host.so (CPU only)."""
+    global _host
+    if _host is None:
+        _host = _load("libstereo_host.so")
+        _declare_host(_host)
+    return _host
+
+
+def available() -> bool:
+    return (LIBDIR / "libstereo_amd.so").exists()
+
+
+# ----------------------------------------------------------------------------- structs
+class SaConvSrc(C.Structure):
+    _fields_ = [("ptr", C.c_void_p), ("channels", C.c_int32), ("stride", C.c_int32)]
+
+
+class SaConvArgs(C.Structure):
+    _fields_ = [
+        ("src", SaConvSrc * 4), ("nsrc", C.c_int32),
+        ("N", C.c_int32), ("H", C.c_int32), ("W", C.c_int32), ("Cin", C.c_int32),
+        ("KH", C.c_int32), ("KW", C.c_int32), ("sh", C.c_int32), ("sw", C.c_int32),
+        ("ph", C.c_int32), ("pw", C.c_int32), ("dh", C.c_int32), ("dw", C.c_int32),
+        ("Ho", C.c_int32), ("Wo", C.c_int32),
+        ("weight", C.c_void_p), ("bias", C.c_void_p),
+        ("Cout", C.c_int32), ("Kpad", C.c_int32),
+        ("out", C.c_void_p), ("out_stride", C.c_int32),
+        ("epi", C.c_int32), ("act", C.c_int32), ("act2", C.c_int32),
+        ("alpha", C.c_float), ("scale", C.c_float),
+        ("res", C.c_void_p), ("res_stride", C.c_int32),
+        ("ctx", C.c_void_p), ("ctx_stride", C.c_int32),
+        ("aux", C.c_void_p), ("aux_stride", C.c_int32),
+        ("hbuf", C.c_void_p), ("h_stride", C.c_int32),
+        ("rh", C.c_void_p), ("rh_stride", C.c_int32),
+        ("stats", C.c_void_p),
+        ("tile_cfg", C.c_int32), ("_pad", C.c_int32),
+    ]
+
+
+class SaNormArgs(C.Structure):
+    _fields_ = [
+        ("x", C.c_void_p), ("x_stride", C.c_int32),
+        ("stats", C.c_void_p),
+        ("res", C.c_void_p), ("res_stride", C.c_int32),
+        ("res_stats", C.c_void_p),
+        ("out", C.c_void_p), ("out_stride", C.c_int32),
+        ("N", C.c_int32), ("HW", C.c_int32), ("C", C.c_int32),
+        ("act", C.c_int32), ("act2", C.c_int32),
+        ("eps", C.c_float), ("alpha", C.c_float),
+    ]
+
+
+ACT = {"none": 0, "relu": 1, "leaky": 2, "tanh": 3, "sigmoid": 4}
+EPI = {"store": 0, "gru_zr": 1, "gru_q": 2, "flow_acc": 3, "store_f32": 4}
+PRE = {"raw": 0, "unit": 1, "imagenet": 2, "signed": 3}
+
+_i = C.c_int
+_p = C.c_void_p
+_f = C.c_float
+
+
+def _declare_dev(lib):
+    sig = {
+        "sa_conv2d": (_i, [C.POINTER(SaConvArgs), _p]),
+        "sa_instnorm_apply": (_i, [C.POINTER(SaNormArgs), _p]),
+        "sa_avgpool3s2": (_i, [_p, _i, _p, _i, _i, _i, _i, _i, _p]),
+        "sa_avgpool_k": (_i, [_p, _i, _p, _i, _i, _i, _i, _i, _i, _p]),
+        "sa_interp_bilinear": (_i, [_p, _i, _p, _i, _i, _i, _i, _i, _i, _i, _i, _f, _p]),
+        "sa_corr1d_pyramid": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
+        "sa_corr1d_lookup": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _p, _i, _i, _p, _i, _p]),
+        "sa_convex_upsample": (_i, [_p, _i, _p, _i, _i, _i, _i, _f, _p, _p]),
+        "sa_preprocess": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, _p]),
+        "sa_remap_bgr": (_i, [_p, _i, _i, _i, _p, _i, _i, _i, _p, _p]),
+        "sa_reproject": (_i, [_p, _i, _f, _p, _i, _i, _i, _p, _p, _p, _p]),
+        "sa_version": (C.c_char_p, []),
+        "sa_last_error": (C.c_char_p, []),
+        "sa_engine_create": (_p, [C.c_char_p, C.c_char_p, _i, _i, _i, _i, _i, _i, C.c_ulonglong]),
+        "sa_engine_destroy": (None, [_p]),
+        "sa_engine_set_q": (_i, [_p, _p]),
+        "sa_engine_set_rectify_maps": (_i, [_p, _p, _p]),
+        "sa_engine_run_device": (_i, [_p, _p, _p, _p, _p, _i, _p, _p, _p]),
+        "sa_engine_run_host": (_i, [_p, _p, _p, _p, _p, _i]),
+        "sa_engine_device_bytes": (C.c_longlong, [_p]),
+        "sa_engine_aux_output": (_p, [_p, C.POINTER(_i)]),
+        "sa_engine_stream": (_p, [_p]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.restype = res
+        fn.argtypes = args
+
+
+def _declare_host(lib):
+    # geometry / calibration / image io; declared lazily by stereoalgorithms_amd.utils modules
+    pass
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = ""
+        try:
+            msg = dev().sa_last_error().decode()
+        except Exception:  # pragma: no cover
+            pass
+        raise RuntimeError(f"{what} failed (rc={rc}) {msg}")
+
+
+def on_gpu_box() -> bool:
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:  # pragma: no cover
+        return False
+
+
+def require_native():
+    """Fail loudly when the native library is missing on a GPU machine."""
+    if not available():
+        raise NativeMissing("libstereo_amd.so missing: build it before running on the GPU")
+    return dev()
+
+
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")

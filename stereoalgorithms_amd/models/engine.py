@@ -1,0 +1,104 @@
+"""Python handle on the native StereoEngine (csrc/runtime/engine.cpp).
+
+One engine = one model on one GPU with a static memory plan and a captured whole-frame hipGraph.
+``run`` works on torch CUDA tensors and launches on the current torch stream, so it composes with
+torch.distributed (RCCL) collectives in the data-parallel path (``parallel.dp``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from .. import _native as N
+
+MODEL_PRESETS = (
+    "raftstereo-sceneflow", "raftstereo-realtime",
+    "crestereo-iter2", "crestereo-iter5", "crestereo-iter10",
+    "hitnet-d400", "fastacvnet-plus",
+)
+
+
+class NativeStereoEngine:
+    def __init__(self, model: str = "", weights: str | None = None, height: int = 480, width: int = 640,
+                 batch: int = 1, iters: int = -1, device: int = 0, use_graph: bool = True, seed: int = 0):
+        lib = N.require_native()
+        self._lib = lib
+        self.height, self.width, self.batch = height, width, batch
+        self.device = torch.device("cuda", device)
+        h = lib.sa_engine_create(model.encode(), (weights or "").encode(), height, width, batch, iters, device,
+                                 int(use_graph), seed)
+        if not h:
+            raise RuntimeError(f"engine creation failed: {lib.sa_last_error().decode()}")
+        self._h = h
+        self.model = model
+        self.has_q = False
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.sa_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def device_bytes(self) -> int:
+        return int(self._lib.sa_engine_device_bytes(self._h))
+
+    def set_Q(self, Q):
+        q = np.ascontiguousarray(np.asarray(Q, dtype=np.float32).reshape(16))
+        N.check(self._lib.sa_engine_set_q(self._h, q.ctypes.data_as(C.c_void_p)), "set_Q")
+        self.has_q = True
+
+    def set_rectify_maps(self, map_left: np.ndarray, map_right: np.ndarray):
+        ml = np.ascontiguousarray(map_left, dtype=np.float32)
+        mr = np.ascontiguousarray(map_right, dtype=np.float32)
+        assert ml.shape == (self.height, self.width, 2) and mr.shape == ml.shape
+        N.check(self._lib.sa_engine_set_rectify_maps(self._h, ml.ctypes.data_as(C.c_void_p),
+                                                     mr.ctypes.data_as(C.c_void_p)), "set_rectify_maps")
+
+    def run(self, left: torch.Tensor, right: torch.Tensor, cloud: bool = False, rectify: bool = False,
+            out: torch.Tensor | None = None, rectified: bool = False):
+        """left/right: uint8 BGR [B,H,W,3] CUDA tensors -> disparity fp32 [B,H,W] (+cloud [B,H,W,6])."""
+        b, h, w = self.batch, self.height, self.width
+        assert left.shape == (b, h, w, 3) and left.dtype == torch.uint8 and left.is_cuda
+        left, right = left.contiguous(), right.contiguous()
+        disp = out if out is not None else torch.empty(b, h, w, dtype=torch.float32, device=left.device)
+        pc = torch.empty(b, h, w, 6, dtype=torch.float32, device=left.device) if cloud else None
+        rl = torch.empty_like(left) if (rectify and rectified) else None
+        rr = torch.empty_like(right) if (rectify and rectified) else None
+        stream = C.c_void_p(torch.cuda.current_stream(left.device).cuda_stream)
+        N.check(self._lib.sa_engine_run_device(
+            self._h, C.c_void_p(left.data_ptr()), C.c_void_p(right.data_ptr()), C.c_void_p(disp.data_ptr()),
+            C.c_void_p(pc.data_ptr() if pc is not None else 0), int(rectify), stream,
+            C.c_void_p(rl.data_ptr() if rl is not None else 0), C.c_void_p(rr.data_ptr() if rr is not None else 0)),
+            "engine run")
+        res = [disp]
+        if cloud:
+            res.append(pc)
+        if rectify and rectified:
+            res += [rl, rr]
+        return res[0] if len(res) == 1 else tuple(res)
+
+    def run_host(self, left: np.ndarray, right: np.ndarray, cloud: bool = True, rectify: bool = False):
+        """The reference's timed region: host BGR in, host disparity (+cloud) out."""
+        b, h, w = self.batch, self.height, self.width
+        left = np.ascontiguousarray(left, dtype=np.uint8).reshape(b, h, w, 3)
+        right = np.ascontiguousarray(right, dtype=np.uint8).reshape(b, h, w, 3)
+        disp = np.empty((b, h, w), np.float32)
+        pc = np.empty((b, h, w, 6), np.float32) if cloud else None
+        N.check(self._lib.sa_engine_run_host(self._h, left.ctypes.data_as(C.c_void_p), right.ctypes.data_as(C.c_void_p),
+                                             disp.ctypes.data_as(C.c_void_p),
+                                             pc.ctypes.data_as(C.c_void_p) if pc is not None else None,
+                                             int(rectify)), "engine run_host")
+        return (disp, pc, left, right) if cloud else (disp, left, right)
+
+    def low_res_flow(self) -> int:
+        n = C.c_int(0)
+        self._lib.sa_engine_aux_output(self._h, C.byref(n))
+        return n.value

@@ -1,0 +1,232 @@
+"""Torch-facing wrappers over the hand-written HIP kernels (NHWC fp16 on the GPU).
+
+These are thin: they validate shapes, pack weights, fill the C launch structs and launch on the
+current torch stream.  Used by the numerics tests (each op vs. a PyTorch fp32 reference) and by
+Python-level tooling; the production path is the native engine (``models.engine``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from typing import Sequence
+
+import torch
+
+from .. import _native as N
+
+__all__ = [
+    "pack_conv_weight", "conv2d", "instnorm_apply", "avgpool3s2", "avgpool_k", "interp_bilinear",
+    "corr1d_pyramid", "corr1d_lookup", "convex_upsample", "preprocess", "remap_bgr", "reproject",
+]
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t: torch.Tensor | None):
+    return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
+
+
+def _pix_stride(t: torch.Tensor) -> int:
+    """NHWC tensor (possibly a channel slice): elements between consecutive pixels."""
+    assert t.dim() == 4 and t.stride(3) == 1, "expect NHWC with unit channel stride"
+    n, h, w, c = t.shape
+    s = t.stride(2)
+    assert t.stride(1) == w * s and (n == 1 or t.stride(0) == h * w * s), "pixels must be uniformly strided"
+    return s
+
+
+def pack_conv_weight(w: torch.Tensor, segs: Sequence[tuple[int, int]] | None = None):
+    """[Cout, Cin, KH, KW] -> fp16 [round_up(Cout,128), Kpad], K ordered (kh, kw, ci_padded)."""
+    cout, cin, kh, kw = w.shape
+    segs = list(segs) if segs else [(cin, (cin + 7) // 8 * 8)]
+    assert sum(r for r, _ in segs) == cin
+    cin_pad = sum(p for _, p in segs)
+    wp = torch.zeros(cout, kh, kw, cin_pad, dtype=torch.float32, device=w.device)
+    rc = pc = 0
+    wt = w.permute(0, 2, 3, 1).float()
+    for r, p in segs:
+        wp[..., pc:pc + r] = wt[..., rc:rc + r]
+        rc += r
+        pc += p
+    k = kh * kw * cin_pad
+    kpad = (k + 31) // 32 * 32
+    cpad = (cout + 127) // 128 * 128
+    out = torch.zeros(cpad, kpad, dtype=torch.float16, device=w.device)
+    out[:cout, :k] = wp.reshape(cout, k).half()
+    return out.contiguous(), kpad, cin_pad
+
+
+def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1, act="none",
+           act2="none", res=None, out=None, epi="store", scale=1.0, alpha=0.01, stats=None,
+           ctx=None, aux=None, hbuf=None, rh=None, tile_cfg=-1):
+    if isinstance(xs, torch.Tensor):
+        xs = [xs]
+    n, h, w, _ = xs[0].shape
+    sh = sw = stride if isinstance(stride, int) else None
+    if sh is None:
+        sh, sw = stride
+    if pad is None:
+        ph, pw = (kh // 2) * dil, (kw // 2) * dil
+    elif isinstance(pad, int):
+        ph = pw = pad
+    else:
+        ph, pw = pad
+    ho = (h + 2 * ph - dil * (kh - 1) - 1) // sh + 1
+    wo = (w + 2 * pw - dil * (kw - 1) - 1) // sw + 1
+    a = N.SaConvArgs()
+    cin = 0
+    for i, x in enumerate(xs):
+        assert x.dtype == torch.float16 and x.is_cuda
+        a.src[i].ptr = x.data_ptr()
+        a.src[i].channels = x.shape[3]
+        a.src[i].stride = _pix_stride(x)
+        cin += x.shape[3]
+    a.nsrc = len(xs)
+    a.N, a.H, a.W, a.Cin = n, h, w, cin
+    a.KH, a.KW, a.sh, a.sw, a.ph, a.pw, a.dh, a.dw = kh, kw, sh, sw, ph, pw, dil, dil
+    a.Ho, a.Wo = ho, wo
+    if out is None:
+        if epi == "store_f32":
+            out = torch.empty(n, ho, wo, cout, dtype=torch.float32, device=xs[0].device)
+        else:
+            out = torch.empty(n, ho, wo, cout, dtype=torch.float16, device=xs[0].device)
+    a.weight = wpacked.data_ptr()
+    a.bias = bias.data_ptr() if bias is not None else None
+    a.Cout, a.Kpad = cout, kpad
+    a.out = out.data_ptr()
+    a.out_stride = out.stride(2) if out.dim() == 4 else 1
+    a.epi, a.act, a.act2 = N.EPI[epi], N.ACT[act], N.ACT[act2]
+    a.alpha, a.scale = alpha, scale
+    if res is not None:
+        a.res, a.res_stride = res.data_ptr(), _pix_stride(res)
+    if ctx is not None:
+        a.ctx, a.ctx_stride = ctx.data_ptr(), _pix_stride(ctx)
+    if aux is not None:
+        a.aux, a.aux_stride = aux.data_ptr(), _pix_stride(aux)
+    if hbuf is not None:
+        a.hbuf, a.h_stride = hbuf.data_ptr(), _pix_stride(hbuf)
+    if rh is not None:
+        a.rh, a.rh_stride = rh.data_ptr(), _pix_stride(rh)
+    if stats is not None:
+        assert stats.dtype == torch.float64
+        a.stats = stats.data_ptr()
+    a.tile_cfg = tile_cfg
+    N.check(N.dev().sa_conv2d(C.byref(a), _stream()), "sa_conv2d")
+    return out
+
+
+def instnorm_apply(x, stats, act="none", res=None, res_stats=None, act2="none", eps=1e-5, out=None):
+    n, h, w, c = x.shape
+    out = torch.empty_like(x) if out is None else out
+    a = N.SaNormArgs()
+    a.x, a.x_stride = x.data_ptr(), _pix_stride(x)
+    a.stats = stats.data_ptr()
+    if res is not None:
+        a.res, a.res_stride = res.data_ptr(), _pix_stride(res)
+    if res_stats is not None:
+        a.res_stats = res_stats.data_ptr()
+    a.out, a.out_stride = out.data_ptr(), _pix_stride(out)
+    a.N, a.HW, a.C = n, h * w, c
+    a.act, a.act2 = N.ACT[act], N.ACT[act2]
+    a.eps, a.alpha = eps, 0.01
+    N.check(N.dev().sa_instnorm_apply(C.byref(a), _stream()), "sa_instnorm_apply")
+    return out
+
+
+def avgpool3s2(x, out=None):
+    n, h, w, c = x.shape
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    out = torch.empty(n, ho, wo, c, dtype=x.dtype, device=x.device) if out is None else out
+    N.check(N.dev().sa_avgpool3s2(_ptr(x), _pix_stride(x), _ptr(out), _pix_stride(out), n, h, w, c,
+                                  _stream()), "avgpool3s2")
+    return out
+
+
+def avgpool_k(x, k, out=None):
+    n, h, w, c = x.shape
+    out = torch.empty(n, h // k, w // k, c, dtype=x.dtype, device=x.device) if out is None else out
+    N.check(N.dev().sa_avgpool_k(_ptr(x), _pix_stride(x), _ptr(out), _pix_stride(out), n, h, w, c, k,
+                                 _stream()), "avgpool_k")
+    return out
+
+
+def interp_bilinear(x, size, align_corners=True, mul=1.0, out=None):
+    n, h, w, c = x.shape
+    ho, wo = size
+    out = torch.empty(n, ho, wo, c, dtype=x.dtype, device=x.device) if out is None else out
+    N.check(N.dev().sa_interp_bilinear(_ptr(x), _pix_stride(x), _ptr(out), _pix_stride(out), n, h, w, c,
+                                       ho, wo, int(align_corners), float(mul), _stream()), "interp")
+    return out
+
+
+def corr1d_pyramid(f1, f2, levels=4):
+    """f1, f2: [B,H,W,C] fp16 -> list of fp32 levels [B,H,W1,W2>>l] (views of one buffer)."""
+    b, h, w1, c = f1.shape
+    w2 = f2.shape[2]
+    sizes = []
+    wl = w2
+    for _ in range(levels):
+        sizes.append(wl)
+        wl >>= 1
+    buf = torch.empty(sum(b * h * w1 * s for s in sizes), dtype=torch.float32, device=f1.device)
+    assert f1.is_contiguous() and f2.is_contiguous()
+    N.check(N.dev().sa_corr1d_pyramid(_ptr(f1), _ptr(f2), c, b, h, w1, w2, c, levels, _ptr(buf), _stream()),
+            "corr1d_pyramid")
+    out, off = [], 0
+    for s in sizes:
+        out.append(buf[off:off + b * h * w1 * s].view(b, h, w1, s))
+        off += b * h * w1 * s
+    return buf, out
+
+
+def corr1d_lookup(pyr_buf, flow, b, h, w1, w2, levels=4, radius=4, out_channels=None,
+                  flow_out=None, flow_out2=None):
+    nfeat = levels * (2 * radius + 1)
+    oc = out_channels or (nfeat + 7) // 8 * 8
+    out = torch.empty(b, h, w1, oc, dtype=torch.float16, device=flow.device)
+    fo_ptr, fo_s, fo_c = (0, 0, 0) if flow_out is None else (flow_out.data_ptr(), _pix_stride(flow_out), flow_out.shape[3])
+    fo2_ptr, fo2_s = (0, 0) if flow_out2 is None else (flow_out2.data_ptr(), _pix_stride(flow_out2))
+    N.check(N.dev().sa_corr1d_lookup(_ptr(pyr_buf), _ptr(flow), b, h, w1, w2, levels, radius, _ptr(out), oc, oc,
+                                     C.c_void_p(fo_ptr), fo_s, fo_c, C.c_void_p(fo2_ptr), fo2_s, _stream()),
+            "corr1d_lookup")
+    return out
+
+
+def convex_upsample(mask, flow, factor, sign=1.0):
+    b, h, w, _ = mask.shape
+    out = torch.empty(b, h * factor, w * factor, dtype=torch.float32, device=mask.device)
+    N.check(N.dev().sa_convex_upsample(_ptr(mask), _pix_stride(mask), _ptr(flow), b, h, w, factor, float(sign),
+                                       _ptr(out), _stream()), "convex_upsample")
+    return out
+
+
+def preprocess(bgr, mode="signed", out=None, c_off=0, zero_to=8, out_channels=8):
+    b, h, w, _ = bgr.shape
+    assert bgr.dtype == torch.uint8 and bgr.is_contiguous()
+    out = torch.zeros(b, h, w, out_channels, dtype=torch.float16, device=bgr.device) if out is None else out
+    N.check(N.dev().sa_preprocess(_ptr(bgr), b, h, w, N.PRE[mode], _ptr(out), _pix_stride(out), c_off, zero_to,
+                                  _stream()), "preprocess")
+    return out
+
+
+def remap_bgr(src, maps):
+    """src u8 [B,Hs,Ws,3]; maps fp32 [nmaps,H,W,2] (x, y) -> [B,H,W,3]"""
+    b, hs, ws, _ = src.shape
+    nm, h, w, _ = maps.shape
+    out = torch.empty(b, h, w, 3, dtype=torch.uint8, device=src.device)
+    N.check(N.dev().sa_remap_bgr(_ptr(src), b, hs, ws, _ptr(maps.contiguous()), nm, h, w, _ptr(out), _stream()),
+            "remap")
+    return out
+
+
+def reproject(disp, left_bgr, Q, sign=1.0):
+    """disp fp32 [B,H,W]; Q 4x4 (host array-like) -> (signed disparity, cloud [B,H,W,6])"""
+    b, h, w = disp.shape
+    q = (C.c_float * 16)(*[float(v) for v in torch.as_tensor(Q, dtype=torch.float64).flatten().tolist()])
+    dout = torch.empty_like(disp)
+    cloud = torch.empty(b, h, w, 6, dtype=torch.float32, device=disp.device)
+    N.check(N.dev().sa_reproject(_ptr(disp.contiguous()), 1, float(sign), _ptr(left_bgr.contiguous()), b, h, w,
+                                 C.cast(q, C.c_void_p), _ptr(dout), _ptr(cloud), _stream()), "reproject")
+    return dout, cloud

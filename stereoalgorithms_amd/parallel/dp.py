@@ -1,0 +1,70 @@
+"""Data-parallel frame sharding over torch.distributed (RCCL on ROCm, gloo on CPU).
+
+The reference is single-GPU, batch 1 (RAFTStereo/include/TRTRAFTStereo.h:15); this is
+the new multi-GPU capability required by BASELINE.json: one process per GPU, each rank owns a
+contiguous shard of the stereo pairs, runs them through its own hipGraph-captured engine, and the
+disparity maps are all-gathered over xGMI.  xGMI is point-to-point, so one large all-gather of the
+whole shard (B x H x W fp32 per rank, ~9.8 MB at B = 8) is issued per step rather than per-frame
+collectives.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(total: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous block [start, end) of `total` items for `rank`; remainders go to low ranks."""
+    base, rem = divmod(total, world)
+    start = rank * base + min(rank, rem)
+    return start, start + base + (1 if rank < rem else 0)
+
+
+def shard_indices_round_robin(total: int, world: int, rank: int) -> list[int]:
+    """Frame i goes to rank i % world (stream ordering for camera feeds)."""
+    return list(range(rank, total, world))
+
+
+@dataclass
+class DataParallelStereo:
+    engine: object  # anything with .run(left, right) -> [B,H,W] and .batch
+    world_size: int = 1
+    rank: int = 0
+    gather: bool = True
+
+    def __post_init__(self):
+        self._out = None
+
+    def step(self, left: torch.Tensor, right: torch.Tensor) -> torch.Tensor:
+        """left/right: this rank's shard [B,H,W,3] u8 -> gathered disparity [world*B,H,W]."""
+        disp = self.engine.run(left, right)
+        if self.world_size == 1 or not self.gather:
+            return disp
+        return all_gather_disparity(disp, self.world_size, self._buffer(disp))
+
+    def _buffer(self, disp):
+        shape = (self.world_size * disp.shape[0],) + tuple(disp.shape[1:])
+        if self._out is None or self._out.shape != shape or self._out.device != disp.device:
+            self._out = torch.empty(shape, dtype=disp.dtype, device=disp.device)
+        return self._out
+
+
+def all_gather_disparity(disp: torch.Tensor, world: int, out: torch.Tensor | None = None) -> torch.Tensor:
+    """One all-gather of the whole shard (rank-major), RCCL/xGMI on GPU, gloo on CPU."""
+    if out is None:
+        out = torch.empty((world * disp.shape[0],) + tuple(disp.shape[1:]), dtype=disp.dtype, device=disp.device)
+    if disp.is_cuda:
+        dist.all_gather_into_tensor(out, disp.contiguous())
+    else:  # gloo lacks all_gather_into_tensor on older builds
+        parts = list(out.chunk(world, dim=0))
+        dist.all_gather(parts, disp.contiguous())
+    return out
+
+
+def gather_to_rank0(disp: torch.Tensor, world: int, rank: int):
+    """Point-cloud style output: only rank 0 receives the full set."""
+    parts = [torch.empty_like(disp) for _ in range(world)] if rank == 0 else None
+    dist.gather(disp.contiguous(), parts, dst=0)
+    return torch.cat(parts, 0) if rank == 0 else None

@@ -1,0 +1,245 @@
+"""Numerics of every hand-written HIP kernel vs. a plain PyTorch fp32 reference of the same op."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def ops():
+    from stereoalgorithms_amd import ops as O
+    return O
+
+
+def nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(x):
+    return x.permute(0, 3, 1, 2).float()
+
+
+def rel_err(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("cin,cout,k,stride,hw,cfg", [
+    (64, 64, 3, 1, (24, 40), -1),
+    (64, 96, 3, 2, (30, 41), -1),
+    (128, 256, 3, 1, (20, 32), 0),
+    (128, 256, 3, 1, (20, 32), 1),
+    (256, 2, 3, 1, (12, 16), 2),
+    (256, 144, 1, 1, (12, 16), 3),
+    (8, 64, 7, 2, (33, 47), -1),
+    (96, 128, 1, 2, (21, 19), -1),
+])
+def test_conv2d_vs_torch(cin, cout, k, stride, hw, cfg):
+    O = ops()
+    torch.manual_seed(0)
+    n = 2
+    x = torch.randn(n, cin, *hw, device=DEV)
+    w = torch.randn(cout, cin, k, k, device=DEV) / math.sqrt(cin * k * k)
+    b = torch.randn(cout, device=DEV) * 0.1
+    ref = F.relu(F.conv2d(x.half().float(), w.half().float(), b, stride=stride, padding=k // 2))
+    wp, kpad, _ = O.pack_conv_weight(w)
+    out = O.conv2d(nhwc(x).half(), wp, kpad, cout, k, k, bias=b.float().contiguous(), stride=stride, act="relu",
+                   tile_cfg=cfg)
+    torch.cuda.synchronize()
+    assert out.shape == (n, ref.shape[2], ref.shape[3], cout)
+    assert rel_err(nchw(out), ref) < 2e-3
+
+
+def test_conv2d_multisource_concat_and_residual():
+    O = ops()
+    torch.manual_seed(1)
+    n, h, w = 2, 17, 23
+    a = torch.randn(n, 128, h, w, device=DEV)
+    big = torch.randn(n, h, w, 256, device=DEV).half()  # second source is a channel slice of a wider buffer
+    bsl = big[..., 64:192]
+    wt = torch.randn(96, 256, 3, 3, device=DEV) / math.sqrt(256 * 9)
+    res = torch.randn(n, h, w, 96, device=DEV).half()
+    ref = F.conv2d(torch.cat([a.half().float(), nchw(bsl)], 1), wt.half().float(), padding=1)
+    ref = F.relu(ref + nchw(res))
+    wp, kpad, _ = O.pack_conv_weight(wt)
+    out = O.conv2d([nhwc(a).half(), bsl], wp, kpad, 96, 3, 3, res=res, act="none", act2="relu")
+    torch.cuda.synchronize()
+    assert rel_err(nchw(out), ref) < 2e-3
+
+
+def test_conv2d_padded_channels_and_output_slice():
+    O = ops()
+    torch.manual_seed(2)
+    n, h, w = 1, 15, 20
+    x = torch.randn(n, 36, h, w, device=DEV)
+    wt = torch.randn(64, 36, 1, 1, device=DEV) / 6
+    xp = torch.zeros(n, h, w, 40, device=DEV, dtype=torch.float16)
+    xp[..., :36] = nhwc(x).half()
+    wp, kpad, cin_pad = O.pack_conv_weight(wt, [(36, 40)])
+    assert cin_pad == 40
+    buf = torch.zeros(n, h, w, 128, device=DEV, dtype=torch.float16)
+    O.conv2d(xp, wp, kpad, 64, 1, 1, out=buf[..., 64:128], act="relu")
+    torch.cuda.synchronize()
+    ref = F.relu(F.conv2d(x.half().float(), wt.half().float()))
+    assert rel_err(nchw(buf[..., 64:]), ref) < 2e-3
+    assert buf[..., :64].abs().max().item() == 0
+
+
+def test_conv2d_gru_epilogues():
+    O = ops()
+    torch.manual_seed(3)
+    n, hd, h, w = 2, 128, 12, 16
+    net = torch.randn(n, hd, h, w, device=DEV).tanh()
+    x = torch.randn(n, 256, h, w, device=DEV)
+    cz, cr, cq = (torch.randn(n, hd, h, w, device=DEV) * 0.5 for _ in range(3))
+    wz, wr, wq = (torch.randn(hd, hd + 256, 3, 3, device=DEV) / math.sqrt((hd + 256) * 9) for _ in range(3))
+    bz, br, bq = (torch.randn(hd, device=DEV) * 0.1 for _ in range(3))
+    hx = torch.cat([net, x], 1).half().float()
+    z = torch.sigmoid(F.conv2d(hx, wz.half().float(), bz, padding=1) + cz.half().float())
+    r = torch.sigmoid(F.conv2d(hx, wr.half().float(), br, padding=1) + cr.half().float())
+    rh = (r * net.half().float()).half().float()
+    q = torch.tanh(F.conv2d(torch.cat([rh, x.half().float()], 1), wq.half().float(), bq, padding=1) + cq.half().float())
+    ref = (1 - z) * net.half().float() + z * q
+
+    net_h = nhwc(net).half()
+    ctx = nhwc(torch.cat([cz, cr, cq], 1)).half()
+    xh = nhwc(x).half()
+    wzr, kpad, _ = O.pack_conv_weight(torch.cat([wz, wr], 0))
+    wqp, kpq, _ = O.pack_conv_weight(wq)
+    zb = torch.empty(n, h, w, hd, device=DEV, dtype=torch.float16)
+    rhb = torch.empty_like(zb)
+    O.conv2d([net_h, xh], wzr, kpad, 2 * hd, 3, 3, bias=torch.cat([bz, br]).contiguous(), out=zb, epi="gru_zr",
+             ctx=ctx, aux=zb, hbuf=net_h, rh=rhb)
+    O.conv2d([rhb, xh], wqp, kpq, hd, 3, 3, bias=bq.contiguous(), out=net_h, epi="gru_q", ctx=ctx[..., 2 * hd:],
+             aux=zb, hbuf=net_h)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(zb), z) < 3e-3
+    assert rel_err(nchw(net_h), ref) < 3e-3
+
+
+def test_conv2d_flow_acc_and_stats():
+    O = ops()
+    torch.manual_seed(4)
+    n, h, w = 2, 10, 14
+    x = torch.randn(n, 256, h, w, device=DEV)
+    wt = torch.randn(1, 256, 3, 3, device=DEV) / 48
+    b = torch.tensor([0.3], device=DEV)
+    flow = torch.randn(n, h, w, device=DEV)
+    ref = flow + F.conv2d(x.half().float(), wt.half().float(), b, padding=1)[:, 0]
+    wp, kpad, _ = O.pack_conv_weight(wt)
+    O.conv2d(nhwc(x).half(), wp, kpad, 1, 3, 3, bias=b, out=flow.view(n, h, w, 1), epi="flow_acc")
+    torch.cuda.synchronize()
+    assert rel_err(flow, ref) < 2e-3
+    # instance-norm statistics fused in the epilogue + apply kernel
+    w2 = torch.randn(64, 256, 3, 3, device=DEV) / 48
+    wp2, kp2, _ = O.pack_conv_weight(w2)
+    stats = torch.zeros(n, 64, 2, dtype=torch.float64, device=DEV)
+    y = O.conv2d(nhwc(x).half(), wp2, kp2, 64, 3, 3, stats=stats)
+    out = O.instnorm_apply(y, stats, act="relu")
+    torch.cuda.synchronize()
+    yr = F.conv2d(x.half().float(), w2.half().float(), padding=1)
+    assert rel_err(stats[..., 0].float(), yr.sum((2, 3))) < 1e-2
+    ref2 = F.relu(F.instance_norm(yr))
+    assert rel_err(nchw(out), ref2) < 5e-3
+
+
+def test_pool_interp():
+    O = ops()
+    torch.manual_seed(5)
+    x = torch.randn(2, 64, 15, 21, device=DEV)
+    xh = nhwc(x).half()
+    p = O.avgpool3s2(xh)
+    assert rel_err(nchw(p), F.avg_pool2d(x.half().float(), 3, 2, 1)) < 2e-3
+    for ac in (True, False):
+        it = O.interp_bilinear(xh, (31, 40), align_corners=ac)
+        ref = F.interpolate(x.half().float(), (31, 40), mode="bilinear", align_corners=ac)
+        assert rel_err(nchw(it), ref) < 2e-3
+    pk = O.avgpool_k(xh, 2)
+    assert rel_err(nchw(pk), F.avg_pool2d(x.half().float(), 2)) < 2e-3
+
+
+def test_corr_pyramid_and_lookup_vs_oracle():
+    from stereoalgorithms_amd.models.raft_stereo import CorrBlock1D, coords_grid
+    O = ops()
+    torch.manual_seed(6)
+    b, c, h, w = 2, 256, 6, 40
+    f1 = torch.randn(b, c, h, w, device=DEV)
+    f2 = torch.randn(b, c, h, w, device=DEV)
+    f1h, f2h = nhwc(f1).half(), nhwc(f2).half()
+    buf, levels = O.corr1d_pyramid(f1h, f2h, levels=4)
+    cb = CorrBlock1D(f1.half().float(), f2.half().float(), 4, 4)
+    for l in range(4):
+        ref = cb.pyramid[l].view(b, h, w, -1)
+        assert rel_err(levels[l], ref) < 1e-4
+    flow = torch.randn(b, h, w, device=DEV) * 6 - 3
+    feat = O.corr1d_lookup(buf, flow, b, h, w, w)
+    coords = coords_grid(b, h, w, DEV)
+    coords[:, 0] += flow
+    ref = cb(coords)  # [b,36,h,w]
+    torch.cuda.synchronize()
+    assert feat.shape[-1] == 40
+    assert rel_err(nchw(feat[..., :36]), ref) < 2e-3
+    assert feat[..., 36:].abs().max().item() == 0
+
+
+def test_convex_upsample_vs_oracle():
+    from stereoalgorithms_amd.models.raft_stereo import RAFTStereo
+    O = ops()
+    torch.manual_seed(7)
+    m = RAFTStereo("raftstereo-realtime")
+    b, h, w, f = 2, 6, 9, 8
+    mask = torch.randn(b, 9 * f * f, h, w, device=DEV)
+    flow = torch.randn(b, 2, h, w, device=DEV)
+    ref = m.upsample_flow(flow, mask.half().float())[:, 0]
+    out = O.convex_upsample(nhwc(mask).half(), flow[:, 0].contiguous(), f, sign=-1.0)
+    torch.cuda.synchronize()
+    assert rel_err(out, -ref) < 1e-4
+
+
+def test_preprocess_modes():
+    O = ops()
+    torch.manual_seed(8)
+    img = torch.randint(0, 256, (2, 17, 23, 3), dtype=torch.uint8, device=DEV)
+    rgb = img.flip(-1).float()
+    for mode, fn in [("raw", lambda v: v), ("unit", lambda v: v / 255), ("signed", lambda v: 2 * v / 255 - 1),
+                     ("imagenet", lambda v: (v / 255 - torch.tensor([0.485, 0.456, 0.406], device=DEV))
+                      / torch.tensor([0.229, 0.224, 0.225], device=DEV))]:
+        out = O.preprocess(img, mode)
+        torch.cuda.synchronize()
+        assert rel_err(out[..., :3], fn(rgb)) < 1e-3
+        assert out[..., 3:].abs().max().item() == 0
+
+
+def test_remap_matches_numpy_reference():
+    from stereoalgorithms_amd.utils.geometry import remap_bilinear_u8
+    O = ops()
+    rng = np.random.default_rng(0)
+    src = rng.integers(0, 256, (1, 20, 30, 3), dtype=np.uint8)
+    ys, xs = np.mgrid[0:18, 0:25].astype(np.float32)
+    maps = np.stack([xs * 1.1 + 0.37 * np.sin(ys) - 1.3, ys * 0.97 + 0.21 * np.cos(xs) + 0.6], -1)[None]
+    out = O.remap_bgr(torch.from_numpy(src).to(DEV), torch.from_numpy(maps).to(DEV)).cpu().numpy()
+    ref = remap_bilinear_u8(src[0], maps[0])
+    assert np.abs(out[0].astype(int) - ref.astype(int)).max() <= 1
+
+
+def test_reproject_matches_Q():
+    O = ops()
+    torch.manual_seed(9)
+    b, h, w = 1, 8, 12
+    d = torch.rand(b, h, w, device=DEV) * 40 + 1
+    img = torch.randint(0, 256, (b, h, w, 3), dtype=torch.uint8, device=DEV)
+    Q = np.array([[1, 0, 0, -320.5], [0, 1, 0, -240.2], [0, 0, 0, 500.0], [0, 0, 1 / 60.0, 0]], np.float64)
+    dout, cloud = O.reproject(-d, img, Q, sign=-1.0)
+    torch.cuda.synchronize()
+    ys, xs = torch.meshgrid(torch.arange(h, device=DEV).float(), torch.arange(w, device=DEV).float(), indexing="ij")
+    Wh = d[0] / 60.0
+    X = (xs - 320.5) / Wh
+    Z = 500.0 / Wh
+    assert torch.allclose(dout, d)
+    assert torch.allclose(cloud[0, ..., 0], X, rtol=1e-4, atol=1e-3)
+    assert torch.allclose(cloud[0, ..., 2], Z.expand_as(X), rtol=1e-4)
+    assert torch.equal(cloud[0, ..., 3:].round().to(torch.uint8), img[0].flip(-1))
