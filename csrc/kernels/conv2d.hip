@@ -232,9 +232,18 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
   const int cc = tid % CPR;
   const int co = n0 + cc * 8;
   const bool do_stats = p.stats != nullptr;
-  float ssum[8], ssq[8];
+  // Instance-norm statistics: per-thread partial sums for the (at most) two images a BM-row tile
+  // can straddle, reduced across the block in LDS, then ONE double atomic per (block, image,
+  // channel).  Per-thread atomics to the same N*C addresses serialise at the memory side
+  // (MI355X_MICROARCH.md, global float atomics: one-row contention is ~14x slower) and cost
+  // 20 ms per full-resolution RAFT fnet conv.  Tiles spanning > 2 images (HWo < BM, tiny test
+  // shapes only) fall back to per-thread atomics.
+  const int img_lo = m0 / HWo;
+  const int m_last = (m0 + BM < M ? m0 + BM : M) - 1;
+  const bool block_reduce = (m_last / HWo) - img_lo <= 1;
+  float ssum[8], ssq[8], ssum1[8], ssq1[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) ssum[j] = ssq[j] = 0.f;
+  for (int j = 0; j < 8; ++j) ssum[j] = ssq[j] = ssum1[j] = ssq1[j] = 0.f;
   int cur_img = -1;
   const int nvalid = p.Cout - co;  // channels valid in this chunk (may be <=0 or <8)
 
@@ -286,15 +295,31 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
           for (int j = 0; j < 8 && j < nvalid; ++j) op[j] = v[j];
         }
         if (do_stats) {
-          int img = m / HWo;
-          if (img != cur_img) {
-            flush_stats(cur_img);
-            cur_img = img;
-          }
+          const int img = m / HWo;
+          if (block_reduce) {
+            if (img == img_lo) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            ssum[j] += v[j];
-            ssq[j] += v[j] * v[j];
+              for (int j = 0; j < 8; ++j) {
+                ssum[j] += v[j];
+                ssq[j] += v[j] * v[j];
+              }
+            } else {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                ssum1[j] += v[j];
+                ssq1[j] += v[j] * v[j];
+              }
+            }
+          } else {
+            if (img != cur_img) {
+              flush_stats(cur_img);
+              cur_img = img;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              ssum[j] += v[j];
+              ssq[j] += v[j] * v[j];
+            }
           }
         }
       } else if (p.epi == SA_EPI_GRU_ZR) {
@@ -335,7 +360,49 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
       }
     }
   }
-  if (do_stats) flush_stats(cur_img);
+  if (do_stats) {
+    if (!block_reduce) {
+      flush_stats(cur_img);
+      return;
+    }
+    // wave reduction over the lanes sharing a channel chunk (lane bits >= log2(CPR)), then the
+    // 4 waves' partials meet in LDS red[q][wave][BN] (q = sum0, sq0, sum1, sq1; reuses C tile)
+#pragma unroll
+    for (int off = CPR; off < 64; off <<= 1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        ssum[j] += __shfl_xor(ssum[j], off);
+        ssq[j] += __shfl_xor(ssq[j], off);
+        ssum1[j] += __shfl_xor(ssum1[j], off);
+        ssq1[j] += __shfl_xor(ssq1[j], off);
+      }
+    }
+    constexpr int RG = 4;
+    static_assert(4 * RG * BN * 4 <= C::SMEM, "stats reduction must fit in the staging LDS");
+    float* red = reinterpret_cast<float*>(smem);
+    __syncthreads();  // everyone finished reading the C tile
+    if (lane < CPR) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int col = cc * 8 + j;
+        red[(0 * RG + wave) * BN + col] = ssum[j];
+        red[(1 * RG + wave) * BN + col] = ssq[j];
+        red[(2 * RG + wave) * BN + col] = ssum1[j];
+        red[(3 * RG + wave) * BN + col] = ssq1[j];
+      }
+    }
+    __syncthreads();
+    const bool two = (m_last / HWo) != img_lo;
+    for (int t = tid; t < 4 * BN; t += 256) {
+      const int q = t / BN, col = t - q * BN;
+      const int c = n0 + col;
+      if (c >= p.Cout || (q >= 2 && !two)) continue;
+      float acc = 0.f;
+      for (int r = 0; r < RG; ++r) acc += red[(q * RG + r) * BN + col];
+      const int img = img_lo + (q >> 1);
+      atomicAdd(p.stats + ((size_t)img * p.Cout + c) * 2 + (q & 1), (double)acc);
+    }
+  }
 }
 
 template <int BM, int BN, int WM, int WN>

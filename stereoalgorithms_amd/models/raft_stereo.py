@@ -335,7 +335,22 @@ def build(preset: str, seed: int = 0) -> RAFTStereo:
     """Seeded random-init RAFT-Stereo of a named preset (eval mode)."""
     torch.manual_seed(seed)
     m = RAFTStereo(preset).eval()
+    randomize_norm_stats(m, seed)
     return m
+
+
+def randomize_norm_stats(m: nn.Module, seed: int = 0):
+    """Non-trivial BatchNorm affine/running statistics so that BN folding is actually exercised
+    (PyTorch's default init is the identity transform)."""
+    g = torch.Generator().manual_seed(seed + 7)
+    for mod in m.modules():
+        if isinstance(mod, nn.BatchNorm2d):
+            c = mod.num_features
+            with torch.no_grad():
+                mod.weight.copy_(0.75 + 0.5 * torch.rand(c, generator=g))
+                mod.bias.copy_(0.1 * torch.randn(c, generator=g))
+                mod.running_mean.copy_(0.1 * torch.randn(c, generator=g))
+                mod.running_var.copy_(0.75 + 0.5 * torch.rand(c, generator=g))
 
 
 def config_dict(preset: str) -> dict:

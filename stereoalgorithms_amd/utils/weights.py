@@ -15,7 +15,8 @@ FORMAT = "stereoalgorithms_amd/1"
 
 
 def save_model(model: torch.nn.Module, path: str | Path, preset: str, extra: dict | None = None) -> Path:
-    sd = {k: v.detach().float().contiguous().cpu() for k, v in model.state_dict().items()
+    # clone: aliased parameters (e.g. norm3 == downsample.1) must be stored as separate tensors
+    sd = {k: v.detach().to(torch.float32).cpu().clone().contiguous() for k, v in model.state_dict().items()
           if v.dtype.is_floating_point}
     meta = {"model": preset, "format": FORMAT}
     if extra:
