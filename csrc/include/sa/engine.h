@@ -92,6 +92,7 @@ class StereoEngine {
   EngineConfig cfg_;
   DeviceArena arena_;
   hipStream_t stream_ = nullptr;
+  hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;
   std::unique_ptr<WeightStore> store_;
   uint8_t* in_left_ = nullptr;   // model input (rectified or raw copy)
   uint8_t* in_right_ = nullptr;
@@ -103,6 +104,7 @@ class StereoEngine {
   float Q_[16];
   bool have_Q_ = false;
   GraphExec graph_[2];  // [no rectify, rectify]
+  SplitKWorkspace splitk_;
   uint8_t* pin_in_ = nullptr;
   float* pin_out_ = nullptr;
   long launches_per_frame_ = 0;

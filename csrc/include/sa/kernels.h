@@ -15,6 +15,12 @@
 extern "C" {
 #endif
 
+// Instance-norm statistics are accumulated as 64-bit fixed point (value * 2^24) with integer
+// atomics: integer addition is associative, so the sums -- and every replay of a captured frame --
+// are bitwise deterministic regardless of the order blocks arrive in.
+typedef long long sa_stat_t;
+#define SA_STAT_SCALE 16777216.0
+
 enum SaAct { SA_ACT_NONE = 0, SA_ACT_RELU = 1, SA_ACT_LEAKY = 2, SA_ACT_TANH = 3, SA_ACT_SIGMOID = 4 };
 
 enum SaEpi {
@@ -55,9 +61,17 @@ typedef struct {
   int32_t h_stride;
   void* rh;  // GRU r*h output fp16 (ZR)
   int32_t rh_stride;
-  double* stats;  // optional per-(n, cout) {sum, sumsq} of the stored value (instance norm)
+  sa_stat_t* stats;  // optional per-(n, cout) fixed-point {sum, sumsq} of the stored value
   int32_t tile_cfg;  // -1 = auto
-  int32_t _pad;
+  // split-K: 0 = auto (needs ws/counters), 1 = off, >1 = forced slice count.  Slices write fp32
+  // partial slabs to `ws`; the last-arriving block of a tile (agent-scope counter) sums them and
+  // runs the fused epilogue.  `counters` must be zero-initialised once (arrivers reset them).
+  int32_t splitk;
+  float* ws;
+  int32_t* counters;
+  int64_t ws_floats;
+  int32_t n_counters;
+  int32_t _pad2;
 } SaConvArgs;
 
 int sa_conv2d(const SaConvArgs* a, hipStream_t stream);
@@ -66,9 +80,9 @@ int sa_conv2d(const SaConvArgs* a, hipStream_t stream);
 // Instance-norm apply (biased var, eps): y = act(norm(x)); if res: y = act2(resnorm(res) + y)
 typedef struct {
   const void* x; int32_t x_stride;
-  const double* stats;      // [N][C][2] sums of x
+  const sa_stat_t* stats;      // [N][C][2] fixed-point sums of x
   const void* res; int32_t res_stride;
-  const double* res_stats;  // NULL -> residual used raw
+  const sa_stat_t* res_stats;  // NULL -> residual used raw
   void* out; int32_t out_stride;
   int32_t N, HW, C;
   int32_t act, act2;

@@ -93,6 +93,24 @@ class WeightStore {
   std::map<std::string, std::string> meta_;
 };
 
+// ------------------------------------------------------------------ split-K workspace
+// fp32 partial slabs + arrival counters shared by every conv of one engine (its kernels run in
+// stream order, so one workspace suffices).  Installed thread-locally while a frame is
+// recorded; ConvLayer launches pick it up and let sa_conv2d choose the split.
+struct SplitKWorkspace {
+  float* ws = nullptr;
+  int32_t* counters = nullptr;
+  int64_t ws_floats = 0;
+  int32_t n_counters = 0;
+  void alloc(DeviceArena& a, int64_t floats, int32_t counters);
+};
+const SplitKWorkspace* current_splitk();
+struct ScopedSplitK {
+  const SplitKWorkspace* prev;
+  explicit ScopedSplitK(const SplitKWorkspace* w);
+  ~ScopedSplitK();
+};
+
 // ------------------------------------------------------------------ conv layers
 // Describes how the conv's (padded) input channels map to the checkpoint's input channels:
 // a list of {real, padded} segments concatenated along channels.
@@ -125,7 +143,7 @@ class ConvLayer {
   // Fill launch args for inputs (channel-concatenated sources) -> output view.
   SaConvArgs args(const std::vector<Tensor>& srcs, const Tensor& out) const;
   void run(hipStream_t s, const std::vector<Tensor>& srcs, const Tensor& out, int act = SA_ACT_NONE,
-           const Tensor* res = nullptr, int act2 = SA_ACT_NONE, double* stats = nullptr,
+           const Tensor* res = nullptr, int act2 = SA_ACT_NONE, sa_stat_t* stats = nullptr,
            float alpha = 0.01f) const;
   void launch(hipStream_t s, SaConvArgs& a) const;
 

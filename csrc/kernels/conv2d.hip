@@ -86,7 +86,11 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
   const int M = p.N * HWo;
   const int m0 = blockIdx.x * BM;
   const int n0 = blockIdx.y * BN;
-  const int nk = p.Kpad / C::BK;
+  // split-K slice of the K loop handled by this block
+  const int S = gridDim.z, z = blockIdx.z;
+  const int nk_all = p.Kpad / C::BK;
+  const int kt0 = (int)((long)z * nk_all / S);
+  const int nk = (int)((long)(z + 1) * nk_all / S) - kt0;
   const int taps = p.KH * p.KW;
 
   // ---------------- per-thread A-row precompute ----------------
@@ -111,7 +115,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
   // k-position tracking for this thread's chunk
   int k_tap, k_ci;
   {
-    int kc = cth * 8;
+    int kc = kt0 * C::BK + cth * 8;
     k_tap = kc / p.Cin;
     k_ci = kc - k_tap * p.Cin;
   }
@@ -151,8 +155,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
       int q = tid + 256 * i;
       if (q < C::B_CH) {
         int row = q >> 2;
-        rb[i] = *reinterpret_cast<const half8*>(wptr + (size_t)(n0 + row) * p.Kpad + kt * C::BK +
-                                                 (q & 3) * 8);
+        rb[i] = *reinterpret_cast<const half8*>(wptr + (size_t)(n0 + row) * p.Kpad +
+                                                 (kt0 + kt) * C::BK + (q & 3) * 8);
       }
     }
     // advance k position by BK for the next tile
@@ -213,6 +217,55 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
     __syncthreads();
   }
 
+  // ---------------- split-K: partial slabs + last-arriver reduction ----------------
+  // Protocol of cdna_hip_programming.md "Projection GEMM at M = 256" item 2 (agent-scope release
+  // by every slice, acquire by the last arriver), valid for any placement of slices over XCDs.
+  if (S > 1) {
+    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+    constexpr int SLAB = BM * BN;
+    float* slab = p.ws + ((size_t)tile * S + z) * SLAB;
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) slab[((i * C::FN + j) * 4 + r) * 256 + tid] = acc[i][j][r];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int old = __hip_atomic_fetch_add(p.counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == S - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(p.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      *flag = last;
+    }
+    __syncthreads();
+    const int last = *flag;
+    __syncthreads();
+    if (!last) return;
+    // fixed summation order over all slices (own slab included) => bitwise deterministic
+    // regardless of which slice arrives last
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int sl = 0; sl < S; ++sl) {
+      const float* os = p.ws + ((size_t)tile * S + sl) * SLAB;
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += os[((i * C::FN + j) * 4 + r) * 256 + tid];
+    }
+  }
+
   // ---------------- epilogue: stage C through LDS ----------------
   float* ct = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -250,9 +303,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
   auto flush_stats = [&](int img) {
     if (img < 0) return;
     for (int j = 0; j < 8 && j < nvalid; ++j) {
-      double* sp = p.stats + ((size_t)img * p.Cout + co + j) * 2;
-      atomicAdd(sp, (double)ssum[j]);
-      atomicAdd(sp + 1, (double)ssq[j]);
+      unsigned long long* sp = reinterpret_cast<unsigned long long*>(p.stats) + ((size_t)img * p.Cout + co + j) * 2;
+      atomicAdd(sp, (unsigned long long)__double2ll_rn((double)ssum[j] * SA_STAT_SCALE));
+      atomicAdd(sp + 1, (unsigned long long)__double2ll_rn((double)ssq[j] * SA_STAT_SCALE));
       ssum[j] = ssq[j] = 0.f;
     }
   };
@@ -400,7 +453,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
       float acc = 0.f;
       for (int r = 0; r < RG; ++r) acc += red[(q * RG + r) * BN + col];
       const int img = img_lo + (q >> 1);
-      atomicAdd(p.stats + ((size_t)img * p.Cout + c) * 2 + (q & 1), (double)acc);
+      atomicAdd(reinterpret_cast<unsigned long long*>(p.stats) + ((size_t)img * p.Cout + c) * 2 + (q & 1),
+                (unsigned long long)__double2ll_rn((double)acc * SA_STAT_SCALE));
     }
   }
 }
@@ -408,7 +462,26 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
 template <int BM, int BN, int WM, int WN>
 int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
   const int M = a->N * a->Ho * a->Wo;
-  dim3 grid((M + BM - 1) / BM, (a->Cout + BN - 1) / BN);
+  const int gx = (M + BM - 1) / BM, gy = (a->Cout + BN - 1) / BN;
+  const long tiles = (long)gx * gy;
+  const int nk = a->Kpad / 32;
+  int S = a->splitk;
+  if (S == 0) {
+    // auto: split the K loop when the tile grid cannot fill 256 CUs (small-M levels of the
+    // RAFT GRU pyramid at batch 1); keep >= 4 k-steps of 32 per slice
+    S = 1;
+    if (a->ws && a->counters && !a->stats && tiles < 320) {
+      S = (int)((640 + tiles - 1) / tiles);
+      if (S > 8) S = 8;
+      if (S > nk / 4) S = nk / 4;
+      while (S > 1 && ((long)S * tiles * BM * BN > a->ws_floats || tiles > a->n_counters)) --S;
+      if (S < 1) S = 1;
+    }
+  }
+  if (S > 1 && (a->stats || !a->ws || !a->counters || (long)S * tiles * BM * BN > a->ws_floats ||
+                tiles > a->n_counters || S > nk))
+    return -4;
+  dim3 grid(gx, gy, S);
   hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN>), grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
 }

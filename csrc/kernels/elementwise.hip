@@ -48,12 +48,12 @@ __global__ void instnorm_apply_kernel(const SaNormArgs a) {
     const int c = c8 * 8;
     float v[8];
     ld8(reinterpret_cast<const f16*>(a.x) + pix * a.x_stride + c, v);
-    const double inv = 1.0 / (double)a.HW;
+    const double inv = 1.0 / ((double)a.HW * SA_STAT_SCALE);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const double* s = a.stats + ((long)n * a.C + c + j) * 2;
-      double mean = s[0] * inv;
-      double var = s[1] * inv - mean * mean;
+      const sa_stat_t* s = a.stats + ((long)n * a.C + c + j) * 2;
+      double mean = (double)s[0] * inv;
+      double var = (double)s[1] * inv - mean * mean;
       float rstd = rsqrtf((float)(var > 0.0 ? var : 0.0) + a.eps);
       v[j] = act_apply((v[j] - (float)mean) * rstd, a.act, a.alpha);
     }
@@ -63,9 +63,9 @@ __global__ void instnorm_apply_kernel(const SaNormArgs a) {
       if (a.res_stats) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const double* s = a.res_stats + ((long)n * a.C + c + j) * 2;
-          double mean = s[0] * inv;
-          double var = s[1] * inv - mean * mean;
+          const sa_stat_t* s = a.res_stats + ((long)n * a.C + c + j) * 2;
+          double mean = (double)s[0] * inv;
+          double var = (double)s[1] * inv - mean * mean;
           float rstd = rsqrtf((float)(var > 0.0 ? var : 0.0) + a.eps);
           r[j] = (r[j] - (float)mean) * rstd;
         }

@@ -9,8 +9,8 @@ Norm parse_norm(const std::string& s) {
   throw Error("unsupported norm " + s);
 }
 
-void instnorm(hipStream_t s, const Tensor& x, const double* stats, const Tensor& out, int act,
-              const Tensor* res, const double* res_stats, int act2) {
+void instnorm(hipStream_t s, const Tensor& x, const sa_stat_t* stats, const Tensor& out, int act,
+              const Tensor* res, const sa_stat_t* res_stats, int act2) {
   SaNormArgs a{};
   a.x = x.ptr;
   a.x_stride = x.stride;

@@ -11,30 +11,30 @@ namespace sa {
 enum class Norm { None, Batch, Instance };
 Norm parse_norm(const std::string& s);
 
-// Per-forward statistics buffers (double {sum, sumsq} per (n, c)), zeroed by one memset.
+// Per-forward instance-norm statistics (fixed-point {sum, sumsq} per (n, c)), zeroed by one memset.
 class StatsPool {
  public:
-  double* take(int n, int c) {
+  sa_stat_t* take(int n, int c) {
     size_t need = (size_t)n * c * 2;
     reserve_.push_back(need);
     offs_.push_back(total_);
     total_ += need;
-    return reinterpret_cast<double*>((size_t)offs_.size());  // placeholder resolved in finalize
+    return reinterpret_cast<sa_stat_t*>((size_t)offs_.size());  // placeholder resolved in finalize
   }
   void finalize(DeviceArena& a) {
-    base_ = (double*)a.alloc(std::max<size_t>(total_, 1) * sizeof(double));
+    base_ = (sa_stat_t*)a.alloc(std::max<size_t>(total_, 1) * sizeof(sa_stat_t));
   }
-  double* resolve(double* handle) const {
+  sa_stat_t* resolve(sa_stat_t* handle) const {
     if (!handle) return nullptr;
     size_t idx = (size_t)handle - 1;
     return base_ + offs_[idx];
   }
-  void zero(hipStream_t s) const { HIP_CHECK(hipMemsetAsync(base_, 0, std::max<size_t>(total_, 1) * sizeof(double), s)); }
+  void zero(hipStream_t s) const { HIP_CHECK(hipMemsetAsync(base_, 0, std::max<size_t>(total_, 1) * sizeof(sa_stat_t), s)); }
 
  private:
   std::vector<size_t> reserve_, offs_;
   size_t total_ = 0;
-  double* base_ = nullptr;
+  sa_stat_t* base_ = nullptr;
 };
 
 // ResidualBlock of RAFT-Stereo / CREStereo extractors (upstream core/extractor.py):
@@ -45,14 +45,14 @@ struct ResBlock {
   bool has_down = false;
   Norm norm = Norm::None;
   Tensor y1, a1, y2, yd, out;
-  double *st1 = nullptr, *st2 = nullptr, *std_ = nullptr;  // StatsPool handles
+  sa_stat_t *st1 = nullptr, *st2 = nullptr, *std_ = nullptr;  // StatsPool handles
   void build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std::string& prefix, int in_planes,
              int planes, int stride, Norm norm, int N, int H, int W);
   void run(hipStream_t s, const StatsPool& sp, const Tensor& x) const;
 };
 
 // norm apply helper
-void instnorm(hipStream_t s, const Tensor& x, const double* stats, const Tensor& out, int act,
-              const Tensor* res = nullptr, const double* res_stats = nullptr, int act2 = SA_ACT_NONE);
+void instnorm(hipStream_t s, const Tensor& x, const sa_stat_t* stats, const Tensor& out, int act,
+              const Tensor* res = nullptr, const sa_stat_t* res_stats = nullptr, int act2 = SA_ACT_NONE);
 
 }  // namespace sa

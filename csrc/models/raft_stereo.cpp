@@ -73,7 +73,7 @@ class RaftStereo : public StereoEngine {
     ConvLayer conv1;
     Norm norm;
     Tensor c1y, c1a;
-    double* c1st = nullptr;
+    sa_stat_t* c1st = nullptr;
     std::vector<ResBlock> layers;  // layer1..3 (2 blocks each)
   };
   void build_trunk(Encoder& e, WeightSource& src, const std::string& p, Norm norm, int N);

@@ -3,6 +3,7 @@
 #include "sa/engine.h"
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 namespace sa {
@@ -77,6 +78,8 @@ StereoEngine::~StereoEngine() {
   graph_[1].reset();
   if (pin_in_) (void)hipHostFree(pin_in_);
   if (pin_out_) (void)hipHostFree(pin_out_);
+  if (ev_in_) (void)hipEventDestroy(ev_in_);
+  if (ev_out_) (void)hipEventDestroy(ev_out_);
   if (stream_) (void)hipStreamDestroy(stream_);
   arena_.release();
 }
@@ -106,7 +109,15 @@ std::unique_ptr<StereoEngine> StereoEngine::create(const EngineConfig& cfg_in) {
 
 void StereoEngine::init() {
   HIP_CHECK(hipSetDevice(cfg_.device));
-  HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  if (const char* e = std::getenv("SA_NO_GRAPH"))
+    if (e[0] == '1') cfg_.use_graph = false;  // debugging: eager launches (with SA_DEBUG_SYNC=1)
+  // A blocking stream (like the reference's cudaStreamCreate, TRTRAFTStereo.cpp:85): frames are
+  // implicitly ordered after work already queued on the legacy default stream by the host
+  // program (observed: a graph replayed on a non-blocking stream while torch kernels were still
+  // in flight on the default stream faulted).
+  HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamDefault));
+  HIP_CHECK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
   const size_t img = (size_t)B() * H() * W() * 3;
   in_left_ = (uint8_t*)arena_.alloc(img);
   in_right_ = (uint8_t*)arena_.alloc(img);
@@ -116,6 +127,7 @@ void StereoEngine::init() {
   cloud_ = (float*)arena_.alloc((size_t)B() * H() * W() * 6 * 4);
   HIP_CHECK(hipHostMalloc((void**)&pin_in_, 2 * img, hipHostMallocDefault));
   HIP_CHECK(hipHostMalloc((void**)&pin_out_, (size_t)B() * H() * W() * 7 * 4 + 2 * img, hipHostMallocDefault));
+  splitk_.alloc(arena_, 16l << 20, 8192);  // 64 MiB of fp32 slabs, 8192 tile counters
   WeightSource src{store_.get(), cfg_.weights.empty(), cfg_.seed};
   build(src);
   store_.reset();  // host copies no longer needed
@@ -138,6 +150,7 @@ void StereoEngine::set_rectify_maps(const float* ml, const float* mr) {
 }
 
 void StereoEngine::frame(hipStream_t s, bool rectify) {
+  ScopedSplitK sk(&splitk_);
   if (rectify) {
     SA_REQUIRE(rect_maps_ != nullptr, "rectification requested but no maps set");
     // left images use map 0, right images map 1 (maps laid out [2][H][W][2])
@@ -156,13 +169,23 @@ void StereoEngine::frame(hipStream_t s, bool rectify) {
 
 void StereoEngine::launch_frame(hipStream_t s, bool rectify) {
   GraphExec& g = graph_[rectify ? 1 : 0];
+  // The frame always executes on the engine's own stream (where its graphs were captured); a
+  // caller stream is ordered against it with events on both sides, so graph execs are never
+  // replayed on a foreign (e.g. the legacy null) stream.
+  const bool foreign = s != stream_;
+  if (foreign) {
+    HIP_CHECK(hipEventRecord(ev_in_, s));
+    HIP_CHECK(hipStreamWaitEvent(stream_, ev_in_, 0));
+  }
   if (cfg_.use_graph) {
-    // capture on the engine's own (non-blocking) stream — capture cannot use the legacy null
-    // stream torch hands out by default — then replay on the caller's stream.
     if (!g.ready()) g.capture(stream_, [&] { frame(stream_, rectify); });
-    g.launch(s);
+    g.launch(stream_);
   } else {
-    frame(s, rectify);
+    frame(stream_, rectify);
+  }
+  if (foreign) {
+    HIP_CHECK(hipEventRecord(ev_out_, stream_));
+    HIP_CHECK(hipStreamWaitEvent(s, ev_out_, 0));
   }
   launches_per_frame_++;
 }

@@ -266,6 +266,15 @@ SaConvArgs ConvLayer::args(const std::vector<Tensor>& srcs, const Tensor& out) c
   a.scale = 1.f;
   a.alpha = 0.01f;
   a.tile_cfg = -1;
+  if (const SplitKWorkspace* sk = current_splitk()) {
+    a.splitk = 0;  // auto
+    a.ws = sk->ws;
+    a.counters = sk->counters;
+    a.ws_floats = sk->ws_floats;
+    a.n_counters = sk->n_counters;
+  } else {
+    a.splitk = 1;
+  }
   return a;
 }
 
@@ -277,7 +286,7 @@ void ConvLayer::launch(hipStream_t s, SaConvArgs& a) const {
 }
 
 void ConvLayer::run(hipStream_t s, const std::vector<Tensor>& srcs, const Tensor& out, int act,
-                    const Tensor* res, int act2, double* stats, float alpha) const {
+                    const Tensor* res, int act2, sa_stat_t* stats, float alpha) const {
   SaConvArgs a = args(srcs, out);
   SA_REQUIRE(out.c >= cout_ || stats == nullptr, "conv output view too narrow");
   a.act = act;
@@ -289,6 +298,19 @@ void ConvLayer::run(hipStream_t s, const std::vector<Tensor>& srcs, const Tensor
   }
   a.stats = stats;
   launch(s, a);
+}
+
+static thread_local const SplitKWorkspace* g_splitk = nullptr;
+const SplitKWorkspace* current_splitk() { return g_splitk; }
+ScopedSplitK::ScopedSplitK(const SplitKWorkspace* w) : prev(g_splitk) { g_splitk = w; }
+ScopedSplitK::~ScopedSplitK() { g_splitk = prev; }
+
+void SplitKWorkspace::alloc(DeviceArena& a, int64_t floats, int32_t ncnt) {
+  ws = (float*)a.alloc((size_t)floats * 4);
+  counters = (int32_t*)a.alloc((size_t)ncnt * 4);
+  HIP_CHECK(hipMemset(counters, 0, (size_t)ncnt * 4));
+  ws_floats = floats;
+  n_counters = ncnt;
 }
 
 void GraphExec::reset() {

@@ -22,7 +22,7 @@ ARCH = os.environ.get("SA_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX_HOST", "g++")
 
-HOST_DIRS = ("geometry", "io")  # CPU-only sources -> libstereo_host.so
+HOST_DIRS = ("host",)  # CPU-only sources -> libstereo_host.so
 DEVICE_DIRS = ("kernels", "runtime", "models", "api")
 
 COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC / 'include'}", "-Wall", "-Wno-unused-function"]
@@ -92,14 +92,9 @@ def build(jobs: int | None = None, verbose: bool = False) -> dict:
     host_objs = [OBJDIR / "host" / (s.stem + s.suffix + ".o") for s in host_src]
     dev_objs = [OBJDIR / "dev" / (s.stem + s.suffix + ".o") for s in dev_src]
     if host_objs:
-        _link(host_objs, host_lib, True, extra=["-ljpeg", "-lpng16"] if _has_img_libs() else [])
+        _link(host_objs, host_lib, True, extra=["-lz"])
     _link(dev_objs, dev_lib, False, extra=[f"-L{LIBDIR}", "-lstereo_host", "-Wl,-rpath,$ORIGIN"] if host_objs else [])
     return {"compiled": built, "libs": [str(host_lib), str(dev_lib)]}
-
-
-def _has_img_libs() -> bool:
-    libdir = Path("/usr/lib/x86_64-linux-gnu")
-    return (libdir / "libjpeg.so").exists() and (libdir / "libpng16.so").exists()
 
 
 if __name__ == "__main__":

@@ -74,7 +74,9 @@ class SaConvArgs(C.Structure):
         ("hbuf", C.c_void_p), ("h_stride", C.c_int32),
         ("rh", C.c_void_p), ("rh_stride", C.c_int32),
         ("stats", C.c_void_p),
-        ("tile_cfg", C.c_int32), ("_pad", C.c_int32),
+        ("tile_cfg", C.c_int32), ("splitk", C.c_int32),
+        ("ws", C.c_void_p), ("counters", C.c_void_p), ("ws_floats", C.c_int64),
+        ("n_counters", C.c_int32), ("_pad2", C.c_int32),
     ]
 
 

@@ -15,7 +15,7 @@ import torch
 from .. import _native as N
 
 __all__ = [
-    "pack_conv_weight", "conv2d", "instnorm_apply", "avgpool3s2", "avgpool_k", "interp_bilinear",
+    "splitk_workspace", "pack_conv_weight", "conv2d", "instnorm_apply", "avgpool3s2", "avgpool_k", "interp_bilinear",
     "corr1d_pyramid", "corr1d_lookup", "convex_upsample", "preprocess", "remap_bgr", "reproject",
 ]
 
@@ -35,6 +35,11 @@ def _pix_stride(t: torch.Tensor) -> int:
     s = t.stride(2)
     assert t.stride(1) == w * s and (n == 1 or t.stride(0) == h * w * s), "pixels must be uniformly strided"
     return s
+
+
+def splitk_workspace(floats: int = 1 << 22, counters: int = 4096, device="cuda"):
+    return (torch.empty(floats, dtype=torch.float32, device=device),
+            torch.zeros(counters, dtype=torch.int32, device=device))
 
 
 def pack_conv_weight(w: torch.Tensor, segs: Sequence[tuple[int, int]] | None = None):
@@ -60,7 +65,9 @@ def pack_conv_weight(w: torch.Tensor, segs: Sequence[tuple[int, int]] | None = N
 
 def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1, act="none",
            act2="none", res=None, out=None, epi="store", scale=1.0, alpha=0.01, stats=None,
-           ctx=None, aux=None, hbuf=None, rh=None, tile_cfg=-1):
+           ctx=None, aux=None, hbuf=None, rh=None, tile_cfg=-1, splitk=1, workspace=None):
+    """NHWC fp16 implicit-GEMM conv.  ``splitk``: 1 = off, 0 = auto, >1 = forced; needs
+    ``workspace`` = (fp32 slab tensor, int32 counter tensor zero-initialised)."""
     if isinstance(xs, torch.Tensor):
         xs = [xs]
     n, h, w, _ = xs[0].shape
@@ -110,9 +117,14 @@ def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1
     if rh is not None:
         a.rh, a.rh_stride = rh.data_ptr(), _pix_stride(rh)
     if stats is not None:
-        assert stats.dtype == torch.float64
+        assert stats.dtype == torch.int64  # fixed point, value * 2^24
         a.stats = stats.data_ptr()
     a.tile_cfg = tile_cfg
+    a.splitk = splitk
+    if workspace is not None:
+        ws, cnt = workspace
+        assert ws.dtype == torch.float32 and cnt.dtype == torch.int32
+        a.ws, a.counters, a.ws_floats, a.n_counters = ws.data_ptr(), cnt.data_ptr(), ws.numel(), cnt.numel()
     N.check(N.dev().sa_conv2d(C.byref(a), _stream()), "sa_conv2d")
     return out
 
