@@ -24,6 +24,9 @@ import time
 
 import numpy as np
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import stereoalgorithms_amd  # noqa: E402,F401  (HIP runtime env defaults before torch touches the GPU)
+
 BASELINE_MS = {"raftstereo-sceneflow": 38.0, "raftstereo-realtime": 11.0}  # RTX 3090, README_en.md:139-141
 
 

@@ -25,6 +25,14 @@ CXX = os.environ.get("CXX_HOST", "g++")
 HOST_DIRS = ("host",)  # CPU-only sources -> libstereo_host.so
 DEVICE_DIRS = ("kernels", "runtime", "models", "api")
 
+BINDIR = Path(__file__).resolve().parent / "bin"
+# csrc/abi source -> library exporting the reference's symbol names
+ABI_LIBS = {"raftstereo_abi.cpp": "libRAFTStereo.so", "hitnet_abi.cpp": "libHitNet.so",
+            "crestereo_abi.cpp": "libCREStereo.so", "fastacvnet_abi.cpp": "libFastACVNet_plus.so"}
+# apps source -> ABI library it links (reference demo executable names)
+APPS = {"raft_stereo_demo.cpp": "libRAFTStereo.so", "HitNet_demo.cpp": "libHitNet.so",
+        "crestereo_demo.cpp": "libCREStereo.so", "fastacvnet_plus_demo.cpp": "libFastACVNet_plus.so"}
+
 COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC / 'include'}", "-Wall", "-Wno-unused-function"]
 
 
@@ -45,7 +53,7 @@ def _compile(src: Path, obj: Path, host_only: bool, hmt: float, verbose: bool) -
         return None
     obj.parent.mkdir(parents=True, exist_ok=True)
     if host_only:
-        cmd = [CXX, *COMMON_FLAGS, "-c", str(src), "-o", str(obj)]
+        cmd = [CXX, *COMMON_FLAGS, f"-I{CSRC / 'abi'}", "-c", str(src), "-o", str(obj)]
     else:
         cmd = [HIPCC, f"--offload-arch={ARCH}", *COMMON_FLAGS, "-c", str(src), "-o", str(obj)]
         if src.suffix == ".hip":
@@ -59,13 +67,13 @@ def _compile(src: Path, obj: Path, host_only: bool, hmt: float, verbose: bool) -
     return str(src.relative_to(ROOT))
 
 
-def _link(objs, out: Path, host_only: bool, extra=()):
+def _link(objs, out: Path, host_only: bool, extra=(), shared: bool = True):
     newest = max(o.stat().st_mtime for o in objs)
     if out.exists() and out.stat().st_mtime >= newest:
         return False
     out.parent.mkdir(parents=True, exist_ok=True)
     if host_only:
-        cmd = [CXX, "-shared", "-o", str(out), *map(str, objs), *extra]
+        cmd = [CXX, *(["-shared"] if shared else []), "-o", str(out), *map(str, objs), *extra]
     else:
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", str(out), *map(str, objs), *extra]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -94,7 +102,30 @@ def build(jobs: int | None = None, verbose: bool = False) -> dict:
     if host_objs:
         _link(host_objs, host_lib, True, extra=["-lz"])
     _link(dev_objs, dev_lib, False, extra=[f"-L{LIBDIR}", "-lstereo_host", "-Wl,-rpath,$ORIGIN"] if host_objs else [])
-    return {"compiled": built, "libs": [str(host_lib), str(dev_lib)]}
+    libs = [str(host_lib), str(dev_lib)]
+    # reference-compatible per-model C ABI libraries + demo executables (host compiler, link the
+    # engine library)
+    abi_built = []
+    for src, lib in ABI_LIBS.items():
+        s = CSRC / "abi" / src
+        obj = OBJDIR / "abi" / (s.stem + ".o")
+        r = _compile(s, obj, True, hmt, verbose)
+        if r:
+            abi_built.append(r)
+        out = LIBDIR / lib
+        _link([obj], out, True, extra=[f"-L{LIBDIR}", "-lstereo_amd", "-lstereo_host", "-Wl,-rpath,$ORIGIN"])
+        libs.append(str(out))
+    BINDIR.mkdir(parents=True, exist_ok=True)
+    for app, lib in APPS.items():
+        s = ROOT / "apps" / app
+        obj = OBJDIR / "apps" / (s.stem + ".o")
+        r = _compile(s, obj, True, max(hmt, (ROOT / "apps" / "demo_main.h").stat().st_mtime), verbose)
+        if r:
+            abi_built.append(r)
+        libname = lib[3:-3]
+        _link([obj], BINDIR / s.stem, True, shared=False,
+              extra=[f"-L{LIBDIR}", f"-l{libname}", "-lstereo_host", "-Wl,-rpath,$ORIGIN/../lib"])
+    return {"compiled": built + abi_built, "libs": libs}
 
 
 if __name__ == "__main__":

@@ -7,6 +7,7 @@ import pytest
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+import stereoalgorithms_amd  # noqa: E402,F401  (sets HIP runtime env before torch initialises the GPU)
 
 FIXTURES = ROOT / "tests" / "fixtures"
 
