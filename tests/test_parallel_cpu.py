@@ -1,0 +1,80 @@
+"""Data-parallel frame sharding (parallel/dp.py) on CPU: gloo process groups, world sizes 2 and 4,
+a stand-in engine with the native engine's run() contract.  The RCCL path is the same code with
+the nccl backend (bench.py on GPUs)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from stereoalgorithms_amd.parallel import dp
+
+
+def test_shard_range_covers_all_frames():
+    for total in (1, 7, 64, 65):
+        for world in (1, 2, 3, 8):
+            spans = [dp.shard_range(total, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == total
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [e - s for s, e in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_round_robin_shards_partition():
+    got = sorted(i for r in range(3) for i in dp.shard_indices_round_robin(10, 3, r))
+    assert got == list(range(10))
+
+
+class FakeEngine:
+    """Deterministic per-frame 'disparity' = mean of the left image + frame marker."""
+
+    def __init__(self, batch, h, w):
+        self.batch, self.height, self.width = batch, h, w
+
+    def run(self, left, right):
+        return (left.float().mean(-1) - right.float().mean(-1)).contiguous()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, B, H, W, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(1234)
+        all_l = torch.randint(0, 255, (world * B, H, W, 3), generator=g, dtype=torch.uint8)
+        all_r = torch.randint(0, 255, (world * B, H, W, 3), generator=g, dtype=torch.uint8)
+        s, e = dp.shard_range(world * B, world, rank)
+        eng = FakeEngine(B, H, W)
+        step = dp.DataParallelStereo(eng, world_size=world, rank=rank)
+        out = step.step(all_l[s:e], all_r[s:e])
+        ref = eng.run(all_l, all_r)
+        ok = out.shape == (world * B, H, W) and torch.equal(out, ref)
+        r0 = dp.gather_to_rank0(eng.run(all_l[s:e], all_r[s:e]), world, rank)
+        if rank == 0:
+            ok = ok and torch.equal(r0, ref)
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_allgather_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 2, 6, 8, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert all(res[r] for r in range(world)), res
