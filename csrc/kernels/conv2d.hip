@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
 
+#include <cstdlib>
+
 #include "sa/kernels.h"
 
 namespace {
@@ -53,9 +55,11 @@ __device__ __forceinline__ void store8(f16* p, const float* v) {
   *reinterpret_cast<half8*>(p) = h;
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool GL = false>
 struct ConvCfg {
-  static constexpr int BK = 32;
+  // GL: global->LDS DMA staging (global_load_lds_dwordx4) with BK = 64; otherwise register
+  // staging with BK = 32 (kept for K not a multiple of 64)
+  static constexpr int BK = GL ? 64 : 32;
   static constexpr int TM = BM / WM, TN = BN / WN;
   static constexpr int FM = TM / 16, FN = TN / 16;
   static constexpr int A_CH = BM * 4, B_CH = BN * 4;  // 16-byte chunks per stage
@@ -72,9 +76,15 @@ struct ConvCfg {
 // swizzled byte offset of (row, 16B-chunk) inside a [rows][32 halfs] stage buffer
 __device__ __forceinline__ int swz(int row, int c) { return row * 64 + ((c ^ (((row >> 3) & 1) * 3)) << 4); }
 
-template <int BM, int BN, int WM, int WN>
+// 16 zero bytes in global memory: the source of every padded / out-of-range im2col chunk in the
+// DMA path (a masked-off lane would leave stale LDS behind)
+__device__ __attribute__((aligned(16))) const unsigned char g_zero16[64] = {0};
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+template <int BM, int BN, int WM, int WN, bool GL>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
-  using C = ConvCfg<BM, BN, WM, WN>;
+  using C = ConvCfg<BM, BN, WM, WN, GL>;
   __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
 
   const int tid = threadIdx.x;
@@ -93,6 +103,116 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
   const int nk = (int)((long)(z + 1) * nk_all / S) - kt0;
   const int taps = p.KH * p.KW;
 
+  floatx4 acc[C::FM][C::FN];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (GL) {
+    // ---------------- DMA staging: [rows][64 halfs] (128 B) per stage, chunk XOR-swizzled ----------
+    // LDS image is lane-linear per wave instruction (q*16 = row*128 + pch*16); the swizzle lives on
+    // the SOURCE side: slot q fetches logical chunk lch = pch ^ ((row>>1)&7), so the fragment reads
+    // (16 rows x one chunk per ds_read_b128 lane group) hit 16 distinct 16-B bank slots.
+    // 16-B chunks per thread per stage (>= 1 so every config instantiates; BN < 32 never takes
+    // this path, see launch_cfg)
+    constexpr int NA = BM / 32 > 0 ? BM / 32 : 1, NB = BN / 32 > 0 ? BN / 32 : 1;
+    const int sb1 = p.src[0].channels;
+    const int sb2 = sb1 + (p.nsrc > 1 ? p.src[1].channels : 0);
+    const int sb3 = sb2 + (p.nsrc > 2 ? p.src[2].channels : 0);
+    int a_ih0[NA], a_iw0[NA], a_nb[NA], a_tap[NA], a_ci[NA];
+    bool a_ok[NA];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int q = (wave * NA + i) * 64 + lane;
+      const int row = q >> 3, pch = q & 7;
+      const int lch = pch ^ ((row >> 1) & 7);
+      const int m = m0 + row;
+      a_ok[i] = m < M;
+      const int mm = a_ok[i] ? m : 0;
+      const int n = mm / HWo;
+      const int r = mm - n * HWo;
+      const int oh = r / p.Wo, ow = r - oh * p.Wo;
+      a_ih0[i] = oh * p.sh - p.ph;
+      a_iw0[i] = ow * p.sw - p.pw;
+      a_nb[i] = n * p.H;
+      const int kc = kt0 * C::BK + lch * 8;
+      a_tap[i] = kc / p.Cin;
+      a_ci[i] = kc - a_tap[i] * p.Cin;
+    }
+    const f16* wbase[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int q = (wave * NB + i) * 64 + lane;
+      const int row = q >> 3, pch = q & 7;
+      const int lch = pch ^ ((row >> 1) & 7);
+      wbase[i] = reinterpret_cast<const f16*>(p.weight) + (size_t)(n0 + row) * p.Kpad + (size_t)kt0 * C::BK + lch * 8;
+    }
+    const void* zero_src = g_zero16;
+    auto issue = [&](int kt, int buf) {
+      char* sa = smem + buf * (C::A_BYTES + C::B_BYTES);
+      char* sb = sa + C::A_BYTES;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int tap = a_tap[i], ci = a_ci[i];
+        const int kh = tap / p.KW, kw = tap - kh * p.KW;
+        const int ih = a_ih0[i] + kh * p.dh, iw = a_iw0[i] + kw * p.dw;
+        const bool ok = a_ok[i] && tap < taps && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+        const int s = (ci >= sb1) + (ci >= sb2) + (ci >= sb3);
+        const int cbase = s == 0 ? 0 : (s == 1 ? sb1 : (s == 2 ? sb2 : sb3));
+        const void* g = zero_src;
+        if (ok) {
+          const size_t pix = (size_t)(a_nb[i] + ih) * p.W + iw;
+          g = reinterpret_cast<const f16*>(p.src[s].ptr) + pix * p.src[s].stride + (ci - cbase);
+        }
+        __builtin_amdgcn_global_load_lds(g, (lds_void_t*)(sa + (wave * NA + i) * 1024), 16, 0, 0);
+        // next k-step of this chunk
+        int nci = ci + C::BK, ntap = tap;
+        while (nci >= p.Cin) {
+          nci -= p.Cin;
+          ++ntap;
+        }
+        a_ci[i] = nci;
+        a_tap[i] = ntap;
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+        // (explicit void* source: a typed _Float16* argument makes the host pass drop the kernel stub)
+        __builtin_amdgcn_global_load_lds((const void*)(wbase[i] + (size_t)kt * C::BK),
+                                         (lds_void_t*)(sb + (wave * NB + i) * 1024), 16, 0, 0);
+    };
+    // fragment read: row = lane&15 (+16 i), logical chunk = (lane>>4) + 4*kk
+    const int frow = lane & 15;
+    if (nk > 0) issue(0, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // stage kt landed for every wave; buffer cur^1 no longer read
+      if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
+      const char* sa = smem + cur * (C::A_BYTES + C::B_BYTES);
+      const char* sb = sa + C::A_BYTES;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        half8 af[C::FM], bf[C::FN];
+        const int lc = (lane >> 4) + 4 * kk;
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+          const int row = wm * C::TM + i * 16 + frow;
+          af[i] = *reinterpret_cast<const half8*>(sa + row * 128 + ((lc ^ ((row >> 1) & 7)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) {
+          const int row = wn * C::TN + j * 16 + frow;
+          bf[j] = *reinterpret_cast<const half8*>(sb + row * 128 + ((lc ^ ((row >> 1) & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int j = 0; j < C::FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // all fragment reads done before the epilogue reuses LDS
+  } else {
   // ---------------- per-thread A-row precompute ----------------
   const int cth = tid & 3;  // chunk index this thread loads (constant over k)
   int a_ih0[C::A_PT], a_iw0[C::A_PT], a_nb[C::A_PT];
@@ -182,11 +302,6 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
     }
   };
 
-  floatx4 acc[C::FM][C::FN];
-#pragma unroll
-  for (int i = 0; i < C::FM; ++i)
-#pragma unroll
-    for (int j = 0; j < C::FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   // fragment read offsets (row = lane&15, chunk = lane>>4, swizzled)
   const int frow = lane & 15;
@@ -216,6 +331,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
     if (kt + 1 < nk) store_tile(cur ^ 1);
     __syncthreads();
   }
+
+  }  // register-staged path
 
   // ---------------- split-K: partial slabs + last-arriver reduction ----------------
   // Protocol of cdna_hip_programming.md "Projection GEMM at M = 256" item 2 (agent-scope release
@@ -459,12 +576,20 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
   }
 }
 
+template <int BM, int BN, int WM, int WN, bool GL>
+void launch_kernel(dim3 grid, const SaConvArgs* a, hipStream_t stream) {
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, GL>), grid, dim3(256), 0, stream, *a);
+}
+
 template <int BM, int BN, int WM, int WN>
 int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
+  // DMA path whenever K (and so every k-step) is 64-aligned
+  constexpr bool can_gl = BN >= 32 && BM >= 32;  // whole-wave DMA instructions per stage
+  const bool gl = can_gl && a->Kpad % 64 == 0 && !(std::getenv("SA_CONV_NO_GLDS"));
   const int M = a->N * a->Ho * a->Wo;
   const int gx = (M + BM - 1) / BM, gy = (a->Cout + BN - 1) / BN;
   const long tiles = (long)gx * gy;
-  const int nk = a->Kpad / 32;
+  const int nk = a->Kpad / (gl ? 64 : 32);
   int S = a->splitk;
   if (S == 0) {
     // auto: split the K loop when the tile grid cannot fill 256 CUs (small-M levels of the
@@ -482,7 +607,8 @@ int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
                 tiles > a->n_counters || S > nk))
     return -4;
   dim3 grid(gx, gy, S);
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN>), grid, dim3(256), 0, stream, *a);
+  if (gl) launch_kernel<BM, BN, WM, WN, true>(grid, a, stream);
+  else launch_kernel<BM, BN, WM, WN, false>(grid, a, stream);
   return (int)hipGetLastError();
 }
 

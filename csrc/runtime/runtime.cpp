@@ -140,7 +140,7 @@ void ConvLayer::upload(DeviceArena& arena, const std::vector<float>& w, const st
   cin_pad_ = pad_sum;
   const int KH = spec_.kh, KW = spec_.kw;
   const int K = KH * KW * cin_pad_;
-  kpad_ = round_up(K, 32);
+  kpad_ = round_up(K, 64);  // 64-aligned K enables the DMA-staged BK=64 conv path
   const int cout_pad = round_up(cout, 128);
   std::vector<uint16_t> packed((size_t)cout_pad * kpad_, 0);
   // padded channel -> real channel index (or -1)

@@ -56,7 +56,7 @@ def pack_conv_weight(w: torch.Tensor, segs: Sequence[tuple[int, int]] | None = N
         rc += r
         pc += p
     k = kh * kw * cin_pad
-    kpad = (k + 31) // 32 * 32
+    kpad = (k + 63) // 64 * 64  # 64-aligned K -> DMA-staged BK=64 kernel path
     cpad = (cout + 127) // 128 * 128
     out = torch.zeros(cpad, kpad, dtype=torch.float16, device=w.device)
     out[:cout, :k] = wp.reshape(cout, k).half()

@@ -98,6 +98,31 @@ def test_conv2d_splitk_gru_epilogue():
     assert rel_err(nchw(rhb), r * net.half().float()) < 3e-3
 
 
+@pytest.mark.parametrize("cfg", [0, 1, 3])
+def test_conv2d_register_vs_dma_paths(cfg, monkeypatch):
+    """K padded to 32 only (odd multiple) forces the register-staged BK=32 loop; the default 64-padded
+    weights take the global->LDS DMA path.  Both must equal the torch reference."""
+    O = ops()
+    torch.manual_seed(7)
+    n, cin, cout, h, w = 2, 40, 128 if cfg == 0 else 64, 13, 21
+    x = torch.randn(n, cin, h, w, device=DEV)
+    wt = torch.randn(cout, cin, 3, 3, device=DEV) / math.sqrt(cin * 9)
+    ref = F.conv2d(x.half().float(), wt.half().float(), padding=1)
+    wp, kpad, _ = O.pack_conv_weight(wt)
+    assert kpad % 64 == 0
+    out = O.conv2d(nhwc(x).half(), wp, kpad, cout, 3, 3, tile_cfg=cfg)
+    # K = 9 * 40 = 360 -> 384 (64-aligned) vs 384 - 32... build a 32-aligned (non 64) packing
+    k = 9 * cin
+    k32 = (k + 31) // 32 * 32
+    assert k32 % 64 != 0
+    wp32 = torch.zeros(wp.shape[0], k32, dtype=wp.dtype, device=DEV)
+    wp32[:, :k] = wp[:, :k]
+    out32 = O.conv2d(nhwc(x).half(), wp32.contiguous(), k32, cout, 3, 3, tile_cfg=cfg)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(out), ref) < 2e-3
+    assert rel_err(nchw(out32), ref) < 2e-3
+
+
 def test_conv2d_multisource_concat_and_residual():
     O = ops()
     torch.manual_seed(1)
