@@ -27,7 +27,7 @@ enum SaEpi {
   SA_EPI_STORE = 0,     // y = act(acc*scale + bias) [; y = act2(y + res)] -> fp16
   SA_EPI_GRU_ZR = 1,    // z = sig(acc+b+cz) -> aux ; r = sig(acc+b+cr) -> rh = r*h
   SA_EPI_GRU_Q = 2,     // q = tanh(acc+b+cq) ; h = (1-z)h + zq  (in place on h)
-  SA_EPI_FLOW_ACC = 3,  // fp32 out[m*out_stride] += acc(ch0)*scale + bias  (RAFT coords1 += delta)
+  SA_EPI_FLOW_ACC = 3,  // fp32 out[m*out_stride + c] += acc*scale + bias for c < min(Cout, out_stride)
   SA_EPI_STORE_F32 = 4  // y = act(acc*scale + bias) -> fp32
 };
 
@@ -53,7 +53,7 @@ typedef struct {
   float scale;  // multiplies acc before bias
   const void* res;  // residual fp16 (SA_EPI_STORE)
   int32_t res_stride;
-  const void* ctx;  // GRU context biases fp16: ZR reads [cz | cr], Q reads cq
+  const void* ctx;  // GRU context biases fp16: ZR reads [cz | cr], Q reads cq (NULL = none)
   int32_t ctx_stride;
   void* aux;  // GRU z buffer fp16
   int32_t aux_stride;
@@ -119,6 +119,10 @@ int sa_corr1d_lookup(const float* pyr, const float* flow, int B, int H, int W1, 
 // (x component).  Writes full-res fp32 output = sign * (f * flow) combination.
 int sa_convex_upsample(const void* mask, int mask_stride, const float* flow, int B, int H, int W,
                        int factor, float sign, float* out, hipStream_t stream);
+// multi-channel variant: flow fp32 [B][H][W][fc]; out fp32 [B][H*f][W*f][oc] gets the first oc
+// channels of sign * convex(f * flow)
+int sa_convex_upsample_c(const void* mask, int mask_stride, const float* flow, int fc, int B, int H, int W,
+                         int factor, float sign, float* out, int oc, hipStream_t stream);
 
 // ---- pre / post processing ------------------------------------------------------------------
 enum SaNormMode {
@@ -140,6 +144,42 @@ int sa_remap_bgr(const uint8_t* src, int B, int Hs, int Ws, const float* maps, i
 int sa_reproject(const float* disp_in, int disp_stride, float sign, const uint8_t* left_bgr,
                  int B, int H, int W, const float* Q16, float* disp_out, float* cloud,
                  hipStream_t stream);
+
+// ---- CREStereo / Fast-ACVNet+ / HITNet ops (stereo_ops.hip) ---------------------------------
+typedef struct {
+  const void* f1; int32_t f1_stride;      // left features fp16 NHWC, C channels (4 groups)
+  const void* f2; int32_t f2_stride;      // right features
+  const float* flow;                      // fp32 [N][H][W][2]
+  const void* offset; int32_t offset_stride;  // fp16 [N][H][W][18] learned (x, y) offsets or NULL
+  int32_t N, H, W, C;
+  int32_t small_patch;  // 0: 1x9 window, 1: 3x3
+  int32_t iter_mode;    // 1: warp-then-window (replicate pad); 0: offset sampling (zero pad)
+  void* out; int32_t out_stride; int32_t out_channels;  // fp16, 36 used, rest zero-filled
+} SaAgclArgs;
+int sa_agcl_corr(const SaAgclArgs* a, hipStream_t stream);
+
+int sa_linear_attention(const void* q, int qs, const void* k, int ks, const void* v, int vs, void* out, int os,
+                        int N, int L, int S, int heads, int dim, float eps, hipStream_t stream);
+int sa_layernorm(const void* x, int xs, const float* gamma, const float* beta, const void* res, int rs, void* out,
+                 int os, long rows, int C, float eps, hipStream_t stream);
+
+// out[p][c] = act(x[p][c]*scale + add[p][c] + bcast[p % period][c]) over P pixels x C channels
+typedef struct {
+  const void* x; int32_t x_stride;
+  const void* add; int32_t add_stride;   // optional fp16 addend
+  const float* bcast; int64_t bcast_period;  // optional fp32 [period][C] addend
+  void* out; int32_t out_stride;
+  int64_t P; int32_t C;
+  int32_t act; float scale;
+} SaEwArgs;
+int sa_ew(const SaEwArgs* a, hipStream_t stream);
+
+// fp32 flow [P][fc] -> fp16 (fx, fy, 0...) into out1 (c1 channels, stride s1) and/or (fx, fy) into out2
+int sa_flow_features(const float* flow, int fc, long P, void* out1, int s1, int c1, void* out2, int s2,
+                     hipStream_t stream);
+// fp32 NHWC bilinear resize (align_corners=True) x mul
+int sa_interp_flow(const float* x, float* out, int N, int H, int W, int C, int Ho, int Wo, float mul,
+                   hipStream_t stream);
 
 #ifdef __cplusplus
 }

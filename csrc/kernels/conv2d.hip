@@ -494,9 +494,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
         }
       } else if (p.epi == SA_EPI_GRU_ZR) {
         const int Hd = p.Cout >> 1;
-        const f16* cptr = reinterpret_cast<const f16*>(p.ctx) + (size_t)m * p.ctx_stride + co;
-        float c8[8];
-        load8(cptr, c8);
+        float c8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (p.ctx) load8(reinterpret_cast<const f16*>(p.ctx) + (size_t)m * p.ctx_stride + co, c8);
         if (co < Hd) {
           float z[8];
 #pragma unroll
@@ -511,8 +510,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
           store8(reinterpret_cast<f16*>(p.rh) + (size_t)m * p.rh_stride + ch, rh);
         }
       } else if (p.epi == SA_EPI_GRU_Q) {
-        float c8[8], z8[8], h8[8];
-        load8(reinterpret_cast<const f16*>(p.ctx) + (size_t)m * p.ctx_stride + co, c8);
+        float c8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, z8[8], h8[8];
+        if (p.ctx) load8(reinterpret_cast<const f16*>(p.ctx) + (size_t)m * p.ctx_stride + co, c8);
         load8(reinterpret_cast<const f16*>(p.aux) + (size_t)m * p.aux_stride + co, z8);
         f16* hp = reinterpret_cast<f16*>(p.hbuf) + (size_t)m * p.h_stride + co;
         load8(hp, h8);
@@ -523,9 +522,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
         }
         store8(hp, h8);
       } else if (p.epi == SA_EPI_FLOW_ACC) {
-        if (co == 0) {
+        if (co == 0) {  // flow state += delta (RAFT: x only, stride 1; CREStereo: x and y)
           float* fp = reinterpret_cast<float*>(p.out) + (size_t)m * p.out_stride;
-          *fp += v[0];
+          const int nc = p.Cout < p.out_stride ? p.Cout : p.out_stride;
+          for (int j = 0; j < nc && j < 8; ++j) fp[j] += v[j];
         }
       }
     }
@@ -583,9 +583,14 @@ void launch_kernel(dim3 grid, const SaConvArgs* a, hipStream_t stream) {
 
 template <int BM, int BN, int WM, int WN>
 int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
-  // DMA path whenever K (and so every k-step) is 64-aligned
+  // DMA path (opt-in, SA_CONV_GLDS=1): measured 14% slower than register staging on the RAFT-SF
+  // batch-8 frame (108 vs 95 ms, one vmcnt(0)+barrier per 64-deep k-step), kept for tuning.
   constexpr bool can_gl = BN >= 32 && BM >= 32;  // whole-wave DMA instructions per stage
-  const bool gl = can_gl && a->Kpad % 64 == 0 && !(std::getenv("SA_CONV_NO_GLDS"));
+  static const bool want_gl = [] {
+    const char* e = std::getenv("SA_CONV_GLDS");
+    return e && e[0] == '1';
+  }();
+  const bool gl = can_gl && want_gl && a->Kpad % 64 == 0;
   const int M = a->N * a->Ho * a->Wo;
   const int gx = (M + BM - 1) / BM, gy = (a->Cout + BN - 1) / BN;
   const long tiles = (long)gx * gy;

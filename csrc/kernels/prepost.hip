@@ -147,7 +147,52 @@ __global__ void convex_upsample_kernel(const f16* __restrict__ mask, int mstride
   out[i] = sign * (float)f * num / den;
 }
 
+// multi-channel convex upsampling (CREStereo flow has x and y)
+__global__ void convex_upsample_c_kernel(const f16* __restrict__ mask, int mstride, const float* __restrict__ flow,
+                                         int fc, int B, int H, int W, int f, float sign, float* __restrict__ out,
+                                         int oc) {
+  const int Ho = H * f, Wo = W * f;
+  const long total = (long)B * Ho * Wo;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / ((long)Ho * Wo));
+    const long p = i - (long)b * Ho * Wo;
+    const int oy = (int)(p / Wo), ox = (int)(p % Wo);
+    const int h = oy / f, w = ox / f, fy = oy - h * f, fx = ox - w * f;
+    const long lp = ((long)b * H + h) * W + w;
+    const f16* m = mask + lp * mstride + fy * f + fx;
+    float mv[9], mx = -1e30f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      mv[k] = (float)m[k * f * f];
+      mx = fmaxf(mx, mv[k]);
+    }
+    float den = 0.f, num[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int yy = h + k / 3 - 1, xx = w + k % 3 - 1;
+      const float e = __expf(mv[k] - mx);
+      den += e;
+      if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+        const float* fv = flow + (((long)b * H + yy) * W + xx) * fc;
+        for (int c = 0; c < oc; ++c) num[c] += e * fv[c];
+      }
+    }
+    for (int c = 0; c < oc; ++c) out[i * oc + c] = sign * (float)f * num[c] / den;
+  }
+}
+
 }  // namespace
+
+extern "C" int sa_convex_upsample_c(const void* mask, int mask_stride, const float* flow, int fc, int B, int H,
+                                    int W, int factor, float sign, float* out, int oc, hipStream_t stream) {
+  if (oc < 1 || oc > 4 || oc > fc) return -2;
+  const long total = (long)B * H * W * factor * factor;
+  long g = (total + 255) / 256;
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL(convex_upsample_c_kernel, dim3((unsigned)g), dim3(256), 0, stream, (const f16*)mask,
+                     mask_stride, flow, fc, B, H, W, factor, sign, out, oc);
+  return (int)hipGetLastError();
+}
 
 extern "C" int sa_preprocess(const uint8_t* bgr, int B, int H, int W, int mode, void* out,
                              int out_stride, int c_off, int zero_to, hipStream_t stream) {

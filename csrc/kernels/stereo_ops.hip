@@ -1,0 +1,305 @@
+// Model-specific stereo kernels for CREStereo / Fast-ACVNet+ / HITNet (NHWC; fp16 features, fp32
+// flow / disparity state).
+//
+//   * sa_agcl_corr        — CREStereo Adaptive Group Correlation (4 channel groups x 9 taps, 1x9 or
+//                           3x3 window; "iter" mode warps the right features by the flow and takes
+//                           the window with replicate padding, "offset" mode samples the right
+//                           features at flow + window + learned offset with zero padding)
+//   * sa_linear_attention — LoFTR linear attention (ELU+1 kernel, KV/Ksum reduction per head staged
+//                           through LDS, fp32 math)
+//   * sa_layernorm        — row LayerNorm with optional residual add
+//   * sa_ew               — elementwise activation / scale / add of channel slices (+ broadcast
+//                           addend, e.g. a positional encoding)
+//   * sa_flow_features    — fp32 flow -> fp16 motion-encoder inputs (concat-free)
+//   * sa_interp_flow      — fp32 multi-channel bilinear resize (align_corners) with scale
+// Upstream ops: SURVEY.md §2.6 (grid_sample / local group correlation / linear attention rows).
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include "sa/kernels.h"
+
+namespace {
+typedef _Float16 f16;
+typedef f16 half8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float act_apply(float v, int act, float alpha) {
+  switch (act) {
+    case SA_ACT_RELU: return v > 0.f ? v : 0.f;
+    case SA_ACT_LEAKY: return v > 0.f ? v : v * alpha;
+    case SA_ACT_TANH: return tanhf(v);
+    case SA_ACT_SIGMOID: return 1.f / (1.f + __expf(-v));
+    default: return v;
+  }
+}
+
+inline int grid_for(long work, int block = 256) {
+  long g = (work + block - 1) / block;
+  if (g > 16384) g = 16384;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+// ------------------------------------------------------------------ AGCL correlation
+// one thread per (pixel, group, tap); the 64 channels of the group are read as 8 half8 vectors
+__global__ void agcl_kernel(const SaAgclArgs a) {
+  const int ntap = 9, G = 4;
+  const long total = (long)a.N * a.H * a.W * G * ntap;
+  const int Cg = a.C / G;
+  const int px = a.small_patch ? 3 : 9, py = a.small_patch ? 3 : 1;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int k = (int)(i % ntap);
+    const int g = (int)((i / ntap) % G);
+    const long pix = i / (ntap * G);
+    const int w = (int)(pix % a.W);
+    const int h = (int)((pix / a.W) % a.H);
+    const int n = (int)(pix / ((long)a.W * a.H));
+    const int dx = k % px - px / 2, dy = k / px - py / 2;
+    float sx, sy;
+    if (a.iter_mode) {
+      int hh = h + dy, ww = w + dx;
+      hh = hh < 0 ? 0 : (hh >= a.H ? a.H - 1 : hh);
+      ww = ww < 0 ? 0 : (ww >= a.W ? a.W - 1 : ww);
+      const float* f = a.flow + (((long)n * a.H + hh) * a.W + ww) * 2;
+      sx = (float)ww + f[0];
+      sy = (float)hh + f[1];
+    } else {
+      const float* f = a.flow + pix * 2;
+      sx = (float)w + f[0] + (float)dx;
+      sy = (float)h + f[1] + (float)dy;
+      if (a.offset) {
+        const f16* o = reinterpret_cast<const f16*>(a.offset) + pix * a.offset_stride + k * 2;
+        sx += (float)o[0];
+        sy += (float)o[1];
+      }
+    }
+    const float x0f = floorf(sx), y0f = floorf(sy);
+    const int x0 = (int)x0f, y0 = (int)y0f;
+    const float ax = sx - x0f, ay = sy - y0f;
+    const f16* lp = reinterpret_cast<const f16*>(a.f1) + pix * a.f1_stride + g * Cg;
+    float acc = 0.f;
+    const float wts[4] = {(1.f - ax) * (1.f - ay), ax * (1.f - ay), (1.f - ax) * ay, ax * ay};
+    const bool finite = isfinite(sx) && isfinite(sy);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int xx = x0 + (t & 1), yy = y0 + (t >> 1);
+      if (!finite || xx < 0 || xx >= a.W || yy < 0 || yy >= a.H || wts[t] == 0.f) continue;
+      const f16* rp = reinterpret_cast<const f16*>(a.f2) + (((long)n * a.H + yy) * a.W + xx) * a.f2_stride + g * Cg;
+      float s = 0.f;
+      for (int c = 0; c < Cg; c += 8) {
+        const half8 l8 = *reinterpret_cast<const half8*>(lp + c);
+        const half8 r8 = *reinterpret_cast<const half8*>(rp + c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += (float)l8[j] * (float)r8[j];
+      }
+      acc += wts[t] * s;
+    }
+    reinterpret_cast<f16*>(a.out)[pix * a.out_stride + g * ntap + k] = (f16)(acc / (float)Cg);
+  }
+}
+
+__global__ void zero_tail_kernel(f16* out, int stride, long P, int c0, int c1) {
+  const int n = c1 - c0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < P * n; i += (long)gridDim.x * blockDim.x)
+    out[(i / n) * stride + c0 + (int)(i % n)] = (f16)0.f;
+}
+
+// ------------------------------------------------------------------ linear attention
+// grid (N, heads); 256 threads.  Phase 1: KV[d][v] = sum_s phi(K)[s][d] V[s][v], Ksum[d] = sum_s
+// phi(K)[s][d] with 64-token tiles staged in LDS.  Phase 2: out[l][v] = sum_d phi(Q)[l][d] KV[d][v] /
+// (sum_d phi(Q)[l][d] Ksum[d] + eps).
+template <int D>
+__global__ void linear_attn_kernel(const f16* __restrict__ q, int qs, const f16* __restrict__ k, int ks,
+                                   const f16* __restrict__ v, int vs, f16* __restrict__ out, int os, int L, int S,
+                                   float eps) {
+  __shared__ float kt[64][D + 1];
+  __shared__ float vt[64][D + 1];
+  __shared__ float kv[D][D + 1];
+  __shared__ float ksum[D];
+  const int n = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
+  const int hoff = h * D;
+  constexpr int PAIRS = D * D / 256;  // (d, v) pairs per thread
+  float acc[PAIRS];
+  float ks_acc = 0.f;
+#pragma unroll
+  for (int j = 0; j < PAIRS; ++j) acc[j] = 0.f;
+  for (int s0 = 0; s0 < S; s0 += 64) {
+    for (int e = tid; e < 64 * D; e += 256) {
+      const int s = e / D, d = e % D;
+      float kk = 0.f, vv = 0.f;
+      if (s0 + s < S) {
+        const long row = (long)n * S + s0 + s;
+        kk = (float)k[row * ks + hoff + d];
+        kk = kk > 0.f ? kk + 1.f : __expf(kk);  // elu(x) + 1
+        vv = (float)v[row * vs + hoff + d];
+      }
+      kt[s][d] = kk;
+      vt[s][d] = vv;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PAIRS; ++j) {
+      const int pidx = tid + 256 * j;
+      const int d = pidx / D, vv = pidx % D;
+      float a = acc[j];
+      for (int s = 0; s < 64; ++s) a += kt[s][d] * vt[s][vv];
+      acc[j] = a;
+    }
+    if (tid < D)
+      for (int s = 0; s < 64; ++s) ks_acc += kt[s][tid];
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < PAIRS; ++j) {
+    const int pidx = tid + 256 * j;
+    kv[pidx / D][pidx % D] = acc[j];
+  }
+  if (tid < D) ksum[tid] = ks_acc;
+  __syncthreads();
+  // phase 2: each thread handles (token, v) outputs
+  for (long e = tid; e < (long)L * D; e += 256) {
+    const int l = (int)(e / D), vv = (int)(e % D);
+    const long row = (long)n * L + l;
+    float num = 0.f, den = 0.f;
+    for (int d = 0; d < D; ++d) {
+      float qq = (float)q[row * qs + hoff + d];
+      qq = qq > 0.f ? qq + 1.f : __expf(qq);
+      num += qq * kv[d][vv];
+      den += qq * ksum[d];
+    }
+    out[row * os + hoff + vv] = (f16)(num / (den + eps));
+  }
+}
+
+// ------------------------------------------------------------------ layer norm (+ residual)
+// one wave per row (C <= 512), fp32 statistics
+__global__ void layernorm_kernel(const f16* __restrict__ x, int xs, const float* __restrict__ gamma,
+                                 const float* __restrict__ beta, const f16* __restrict__ res, int rs,
+                                 f16* __restrict__ out, int os, long rows, int C, float eps) {
+  const int lane = threadIdx.x & 63;
+  const long row = blockIdx.x * (long)(blockDim.x / 64) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const f16* xp = x + row * xs;
+  float v[8];
+  int nv = 0;
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) {
+    v[nv] = (float)xp[c];
+    s += v[nv++];
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const float mean = s / C;
+  float q = 0.f;
+  for (int j = 0; j < nv; ++j) q += (v[j] - mean) * (v[j] - mean);
+  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+  const float rstd = rsqrtf(q / C + eps);
+  int j = 0;
+  for (int c = lane; c < C; c += 64, ++j) {
+    float y = (v[j] - mean) * rstd * gamma[c] + beta[c];
+    if (res) y += (float)res[row * rs + c];
+    out[row * os + c] = (f16)y;
+  }
+}
+
+// ------------------------------------------------------------------ elementwise
+__global__ void ew_kernel(const SaEwArgs a) {
+  const long total = a.P * a.C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long p = i / a.C;
+    const int c = (int)(i % a.C);
+    float v = (float)reinterpret_cast<const f16*>(a.x)[p * a.x_stride + c] * a.scale;
+    if (a.add) v += (float)reinterpret_cast<const f16*>(a.add)[p * a.add_stride + c];
+    if (a.bcast) v += a.bcast[(p % a.bcast_period) * a.C + c];
+    v = act_apply(v, a.act, 0.01f);
+    reinterpret_cast<f16*>(a.out)[p * a.out_stride + c] = (f16)v;
+  }
+}
+
+__global__ void flow_features_kernel(const float* __restrict__ flow, int fc, long P, f16* o1, int s1, int c1,
+                                     f16* o2, int s2) {
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
+    const float fx = flow[p * fc], fy = fc > 1 ? flow[p * fc + 1] : 0.f;
+    if (o1) {
+      f16* d = o1 + p * s1;
+      d[0] = (f16)fx;
+      d[1] = (f16)fy;
+      for (int c = 2; c < c1; ++c) d[c] = (f16)0.f;
+    }
+    if (o2) {
+      f16* d = o2 + p * s2;
+      d[0] = (f16)fx;
+      d[1] = (f16)fy;
+    }
+  }
+}
+
+__global__ void interp_flow_kernel(const float* __restrict__ x, float* __restrict__ out, int N, int H, int W,
+                                   int C, int Ho, int Wo, float mul) {
+  const long total = (long)N * Ho * Wo;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int ow = (int)(i % Wo);
+    const int oh = (int)((i / Wo) % Ho);
+    const int n = (int)(i / ((long)Wo * Ho));
+    const float sy = Ho > 1 ? (float)oh * (float)(H - 1) / (float)(Ho - 1) : 0.f;
+    const float sx = Wo > 1 ? (float)ow * (float)(W - 1) / (float)(Wo - 1) : 0.f;
+    int y0 = (int)floorf(sy), x0 = (int)floorf(sx);
+    y0 = y0 > H - 1 ? H - 1 : y0;
+    x0 = x0 > W - 1 ? W - 1 : x0;
+    const int y1 = y0 + 1 < H ? y0 + 1 : H - 1, x1 = x0 + 1 < W ? x0 + 1 : W - 1;
+    const float ly = sy - y0, lx = sx - x0;
+    for (int c = 0; c < C; ++c) {
+      auto at = [&](int y, int xx) { return x[(((long)n * H + y) * W + xx) * C + c]; };
+      const float v = (1.f - ly) * ((1.f - lx) * at(y0, x0) + lx * at(y0, x1)) + ly * ((1.f - lx) * at(y1, x0) + lx * at(y1, x1));
+      out[i * C + c] = mul * v;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int sa_agcl_corr(const SaAgclArgs* a, hipStream_t stream) {
+  if (a->C % 32 || a->out_channels < 36) return -2;
+  const long total = (long)a->N * a->H * a->W * 36;
+  hipLaunchKernelGGL(agcl_kernel, dim3(grid_for(total)), dim3(256), 0, stream, *a);
+  if (a->out_channels > 36) {
+    const long P = (long)a->N * a->H * a->W;
+    hipLaunchKernelGGL(zero_tail_kernel, dim3(grid_for(P * (a->out_channels - 36))), dim3(256), 0, stream,
+                       (f16*)a->out, a->out_stride, P, 36, a->out_channels);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_linear_attention(const void* q, int qs, const void* k, int ks, const void* v, int vs, void* out,
+                                   int os, int N, int L, int S, int heads, int dim, float eps, hipStream_t stream) {
+  if (dim != 32) return -2;
+  hipLaunchKernelGGL(linear_attn_kernel<32>, dim3(N, heads), dim3(256), 0, stream, (const f16*)q, qs, (const f16*)k,
+                     ks, (const f16*)v, vs, (f16*)out, os, L, S, eps);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_layernorm(const void* x, int xs, const float* gamma, const float* beta, const void* res, int rs,
+                            void* out, int os, long rows, int C, float eps, hipStream_t stream) {
+  if (C > 512) return -2;
+  const long blocks = (rows + 3) / 4;
+  hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (const f16*)x, xs, gamma, beta,
+                     (const f16*)res, rs, (f16*)out, os, rows, C, eps);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_ew(const SaEwArgs* a, hipStream_t stream) {
+  hipLaunchKernelGGL(ew_kernel, dim3(grid_for(a->P * a->C)), dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_flow_features(const float* flow, int fc, long P, void* out1, int s1, int c1, void* out2, int s2,
+                                hipStream_t stream) {
+  hipLaunchKernelGGL(flow_features_kernel, dim3(grid_for(P)), dim3(256), 0, stream, flow, fc, P, (f16*)out1, s1, c1,
+                     (f16*)out2, s2);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_interp_flow(const float* x, float* out, int N, int H, int W, int C, int Ho, int Wo, float mul,
+                              hipStream_t stream) {
+  hipLaunchKernelGGL(interp_flow_kernel, dim3(grid_for((long)N * Ho * Wo)), dim3(256), 0, stream, x, out, N, H, W, C,
+                     Ho, Wo, mul);
+  return (int)hipGetLastError();
+}

@@ -93,4 +93,47 @@ void ResBlock::run(hipStream_t s, const StatsPool& sp, const Tensor& x) const {
   }
 }
 
+void Trunk::build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std::string& p, Norm nrm, int N, int H,
+                  int W, int s1, const int strides[3]) {
+  norm = nrm;
+  src.conv(p + ".conv1", 64, 3, 7, 7);
+  if (norm == Norm::Batch) src.bn(p + ".norm1", 64);
+  ConvSpec sp7;
+  sp7.sh = sp7.sw = s1;
+  conv1.build(a, *src.ws, {p + ".conv1"}, {{3, 8}}, sp7,
+              norm == Norm::Batch ? std::vector<std::string>{p + ".norm1"} : std::vector<std::string>{});
+  int h = conv1.out_h(H), w = conv1.out_w(W);
+  if (norm == Norm::Instance) {
+    c1y = make_tensor(a, N, h, w, 64);
+    c1st = sp.take(N, 64);
+  }
+  c1a = make_tensor(a, N, h, w, 64);
+  const int dims[3] = {64, 96, 128};
+  int inp = 64;
+  layers.resize(6);
+  for (int l = 0; l < 3; ++l)
+    for (int b = 0; b < 2; ++b) {
+      ResBlock& rb = layers[l * 2 + b];
+      rb.build(a, src, sp, p + ".layer" + std::to_string(l + 1) + "." + std::to_string(b), inp, dims[l],
+               b == 0 ? strides[l] : 1, norm, N, h, w);
+      h = rb.out.h;
+      w = rb.out.w;
+      inp = dims[l];
+    }
+}
+
+void Trunk::run(hipStream_t s, const StatsPool& sp, const Tensor& img) const {
+  if (norm == Norm::Instance) {
+    conv1.run(s, {img}, c1y, SA_ACT_NONE, nullptr, SA_ACT_NONE, sp.resolve(c1st));
+    instnorm(s, c1y, sp.resolve(c1st), c1a, SA_ACT_RELU);
+  } else {
+    conv1.run(s, {img}, c1a, SA_ACT_RELU);
+  }
+  const Tensor* x = &c1a;
+  for (const auto& rb : layers) {
+    rb.run(s, sp, *x);
+    x = &rb.out;
+  }
+}
+
 }  // namespace sa

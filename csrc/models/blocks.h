@@ -51,6 +51,21 @@ struct ResBlock {
   void run(hipStream_t s, const StatsPool& sp, const Tensor& x) const;
 };
 
+// BasicEncoder / MultiBasicEncoder trunk shared by RAFT-Stereo and CREStereo (upstream
+// core/extractor.py): conv1 7x7 (stride s1) + norm + ReLU, then layer1..3 of two residual
+// blocks each (dims 64/96/128, first block of each layer strided).
+struct Trunk {
+  ConvLayer conv1;
+  Norm norm = Norm::None;
+  Tensor c1y, c1a;
+  sa_stat_t* c1st = nullptr;
+  std::vector<ResBlock> layers;
+  void build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std::string& prefix, Norm norm, int N, int H,
+             int W, int conv1_stride, const int strides[3]);
+  void run(hipStream_t s, const StatsPool& sp, const Tensor& img) const;
+  const Tensor& out() const { return layers.back().out; }
+};
+
 // norm apply helper
 void instnorm(hipStream_t s, const Tensor& x, const sa_stat_t* stats, const Tensor& out, int act,
               const Tensor* res = nullptr, const sa_stat_t* res_stats = nullptr, int act2 = SA_ACT_NONE);

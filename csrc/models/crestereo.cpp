@@ -1,0 +1,386 @@
+// CREStereo (presets crestereo-iter2 / -iter5 / -iter10) as a native op graph.
+//
+// Reference pins: inputs left/right [1,3,480,640] RGB 0..255, output [1,2,H,W]
+// whose channel 0 is the positive disparity (CREStereo/src/TRTCREStereo.cpp:15-18,130-137); exported
+// "init" variants with 2 / 5 / 10 refinement iterations (README_en.md:222,244-246).  The network
+// follows upstream CREStereo (weight names identical to the PyTorch oracle
+// stereoalgorithms_amd/models/crestereo.py):
+//   preprocess (2x/255-1) -> BasicEncoder (instance norm, 1/4, 256 ch) on both images (batched)
+//   -> net = tanh / inp = relu split -> 1/8 and 1/16 avg-pooled pyramids
+//   -> 1/16: sine PE + LoFTR linear-attention self layer, cross layer (computed once: the AGCL
+//      attention input never changes between iterations)
+//   -> cascade 1/16 (iters/2) -> 1/8 (iters/2) -> 1/4 (iters): AGCL correlation (1x9 / 3x3
+//      alternating, learned offsets on the coarse levels), motion encoder, SepConvGRU (1x5 then 5x1,
+//      gates fused into the conv epilogues), flow head accumulating into the fp32 flow state; the
+//      mask head and convex upsampling run only on each stage's last iteration
+//   -> disparity = -convex_upsample(flow)[x] (the reference reads channel 0 of -flow_up).
+// The whole frame is one hipGraph (base class).
+#include <cmath>
+
+#include "blocks.h"
+
+namespace sa {
+namespace {
+
+int preset_iters(const std::string& name) {
+  if (name == "crestereo-iter2") return 2;
+  if (name == "crestereo-iter5" || name == "crestereo") return 5;
+  if (name == "crestereo-iter10") return 10;
+  throw Error("unknown CREStereo preset " + name);
+}
+
+// nn.Linear [out, in] -> conv weight [out, in, 1, 1] under "<name>.weight" (reshape in place)
+void linear_as_conv(WeightSource& src, const std::string& name, int out, int in) {
+  src.linear(name, out, in, false);
+  HostTensor t = src.ws->get(name + ".weight");
+  if (t.shape.size() == 2) {
+    t.shape = {out, in, 1, 1};
+    src.ws->put(name + ".weight", std::move(t));
+  }
+}
+
+struct AttnLayer {
+  ConvLayer q, kv, merge, mlp0, mlp2;
+  float *n1g = nullptr, *n1b = nullptr, *n2g = nullptr, *n2b = nullptr;
+  Tensor qb, kvb, att, m2, cat, h1, h2;
+  int N = 0, L = 0;
+  void build(DeviceArena& a, WeightSource& src, const std::string& p, int N_, int L_) {
+    N = N_;
+    L = L_;
+    for (const char* n : {"q_proj", "k_proj", "v_proj", "merge"}) linear_as_conv(src, p + "." + n, 256, 256);
+    linear_as_conv(src, p + ".mlp.0", 512, 512);
+    linear_as_conv(src, p + ".mlp.2", 256, 512);
+    src.ln(p + ".norm1", 256);
+    src.ln(p + ".norm2", 256);
+    const WeightStore& ws = *src.ws;
+    ConvSpec s1;
+    s1.kh = s1.kw = 1;
+    q.build(a, ws, {p + ".q_proj"}, {{256, 256}}, s1);
+    kv.build(a, ws, {p + ".k_proj", p + ".v_proj"}, {{256, 256}}, s1);
+    merge.build(a, ws, {p + ".merge"}, {{256, 256}}, s1);
+    mlp0.build(a, ws, {p + ".mlp.0"}, {{256, 256}, {256, 256}}, s1);
+    mlp2.build(a, ws, {p + ".mlp.2"}, {{512, 512}}, s1);
+    auto up = [&](const std::string& n) {
+      const auto& v = ws.get(n).data;
+      float* d = (float*)a.alloc(v.size() * 4);
+      HIP_CHECK(hipMemcpy(d, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+      return d;
+    };
+    n1g = up(p + ".norm1.weight");
+    n1b = up(p + ".norm1.bias");
+    n2g = up(p + ".norm2.weight");
+    n2b = up(p + ".norm2.bias");
+    qb = make_tensor(a, N, 1, L, 256);
+    kvb = make_tensor(a, N, 1, L, 512);
+    att = make_tensor(a, N, 1, L, 256);
+    m2 = make_tensor(a, N, 1, L, 256);
+    cat = make_tensor(a, N, 1, L, 256);  // normalised message (concat partner of x)
+    h1 = make_tensor(a, N, 1, L, 512);
+    h2 = make_tensor(a, N, 1, L, 256);
+  }
+  // out = x + norm2(mlp([x, norm1(merge(attn(q(x), k(src), v(src))))])); x/src/out: [N][1][L][256]
+  void run(hipStream_t s, const Tensor& x, const Tensor& source, const Tensor& out) const {
+    q.run(s, {x}, qb);
+    kv.run(s, {source}, kvb);
+    int rc = sa_linear_attention(qb.ptr, qb.stride, kvb.ptr, kvb.stride, kvb.slice_c(256, 256).ptr, kvb.stride,
+                                 att.ptr, att.stride, N, L, L, 8, 32, 1e-6f, s);
+    SA_REQUIRE(rc == 0, "linear attention failed");
+    merge.run(s, {att}, m2);
+    rc = sa_layernorm(m2.ptr, m2.stride, n1g, n1b, nullptr, 0, cat.ptr, cat.stride, (long)N * L, 256, 1e-5f, s);
+    SA_REQUIRE(rc == 0, "layernorm failed");
+    mlp0.run(s, {x, cat}, h1, SA_ACT_RELU);
+    mlp2.run(s, {h1}, h2);
+    rc = sa_layernorm(h2.ptr, h2.stride, n2g, n2b, x.ptr, x.stride, out.ptr, out.stride, (long)N * L, 256, 1e-5f, s);
+    SA_REQUIRE(rc == 0, "layernorm failed");
+  }
+};
+
+// per-resolution state of the cascaded update
+struct Level {
+  int h = 0, w = 0;
+  Tensor net, xin, corr, cor1, corflo, flo1, flowfeat, z, rh, fh, mask;
+  float* flow = nullptr;
+  void build(DeviceArena& a, int B, int h_, int w_) {
+    h = h_;
+    w = w_;
+    net = make_tensor(a, B, h, w, 128);
+    xin = make_tensor(a, B, h, w, 256);  // [inp 128 | motion 126 | flow 2]
+    corr = make_tensor(a, B, h, w, 40);
+    cor1 = make_tensor(a, B, h, w, 256);
+    corflo = make_tensor(a, B, h, w, 256);  // [cor 192 | flo 64]
+    flo1 = make_tensor(a, B, h, w, 128);
+    flowfeat = make_tensor(a, B, h, w, 8);
+    z = make_tensor(a, B, h, w, 128);
+    rh = make_tensor(a, B, h, w, 128);
+    fh = make_tensor(a, B, h, w, 512);
+    mask = make_tensor(a, B, h, w, 144);
+    flow = (float*)a.alloc((size_t)B * h * w * 2 * 4);
+  }
+};
+
+class CreStereo : public StereoEngine {
+ public:
+  explicit CreStereo(const EngineConfig& cfg) : StereoEngine(cfg), iters_(preset_iters(cfg.model)) {
+    if (cfg.iters > 0) iters_ = cfg.iters;
+  }
+  const char* name() const override { return "CREStereo"; }
+
+ protected:
+  void build(WeightSource& src) override;
+  void forward(hipStream_t s) override;
+
+ private:
+  void update(hipStream_t s, Level& L, const Tensor& f1, const Tensor& f2, const Tensor* offset, bool small_patch,
+              bool iter_mode, bool want_mask) const;
+
+  int iters_;
+  StatsPool sp_;
+  Tensor img_, fmap_, fmap8_, fmap16_, pe16_, tok_, selfo_, cross1_, cross2_, off8_, off16_;
+  Trunk fnet_;
+  ConvLayer fconv2_, offc8_, offc16_;
+  AttnLayer self_, cross_;
+  ConvLayer convc1_, convc2_, convf1_, convf2_, mconv_, zr_[2], q_[2], fh1_, fh1mask_, fh2_, mask2_;
+  Level lv_[3];  // 0: 1/4, 1: 1/8, 2: 1/16
+  float *flowup4_ = nullptr, *flowup2_ = nullptr, *pe_ = nullptr;
+};
+
+void CreStereo::build(WeightSource& src) {
+  DeviceArena& a = arena_;
+  const int B = this->B();
+  SA_REQUIRE(H() % 16 == 0 && W() % 16 == 0, "CREStereo needs H, W multiples of 16");
+  img_ = make_tensor(a, 2 * B, H(), W(), 8);
+  const int strides[3] = {1, 2, 1};
+  fnet_.build(a, src, sp_, "fnet", Norm::Instance, 2 * B, H(), W(), 2, strides);
+  const int h4 = fnet_.out().h, w4 = fnet_.out().w;
+  src.conv("fnet.conv2", 256, 128, 1, 1);
+  ConvSpec s1, s3;
+  s1.kh = s1.kw = 1;
+  fconv2_.build(a, *src.ws, {"fnet.conv2"}, {{128, 128}}, s1);
+  fmap_ = make_tensor(a, 2 * B, h4, w4, 256);
+  fmap8_ = make_tensor(a, 2 * B, h4 / 2, w4 / 2, 256);
+  fmap16_ = make_tensor(a, 2 * B, h4 / 4, w4 / 4, 256);
+  const int h16 = h4 / 4, w16 = w4 / 4, L = h16 * w16;
+  // offsets: range * (sigmoid(o) - 0.5) * 2 == tanh(o / 2)  (range_8 = range_16 = 1)
+  src.conv("conv_offset_8", 18, 256, 3, 3);
+  src.conv("conv_offset_16", 18, 256, 3, 3);
+  offc8_.build(a, *src.ws, {"conv_offset_8"}, {{256, 256}}, s3, {}, 0.5f);
+  offc16_.build(a, *src.ws, {"conv_offset_16"}, {{256, 256}}, s3, {}, 0.5f);
+  off8_ = make_tensor(a, B, h4 / 2, w4 / 2, 24);
+  off16_ = make_tensor(a, B, h16, w16, 24);
+  // sine position encoding (CREStereo frequency quirk: div_term = exp(-[0, 2, 4, ...]))
+  {
+    std::vector<float> pe((size_t)L * 256);
+    for (int y = 0; y < h16; ++y)
+      for (int x = 0; x < w16; ++x)
+        for (int i = 0; i < 64; ++i) {
+          const float div = std::exp(-(float)(2 * i));
+          float* p = &pe[((size_t)y * w16 + x) * 256];
+          p[4 * i + 0] = std::sin((float)(x + 1) * div);
+          p[4 * i + 1] = std::cos((float)(x + 1) * div);
+          p[4 * i + 2] = std::sin((float)(y + 1) * div);
+          p[4 * i + 3] = std::cos((float)(y + 1) * div);
+        }
+    pe_ = (float*)a.alloc(pe.size() * 4);
+    HIP_CHECK(hipMemcpy(pe_, pe.data(), pe.size() * 4, hipMemcpyHostToDevice));
+  }
+  tok_ = make_tensor(a, 2 * B, 1, L, 256);
+  selfo_ = make_tensor(a, 2 * B, 1, L, 256);
+  cross1_ = make_tensor(a, B, 1, L, 256);
+  cross2_ = make_tensor(a, B, 1, L, 256);
+  self_.build(a, src, "self_att_fn.layers.0", 2 * B, L);
+  cross_.build(a, src, "cross_att_fn.layers.0", B, L);
+
+  // update block (shared by all three levels)
+  const std::string u = "update_block.";
+  src.conv(u + "encoder.convc1", 256, 36, 1, 1);
+  src.conv(u + "encoder.convc2", 192, 256, 3, 3);
+  src.conv(u + "encoder.convf1", 128, 2, 7, 7);
+  src.conv(u + "encoder.convf2", 64, 128, 3, 3);
+  src.conv(u + "encoder.conv", 126, 256, 3, 3);
+  const WeightStore& ws = *src.ws;
+  convc1_.build(a, ws, {u + "encoder.convc1"}, {{36, 40}}, s1);
+  convc2_.build(a, ws, {u + "encoder.convc2"}, {{256, 256}}, s3);
+  convf1_.build(a, ws, {u + "encoder.convf1"}, {{2, 8}}, s3);
+  convf2_.build(a, ws, {u + "encoder.convf2"}, {{128, 128}}, s3);
+  mconv_.build(a, ws, {u + "encoder.conv"}, {{256, 256}}, s3);
+  for (int d = 0; d < 2; ++d) {
+    const std::string sfx = d == 0 ? "1" : "2";
+    for (const char* g : {"convz", "convr", "convq"})
+      src.conv(u + "gru." + g + sfx, 128, 384, d == 0 ? 1 : 5, d == 0 ? 5 : 1);
+    ConvSpec sp;  // (1,5) pad (0,2) / (5,1) pad (2,0)
+    zr_[d].build(a, ws, {u + "gru.convz" + sfx, u + "gru.convr" + sfx}, {{128, 128}, {256, 256}}, sp);
+    q_[d].build(a, ws, {u + "gru.convq" + sfx}, {{128, 128}, {256, 256}}, sp);
+  }
+  src.conv(u + "flow_head.conv1", 256, 128, 3, 3);
+  src.conv(u + "flow_head.conv2", 2, 256, 3, 3);
+  src.conv(u + "mask.0", 256, 128, 3, 3);
+  src.conv(u + "mask.2", 144, 256, 1, 1);
+  fh1_.build(a, ws, {u + "flow_head.conv1"}, {{128, 128}}, s3);
+  fh1mask_.build(a, ws, {u + "flow_head.conv1", u + "mask.0"}, {{128, 128}}, s3);
+  fh2_.build(a, ws, {u + "flow_head.conv2"}, {{256, 256}}, s3);
+  mask2_.build(a, ws, {u + "mask.2"}, {{256, 256}}, s1, {}, 0.25f);
+
+  lv_[0].build(a, B, h4, w4);
+  lv_[1].build(a, B, h4 / 2, w4 / 2);
+  lv_[2].build(a, B, h16, w16);
+  flowup4_ = (float*)a.alloc((size_t)B * h4 * w4 * 2 * 4);
+  flowup2_ = (float*)a.alloc((size_t)B * (h4 * 2) * (w4 * 2) * 2 * 4);
+  sp_.finalize(a);
+}
+
+static void check(int rc, const char* what) { SA_REQUIRE(rc == 0, "%s failed (rc=%d)", what, rc); }
+
+void CreStereo::update(hipStream_t s, Level& L, const Tensor& f1, const Tensor& f2, const Tensor* offset,
+                       bool small_patch, bool iter_mode, bool want_mask) const {
+  const int B = this->B();
+  SaAgclArgs ag{};
+  ag.f1 = f1.ptr;
+  ag.f1_stride = f1.stride;
+  ag.f2 = f2.ptr;
+  ag.f2_stride = f2.stride;
+  ag.flow = L.flow;
+  ag.offset = offset ? offset->ptr : nullptr;
+  ag.offset_stride = offset ? offset->stride : 0;
+  ag.N = B;
+  ag.H = L.h;
+  ag.W = L.w;
+  ag.C = 256;
+  ag.small_patch = small_patch;
+  ag.iter_mode = iter_mode;
+  ag.out = L.corr.ptr;
+  ag.out_stride = L.corr.stride;
+  ag.out_channels = L.corr.c;
+  check(sa_agcl_corr(&ag, s), "agcl");
+  const long P = (long)B * L.h * L.w;
+  check(sa_flow_features(L.flow, 2, P, L.flowfeat.ptr, L.flowfeat.stride, 8, L.xin.slice_c(254, 2).ptr,
+                         L.xin.stride, s),
+        "flow features");
+  // motion encoder -> xin[128:254]
+  convc1_.run(s, {L.corr}, L.cor1, SA_ACT_RELU);
+  convc2_.run(s, {L.cor1}, L.corflo.slice_c(0, 192), SA_ACT_RELU);
+  convf1_.run(s, {L.flowfeat}, L.flo1, SA_ACT_RELU);
+  convf2_.run(s, {L.flo1}, L.corflo.slice_c(192, 64), SA_ACT_RELU);
+  mconv_.run(s, {L.corflo}, L.xin.slice_c(128, 126), SA_ACT_RELU);
+  // SepConvGRU: horizontal then vertical; z/r and q gates fused into the conv epilogues
+  for (int d = 0; d < 2; ++d) {
+    SaConvArgs za = zr_[d].args({L.net, L.xin}, L.z);
+    za.epi = SA_EPI_GRU_ZR;
+    za.aux = L.z.ptr;
+    za.aux_stride = L.z.stride;
+    za.hbuf = L.net.ptr;
+    za.h_stride = L.net.stride;
+    za.rh = L.rh.ptr;
+    za.rh_stride = L.rh.stride;
+    zr_[d].launch(s, za);
+    SaConvArgs qa = q_[d].args({L.rh, L.xin}, L.net);
+    qa.epi = SA_EPI_GRU_Q;
+    qa.aux = L.z.ptr;
+    qa.aux_stride = L.z.stride;
+    qa.hbuf = L.net.ptr;
+    qa.h_stride = L.net.stride;
+    q_[d].launch(s, qa);
+  }
+  if (want_mask) fh1mask_.run(s, {L.net}, L.fh, SA_ACT_RELU);
+  else fh1_.run(s, {L.net}, L.fh.slice_c(0, 256), SA_ACT_RELU);
+  SaConvArgs fa = fh2_.args({L.fh.slice_c(0, 256)}, Tensor{L.flow, B, L.h, L.w, 2, 2, DT::F32});
+  fa.epi = SA_EPI_FLOW_ACC;
+  fh2_.launch(s, fa);
+  if (want_mask) mask2_.run(s, {L.fh.slice_c(256, 256)}, L.mask);
+}
+
+void CreStereo::forward(hipStream_t s) {
+  const int B = this->B();
+  sp_.zero(s);
+  check(sa_preprocess(in_left_, B, H(), W(), SA_PRE_SIGNED, img_.ptr, 8, 0, 8, s), "preprocess");
+  check(sa_preprocess(in_right_, B, H(), W(), SA_PRE_SIGNED, img_.slice_n(B, B).ptr, 8, 0, 8, s), "preprocess");
+  fnet_.run(s, sp_, img_);
+  fconv2_.run(s, {fnet_.out()}, fmap_);
+  Level &L4 = lv_[0], &L8 = lv_[1], &L16 = lv_[2];
+  const int h4 = L4.h, w4 = L4.w;
+  check(sa_avgpool_k(fmap_.ptr, 256, fmap8_.ptr, 256, 2 * B, h4, w4, 256, 2, s), "pool8");
+  check(sa_avgpool_k(fmap_.ptr, 256, fmap16_.ptr, 256, 2 * B, h4, w4, 256, 4, s), "pool16");
+  offc8_.run(s, {fmap8_.slice_n(0, B)}, off8_, SA_ACT_TANH);
+  offc16_.run(s, {fmap16_.slice_n(0, B)}, off16_, SA_ACT_TANH);
+  // net = tanh(fmap1[:128]), inp = relu(fmap1[128:]) at 1/4, pooled to 1/8 and 1/16
+  {
+    SaEwArgs e{};
+    e.x = fmap_.ptr;
+    e.x_stride = 256;
+    e.out = L4.net.ptr;
+    e.out_stride = L4.net.stride;
+    e.P = (long)B * h4 * w4;
+    e.C = 128;
+    e.act = SA_ACT_TANH;
+    e.scale = 1.f;
+    check(sa_ew(&e, s), "tanh");
+    e.x = fmap_.slice_c(128, 128).ptr;
+    e.out = L4.xin.ptr;
+    e.out_stride = L4.xin.stride;
+    e.act = SA_ACT_RELU;
+    check(sa_ew(&e, s), "relu");
+  }
+  for (int l = 1; l < 3; ++l) {
+    const int k = l == 1 ? 2 : 4;
+    check(sa_avgpool_k(L4.net.ptr, L4.net.stride, lv_[l].net.ptr, lv_[l].net.stride, B, h4, w4, 128, k, s), "pool");
+    check(sa_avgpool_k(L4.xin.ptr, L4.xin.stride, lv_[l].xin.ptr, lv_[l].xin.stride, B, h4, w4, 128, k, s), "pool");
+  }
+  // 1/16 tokens: pooled features + position encoding -> self attention (both images batched) ->
+  // cross attention (left attends to right, then right to the updated left)
+  {
+    const int L = L16.h * L16.w;
+    SaEwArgs e{};
+    e.x = fmap16_.ptr;
+    e.x_stride = 256;
+    e.bcast = pe_;
+    e.bcast_period = L;
+    e.out = tok_.ptr;
+    e.out_stride = 256;
+    e.P = (long)2 * B * L;
+    e.C = 256;
+    e.act = SA_ACT_NONE;
+    e.scale = 1.f;
+    check(sa_ew(&e, s), "pos enc");
+    self_.run(s, tok_, tok_, selfo_);
+    cross_.run(s, selfo_.slice_n(0, B), selfo_.slice_n(B, B), cross1_);
+    cross_.run(s, selfo_.slice_n(B, B), cross1_, cross2_);
+  }
+  const Tensor c16l{cross1_.ptr, B, L16.h, L16.w, 256, 256, DT::F16};
+  const Tensor c16r{cross2_.ptr, B, L16.h, L16.w, 256, 256, DT::F16};
+
+  // RUM 1/16
+  HIP_CHECK(hipMemsetAsync(L16.flow, 0, (size_t)B * L16.h * L16.w * 2 * 4, s));
+  const int n_coarse = iters_ / 2;
+  for (int it = 0; it < n_coarse; ++it)
+    update(s, L16, c16l, c16r, &off16_, it % 2 == 1, false, it == n_coarse - 1);
+  if (n_coarse > 0) {
+    check(sa_convex_upsample_c(L16.mask.ptr, L16.mask.stride, L16.flow, 2, B, L16.h, L16.w, 4, 1.f, flowup4_, 2, s),
+          "convex16");
+  } else {
+    HIP_CHECK(hipMemsetAsync(flowup4_, 0, (size_t)B * h4 * w4 * 2 * 4, s));
+  }
+  check(sa_interp_flow(flowup4_, L8.flow, B, h4, w4, 2, L8.h, L8.w, -(float)L8.h / (float)h4, s), "interp8");
+  // RUM 1/8
+  for (int it = 0; it < n_coarse; ++it)
+    update(s, L8, fmap8_.slice_n(0, B), fmap8_.slice_n(B, B), &off8_, it % 2 == 1, false, it == n_coarse - 1);
+  const int h2 = 4 * L8.h, w2 = 4 * L8.w;
+  if (n_coarse > 0) {
+    check(sa_convex_upsample_c(L8.mask.ptr, L8.mask.stride, L8.flow, 2, B, L8.h, L8.w, 4, 1.f, flowup2_, 2, s),
+          "convex8");
+    check(sa_interp_flow(flowup2_, L4.flow, B, h2, w2, 2, h4, w4, -(float)h4 / (float)h2, s), "interp4");
+  } else {
+    check(sa_interp_flow(L8.flow, L4.flow, B, L8.h, L8.w, 2, h4, w4, -(float)h4 / (float)L8.h, s), "interp4");
+  }
+  // RUM 1/4
+  for (int it = 0; it < iters_; ++it)
+    update(s, L4, fmap_.slice_n(0, B), fmap_.slice_n(B, B), nullptr, it % 2 == 1, true, it == iters_ - 1);
+  // disparity = channel 0 of -convex_upsample(flow)
+  check(sa_convex_upsample_c(L4.mask.ptr, L4.mask.stride, L4.flow, 2, B, h4, w4, 4, -1.f, disp_, 1, s), "convex4");
+}
+
+}  // namespace
+
+std::unique_ptr<StereoEngine> make_crestereo(const EngineConfig& cfg) {
+  return std::unique_ptr<StereoEngine>(new CreStereo(cfg));
+}
+
+}  // namespace sa

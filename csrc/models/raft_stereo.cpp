@@ -69,21 +69,12 @@ class RaftStereo : public StereoEngine {
   void forward(hipStream_t s) override;
 
  private:
-  struct Encoder {  // BasicEncoder / MultiBasicEncoder trunk (conv1 + layer1..3)
-    ConvLayer conv1;
-    Norm norm;
-    Tensor c1y, c1a;
-    sa_stat_t* c1st = nullptr;
-    std::vector<ResBlock> layers;  // layer1..3 (2 blocks each)
-  };
-  void build_trunk(Encoder& e, WeightSource& src, const std::string& p, Norm norm, int N);
-  void run_trunk(hipStream_t s, const Encoder& e, const Tensor& img) const;
   void gru(hipStream_t s, int lvl, const std::vector<Tensor>& x) const;
 
   RaftCfg rc_;
   StatsPool sp_;
   Tensor img_;  // [2B][H][W][8] preprocessed
-  Encoder fnet_, cnet_;
+  Trunk fnet_, cnet_;
   ConvLayer fconv2_;          // fnet.conv2 (1x1 128->256) (non-shared)
   ResBlock shared_rb_;        // conv2.0 (shared backbone)
   ConvLayer shared_conv_;     // conv2.1
@@ -107,53 +98,6 @@ class RaftStereo : public StereoEngine {
   int lh_[3], lw_[3];
 };
 
-void RaftStereo::build_trunk(Encoder& e, WeightSource& src, const std::string& p, Norm norm, int N) {
-  DeviceArena& a = arena_;
-  e.norm = norm;
-  const int s1 = 1 + (rc_.n_downsample > 2);
-  src.conv(p + ".conv1", 64, 3, 7, 7);
-  if (norm == Norm::Batch) src.bn(p + ".norm1", 64);
-  ConvSpec sp7;
-  sp7.sh = sp7.sw = s1;
-  e.conv1.build(a, *src.ws, {p + ".conv1"}, {{3, 8}}, sp7,
-                norm == Norm::Batch ? std::vector<std::string>{p + ".norm1"} : std::vector<std::string>{});
-  int h = conv_out(H(), 7, s1, 3), w = conv_out(W(), 7, s1, 3);
-  if (norm == Norm::Instance) {
-    e.c1y = make_tensor(a, N, h, w, 64);
-    e.c1st = sp_.take(N, 64);
-  }
-  e.c1a = make_tensor(a, N, h, w, 64);
-  const int dims[3] = {64, 96, 128};
-  const int strides[3] = {1, 1 + (rc_.n_downsample > 1), 1 + (rc_.n_downsample > 0)};
-  int inp = 64;
-  e.layers.resize(6);
-  for (int l = 0; l < 3; ++l) {
-    for (int b = 0; b < 2; ++b) {
-      ResBlock& rb = e.layers[l * 2 + b];
-      int st = b == 0 ? strides[l] : 1;
-      rb.build(a, src, sp_, p + ".layer" + std::to_string(l + 1) + "." + std::to_string(b), inp,
-               dims[l], st, norm, N, h, w);
-      h = rb.out.h;
-      w = rb.out.w;
-      inp = dims[l];
-    }
-  }
-}
-
-void RaftStereo::run_trunk(hipStream_t s, const Encoder& e, const Tensor& img) const {
-  if (e.norm == Norm::Instance) {
-    e.conv1.run(s, {img}, e.c1y, SA_ACT_NONE, nullptr, SA_ACT_NONE, sp_.resolve(e.c1st));
-    instnorm(s, e.c1y, sp_.resolve(e.c1st), e.c1a, SA_ACT_RELU);
-  } else {
-    e.conv1.run(s, {img}, e.c1a, SA_ACT_RELU);
-  }
-  const Tensor* x = &e.c1a;
-  for (const auto& rb : e.layers) {
-    rb.run(s, sp_, *x);
-    x = &rb.out;
-  }
-}
-
 void RaftStereo::build(WeightSource& src) {
   DeviceArena& a = arena_;
   const int Bn = B();
@@ -161,11 +105,14 @@ void RaftStereo::build(WeightSource& src) {
   img_ = make_tensor(a, 2 * Bn, H(), W(), 8);
 
   // ---------------- encoders ----------------
-  build_trunk(cnet_, src, "cnet", rc_.context_norm, rc_.shared ? 2 * Bn : Bn);
-  lh_[0] = cnet_.layers.back().out.h;
-  lw_[0] = cnet_.layers.back().out.w;
+  // conv1 stride 1 + (n_downsample > 2); layer strides 1, 1 + (n_downsample > 1), 1 + (n_downsample > 0)
+  const int c1s = 1 + (rc_.n_downsample > 2);
+  const int strides[3] = {1, 1 + (rc_.n_downsample > 1), 1 + (rc_.n_downsample > 0)};
+  cnet_.build(a, src, sp_, "cnet", rc_.context_norm, rc_.shared ? 2 * Bn : Bn, H(), W(), c1s, strides);
+  lh_[0] = cnet_.out().h;
+  lw_[0] = cnet_.out().w;
   if (!rc_.shared) {
-    build_trunk(fnet_, src, "fnet", Norm::Instance, 2 * Bn);
+    fnet_.build(a, src, sp_, "fnet", Norm::Instance, 2 * Bn, H(), W(), c1s, strides);
     src.conv("fnet.conv2", 256, 128, 1, 1);
     ConvSpec s1;
     fconv2_.build(a, *src.ws, {"fnet.conv2"}, {{128, 128}}, s1);
@@ -342,16 +289,16 @@ void RaftStereo::forward(hipStream_t s) {
 
   // encoders
   if (rc_.shared) {
-    run_trunk(s, cnet_, img_);
-    const Tensor& v = cnet_.layers.back().out;
+    cnet_.run(s, sp_, img_);
+    const Tensor& v = cnet_.out();
     shared_rb_.run(s, sp_, v);
     shared_conv_.run(s, {shared_rb_.out}, fmap_);
   } else {
-    run_trunk(s, cnet_, img_.slice_n(0, Bn));
-    run_trunk(s, fnet_, img_);
-    fconv2_.run(s, {fnet_.layers.back().out}, fmap_);
+    cnet_.run(s, sp_, img_.slice_n(0, Bn));
+    fnet_.run(s, sp_, img_);
+    fconv2_.run(s, {fnet_.out()}, fmap_);
   }
-  Tensor x = cnet_.layers.back().out.slice_n(0, Bn);
+  Tensor x = cnet_.out().slice_n(0, Bn);
   Tensor lvl_in[3];
   lvl_in[0] = x;
   if (rc_.n_gru >= 2) {

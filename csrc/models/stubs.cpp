@@ -2,11 +2,6 @@
 #include "sa/engine.h"
 
 namespace sa {
-#ifndef SA_HAVE_CRESTEREO
-std::unique_ptr<StereoEngine> make_crestereo(const EngineConfig& cfg) {
-  throw Error("CREStereo native engine not built (preset " + cfg.model + ")");
-}
-#endif
 #ifndef SA_HAVE_HITNET
 std::unique_ptr<StereoEngine> make_hitnet(const EngineConfig& cfg) {
   throw Error("HITNet native engine not built (preset " + cfg.model + ")");

@@ -93,6 +93,24 @@ class SaNormArgs(C.Structure):
     ]
 
 
+class SaAgclArgs(C.Structure):
+    _fields_ = [
+        ("f1", C.c_void_p), ("f1_stride", C.c_int32), ("f2", C.c_void_p), ("f2_stride", C.c_int32),
+        ("flow", C.c_void_p), ("offset", C.c_void_p), ("offset_stride", C.c_int32),
+        ("N", C.c_int32), ("H", C.c_int32), ("W", C.c_int32), ("C", C.c_int32),
+        ("small_patch", C.c_int32), ("iter_mode", C.c_int32),
+        ("out", C.c_void_p), ("out_stride", C.c_int32), ("out_channels", C.c_int32),
+    ]
+
+
+class SaEwArgs(C.Structure):
+    _fields_ = [
+        ("x", C.c_void_p), ("x_stride", C.c_int32), ("add", C.c_void_p), ("add_stride", C.c_int32),
+        ("bcast", C.c_void_p), ("bcast_period", C.c_int64), ("out", C.c_void_p), ("out_stride", C.c_int32),
+        ("P", C.c_int64), ("C", C.c_int32), ("act", C.c_int32), ("scale", C.c_float),
+    ]
+
+
 ACT = {"none": 0, "relu": 1, "leaky": 2, "tanh": 3, "sigmoid": 4}
 EPI = {"store": 0, "gru_zr": 1, "gru_q": 2, "flow_acc": 3, "store_f32": 4}
 PRE = {"raw": 0, "unit": 1, "imagenet": 2, "signed": 3}
@@ -115,6 +133,13 @@ def _declare_dev(lib):
         "sa_preprocess": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, _p]),
         "sa_remap_bgr": (_i, [_p, _i, _i, _i, _p, _i, _i, _i, _p, _p]),
         "sa_reproject": (_i, [_p, _i, _f, _p, _i, _i, _i, _p, _p, _p, _p]),
+        "sa_agcl_corr": (_i, [C.POINTER(SaAgclArgs), _p]),
+        "sa_linear_attention": (_i, [_p, _i, _p, _i, _p, _i, _p, _i, _i, _i, _i, _i, _i, _f, _p]),
+        "sa_layernorm": (_i, [_p, _i, _p, _p, _p, _i, _p, _i, C.c_long, _i, _f, _p]),
+        "sa_ew": (_i, [C.POINTER(SaEwArgs), _p]),
+        "sa_flow_features": (_i, [_p, _i, C.c_long, _p, _i, _i, _p, _i, _p]),
+        "sa_interp_flow": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _f, _p]),
+        "sa_convex_upsample_c": (_i, [_p, _i, _p, _i, _i, _i, _i, _i, _f, _p, _i, _p]),
         "sa_version": (C.c_char_p, []),
         "sa_last_error": (C.c_char_p, []),
         "sa_engine_create": (_p, [C.c_char_p, C.c_char_p, _i, _i, _i, _i, _i, _i, C.c_ulonglong]),

@@ -17,6 +17,7 @@ from .. import _native as N
 __all__ = [
     "splitk_workspace", "pack_conv_weight", "conv2d", "instnorm_apply", "avgpool3s2", "avgpool_k", "interp_bilinear",
     "corr1d_pyramid", "corr1d_lookup", "convex_upsample", "preprocess", "remap_bgr", "reproject",
+    "agcl_corr", "linear_attention", "layernorm", "ew", "interp_flow", "convex_upsample_c",
 ]
 
 
@@ -242,3 +243,72 @@ def reproject(disp, left_bgr, Q, sign=1.0):
     N.check(N.dev().sa_reproject(_ptr(disp.contiguous()), 1, float(sign), _ptr(left_bgr.contiguous()), b, h, w,
                                  C.cast(q, C.c_void_p), _ptr(dout), _ptr(cloud), _stream()), "reproject")
     return dout, cloud
+
+
+# ------------------------------------------------------------------------------ CREStereo ops
+def agcl_corr(f1, f2, flow, offset=None, small_patch=False, iter_mode=False, out_channels=40):
+    """f1/f2: fp16 NHWC [N,H,W,C]; flow fp32 [N,H,W,2]; offset fp16 [N,H,W,>=18] -> fp16 [N,H,W,oc]."""
+    n, h, w, c = f1.shape
+    out = torch.empty(n, h, w, out_channels, dtype=torch.float16, device=f1.device)
+    a = N.SaAgclArgs()
+    a.f1, a.f1_stride = f1.data_ptr(), _pix_stride(f1)
+    a.f2, a.f2_stride = f2.data_ptr(), _pix_stride(f2)
+    assert flow.dtype == torch.float32 and flow.is_contiguous() and flow.shape == (n, h, w, 2)
+    a.flow = flow.data_ptr()
+    if offset is not None:
+        a.offset, a.offset_stride = offset.data_ptr(), _pix_stride(offset)
+    a.N, a.H, a.W, a.C = n, h, w, c
+    a.small_patch, a.iter_mode = int(small_patch), int(iter_mode)
+    a.out, a.out_stride, a.out_channels = out.data_ptr(), out_channels, out_channels
+    N.check(N.dev().sa_agcl_corr(C.byref(a), _stream()), "sa_agcl_corr")
+    return out
+
+
+def linear_attention(q, k, v, heads=8, eps=1e-6):
+    """q: fp16 [N, L, heads*dim], k/v: [N, S, heads*dim] (last dim may be a slice) -> fp16 [N, L, heads*dim]."""
+    n, l, d = q.shape
+    s = k.shape[1]
+    out = torch.empty(n, l, d, dtype=torch.float16, device=q.device)
+    N.check(N.dev().sa_linear_attention(_ptr(q), q.stride(1), _ptr(k), k.stride(1), _ptr(v), v.stride(1), _ptr(out),
+                                        out.stride(1), n, l, s, heads, d // heads, eps, _stream()), "sa_linear_attention")
+    return out
+
+
+def layernorm(x, gamma, beta, res=None, eps=1e-5):
+    rows, c = x.shape[0] * x.shape[1], x.shape[-1]
+    out = torch.empty_like(x)
+    N.check(N.dev().sa_layernorm(_ptr(x), x.stride(1), _ptr(gamma), _ptr(beta), _ptr(res),
+                                 res.stride(1) if res is not None else 0, _ptr(out), out.stride(1), rows, c, eps,
+                                 _stream()), "sa_layernorm")
+    return out
+
+
+def ew(x, act="none", scale=1.0, add=None, bcast=None, period=1):
+    """x: fp16 NHWC (channel slices allowed) -> fp16 contiguous act(x*scale + add + bcast)."""
+    n, h, w, c = x.shape
+    out = torch.empty(n, h, w, c, dtype=torch.float16, device=x.device)
+    a = N.SaEwArgs()
+    a.x, a.x_stride = x.data_ptr(), _pix_stride(x)
+    if add is not None:
+        a.add, a.add_stride = add.data_ptr(), _pix_stride(add)
+    if bcast is not None:
+        a.bcast, a.bcast_period = bcast.data_ptr(), period
+    a.out, a.out_stride = out.data_ptr(), c
+    a.P, a.C, a.act, a.scale = n * h * w, c, N.ACT[act], scale
+    N.check(N.dev().sa_ew(C.byref(a), _stream()), "sa_ew")
+    return out
+
+
+def interp_flow(x, ho, wo, mul=1.0):
+    n, h, w, c = x.shape
+    out = torch.empty(n, ho, wo, c, dtype=torch.float32, device=x.device)
+    N.check(N.dev().sa_interp_flow(_ptr(x), _ptr(out), n, h, w, c, ho, wo, mul, _stream()), "sa_interp_flow")
+    return out
+
+
+def convex_upsample_c(mask, flow, factor, sign=1.0, oc=2):
+    n, h, w, fc = flow.shape
+    out = torch.empty(n, h * factor, w * factor, oc, dtype=torch.float32, device=flow.device)
+    N.check(N.dev().sa_convex_upsample_c(_ptr(mask), _pix_stride(mask), _ptr(flow), fc, n, h, w, factor, sign,
+                                         _ptr(out), oc, _stream()), "sa_convex_upsample_c")
+    return out

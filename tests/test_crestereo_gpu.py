@@ -1,0 +1,111 @@
+"""CREStereo: kernel numerics vs the PyTorch fp32 oracle pieces (models/crestereo.py) and the native
+engine end to end vs the oracle with the same seeded weights."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def ops():
+    from stereoalgorithms_amd import ops as O
+    return O
+
+
+def nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def rel_err(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("small_patch", [False, True])
+@pytest.mark.parametrize("iter_mode", [False, True])
+def test_agcl_vs_oracle(small_patch, iter_mode):
+    from stereoalgorithms_amd.models.crestereo import AGCL
+    O = ops()
+    torch.manual_seed(0)
+    n, c, h, w = 2, 256, 12, 20
+    f1 = torch.randn(n, c, h, w, device=DEV).half().float()
+    f2 = torch.randn(n, c, h, w, device=DEV).half().float()
+    flow = torch.randn(n, 2, h, w, device=DEV) * 3
+    offset = (torch.rand(n, 18, h, w, device=DEV) * 2 - 1).half().float()
+    agcl = AGCL(f1, f2)
+    with torch.no_grad():
+        ref = agcl.corr_iter(flow, small_patch) if iter_mode else agcl.corr_offset(flow, offset, small_patch)
+    out = O.agcl_corr(nhwc(f1).half(), nhwc(f2).half(), nhwc(flow), None if iter_mode else nhwc(offset).half(),
+                      small_patch=small_patch, iter_mode=iter_mode)
+    torch.cuda.synchronize()
+    assert out.shape == (n, h, w, 40) and out[..., 36:].abs().max().item() == 0
+    assert rel_err(out[..., :36].permute(0, 3, 1, 2), ref) < 5e-3
+
+
+def test_linear_attention_layer_pieces():
+    from stereoalgorithms_amd.models.crestereo import LinearAttention
+    O = ops()
+    torch.manual_seed(1)
+    n, L, S, hds, d = 2, 77, 90, 8, 32
+    q = torch.randn(n, L, hds * d, device=DEV).half()
+    kv = torch.randn(n, S, 2 * hds * d, device=DEV).half()
+    k, v = kv[..., :256], kv[..., 256:]
+    ref = LinearAttention()(q.float().view(n, L, hds, d), k.float().reshape(n, S, hds, d),
+                            v.float().reshape(n, S, hds, d)).reshape(n, L, hds * d)
+    out = O.linear_attention(q, k, v, heads=hds)
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < 3e-3
+    x = torch.randn(n, L, 256, device=DEV).half()
+    res = torch.randn(n, L, 256, device=DEV).half()
+    g, b = torch.rand(256, device=DEV) + 0.5, torch.randn(256, device=DEV) * 0.1
+    ln = O.layernorm(x, g, b, res=res)
+    ref = F.layer_norm(x.float(), (256,), g, b) + res.float()
+    assert rel_err(ln, ref) < 2e-3
+
+
+def test_convex_and_interp_flow():
+    from stereoalgorithms_amd.models.crestereo import CREStereo
+    O = ops()
+    torch.manual_seed(2)
+    n, h, w = 2, 7, 9
+    flow = torch.randn(n, 2, h, w, device=DEV)
+    mask = torch.randn(n, 144, h, w, device=DEV).half().float()
+    ref = CREStereo.convex_upsample(flow, mask, 4)
+    out = O.convex_upsample_c(nhwc(mask).half(), nhwc(flow), 4, 1.0, 2)
+    assert rel_err(out.permute(0, 3, 1, 2), ref) < 2e-3
+    ref2 = -0.5 * F.interpolate(flow, size=(5, 6), mode="bilinear", align_corners=True)
+    out2 = O.interp_flow(nhwc(flow), 5, 6, -0.5)
+    assert rel_err(out2.permute(0, 3, 1, 2), ref2) < 1e-5
+
+
+def _pairs(b, h, w, seed=3):
+    from stereoalgorithms_amd.utils.synthetic import batch_pairs
+    l, r = batch_pairs(b, h, w, seed=seed)
+    return torch.from_numpy(l).cuda(), torch.from_numpy(r).cuda()
+
+
+@pytest.mark.parametrize("preset,hw", [("crestereo-iter2", (64, 96)), ("crestereo-iter5", (96, 128))])
+def test_engine_matches_oracle(tmp_path, preset, hw):
+    from stereoalgorithms_amd.models import crestereo as CR
+    from stereoalgorithms_amd.models.engine import NativeStereoEngine
+    from stereoalgorithms_amd.utils.weights import save_model
+    h, w = hw
+    m = CR.build(preset, seed=0)
+    path = save_model(m, tmp_path / "cre.safetensors", preset)
+    left, right = _pairs(2, h, w)
+    eng = NativeStereoEngine("", str(path), h, w, batch=2)
+    disp = eng.run(left, right)
+    disp2 = eng.run(left, right)
+    torch.cuda.synchronize()
+    m = m.cuda()
+    with torch.no_grad():
+        rgb = lambda t: t.flip(-1).permute(0, 3, 1, 2).float()
+        ref = m(rgb(left), rgb(right))[:, 0]
+    rel = rel_err(disp, ref)
+    print(f"{preset}: |ref| {ref.abs().mean().item():.4f} rel {rel:.3e}")
+    assert torch.equal(disp, disp2)
+    assert torch.isfinite(disp).all()
+    assert rel < 3e-2
