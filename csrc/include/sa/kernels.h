@@ -21,7 +21,7 @@ extern "C" {
 typedef long long sa_stat_t;
 #define SA_STAT_SCALE 16777216.0
 
-enum SaAct { SA_ACT_NONE = 0, SA_ACT_RELU = 1, SA_ACT_LEAKY = 2, SA_ACT_TANH = 3, SA_ACT_SIGMOID = 4 };
+enum SaAct { SA_ACT_NONE = 0, SA_ACT_RELU = 1, SA_ACT_LEAKY = 2, SA_ACT_TANH = 3, SA_ACT_SIGMOID = 4, SA_ACT_RELU6 = 5 };
 
 enum SaEpi {
   SA_EPI_STORE = 0,     // y = act(acc*scale + bias) [; y = act2(y + res)] -> fp16
@@ -71,7 +71,16 @@ typedef struct {
   int32_t* counters;
   int64_t ws_floats;
   int32_t n_counters;
-  int32_t _pad2;
+  // 3-D convolution (0 = 2-D): volumes are [N][D][H][W][C]; output slice do reads input slices
+  // do*sd - pd + kd (kd < KD), K ordered (kd, kh, kw, ci)
+  int32_t KD, Di, Do, sd, pd;
+  // transposed-conv output mode: the packed weights hold 4 (2-D) / 8 (3-D) parity classes of
+  // cout_real channels; the epilogue scatters them to the 2x upsampled output (up = 2 or 3)
+  int32_t up, cout_real;
+  // optional channel gate (Fast-ACVNet channelAtt): y *= gate[n][oh][ow][co] after the activation,
+  // broadcast over depth
+  const void* gate;
+  int32_t gate_stride;
 } SaConvArgs;
 
 int sa_conv2d(const SaConvArgs* a, hipStream_t stream);
@@ -180,6 +189,26 @@ int sa_flow_features(const float* flow, int fc, long P, void* out1, int s1, int 
 // fp32 NHWC bilinear resize (align_corners=True) x mul
 int sa_interp_flow(const float* x, float* out, int N, int H, int W, int C, int Ho, int Wo, float mul,
                    hipStream_t stream);
+
+// ---- Fast-ACVNet+ volume ops (volume_ops.hip) -------------------------------------------------
+// depthwise 3x3 conv, pad 1, stride 1/2 (MobileNetV2), fp32 folded weights [C][9] + bias [C]
+int sa_dwconv3x3(const void* x, int xs, const float* w, const float* b, void* out, int os, int N, int H, int W,
+                 int C, int stride, int act, hipStream_t stream);
+// normalised correlation volume [N][D][H][W][os] (channel 0; 1..7 zero)
+int sa_norm_corr_volume(const void* l, int ls, const void* r, int rs, int N, int H, int W, int C, int D, void* out,
+                        int os, hipStream_t stream);
+// softmax over D + top-K planes (indices re-sorted ascending) -> prob / disparity [N][H][W][K] fp32
+int sa_topk_disparity(const void* att, int as, int N, int D, int H, int W, int K, float* prob, float* disp,
+                      hipStream_t stream);
+// attention-weighted concatenation volume [N][K][H][W][2*Cl] at the sampled disparities
+int sa_concat_volume(const void* l, int ls, const void* r, int rs, const float* prob, const float* disp, int N, int H,
+                     int W, int Cl, int K, void* out, int os, hipStream_t stream);
+// top-`top` softmax regression over K cost planes -> disparity [N][H][W] fp32
+int sa_topk_regress(const void* cost, int cs, const float* disp, int N, int K, int H, int W, int top, float* out,
+                    hipStream_t stream);
+// superpixel context upsampling: softmax(9 spx logits) x 3x3 neighbourhood of the 1/f prediction
+int sa_spx_upsample(const void* spx, int ss, const float* pred, int N, int h, int w, int f, float scale, float* out,
+                    hipStream_t stream);
 
 #ifdef __cplusplus
 }

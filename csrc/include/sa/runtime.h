@@ -46,7 +46,8 @@ struct Tensor {
   void* ptr = nullptr;
   int n = 0, h = 0, w = 0, c = 0, stride = 0;
   DT dt = DT::F16;
-  long pixels() const { return (long)n * h * w; }
+  int d = 1;  // depth of a 3-D volume [n][d][h][w][c] (cost volumes)
+  long pixels() const { return (long)n * d * h * w; }
   size_t nbytes() const { return (size_t)pixels() * stride * dt_size(dt); }
   Tensor slice_c(int off, int cnt) const {
     Tensor t = *this;
@@ -56,7 +57,7 @@ struct Tensor {
   }
   Tensor slice_n(int off, int cnt) const {
     Tensor t = *this;
-    t.ptr = (char*)ptr + (size_t)off * h * w * stride * dt_size(dt);
+    t.ptr = (char*)ptr + (size_t)off * d * h * w * stride * dt_size(dt);
     t.n = cnt;
     return t;
   }
@@ -65,6 +66,7 @@ struct Tensor {
 };
 
 Tensor make_tensor(DeviceArena& a, int n, int h, int w, int c, DT dt = DT::F16, int stride = -1);
+Tensor make_volume(DeviceArena& a, int n, int d, int h, int w, int c, DT dt = DT::F16, int stride = -1);
 
 // ------------------------------------------------------------------ host weights
 struct HostTensor {
@@ -120,6 +122,7 @@ struct ChanSeg {
 
 struct ConvSpec {
   int kh = 3, kw = 3, sh = 1, sw = 1, ph = -1, pw = -1, dh = 1, dw = 1;
+  int kd = 0, sd = 1, pd = -1;  // kd > 0: 3-D convolution
 };
 
 class ConvLayer {
@@ -131,14 +134,29 @@ class ConvLayer {
   void build(DeviceArena& arena, const WeightStore& ws, const std::vector<std::string>& wnames,
              const std::vector<ChanSeg>& in_segs, ConvSpec spec,
              const std::vector<std::string>& bn_names = {}, float scale = 1.f, float bn_eps = 1e-5f);
+  // 3-D conv (weight [Cout][Cin][KD][KH][KW], optional BatchNorm3d fold)
+  void build3d(DeviceArena& arena, const WeightStore& ws, const std::string& wname, const std::vector<ChanSeg>& in_segs,
+               ConvSpec spec, const std::string& bn_name = "", float bn_eps = 1e-5f);
+  // ConvTranspose2d/3d(k=4, s=2, p=1) (weight [Cin][Cout][4][4](4), optional bias / BN fold) as a
+  // 3x3(x3) conv producing 4 (8) parity classes scattered by the epilogue (SaConvArgs.up)
+  void build_deconv(DeviceArena& arena, const WeightStore& ws, const std::string& wname, bool is3d,
+                    const std::vector<ChanSeg>& in_segs, const std::string& bn_name = "", float bn_eps = 1e-5f);
   // Build from explicit host arrays (used by the native random-init path and tests).
   void build_raw(DeviceArena& arena, const std::vector<float>& w, const std::vector<float>& b,
                  int cout, int cin, const std::vector<ChanSeg>& in_segs, ConvSpec spec);
 
   int cout() const { return cout_; }
   int cin_padded() const { return cin_pad_; }
-  int out_h(int h) const { return (h + 2 * spec_.ph - spec_.dh * (spec_.kh - 1) - 1) / spec_.sh + 1; }
-  int out_w(int w) const { return (w + 2 * spec_.pw - spec_.dw * (spec_.kw - 1) - 1) / spec_.sw + 1; }
+  int out_h(int h) const {
+    return up_ ? 2 * h : (h + 2 * spec_.ph - spec_.dh * (spec_.kh - 1) - 1) / spec_.sh + 1;
+  }
+  int out_w(int w) const {
+    return up_ ? 2 * w : (w + 2 * spec_.pw - spec_.dw * (spec_.kw - 1) - 1) / spec_.sw + 1;
+  }
+  int out_d(int d) const {
+    if (spec_.kd <= 0) return 1;
+    return up_ == 3 ? 2 * d : (d + 2 * spec_.pd - (spec_.kd - 1) - 1) / spec_.sd + 1;
+  }
 
   // Fill launch args for inputs (channel-concatenated sources) -> output view.
   SaConvArgs args(const std::vector<Tensor>& srcs, const Tensor& out) const;
@@ -149,9 +167,10 @@ class ConvLayer {
 
  private:
   void upload(DeviceArena& arena, const std::vector<float>& w, const std::vector<float>& b, int cout,
-              int cin, const std::vector<ChanSeg>& segs);
+              int cin, const std::vector<ChanSeg>& segs, int kd = 1);
   ConvSpec spec_;
   int cout_ = 0, cin_pad_ = 0, kpad_ = 0;
+  int up_ = 0, cout_real_ = 0;  // transposed-conv parity scatter (2: 2-D, 3: 3-D)
   void* wdev_ = nullptr;
   float* bdev_ = nullptr;
 };

@@ -36,6 +36,7 @@ __device__ __forceinline__ float act_apply(float v, int act, float alpha) {
       return v < 0.f ? -t : t;
     }
     case SA_ACT_SIGMOID: return 1.f / (1.f + __expf(-v));
+    case SA_ACT_RELU6: return v < 0.f ? 0.f : (v > 6.f ? 6.f : v);
     default: return v;
   }
 }
@@ -93,7 +94,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
   const int wm = wave / WN, wn = wave % WN;
 
   const int HWo = p.Ho * p.Wo;
-  const int M = p.N * HWo;
+  // 3-D mode (KD > 0): rows enumerate (n, do, oh, ow); 2-D is KD = Di = Do = 1
+  const int KD = p.KD > 0 ? p.KD : 1, Di = p.Di > 0 ? p.Di : 1, Do = p.Do > 0 ? p.Do : 1;
+  const int sd = p.sd > 0 ? p.sd : 1;
+  const int M = p.N * Do * HWo;
   const int m0 = blockIdx.x * BM;
   const int n0 = blockIdx.y * BN;
   // split-K slice of the K loop handled by this block
@@ -101,7 +105,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
   const int nk_all = p.Kpad / C::BK;
   const int kt0 = (int)((long)z * nk_all / S);
   const int nk = (int)((long)(z + 1) * nk_all / S) - kt0;
-  const int taps = p.KH * p.KW;
+  const int khw = p.KH * p.KW;
+  const int taps = KD * khw;
 
   floatx4 acc[C::FM][C::FN];
 #pragma unroll
@@ -119,7 +124,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
     const int sb1 = p.src[0].channels;
     const int sb2 = sb1 + (p.nsrc > 1 ? p.src[1].channels : 0);
     const int sb3 = sb2 + (p.nsrc > 2 ? p.src[2].channels : 0);
-    int a_ih0[NA], a_iw0[NA], a_nb[NA], a_tap[NA], a_ci[NA];
+    int a_ih0[NA], a_iw0[NA], a_nb[NA], a_d0[NA], a_tap[NA], a_ci[NA];
     bool a_ok[NA];
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
@@ -129,12 +134,14 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
       const int m = m0 + row;
       a_ok[i] = m < M;
       const int mm = a_ok[i] ? m : 0;
-      const int n = mm / HWo;
-      const int r = mm - n * HWo;
+      const int img = mm / HWo;
+      const int r = mm - img * HWo;
       const int oh = r / p.Wo, ow = r - oh * p.Wo;
+      const int n = img / Do, od = img - n * Do;
       a_ih0[i] = oh * p.sh - p.ph;
       a_iw0[i] = ow * p.sw - p.pw;
-      a_nb[i] = n * p.H;
+      a_d0[i] = od * sd - p.pd;
+      a_nb[i] = n * Di + a_d0[i];  // input slice index for kd = 0
       const int kc = kt0 * C::BK + lch * 8;
       a_tap[i] = kc / p.Cin;
       a_ci[i] = kc - a_tap[i] * p.Cin;
@@ -154,14 +161,15 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
         const int tap = a_tap[i], ci = a_ci[i];
-        const int kh = tap / p.KW, kw = tap - kh * p.KW;
-        const int ih = a_ih0[i] + kh * p.dh, iw = a_iw0[i] + kw * p.dw;
-        const bool ok = a_ok[i] && tap < taps && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+        const int kd = tap / khw, t2 = tap - kd * khw;
+        const int kh = t2 / p.KW, kw = t2 - kh * p.KW;
+        const int ih = a_ih0[i] + kh * p.dh, iw = a_iw0[i] + kw * p.dw, dd = a_d0[i] + kd;
+        const bool ok = a_ok[i] && tap < taps && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W && dd >= 0 && dd < Di;
         const int s = (ci >= sb1) + (ci >= sb2) + (ci >= sb3);
         const int cbase = s == 0 ? 0 : (s == 1 ? sb1 : (s == 2 ? sb2 : sb3));
         const void* g = zero_src;
         if (ok) {
-          const size_t pix = (size_t)(a_nb[i] + ih) * p.W + iw;
+          const size_t pix = ((size_t)(a_nb[i] + kd) * p.H + ih) * p.W + iw;
           g = reinterpret_cast<const f16*>(p.src[s].ptr) + pix * p.src[s].stride + (ci - cbase);
         }
         __builtin_amdgcn_global_load_lds(g, (lds_void_t*)(sa + (wave * NA + i) * 1024), 16, 0, 0);
@@ -215,7 +223,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
   } else {
   // ---------------- per-thread A-row precompute ----------------
   const int cth = tid & 3;  // chunk index this thread loads (constant over k)
-  int a_ih0[C::A_PT], a_iw0[C::A_PT], a_nb[C::A_PT];
+  int a_ih0[C::A_PT], a_iw0[C::A_PT], a_nb[C::A_PT], a_d0[C::A_PT];
   bool a_ok[C::A_PT];
 #pragma unroll
   for (int i = 0; i < C::A_PT; ++i) {
@@ -224,12 +232,14 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
     int m = m0 + row;
     bool ok = (q < C::A_CH) && (m < M);
     int mm = ok ? m : 0;
-    int n = mm / HWo;
-    int r = mm - n * HWo;
+    int img = mm / HWo;
+    int r = mm - img * HWo;
     int oh = r / p.Wo, ow = r - oh * p.Wo;
+    int n = img / Do, od = img - n * Do;
     a_ih0[i] = oh * p.sh - p.ph;
     a_iw0[i] = ow * p.sw - p.pw;
-    a_nb[i] = n * p.H;
+    a_d0[i] = od * sd - p.pd;
+    a_nb[i] = n * Di + a_d0[i];
     a_ok[i] = ok;
   }
   // k-position tracking for this thread's chunk
@@ -251,7 +261,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
 
   auto load_tile = [&](int kt) {
     // A: im2col gather
-    int kh = k_tap / p.KW, kw = k_tap - (k_tap / p.KW) * p.KW;
+    int kd = k_tap / khw, t2 = k_tap - kd * khw;
+    int kh = t2 / p.KW, kw = t2 - kh * p.KW;
     bool kok = k_tap < taps;
     int s = (k_ci >= sb1) + (k_ci >= sb2) + (k_ci >= sb3);
     int cbase = s == 0 ? 0 : (s == 1 ? sb1 : (s == 2 ? sb2 : sb3));
@@ -261,9 +272,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
     for (int i = 0; i < C::A_PT; ++i) {
       int ih = a_ih0[i] + kh * p.dh;
       int iw = a_iw0[i] + kw * p.dw;
-      bool ok = a_ok[i] && kok && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+      int dd = a_d0[i] + kd;
+      bool ok = a_ok[i] && kok && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W && dd >= 0 && dd < Di;
       if (ok) {
-        size_t pix = (size_t)(a_nb[i] + ih) * p.W + iw;
+        size_t pix = ((size_t)(a_nb[i] + kd) * p.H + ih) * p.W + iw;
         ra[i] = *reinterpret_cast<const half8*>(sptr + pix * sstride);
       } else {
         ra[i] = zero8;
@@ -456,7 +468,33 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j] + r8[j], p.act2, p.alpha);
         }
-        if (p.epi == SA_EPI_STORE) {
+        if (p.gate) {  // channel attention, broadcast over depth
+          const int img = m / HWo;
+          const size_t gpix = (size_t)(img / Do) * HWo + (m - img * HWo);
+          const f16* gp = reinterpret_cast<const f16*>(p.gate) + gpix * p.gate_stride + co;
+          float g8[8];
+          if (full) load8(gp, g8);
+          else for (int j = 0; j < 8; ++j) g8[j] = j < nvalid ? (float)gp[j] : 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] *= g8[j];
+        }
+        if (p.up) {
+          // transposed conv: channel co + j belongs to parity class (co + j) / cout_real
+          const int img = m / HWo;
+          const int r = m - img * HWo;
+          const int oh = r / p.Wo, ow = r - oh * p.Wo;
+          const int n = img / Do, od = img - n * Do;
+          const int Ho2 = 2 * p.Ho, Wo2 = 2 * p.Wo, Do2 = p.up == 3 ? 2 * Do : 1;
+          for (int j = 0; j < 8 && j < nvalid; ++j) {
+            const int cj = co + j;
+            const int pi = cj / p.cout_real, c = cj - pi * p.cout_real;
+            const int pb = pi & 1, pa = (pi >> 1) & 1, pc = p.up == 3 ? (pi >> 2) : 0;
+            const int dz = p.up == 3 ? 2 * od + pc : 0;
+            const size_t opix = (((size_t)n * Do2 + dz) * Ho2 + 2 * oh + pa) * Wo2 + 2 * ow + pb;
+            if (p.epi == SA_EPI_STORE) reinterpret_cast<f16*>(p.out)[opix * p.out_stride + c] = (f16)v[j];
+            else reinterpret_cast<float*>(p.out)[opix * p.out_stride + c] = v[j];
+          }
+        } else if (p.epi == SA_EPI_STORE) {
           f16* op = reinterpret_cast<f16*>(p.out) + (size_t)m * p.out_stride + co;
           if (full) store8(op, v);
           else for (int j = 0; j < nvalid; ++j) op[j] = (f16)v[j];
@@ -591,7 +629,7 @@ int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
     return e && e[0] == '1';
   }();
   const bool gl = can_gl && want_gl && a->Kpad % 64 == 0;
-  const int M = a->N * a->Ho * a->Wo;
+  const int M = a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
   const int gx = (M + BM - 1) / BM, gy = (a->Cout + BN - 1) / BN;
   const long tiles = (long)gx * gy;
   const int nk = a->Kpad / (gl ? 64 : 32);
@@ -623,7 +661,7 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
   if (a->Kpad % 32 != 0 || a->Cin % 8 != 0 || a->nsrc < 1 || a->nsrc > 4) return -2;
   int cfg = a->tile_cfg;
   if (cfg < 0) {
-    const int M = a->N * a->Ho * a->Wo;
+    const int M = a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
     if (a->Cout <= 16) cfg = 2;
     else if (a->Cout <= 64) cfg = 1;
     else {

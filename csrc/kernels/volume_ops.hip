@@ -1,0 +1,292 @@
+// Cost-volume and backbone kernels for Fast-ACVNet+: depthwise 3x3 conv
+// (MobileNetV2), normalised-correlation volume, softmax + top-k disparity sampling, attention-weighted
+// concatenation volume, top-2 softmax regression and superpixel (spx) context upsampling.
+// Volumes are NDHWC fp16 ([n][d][h][w][c]); disparity samples / probabilities are fp32 [n][h][w][k].
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include "sa/kernels.h"
+
+namespace {
+typedef _Float16 f16;
+typedef f16 half8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float act_apply(float v, int act, float alpha) {
+  switch (act) {
+    case SA_ACT_RELU: return v > 0.f ? v : 0.f;
+    case SA_ACT_LEAKY: return v > 0.f ? v : v * alpha;
+    case SA_ACT_TANH: return tanhf(v);
+    case SA_ACT_SIGMOID: return 1.f / (1.f + __expf(-v));
+    case SA_ACT_RELU6: return v < 0.f ? 0.f : (v > 6.f ? 6.f : v);
+    default: return v;
+  }
+}
+
+inline int grid_for(long work) {
+  long g = (work + 255) / 256;
+  if (g > 16384) g = 16384;
+  return g < 1 ? 1 : (int)g;
+}
+
+// depthwise 3x3, pad 1, stride s; one thread per (output pixel, 8 channels)
+__global__ void dwconv_kernel(const f16* __restrict__ x, int xs, const float* __restrict__ w,
+                              const float* __restrict__ b, f16* __restrict__ out, int os, int N, int H, int W,
+                              int C, int Ho, int Wo, int s, int act) {
+  const int C8 = C >> 3;
+  const long total = (long)N * Ho * Wo * C8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C8) * 8;
+    long p = i / C8;
+    const int ow = (int)(p % Wo);
+    p /= Wo;
+    const int oh = (int)(p % Ho);
+    const int n = (int)(p / Ho);
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = b[c + j];
+    for (int ky = 0; ky < 3; ++ky) {
+      const int ih = oh * s - 1 + ky;
+      if (ih < 0 || ih >= H) continue;
+      for (int kx = 0; kx < 3; ++kx) {
+        const int iw = ow * s - 1 + kx;
+        if (iw < 0 || iw >= W) continue;
+        const half8 v = *reinterpret_cast<const half8*>(x + ((long)(n * H + ih) * W + iw) * xs + c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += (float)v[j] * w[(c + j) * 9 + ky * 3 + kx];
+      }
+    }
+    half8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (f16)act_apply(acc[j], act, 0.01f);
+    *reinterpret_cast<half8*>(out + ((long)(n * Ho + oh) * Wo + ow) * os + c) = o;
+  }
+}
+
+// volume[n][d][h][w][0] = mean_c( l/|l| * r(w-d)/|r| ), channels 1..7 zero (stride-8 volume)
+__global__ void norm_corr_kernel(const f16* __restrict__ l, int ls, const f16* __restrict__ r, int rs, int N, int H,
+                                 int W, int C, int D, f16* __restrict__ out, int os) {
+  const long total = (long)N * D * H * W;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int w = (int)(i % W);
+    const int h = (int)((i / W) % H);
+    const int d = (int)((i / ((long)W * H)) % D);
+    const int n = (int)(i / ((long)W * H * D));
+    float v = 0.f;
+    if (w >= d) {
+      const f16* lp = l + ((long)(n * H + h) * W + w) * ls;
+      const f16* rp = r + ((long)(n * H + h) * W + (w - d)) * rs;
+      float dot = 0.f, nl = 0.f, nr = 0.f;
+      for (int c = 0; c < C; c += 8) {
+        const half8 a = *reinterpret_cast<const half8*>(lp + c);
+        const half8 bb = *reinterpret_cast<const half8*>(rp + c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = (float)a[j], y = (float)bb[j];
+          dot += x * y;
+          nl += x * x;
+          nr += y * y;
+        }
+      }
+      v = dot / ((sqrtf(nl) + 1e-5f) * (sqrtf(nr) + 1e-5f)) / (float)C;
+    }
+    half8 o = {0, 0, 0, 0, 0, 0, 0, 0};
+    o[0] = (f16)v;
+    *reinterpret_cast<half8*>(out + i * os) = o;
+  }
+}
+
+// softmax over D planes, top-K (descending probability, lower index first on ties), selected
+// indices re-sorted ascending; outputs prob and disparity (= index) per sample.  One thread per pixel.
+template <int DMAX>
+__global__ void topk_kernel(const f16* __restrict__ att, int as, int N, int D, int H, int W, int K,
+                            float* __restrict__ prob, float* __restrict__ disp) {
+  const long P = (long)N * H * W;
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
+    const int n = (int)(p / ((long)H * W));
+    const long hw = p - (long)n * H * W;
+    float v[DMAX];
+    float mx = -1e30f;
+    for (int d = 0; d < D; ++d) {
+      v[d] = (float)att[(((long)n * D + d) * H * W + hw) * as];
+      mx = fmaxf(mx, v[d]);
+    }
+    float sum = 0.f;
+    for (int d = 0; d < D; ++d) {
+      v[d] = __expf(v[d] - mx);
+      sum += v[d];
+    }
+    const float inv = 1.f / sum;
+    // selection: rank of each plane = #planes with larger prob (ties: lower index wins)
+    unsigned long long sel = 0ull;
+    for (int d = 0; d < D; ++d) {
+      int rank = 0;
+      for (int e = 0; e < D; ++e) rank += (v[e] > v[d]) || (v[e] == v[d] && e < d);
+      if (rank < K) sel |= 1ull << d;
+    }
+    int k = 0;
+    for (int d = 0; d < D && k < K; ++d)
+      if (sel >> d & 1ull) {
+        prob[p * K + k] = v[d] * inv;
+        disp[p * K + k] = (float)d;
+        ++k;
+      }
+  }
+}
+
+// out[n][k][h][w][c] = p_k * (c < Cl ? left[c] : right(w - d_k)[c - Cl]), linear interpolation along x
+__global__ void concat_volume_kernel(const f16* __restrict__ l, int ls, const f16* __restrict__ r, int rs,
+                                     const float* __restrict__ prob, const float* __restrict__ disp, int N, int H,
+                                     int W, int Cl, int K, f16* __restrict__ out, int os) {
+  const long total = (long)N * K * H * W;
+  const int C = 2 * Cl;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int w = (int)(i % W);
+    const int h = (int)((i / W) % H);
+    const int k = (int)((i / ((long)W * H)) % K);
+    const int n = (int)(i / ((long)W * H * K));
+    const long pix = ((long)n * H + h) * W + w;
+    const float pk = prob[pix * K + k];
+    const float x = (float)w - disp[pix * K + k];
+    const float x0f = floorf(x);
+    const int x0 = (int)x0f;
+    const float a = x - x0f;
+    f16* o = out + i * os;
+    const f16* lp = l + pix * ls;
+    for (int c = 0; c < Cl; c += 8) {
+      const half8 lv = *reinterpret_cast<const half8*>(lp + c);
+      half8 ov;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ov[j] = (f16)((float)lv[j] * pk);
+      *reinterpret_cast<half8*>(o + c) = ov;
+      float rv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int t = 0; t < 2; ++t) {
+        const int xx = x0 + t;
+        const float wt = t ? a : 1.f - a;
+        if (xx < 0 || xx >= W || wt == 0.f) continue;
+        const half8 q = *reinterpret_cast<const half8*>(r + (((long)n * H + h) * W + xx) * rs + c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) rv[j] += wt * (float)q[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ov[j] = (f16)(rv[j] * pk);
+      *reinterpret_cast<half8*>(o + Cl + c) = ov;
+    }
+    (void)C;
+  }
+}
+
+// pred = sum over the top-`top` cost planes (descending, lower index on ties) of
+// softmax(cost) * disparity sample
+__global__ void topk_regress_kernel(const f16* __restrict__ cost, int cs, const float* __restrict__ disp, int N,
+                                    int K, int H, int W, int top, float* __restrict__ out) {
+  const long P = (long)N * H * W;
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
+    const int n = (int)(p / ((long)H * W));
+    const long hw = p - (long)n * H * W;
+    float best[4];
+    int bi[4];
+    for (int t = 0; t < top; ++t) {
+      best[t] = -1e30f;
+      bi[t] = -1;
+    }
+    for (int k = 0; k < K; ++k) {
+      const float v = (float)cost[(((long)n * K + k) * H * W + hw) * cs];
+      for (int t = 0; t < top; ++t)
+        if (v > best[t]) {
+          for (int u = top - 1; u > t; --u) {
+            best[u] = best[u - 1];
+            bi[u] = bi[u - 1];
+          }
+          best[t] = v;
+          bi[t] = k;
+          break;
+        }
+    }
+    float den = 0.f, num = 0.f;
+    for (int t = 0; t < top; ++t) {
+      const float e = __expf(best[t] - best[0]);
+      den += e;
+      num += e * disp[p * K + bi[t]];
+    }
+    out[p] = num / den;
+  }
+}
+
+// full-res out = scale * sum_k softmax(spx[k]) * pred_lowres[3x3 neighbour k of (y/f, x/f)]
+__global__ void spx_upsample_kernel(const f16* __restrict__ spx, int ss, const float* __restrict__ pred, int N, int h,
+                                    int w, int f, float scale, float* __restrict__ out) {
+  const int H = h * f, W = w * f;
+  const long total = (long)N * H * W;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int x = (int)(i % W);
+    const int y = (int)((i / W) % H);
+    const int n = (int)(i / ((long)W * H));
+    const f16* sp = spx + i * ss;
+    float mv[9], mx = -1e30f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      mv[k] = (float)sp[k];
+      mx = fmaxf(mx, mv[k]);
+    }
+    const int cy = y / f, cx = x / f;
+    float den = 0.f, num = 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const float e = __expf(mv[k] - mx);
+      den += e;
+      const int yy = cy + k / 3 - 1, xx = cx + k % 3 - 1;
+      if (yy >= 0 && yy < h && xx >= 0 && xx < w) num += e * pred[((long)n * h + yy) * w + xx];
+    }
+    out[i] = scale * num / den;
+  }
+}
+
+}  // namespace
+
+extern "C" int sa_dwconv3x3(const void* x, int xs, const float* w, const float* b, void* out, int os, int N, int H,
+                            int W, int C, int stride, int act, hipStream_t stream) {
+  if (C % 8 || xs % 8 || os % 8) return -2;
+  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  hipLaunchKernelGGL(dwconv_kernel, dim3(grid_for((long)N * Ho * Wo * (C / 8))), dim3(256), 0, stream,
+                     (const f16*)x, xs, w, b, (f16*)out, os, N, H, W, C, Ho, Wo, stride, act);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_norm_corr_volume(const void* l, int ls, const void* r, int rs, int N, int H, int W, int C, int D,
+                                   void* out, int os, hipStream_t stream) {
+  if (C % 8 || os < 8 || os % 8) return -2;
+  hipLaunchKernelGGL(norm_corr_kernel, dim3(grid_for((long)N * D * H * W)), dim3(256), 0, stream, (const f16*)l, ls,
+                     (const f16*)r, rs, N, H, W, C, D, (f16*)out, os);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_topk_disparity(const void* att, int as, int N, int D, int H, int W, int K, float* prob, float* disp,
+                                 hipStream_t stream) {
+  if (D > 64 || K > D) return -2;
+  hipLaunchKernelGGL(topk_kernel<64>, dim3(grid_for((long)N * H * W)), dim3(256), 0, stream, (const f16*)att, as, N,
+                     D, H, W, K, prob, disp);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_concat_volume(const void* l, int ls, const void* r, int rs, const float* prob, const float* disp,
+                                int N, int H, int W, int Cl, int K, void* out, int os, hipStream_t stream) {
+  if (Cl % 8 || os < 2 * Cl) return -2;
+  hipLaunchKernelGGL(concat_volume_kernel, dim3(grid_for((long)N * K * H * W)), dim3(256), 0, stream, (const f16*)l,
+                     ls, (const f16*)r, rs, prob, disp, N, H, W, Cl, K, (f16*)out, os);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_topk_regress(const void* cost, int cs, const float* disp, int N, int K, int H, int W, int top,
+                               float* out, hipStream_t stream) {
+  if (top < 1 || top > 4 || top > K) return -2;
+  hipLaunchKernelGGL(topk_regress_kernel, dim3(grid_for((long)N * H * W)), dim3(256), 0, stream, (const f16*)cost, cs,
+                     disp, N, K, H, W, top, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_spx_upsample(const void* spx, int ss, const float* pred, int N, int h, int w, int f, float scale,
+                               float* out, hipStream_t stream) {
+  hipLaunchKernelGGL(spx_upsample_kernel, dim3(grid_for((long)N * h * w * f * f)), dim3(256), 0, stream,
+                     (const f16*)spx, ss, pred, N, h, w, f, scale, out);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,410 @@
+// Fast-ACVNet+ (preset fastacvnet-plus) as a native op graph.
+//
+// Reference pins: inputs left_image/right_image [1,3,480,640] ImageNet-normalised
+// RGB (FastACVNet_plus/src/FastACVNet_plus_preprocess.cu:21-29), output H*W positive disparity
+// (TRTFastACVNet_plus.cpp:15-18), export fast_acvnet_plus_generalization_opset16 (README_en.md:272).
+// Network = upstream Fast-ACVNet+ with the parameter names of the PyTorch oracle
+// stereoalgorithms_amd/models/fast_acvnet.py:
+//   MobileNetV2 backbone (1x1 convs on MFMA, depthwise 3x3 kernel) -> transposed-conv FPN up-fusion
+//   (ConvTranspose2d as a 3x3 conv over 4 parity classes, scattered by the conv epilogue) + stems ->
+//   normalised correlation volume (48 planes at 1/4) -> 3-D hourglass (Conv3d = implicit GEMM over
+//   (kd, kh, kw, ci); ConvTranspose3d via 8 parity classes; image-guided channel attention fused into
+//   the producing conv's epilogue as a sigmoid gate) -> softmax + top-24 sampling -> attention-
+//   weighted concatenation volume -> 3-D hourglass -> top-2 regression -> spx upsampling x4.
+// Every concatenation in the upstream graph is a multi-source conv input here (no copies).
+#include <cmath>
+
+#include "blocks.h"
+
+namespace sa {
+namespace {
+
+static void check(int rc, const char* what) { SA_REQUIRE(rc == 0, "%s failed (rc=%d)", what, rc); }
+
+struct DwConv {  // depthwise 3x3 + folded BN
+  float *w = nullptr, *b = nullptr;
+  int C = 0, stride = 1;
+  void build(DeviceArena& a, WeightSource& src, const std::string& conv, const std::string& bn, int c, int s) {
+    C = c;
+    stride = s;
+    src.param(conv + ".weight", {c, 1, 3, 3}, -1.f / 3.f, 1.f / 3.f);
+    src.bn(bn, c);
+    const WeightStore& ws = *src.ws;
+    std::vector<float> wv = ws.get(conv + ".weight").data, bv(c, 0.f);
+    const auto& g = ws.get(bn + ".weight").data;
+    const auto& be = ws.get(bn + ".bias").data;
+    const auto& mu = ws.get(bn + ".running_mean").data;
+    const auto& var = ws.get(bn + ".running_var").data;
+    for (int i = 0; i < c; ++i) {
+      const float sc = g[i] / std::sqrt(var[i] + 1e-5f);
+      for (int k = 0; k < 9; ++k) wv[i * 9 + k] *= sc;
+      bv[i] = be[i] - mu[i] * sc;
+    }
+    w = (float*)a.alloc(wv.size() * 4);
+    b = (float*)a.alloc(bv.size() * 4);
+    HIP_CHECK(hipMemcpy(w, wv.data(), wv.size() * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(b, bv.data(), bv.size() * 4, hipMemcpyHostToDevice));
+  }
+  void run(hipStream_t s, const Tensor& x, const Tensor& out, int act) const {
+    check(sa_dwconv3x3(x.ptr, x.stride, w, b, out.ptr, out.stride, x.n, x.h, x.w, C, stride, act, s), "dwconv");
+  }
+};
+
+// timm InvertedResidual: pw 1x1 (BN, ReLU6) -> dw 3x3 (BN, ReLU6) -> pwl 1x1 (BN) [+ x]
+struct InvRes {
+  ConvLayer pw, pwl;
+  DwConv dw;
+  Tensor t1, t2, out;
+  bool skip = false;
+  void build(DeviceArena& a, WeightSource& src, const std::string& p, int cin, int cout, int stride, int N, int H,
+             int W) {
+    const int mid = cin * 6;
+    skip = stride == 1 && cin == cout;
+    src.conv(p + ".conv_pw", mid, cin, 1, 1, false);
+    src.bn(p + ".bn1", mid);
+    src.conv(p + ".conv_pwl", cout, mid, 1, 1, false);
+    src.bn(p + ".bn3", cout);
+    ConvSpec s1;
+    s1.kh = s1.kw = 1;
+    pw.build(a, *src.ws, {p + ".conv_pw"}, {{cin, cin}}, s1, {p + ".bn1"});
+    dw.build(a, src, p + ".conv_dw", p + ".bn2", mid, stride);
+    pwl.build(a, *src.ws, {p + ".conv_pwl"}, {{mid, mid}}, s1, {p + ".bn3"});
+    const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+    t1 = make_tensor(a, N, H, W, mid);
+    t2 = make_tensor(a, N, Ho, Wo, mid);
+    out = make_tensor(a, N, Ho, Wo, cout);
+  }
+  void run(hipStream_t s, const Tensor& x) const {
+    pw.run(s, {x}, t1, SA_ACT_RELU6);
+    dw.run(s, t1, t2, SA_ACT_RELU6);
+    pwl.run(s, {t2}, out, SA_ACT_NONE, skip ? &x : nullptr, SA_ACT_NONE);
+  }
+};
+
+// upstream BasicConv: conv (no bias) + BN + LeakyReLU(0.01)
+void basic2d(DeviceArena& a, WeightSource& src, ConvLayer& L, const std::string& p, const std::vector<ChanSeg>& segs,
+             int cout, int k, int stride, bool bn = true) {
+  int cin = 0;
+  for (auto sg : segs) cin += sg.real;
+  src.conv(p + ".conv", cout, cin, k, k, false);
+  if (bn) src.bn(p + ".bn", cout);
+  ConvSpec sp;
+  sp.kh = sp.kw = k;
+  sp.sh = sp.sw = stride;
+  L.build(a, *src.ws, {p + ".conv"}, segs, sp, bn ? std::vector<std::string>{p + ".bn"} : std::vector<std::string>{});
+}
+
+void basic3d(DeviceArena& a, WeightSource& src, ConvLayer& L, const std::string& p, const std::vector<ChanSeg>& segs,
+             int cout, int k, int stride) {
+  int cin = 0;
+  for (auto sg : segs) cin += sg.real;
+  const float bound = 1.f / std::sqrt((float)(cin * k * k * k));
+  src.param(p + ".conv.weight", {cout, cin, k, k, k}, -bound, bound);
+  src.bn(p + ".bn", cout);
+  ConvSpec sp;
+  sp.kd = sp.kh = sp.kw = k;
+  sp.sd = sp.sh = sp.sw = stride;
+  L.build3d(a, *src.ws, p + ".conv", segs, sp, p + ".bn");
+}
+
+void deconv(DeviceArena& a, WeightSource& src, ConvLayer& L, const std::string& name, int cin, int cout, bool is3d,
+            const std::string& bn, bool bias = false) {
+  const float bound = 1.f / std::sqrt((float)(cout * (is3d ? 64 : 16)));
+  if (is3d) src.param(name + ".weight", {cin, cout, 4, 4, 4}, -bound, bound);
+  else src.param(name + ".weight", {cin, cout, 4, 4}, -bound, bound);
+  if (bias) src.param(name + ".bias", {cout}, -bound, bound);
+  if (!bn.empty()) src.bn(bn, cout);
+  L.build_deconv(a, *src.ws, name, is3d, {{cin, round_up(cin, 8)}}, bn);
+}
+
+// channelAtt gate: sigmoid(conv1x1(BasicConv1x1(im)))  -> [N][h][w][cv]
+struct Gate {
+  ConvLayer c0, c1;
+  Tensor mid, g;
+  void build(DeviceArena& a, WeightSource& src, const std::string& p, const std::vector<ChanSeg>& im_segs, int cv,
+             int N, int h, int w) {
+    int im = 0;
+    for (auto sg : im_segs) im += sg.real;
+    basic2d(a, src, c0, p + ".im_att.0", im_segs, im / 2, 1, 1);
+    src.conv(p + ".im_att.1", cv, im / 2, 1, 1, true);
+    ConvSpec s1;
+    s1.kh = s1.kw = 1;
+    c1.build(a, *src.ws, {p + ".im_att.1"}, {{im / 2, im / 2}}, s1);
+    mid = make_tensor(a, N, h, w, im / 2);
+    g = make_tensor(a, N, h, w, cv);
+  }
+  void run(hipStream_t s, const std::vector<Tensor>& im) const {
+    c0.run(s, im, mid, SA_ACT_LEAKY);
+    c1.run(s, {mid}, g, SA_ACT_SIGMOID);
+  }
+};
+
+void run_gated(hipStream_t s, const ConvLayer& L, const std::vector<Tensor>& srcs, const Tensor& out, const Gate* g,
+               int act = SA_ACT_LEAKY) {
+  SaConvArgs a = L.args(srcs, out);
+  a.act = act;
+  a.alpha = 0.01f;
+  if (g) {
+    a.gate = g->g.ptr;
+    a.gate_stride = g->g.stride;
+  }
+  L.launch(s, a);
+}
+
+// hourglass / hourglass_att (3-D) with image-guided gates
+struct Hourglass {
+  ConvLayer c1a, c1b, c2a, c2b, up2, agg0, agg1, up1;
+  Gate att8, att16, attup8;
+  Tensor v1a, v1b, v2a, v2b, u2, ag0, ag1, out;
+  void build(DeviceArena& a, WeightSource& src, const std::string& p, int c, int N, int D, int h, int w) {
+    basic3d(a, src, c1a, p + ".conv1.0", {{c, round_up(c, 8)}}, 2 * c, 3, 2);
+    basic3d(a, src, c1b, p + ".conv1.1", {{2 * c, 2 * c}}, 2 * c, 3, 1);
+    basic3d(a, src, c2a, p + ".conv2.0", {{2 * c, 2 * c}}, 4 * c, 3, 2);
+    basic3d(a, src, c2b, p + ".conv2.1", {{4 * c, 4 * c}}, 4 * c, 3, 1);
+    deconv(a, src, up2, p + ".conv2_up.conv", 4 * c, 2 * c, true, p + ".conv2_up.bn");
+    basic3d(a, src, agg0, p + ".agg_0.0", {{2 * c, 2 * c}, {2 * c, 2 * c}}, 2 * c, 1, 1);
+    basic3d(a, src, agg1, p + ".agg_0.1", {{2 * c, 2 * c}}, 2 * c, 3, 1);
+    deconv(a, src, up1, p + ".conv1_up.conv", 2 * c, 1, true, "");
+    att8.build(a, src, p + ".feature_att_8", {{64, 64}}, 2 * c, N, h / 2, w / 2);
+    att16.build(a, src, p + ".feature_att_16", {{192, 192}}, 4 * c, N, h / 4, w / 4);
+    attup8.build(a, src, p + ".feature_att_up_8", {{64, 64}}, 2 * c, N, h / 2, w / 2);
+    v1a = make_volume(a, N, D / 2, h / 2, w / 2, 2 * c);
+    v1b = make_volume(a, N, D / 2, h / 2, w / 2, 2 * c);
+    v2a = make_volume(a, N, D / 4, h / 4, w / 4, 4 * c);
+    v2b = make_volume(a, N, D / 4, h / 4, w / 4, 4 * c);
+    u2 = make_volume(a, N, D / 2, h / 2, w / 2, 2 * c);
+    ag0 = make_volume(a, N, D / 2, h / 2, w / 2, 2 * c);
+    ag1 = make_volume(a, N, D / 2, h / 2, w / 2, 2 * c);
+    out = make_volume(a, N, D, h, w, 1);
+  }
+  void run(hipStream_t s, const Tensor& x, const Tensor& x8, const Tensor& x16) const {
+    att8.run(s, {x8});
+    att16.run(s, {x16});
+    attup8.run(s, {x8});
+    run_gated(s, c1a, {x}, v1a, nullptr);
+    run_gated(s, c1b, {v1a}, v1b, &att8);
+    run_gated(s, c2a, {v1b}, v2a, nullptr);
+    run_gated(s, c2b, {v2a}, v2b, &att16);
+    run_gated(s, up2, {v2b}, u2, nullptr);
+    run_gated(s, agg0, {u2, v1b}, ag0, nullptr);
+    run_gated(s, agg1, {ag0}, ag1, &attup8);
+    run_gated(s, up1, {ag1}, out, nullptr, SA_ACT_NONE);
+  }
+};
+
+class FastAcvNet : public StereoEngine {
+ public:
+  explicit FastAcvNet(const EngineConfig& cfg) : StereoEngine(cfg) {}
+  const char* name() const override { return "FastACVNet_plus"; }
+
+ protected:
+  void build(WeightSource& src) override;
+  void forward(hipStream_t s) override;
+
+ private:
+  static constexpr int kMaxDisp = 192, kTopK = 24;
+  Tensor img_, s0_, b0t_, x2_;
+  ConvLayer stem_conv_, b0pw_;
+  DwConv b0dw_;
+  std::vector<InvRes> blocks_;
+  int i4_ = 0, i8_ = 0, i16_ = 0, i32_ = 0;  // block indices producing x4 / x8 / x16 / x32
+  ConvLayer up32_1_, up32_2_, up16_1_, up16_2_, up8_1_, up8_2_, conv4_;
+  Tensor d16_, x16u_, d8_, x8u_, d4_, x4c_, x4u_;
+  ConvLayer st2a_, st2b_, st4a_, st4b_, mconv_, mdesc_;
+  Tensor st2t_, st2_, st4t_, st4_, m48_, match_;
+  Tensor cvol_, cost0_;
+  ConvLayer corr_stem_;
+  Gate gcorr_, gconcat_;
+  Hourglass hg_att_, hg_;
+  float *prob_ = nullptr, *dsamp_ = nullptr, *pred_ = nullptr;
+  ConvLayer cf0_, cf1_, concat_stem_;
+  Tensor cft_, cfeat_, cvol2_, cost1_;
+  ConvLayer spx4a_, spx4b_, spx2c1_, spx2c2_, spx_;
+  Tensor sx4t_, sx4_, sxu_, sx2_, spxo_;
+};
+
+void FastAcvNet::build(WeightSource& src) {
+  DeviceArena& a = arena_;
+  const int B = this->B(), N2 = 2 * B;
+  SA_REQUIRE(H() % 32 == 0 && W() % 32 == 0, "Fast-ACVNet+ needs H, W multiples of 32");
+  const int H2 = H() / 2, W2 = W() / 2, h = H() / 4, w = W() / 4;
+  img_ = make_tensor(a, N2, H(), W(), 8);
+  // ---------------- MobileNetV2 features (both images batched) ----------------
+  src.conv("feature.conv_stem", 32, 3, 3, 3, false);
+  src.bn("feature.bn1", 32);
+  ConvSpec s3s2;
+  s3s2.sh = s3s2.sw = 2;
+  stem_conv_.build(a, *src.ws, {"feature.conv_stem"}, {{3, 8}}, s3s2, {"feature.bn1"});
+  s0_ = make_tensor(a, N2, H2, W2, 32);
+  b0dw_.build(a, src, "feature.block0.0.0.conv_dw", "feature.block0.0.0.bn1", 32, 1);
+  src.conv("feature.block0.0.0.conv_pw", 16, 32, 1, 1, false);
+  src.bn("feature.block0.0.0.bn2", 16);
+  ConvSpec s1;
+  s1.kh = s1.kw = 1;
+  b0pw_.build(a, *src.ws, {"feature.block0.0.0.conv_pw"}, {{32, 32}}, s1, {"feature.block0.0.0.bn2"});
+  b0t_ = make_tensor(a, N2, H2, W2, 32);
+  x2_ = make_tensor(a, N2, H2, W2, 16);
+  struct StageSpec {
+    const char* name;
+    int sub;  // index inside the Sequential of the Feature block
+    int cout, n, stride;
+  };
+  const StageSpec stages[] = {{"feature.block1", 0, 24, 2, 2}, {"feature.block2", 0, 32, 3, 2},
+                              {"feature.block3", 0, 64, 4, 2}, {"feature.block3", 1, 96, 3, 1},
+                              {"feature.block4", 0, 160, 3, 2}};
+  int cin = 16, hh = H2, ww = W2;
+  blocks_.reserve(16);
+  for (int si = 0; si < 5; ++si) {
+    const StageSpec& st = stages[si];
+    for (int i = 0; i < st.n; ++i) {
+      blocks_.emplace_back();
+      const int s = i == 0 ? st.stride : 1;
+      blocks_.back().build(a, src, std::string(st.name) + "." + std::to_string(st.sub) + "." + std::to_string(i), cin,
+                           st.cout, s, N2, hh, ww);
+      hh = blocks_.back().out.h;
+      ww = blocks_.back().out.w;
+      cin = st.cout;
+    }
+    const int last = (int)blocks_.size() - 1;
+    if (si == 0) i4_ = last;
+    if (si == 1) i8_ = last;
+    if (si == 3) i16_ = last;
+    if (si == 4) i32_ = last;
+  }
+  // ---------------- FeatUp ----------------
+  deconv(a, src, up32_1_, "feature_up.deconv32_16.conv1.conv", 160, 96, false, "feature_up.deconv32_16.conv1.bn");
+  basic2d(a, src, up32_2_, "feature_up.deconv32_16.conv2", {{96, 96}, {96, 96}}, 192, 3, 1);
+  deconv(a, src, up16_1_, "feature_up.deconv16_8.conv1.conv", 192, 32, false, "feature_up.deconv16_8.conv1.bn");
+  basic2d(a, src, up16_2_, "feature_up.deconv16_8.conv2", {{32, 32}, {32, 32}}, 64, 3, 1);
+  deconv(a, src, up8_1_, "feature_up.deconv8_4.conv1.conv", 64, 24, false, "feature_up.deconv8_4.conv1.bn");
+  basic2d(a, src, up8_2_, "feature_up.deconv8_4.conv2", {{24, 24}, {24, 24}}, 48, 3, 1);
+  basic2d(a, src, conv4_, "feature_up.conv4", {{48, 48}}, 48, 3, 1);
+  d16_ = make_tensor(a, N2, h / 4, w / 4, 96);
+  x16u_ = make_tensor(a, N2, h / 4, w / 4, 192);
+  d8_ = make_tensor(a, N2, h / 2, w / 2, 32);
+  x8u_ = make_tensor(a, N2, h / 2, w / 2, 64);
+  d4_ = make_tensor(a, N2, h, w, 24);
+  x4c_ = make_tensor(a, N2, h, w, 48);
+  x4u_ = make_tensor(a, N2, h, w, 48);
+  // ---------------- stems ----------------
+  basic2d(a, src, st2a_, "stem_2.0", {{3, 8}}, 32, 3, 2);
+  src.conv("stem_2.1", 32, 32, 3, 3, false);
+  src.bn("stem_2.2", 32);
+  ConvSpec s3;
+  st2b_.build(a, *src.ws, {"stem_2.1"}, {{32, 32}}, s3, {"stem_2.2"});
+  basic2d(a, src, st4a_, "stem_4.0", {{32, 32}}, 48, 3, 2);
+  src.conv("stem_4.1", 48, 48, 3, 3, false);
+  src.bn("stem_4.2", 48);
+  st4b_.build(a, *src.ws, {"stem_4.1"}, {{48, 48}}, s3, {"stem_4.2"});
+  st2t_ = make_tensor(a, N2, H2, W2, 32);
+  st2_ = make_tensor(a, N2, H2, W2, 32);
+  st4t_ = make_tensor(a, N2, h, w, 48);
+  st4_ = make_tensor(a, N2, h, w, 48);
+  const std::vector<ChanSeg> f0 = {{48, 48}, {48, 48}};  // features_left[0] = [x4u | stem_4x]
+  basic2d(a, src, mconv_, "conv", f0, 48, 3, 1);
+  src.conv("desc", 48, 48, 1, 1, true);
+  mdesc_.build(a, *src.ws, {"desc"}, {{48, 48}}, s1);
+  m48_ = make_tensor(a, N2, h, w, 48);
+  match_ = make_tensor(a, N2, h, w, 48);
+  // ---------------- attention volume ----------------
+  const int D = kMaxDisp / 4;
+  cvol_ = make_volume(a, B, D, h, w, 8);
+  cost0_ = make_volume(a, B, D, h, w, 8);
+  basic3d(a, src, corr_stem_, "corr_stem", {{1, 8}}, 8, 3, 1);
+  gcorr_.build(a, src, "corr_feature_att_4", f0, 8, B, h, w);
+  hg_att_.build(a, src, "hourglass_att", 8, B, D, h, w);
+  prob_ = (float*)a.alloc((size_t)B * h * w * kTopK * 4);
+  dsamp_ = (float*)a.alloc((size_t)B * h * w * kTopK * 4);
+  pred_ = (float*)a.alloc((size_t)B * h * w * 4);
+  // ---------------- concatenation volume ----------------
+  basic2d(a, src, cf0_, "concat_feature.0", f0, 32, 3, 1);
+  src.conv("concat_feature.1", 16, 32, 3, 3, false);
+  cf1_.build(a, *src.ws, {"concat_feature.1"}, {{32, 32}}, s3);
+  cft_ = make_tensor(a, N2, h, w, 32);
+  cfeat_ = make_tensor(a, N2, h, w, 16);
+  cvol2_ = make_volume(a, B, kTopK, h, w, 32);
+  basic3d(a, src, concat_stem_, "concat_stem", {{32, 32}}, 16, 3, 1);
+  gconcat_.build(a, src, "concat_feature_att_4", f0, 16, B, h, w);
+  cost1_ = make_volume(a, B, kTopK, h, w, 16);
+  hg_.build(a, src, "hourglass", 16, B, kTopK, h, w);
+  // ---------------- spx upsampling ----------------
+  basic2d(a, src, spx4a_, "spx_4.0", f0, 32, 3, 1);
+  src.conv("spx_4.1", 32, 32, 3, 3, false);
+  src.bn("spx_4.2", 32);
+  spx4b_.build(a, *src.ws, {"spx_4.1"}, {{32, 32}}, s3, {"spx_4.2"});
+  deconv(a, src, spx2c1_, "spx_2.conv1.conv", 32, 32, false, "spx_2.conv1.bn");
+  basic2d(a, src, spx2c2_, "spx_2.conv2", {{32, 32}, {32, 32}}, 64, 3, 1);
+  deconv(a, src, spx_, "spx.0", 64, 9, false, "", true);
+  sx4t_ = make_tensor(a, B, h, w, 32);
+  sx4_ = make_tensor(a, B, h, w, 32);
+  sxu_ = make_tensor(a, B, H2, W2, 32);
+  sx2_ = make_tensor(a, B, H2, W2, 64);
+  spxo_ = make_tensor(a, B, H(), W(), 16);
+}
+
+void FastAcvNet::forward(hipStream_t s) {
+  const int B = this->B();
+  const int h = H() / 4, w = W() / 4;
+  check(sa_preprocess(in_left_, B, H(), W(), SA_PRE_IMAGENET, img_.ptr, 8, 0, 8, s), "preprocess");
+  check(sa_preprocess(in_right_, B, H(), W(), SA_PRE_IMAGENET, img_.slice_n(B, B).ptr, 8, 0, 8, s), "preprocess");
+  // backbone
+  stem_conv_.run(s, {img_}, s0_, SA_ACT_RELU6);
+  b0dw_.run(s, s0_, b0t_, SA_ACT_RELU6);
+  b0pw_.run(s, {b0t_}, x2_);
+  const Tensor* x = &x2_;
+  for (const auto& b : blocks_) {
+    b.run(s, *x);
+    x = &b.out;
+  }
+  const Tensor &x4 = blocks_[i4_].out, &x8 = blocks_[i8_].out, &x16 = blocks_[i16_].out, &x32 = blocks_[i32_].out;
+  // FeatUp (Conv2x: deconv -> concat(rem) -> conv)
+  up32_1_.run(s, {x32}, d16_, SA_ACT_LEAKY);
+  up32_2_.run(s, {d16_, x16}, x16u_, SA_ACT_LEAKY);
+  up16_1_.run(s, {x16u_}, d8_, SA_ACT_LEAKY);
+  up16_2_.run(s, {d8_, x8}, x8u_, SA_ACT_LEAKY);
+  up8_1_.run(s, {x8u_}, d4_, SA_ACT_LEAKY);
+  up8_2_.run(s, {d4_, x4}, x4c_, SA_ACT_LEAKY);
+  conv4_.run(s, {x4c_}, x4u_, SA_ACT_LEAKY);
+  // stems
+  st2a_.run(s, {img_}, st2t_, SA_ACT_LEAKY);
+  st2b_.run(s, {st2t_}, st2_, SA_ACT_RELU);
+  st4a_.run(s, {st2_}, st4t_, SA_ACT_LEAKY);
+  st4b_.run(s, {st4t_}, st4_, SA_ACT_RELU);
+  const std::vector<Tensor> f0 = {x4u_, st4_};
+  const std::vector<Tensor> f0l = {x4u_.slice_n(0, B), st4_.slice_n(0, B)};
+  // matching descriptors + normalised correlation volume
+  mconv_.run(s, f0, m48_, SA_ACT_LEAKY);
+  mdesc_.run(s, {m48_}, match_);
+  const int D = kMaxDisp / 4;
+  check(sa_norm_corr_volume(match_.ptr, 48, match_.slice_n(B, B).ptr, 48, B, h, w, 48, D, cvol_.ptr, 8, s), "corr vol");
+  gcorr_.run(s, f0l);
+  run_gated(s, corr_stem_, {cvol_}, cost0_, &gcorr_);
+  const Tensor x8l = x8u_.slice_n(0, B), x16l = x16u_.slice_n(0, B);
+  hg_att_.run(s, cost0_, x8l, x16l);
+  check(sa_topk_disparity(hg_att_.out.ptr, hg_att_.out.stride, B, D, h, w, kTopK, prob_, dsamp_, s), "topk");
+  // attention-weighted concatenation volume at the sampled disparities
+  cf0_.run(s, f0, cft_, SA_ACT_LEAKY);
+  cf1_.run(s, {cft_}, cfeat_);
+  check(sa_concat_volume(cfeat_.ptr, 16, cfeat_.slice_n(B, B).ptr, 16, prob_, dsamp_, B, h, w, 16, kTopK, cvol2_.ptr,
+                         32, s),
+        "concat volume");
+  gconcat_.run(s, f0l);
+  run_gated(s, concat_stem_, {cvol2_}, cost1_, &gconcat_);
+  hg_.run(s, cost1_, x8l, x16l);
+  check(sa_topk_regress(hg_.out.ptr, hg_.out.stride, dsamp_, B, kTopK, h, w, 2, pred_, s), "regress");
+  // spx upsampling
+  spx4a_.run(s, f0l, sx4t_, SA_ACT_LEAKY);
+  spx4b_.run(s, {sx4t_}, sx4_, SA_ACT_RELU);
+  spx2c1_.run(s, {sx4_}, sxu_, SA_ACT_LEAKY);
+  spx2c2_.run(s, {sxu_, st2_.slice_n(0, B)}, sx2_, SA_ACT_LEAKY);
+  spx_.run(s, {sx2_}, spxo_);
+  check(sa_spx_upsample(spxo_.ptr, spxo_.stride, pred_, B, h, w, 4, 4.f, disp_, s), "spx upsample");
+}
+
+}  // namespace
+
+std::unique_ptr<StereoEngine> make_fast_acvnet(const EngineConfig& cfg) {
+  return std::unique_ptr<StereoEngine>(new FastAcvNet(cfg));
+}
+
+}  // namespace sa

@@ -7,9 +7,4 @@ std::unique_ptr<StereoEngine> make_hitnet(const EngineConfig& cfg) {
   throw Error("HITNet native engine not built (preset " + cfg.model + ")");
 }
 #endif
-#ifndef SA_HAVE_FASTACV
-std::unique_ptr<StereoEngine> make_fast_acvnet(const EngineConfig& cfg) {
-  throw Error("Fast-ACVNet+ native engine not built (preset " + cfg.model + ")");
-}
-#endif
 }  // namespace sa

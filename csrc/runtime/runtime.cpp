@@ -30,6 +30,19 @@ void DeviceArena::release() {
   total_ = 0;
 }
 
+Tensor make_volume(DeviceArena& a, int n, int d, int h, int w, int c, DT dt, int stride) {
+  Tensor t;
+  t.n = n;
+  t.d = d;
+  t.h = h;
+  t.w = w;
+  t.c = c;
+  t.stride = stride < 0 ? c : stride;
+  t.dt = dt;
+  t.ptr = a.alloc(t.nbytes());
+  return t;
+}
+
 Tensor make_tensor(DeviceArena& a, int n, int h, int w, int c, DT dt, int stride) {
   Tensor t;
   t.n = n;
@@ -128,7 +141,7 @@ static uint16_t float_to_half(float f) {
 }
 
 void ConvLayer::upload(DeviceArena& arena, const std::vector<float>& w, const std::vector<float>& b,
-                       int cout, int cin, const std::vector<ChanSeg>& segs) {
+                       int cout, int cin, const std::vector<ChanSeg>& segs, int KD) {
   int real_sum = 0, pad_sum = 0;
   for (auto s : segs) {
     real_sum += s.real;
@@ -139,7 +152,7 @@ void ConvLayer::upload(DeviceArena& arena, const std::vector<float>& w, const st
   cout_ = cout;
   cin_pad_ = pad_sum;
   const int KH = spec_.kh, KW = spec_.kw;
-  const int K = KH * KW * cin_pad_;
+  const int K = KD * KH * KW * cin_pad_;  // ordered (kd, kh, kw, ci)
   kpad_ = round_up(K, 64);  // 64-aligned K enables the DMA-staged BK=64 conv path
   const int cout_pad = round_up(cout, 128);
   std::vector<uint16_t> packed((size_t)cout_pad * kpad_, 0);
@@ -154,13 +167,14 @@ void ConvLayer::upload(DeviceArena& arena, const std::vector<float>& w, const st
     }
   }
   for (int o = 0; o < cout; ++o)
-    for (int y = 0; y < KH; ++y)
-      for (int x = 0; x < KW; ++x)
-        for (int c = 0; c < cin_pad_; ++c) {
-          int rc = cmap[c];
-          float v = rc < 0 ? 0.f : w[(((size_t)o * cin + rc) * KH + y) * KW + x];
-          packed[(size_t)o * kpad_ + (y * KW + x) * cin_pad_ + c] = float_to_half(v);
-        }
+    for (int z = 0; z < KD; ++z)
+      for (int y = 0; y < KH; ++y)
+        for (int x = 0; x < KW; ++x)
+          for (int c = 0; c < cin_pad_; ++c) {
+            int rc = cmap[c];
+            float v = rc < 0 ? 0.f : w[((((size_t)o * cin + rc) * KD + z) * KH + y) * KW + x];
+            packed[(size_t)o * kpad_ + ((z * KH + y) * KW + x) * cin_pad_ + c] = float_to_half(v);
+          }
   wdev_ = arena.alloc(packed.size() * 2);
   HIP_CHECK(hipMemcpy(wdev_, packed.data(), packed.size() * 2, hipMemcpyHostToDevice));
   std::vector<float> bias(round_up(cout, 8), 0.f);
@@ -216,6 +230,97 @@ void ConvLayer::build(DeviceArena& arena, const WeightStore& ws,
   upload(arena, W, Bv, cout, cin, in_segs);
 }
 
+static void fold_bn(const WeightStore& ws, const std::string& bn, int co, int per, std::vector<float>& w,
+                    std::vector<float>& b, float eps) {
+  const auto& g = ws.get(bn + ".weight").data;
+  const auto& be = ws.get(bn + ".bias").data;
+  const auto& mu = ws.get(bn + ".running_mean").data;
+  const auto& var = ws.get(bn + ".running_var").data;
+  for (int o = 0; o < co; ++o) {
+    const float sc = g[o] / std::sqrt(var[o] + eps);
+    for (int j = 0; j < per; ++j) w[(size_t)o * per + j] *= sc;
+    b[o] = (b[o] - mu[o]) * sc + be[o];
+  }
+}
+
+void ConvLayer::build3d(DeviceArena& arena, const WeightStore& ws, const std::string& wname,
+                        const std::vector<ChanSeg>& in_segs, ConvSpec spec, const std::string& bn, float eps) {
+  const HostTensor& wt = ws.get(wname + ".weight");
+  SA_REQUIRE(wt.shape.size() == 5, "%s: expected 5-D conv weight", wname.c_str());
+  const int co = (int)wt.shape[0], ci = (int)wt.shape[1];
+  spec.kd = (int)wt.shape[2];
+  spec.kh = (int)wt.shape[3];
+  spec.kw = (int)wt.shape[4];
+  if (spec.ph < 0) spec.ph = spec.kh / 2;
+  if (spec.pw < 0) spec.pw = spec.kw / 2;
+  if (spec.pd < 0) spec.pd = spec.kd / 2;
+  std::vector<float> w = wt.data, b(co, 0.f);
+  if (ws.has(wname + ".bias")) b = ws.get(wname + ".bias").data;
+  if (!bn.empty()) fold_bn(ws, bn, co, ci * spec.kd * spec.kh * spec.kw, w, b, eps);
+  spec_ = spec;
+  upload(arena, w, b, co, ci, in_segs, spec.kd);
+}
+
+void ConvLayer::build_deconv(DeviceArena& arena, const WeightStore& ws, const std::string& wname, bool is3d,
+                             const std::vector<ChanSeg>& in_segs, const std::string& bn, float eps) {
+  // out[2i + a] = sum_{dy in {-1,0,1}} in[i + dy] * Wt[a + 1 - 2 dy]  (taps with 0 <= k < 4)
+  const HostTensor& wt = ws.get(wname + ".weight");
+  const int dims = is3d ? 3 : 2;
+  SA_REQUIRE((int)wt.shape.size() == 2 + dims, "%s: expected %d-D transposed-conv weight", wname.c_str(), 2 + dims);
+  for (int k = 0; k < dims; ++k) SA_REQUIRE(wt.shape[2 + k] == 4, "%s: only k=4 s=2 p=1 deconvs", wname.c_str());
+  const int ci = (int)wt.shape[0], co = (int)wt.shape[1];
+  std::vector<float> bias(co, 0.f);
+  if (ws.has(wname + ".bias")) bias = ws.get(wname + ".bias").data;
+  // BN fold on the transposed weight's output channels
+  std::vector<float> tw = wt.data;  // [ci][co][4]^dims
+  const int kvol = is3d ? 64 : 16;
+  if (!bn.empty()) {
+    const auto& g = ws.get(bn + ".weight").data;
+    const auto& be = ws.get(bn + ".bias").data;
+    const auto& mu = ws.get(bn + ".running_mean").data;
+    const auto& var = ws.get(bn + ".running_var").data;
+    for (int o = 0; o < co; ++o) {
+      const float sc = g[o] / std::sqrt(var[o] + eps);
+      for (int i = 0; i < ci; ++i)
+        for (int k = 0; k < kvol; ++k) tw[((size_t)i * co + o) * kvol + k] *= sc;
+      bias[o] = (bias[o] - mu[o]) * sc + be[o];
+    }
+  }
+  const int npar = is3d ? 8 : 4, kd = is3d ? 3 : 1;
+  const int cout = npar * co;
+  std::vector<float> w((size_t)cout * ci * kd * 9, 0.f), b(cout, 0.f);
+  auto kidx = [](int parity, int d) { return parity + 1 - 2 * d; };
+  for (int pi = 0; pi < npar; ++pi) {
+    const int pb = pi & 1, pa = (pi >> 1) & 1, pc = is3d ? (pi >> 2) : 0;
+    for (int o = 0; o < co; ++o) {
+      b[pi * co + o] = bias[o];
+      for (int i = 0; i < ci; ++i)
+        for (int dz = 0; dz < kd; ++dz)
+          for (int dy = 0; dy < 3; ++dy)
+            for (int dx = 0; dx < 3; ++dx) {
+              const int ky = kidx(pa, dy - 1), kx = kidx(pb, dx - 1);
+              const int kz = is3d ? kidx(pc, dz - 1) : 0;
+              if (ky < 0 || ky > 3 || kx < 0 || kx > 3 || kz < 0 || kz > 3) continue;
+              const size_t src = is3d ? ((((size_t)i * co + o) * 4 + kz) * 4 + ky) * 4 + kx
+                                      : (((size_t)i * co + o) * 4 + ky) * 4 + kx;
+              w[((((size_t)(pi * co + o) * ci + i) * kd + dz) * 3 + dy) * 3 + dx] = tw[src];
+            }
+    }
+  }
+  ConvSpec sp;
+  sp.kh = sp.kw = 3;
+  sp.ph = sp.pw = 1;
+  if (is3d) {
+    sp.kd = 3;
+    sp.pd = 1;
+    sp.sd = 1;
+  }
+  spec_ = sp;
+  up_ = is3d ? 3 : 2;
+  cout_real_ = co;
+  upload(arena, w, b, cout, ci, in_segs, kd);
+}
+
 void ConvLayer::build_raw(DeviceArena& arena, const std::vector<float>& w, const std::vector<float>& b,
                           int cout, int cin, const std::vector<ChanSeg>& in_segs, ConvSpec spec) {
   if (spec.ph < 0) spec.ph = (spec.kh / 2) * spec.dh;
@@ -252,10 +357,25 @@ SaConvArgs ConvLayer::args(const std::vector<Tensor>& srcs, const Tensor& out) c
   a.pw = spec_.pw;
   a.dh = spec_.dh;
   a.dw = spec_.dw;
-  a.Ho = out_h(a.H);
-  a.Wo = out_w(a.W);
-  SA_REQUIRE(out.n == a.N && out.h == a.Ho && out.w == a.Wo, "conv output shape mismatch (%dx%dx%d vs %dx%dx%d)",
-             out.n, out.h, out.w, a.N, a.Ho, a.Wo);
+  // GEMM rows enumerate the conv's own output grid; transposed convs scatter 2x (up_)
+  a.Ho = up_ ? a.H : out_h(a.H);
+  a.Wo = up_ ? a.W : out_w(a.W);
+  if (spec_.kd > 0) {
+    a.KD = spec_.kd;
+    a.Di = srcs[0].d;
+    a.Do = up_ == 3 ? srcs[0].d : out_d(srcs[0].d);
+    a.sd = spec_.sd;
+    a.pd = spec_.pd;
+    for (size_t i = 1; i < srcs.size(); ++i) SA_REQUIRE(srcs[i].d == srcs[0].d, "3-D conv sources differ in depth");
+  } else {
+    SA_REQUIRE(srcs[0].d == 1, "2-D conv on a volume");
+  }
+  const int oh = up_ ? 2 * a.Ho : a.Ho, ow = up_ ? 2 * a.Wo : a.Wo;
+  const int od = spec_.kd > 0 ? (up_ == 3 ? 2 * a.Do : a.Do) : 1;
+  SA_REQUIRE(out.n == a.N && out.h == oh && out.w == ow && out.d == od,
+             "conv output shape mismatch (%dx%dx%dx%d vs %dx%dx%dx%d)", out.n, out.d, out.h, out.w, a.N, od, oh, ow);
+  a.up = up_;
+  a.cout_real = cout_real_;
   a.weight = wdev_;
   a.bias = bdev_;
   a.Cout = cout_;
@@ -288,7 +408,7 @@ void ConvLayer::launch(hipStream_t s, SaConvArgs& a) const {
 void ConvLayer::run(hipStream_t s, const std::vector<Tensor>& srcs, const Tensor& out, int act,
                     const Tensor* res, int act2, sa_stat_t* stats, float alpha) const {
   SaConvArgs a = args(srcs, out);
-  SA_REQUIRE(out.c >= cout_ || stats == nullptr, "conv output view too narrow");
+  SA_REQUIRE(out.c >= (up_ ? cout_real_ : cout_) || stats == nullptr, "conv output view too narrow");
   a.act = act;
   a.alpha = alpha;
   if (res) {

@@ -76,7 +76,9 @@ class SaConvArgs(C.Structure):
         ("stats", C.c_void_p),
         ("tile_cfg", C.c_int32), ("splitk", C.c_int32),
         ("ws", C.c_void_p), ("counters", C.c_void_p), ("ws_floats", C.c_int64),
-        ("n_counters", C.c_int32), ("_pad2", C.c_int32),
+        ("n_counters", C.c_int32),
+        ("KD", C.c_int32), ("Di", C.c_int32), ("Do", C.c_int32), ("sd", C.c_int32), ("pd", C.c_int32),
+        ("up", C.c_int32), ("cout_real", C.c_int32), ("gate", C.c_void_p), ("gate_stride", C.c_int32),
     ]
 
 
@@ -111,7 +113,7 @@ class SaEwArgs(C.Structure):
     ]
 
 
-ACT = {"none": 0, "relu": 1, "leaky": 2, "tanh": 3, "sigmoid": 4}
+ACT = {"none": 0, "relu": 1, "leaky": 2, "tanh": 3, "sigmoid": 4, "relu6": 5}
 EPI = {"store": 0, "gru_zr": 1, "gru_q": 2, "flow_acc": 3, "store_f32": 4}
 PRE = {"raw": 0, "unit": 1, "imagenet": 2, "signed": 3}
 
@@ -140,6 +142,12 @@ def _declare_dev(lib):
         "sa_flow_features": (_i, [_p, _i, C.c_long, _p, _i, _i, _p, _i, _p]),
         "sa_interp_flow": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _f, _p]),
         "sa_convex_upsample_c": (_i, [_p, _i, _p, _i, _i, _i, _i, _i, _f, _p, _i, _p]),
+        "sa_dwconv3x3": (_i, [_p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
+        "sa_norm_corr_volume": (_i, [_p, _i, _p, _i, _i, _i, _i, _i, _i, _p, _i, _p]),
+        "sa_topk_disparity": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
+        "sa_concat_volume": (_i, [_p, _i, _p, _i, _p, _p, _i, _i, _i, _i, _i, _p, _i, _p]),
+        "sa_topk_regress": (_i, [_p, _i, _p, _i, _i, _i, _i, _i, _p, _p]),
+        "sa_spx_upsample": (_i, [_p, _i, _p, _i, _i, _i, _i, _f, _p, _p]),
         "sa_version": (C.c_char_p, []),
         "sa_last_error": (C.c_char_p, []),
         "sa_engine_create": (_p, [C.c_char_p, C.c_char_p, _i, _i, _i, _i, _i, _i, C.c_ulonglong]),

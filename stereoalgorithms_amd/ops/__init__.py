@@ -18,6 +18,8 @@ __all__ = [
     "splitk_workspace", "pack_conv_weight", "conv2d", "instnorm_apply", "avgpool3s2", "avgpool_k", "interp_bilinear",
     "corr1d_pyramid", "corr1d_lookup", "convex_upsample", "preprocess", "remap_bgr", "reproject",
     "agcl_corr", "linear_attention", "layernorm", "ew", "interp_flow", "convex_upsample_c",
+    "pack_conv3d_weight", "deconv_as_conv_weight", "conv3d", "dwconv3x3", "norm_corr_volume", "topk_disparity",
+    "concat_volume", "topk_regress", "spx_upsample",
 ]
 
 
@@ -66,9 +68,12 @@ def pack_conv_weight(w: torch.Tensor, segs: Sequence[tuple[int, int]] | None = N
 
 def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1, act="none",
            act2="none", res=None, out=None, epi="store", scale=1.0, alpha=0.01, stats=None,
-           ctx=None, aux=None, hbuf=None, rh=None, tile_cfg=-1, splitk=1, workspace=None):
+           ctx=None, aux=None, hbuf=None, rh=None, tile_cfg=-1, splitk=1, workspace=None, up=0, cout_real=0,
+           gate=None):
     """NHWC fp16 implicit-GEMM conv.  ``splitk``: 1 = off, 0 = auto, >1 = forced; needs
-    ``workspace`` = (fp32 slab tensor, int32 counter tensor zero-initialised)."""
+    ``workspace`` = (fp32 slab tensor, int32 counter tensor zero-initialised).  ``up`` = 2: transposed
+    conv, the 4 parity classes (cout = 4 * cout_real) are scattered to a 2x output.  ``gate``: fp16
+    NHWC multiplier applied after the activation."""
     if isinstance(xs, torch.Tensor):
         xs = [xs]
     n, h, w, _ = xs[0].shape
@@ -96,10 +101,14 @@ def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1
     a.KH, a.KW, a.sh, a.sw, a.ph, a.pw, a.dh, a.dw = kh, kw, sh, sw, ph, pw, dil, dil
     a.Ho, a.Wo = ho, wo
     if out is None:
-        if epi == "store_f32":
-            out = torch.empty(n, ho, wo, cout, dtype=torch.float32, device=xs[0].device)
+        dt = torch.float32 if epi == "store_f32" else torch.float16
+        if up:
+            out = torch.empty(n, 2 * ho, 2 * wo, cout_real, dtype=dt, device=xs[0].device)
         else:
-            out = torch.empty(n, ho, wo, cout, dtype=torch.float16, device=xs[0].device)
+            out = torch.empty(n, ho, wo, cout, dtype=dt, device=xs[0].device)
+    a.up, a.cout_real = up, cout_real
+    if gate is not None:
+        a.gate, a.gate_stride = gate.data_ptr(), _pix_stride(gate)
     a.weight = wpacked.data_ptr()
     a.bias = bias.data_ptr() if bias is not None else None
     a.Cout, a.Kpad = cout, kpad
@@ -311,4 +320,135 @@ def convex_upsample_c(mask, flow, factor, sign=1.0, oc=2):
     out = torch.empty(n, h * factor, w * factor, oc, dtype=torch.float32, device=flow.device)
     N.check(N.dev().sa_convex_upsample_c(_ptr(mask), _pix_stride(mask), _ptr(flow), fc, n, h, w, factor, sign,
                                          _ptr(out), oc, _stream()), "sa_convex_upsample_c")
+    return out
+
+
+# ------------------------------------------------------------------------------ Fast-ACVNet+ ops
+def pack_conv3d_weight(w: torch.Tensor, cin_pad: int | None = None):
+    """[Cout, Cin, KD, KH, KW] -> fp16 [round_up(Cout,128), Kpad], K ordered (kd, kh, kw, ci_padded)."""
+    cout, cin, kd, kh, kw = w.shape
+    cin_pad = cin_pad or (cin + 7) // 8 * 8
+    wp = torch.zeros(cout, kd, kh, kw, cin_pad, dtype=torch.float32, device=w.device)
+    wp[..., :cin] = w.permute(0, 2, 3, 4, 1).float()
+    k = kd * kh * kw * cin_pad
+    kpad = (k + 63) // 64 * 64
+    out = torch.zeros((cout + 127) // 128 * 128, kpad, dtype=torch.float16, device=w.device)
+    out[:cout, :k] = wp.reshape(cout, k).half()
+    return out.contiguous(), kpad, cin_pad
+
+
+def deconv_as_conv_weight(wt: torch.Tensor) -> torch.Tensor:
+    """ConvTranspose{2,3}d(k=4, s=2, p=1) weight [Cin, Cout, 4, 4(, 4)] -> equivalent 3x3(x3) stride-1 conv
+    weight [P*Cout, Cin, (3,) 3, 3] whose output channel p*Cout + o is parity class p (bit0 = x, bit1 = y,
+    bit2 = z) of output channel o:  out[2i + a] = sum_d in[i + d] * Wt[a + 1 - 2d], d in {-1, 0, 1}."""
+    is3d = wt.dim() == 5
+    ci, co = wt.shape[:2]
+    npar = 8 if is3d else 4
+    w = torch.zeros(npar * co, ci, *([3] * (3 if is3d else 2)), dtype=wt.dtype, device=wt.device)
+    for p in range(npar):
+        pb, pa, pc = p & 1, (p >> 1) & 1, p >> 2
+        for dy in range(3):
+            ky = pa + 1 - 2 * (dy - 1)
+            for dx in range(3):
+                kx = pb + 1 - 2 * (dx - 1)
+                if not (0 <= ky < 4 and 0 <= kx < 4):
+                    continue
+                if not is3d:
+                    w[p * co:(p + 1) * co, :, dy, dx] = wt[:, :, ky, kx].t()
+                    continue
+                for dz in range(3):
+                    kz = pc + 1 - 2 * (dz - 1)
+                    if 0 <= kz < 4:
+                        w[p * co:(p + 1) * co, :, dz, dy, dx] = wt[:, :, kz, ky, kx].t()
+    return w
+
+
+def conv3d(x, wpacked, kpad, cout, k=3, stride=1, pad=None, bias=None, act="none", alpha=0.01, gate=None,
+           up=0, cout_real=0, out=None):
+    """NDHWC fp16 volume [N, D, H, W, C] conv (implicit GEMM over (kd, kh, kw, ci)).  ``gate``: fp16
+    [N, H, W, >=cout] multiplied after the activation (broadcast over depth).  ``up`` = 3 scatters the
+    8 parity classes of a transposed conv (cout = 8 * cout_real)."""
+    n, d, h, w, c = x.shape
+    assert x.dtype == torch.float16 and x.is_contiguous()
+    pad = k // 2 if pad is None else pad
+    a = N.SaConvArgs()
+    a.src[0].ptr, a.src[0].channels, a.src[0].stride = x.data_ptr(), c, c
+    a.nsrc = 1
+    a.N, a.H, a.W, a.Cin = n, h, w, c
+    a.KH = a.KW = a.KD = k
+    a.sh = a.sw = a.sd = stride
+    a.ph = a.pw = a.pd = pad
+    a.dh = a.dw = 1
+    a.Ho, a.Wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
+    a.Di, a.Do = d, (d + 2 * pad - k) // stride + 1
+    oc = cout_real if up else cout
+    if out is None:
+        shape = (n, 2 * a.Do, 2 * a.Ho, 2 * a.Wo, oc) if up else (n, a.Do, a.Ho, a.Wo, oc)
+        out = torch.zeros(shape, dtype=torch.float16, device=x.device)
+    a.weight = wpacked.data_ptr()
+    a.bias = bias.data_ptr() if bias is not None else None
+    a.Cout, a.Kpad = cout, kpad
+    a.out, a.out_stride = out.data_ptr(), out.shape[-1]
+    a.epi, a.act, a.alpha, a.scale = N.EPI["store"], N.ACT[act], alpha, 1.0
+    a.tile_cfg, a.splitk = -1, 1
+    a.up, a.cout_real = up, cout_real
+    if gate is not None:
+        a.gate, a.gate_stride = gate.data_ptr(), _pix_stride(gate)
+    N.check(N.dev().sa_conv2d(C.byref(a), _stream()), "sa_conv2d(3d)")
+    return out
+
+
+def dwconv3x3(x, w, b, stride=1, act="none"):
+    """Depthwise 3x3 (pad 1) on fp16 NHWC; w fp32 [C, 9], b fp32 [C]."""
+    n, h, wd, c = x.shape
+    ho, wo = (h - 1) // stride + 1, (wd - 1) // stride + 1
+    out = torch.empty(n, ho, wo, c, dtype=torch.float16, device=x.device)
+    N.check(N.dev().sa_dwconv3x3(_ptr(x), _pix_stride(x), _ptr(w.float().contiguous()), _ptr(b.float().contiguous()),
+                                 _ptr(out), c, n, h, wd, c, stride, N.ACT[act], _stream()), "sa_dwconv3x3")
+    return out
+
+
+def norm_corr_volume(l, r, D, out_channels=8):
+    n, h, w, c = l.shape
+    out = torch.empty(n, D, h, w, out_channels, dtype=torch.float16, device=l.device)
+    N.check(N.dev().sa_norm_corr_volume(_ptr(l), _pix_stride(l), _ptr(r), _pix_stride(r), n, h, w, c, D, _ptr(out),
+                                        out_channels, _stream()), "sa_norm_corr_volume")
+    return out
+
+
+def topk_disparity(att, K):
+    """att: fp16 volume [N, D, H, W, s] (channel 0) -> (prob, disp) fp32 [N, H, W, K]."""
+    n, d, h, w, s = att.shape
+    prob = torch.empty(n, h, w, K, dtype=torch.float32, device=att.device)
+    disp = torch.empty_like(prob)
+    N.check(N.dev().sa_topk_disparity(_ptr(att), s, n, d, h, w, K, _ptr(prob), _ptr(disp), _stream()),
+            "sa_topk_disparity")
+    return prob, disp
+
+
+def concat_volume(l, r, prob, disp, out_channels=None):
+    n, h, w, c = l.shape
+    K = prob.shape[-1]
+    oc = out_channels or 2 * c
+    out = torch.empty(n, K, h, w, oc, dtype=torch.float16, device=l.device)
+    N.check(N.dev().sa_concat_volume(_ptr(l), _pix_stride(l), _ptr(r), _pix_stride(r), _ptr(prob), _ptr(disp), n, h, w,
+                                     c, K, _ptr(out), oc, _stream()), "sa_concat_volume")
+    return out
+
+
+def topk_regress(cost, disp, top=2):
+    """cost: fp16 volume [N, K, H, W, s] (channel 0), disp fp32 [N, H, W, K] -> fp32 [N, H, W]."""
+    n, k, h, w, s = cost.shape
+    out = torch.empty(n, h, w, dtype=torch.float32, device=cost.device)
+    N.check(N.dev().sa_topk_regress(_ptr(cost), s, _ptr(disp), n, k, h, w, top, _ptr(out), _stream()),
+            "sa_topk_regress")
+    return out
+
+
+def spx_upsample(spx, pred, f=4, scale=4.0):
+    """spx: fp16 NHWC [N, f*h, f*w, >=9] logits, pred fp32 [N, h, w] -> fp32 [N, f*h, f*w]."""
+    n, h, w = pred.shape
+    out = torch.empty(n, h * f, w * f, dtype=torch.float32, device=pred.device)
+    N.check(N.dev().sa_spx_upsample(_ptr(spx), _pix_stride(spx), _ptr(pred.contiguous()), n, h, w, f, scale,
+                                    _ptr(out), _stream()), "sa_spx_upsample")
     return out
