@@ -86,6 +86,12 @@ class StereoEngine {
   // (positive disparity, fp32 [B][H][W]).
   virtual void forward(hipStream_t s) = 0;
 
+  // Activation taps (debugging / numerics bisection): with SA_TAP_DIR set and eager launches
+  // (SA_NO_GRAPH=1) each tapped tensor is written to $SA_TAP_DIR/<name>.sat after the stream drains
+  // (int32 header n,d,h,w,c,stride,dtype then the raw strided elements).  No-op otherwise.
+  void tap(hipStream_t s, const char* name, const Tensor& t) const;
+  void tap_f32(hipStream_t s, const char* name, const float* p, int n, int h, int w, int c) const;
+
   void frame(hipStream_t s, bool rectify);  // the captured body
   void launch_frame(hipStream_t s, bool rectify);
 

@@ -210,6 +210,24 @@ int sa_topk_regress(const void* cost, int cs, const float* disp, int N, int K, i
 int sa_spx_upsample(const void* spx, int ss, const float* pred, int N, int h, int w, int f, float scale, float* out,
                     hipStream_t stream);
 
+// ---- HITNet tile hypotheses (hitnet_ops.hip) --------------------------------------------------
+// L1 tile matching cost over d in [0, D) + argmin -> cmin (fp16, channel 0 of a stride-cs pixel; 1..7
+// zero) and d_init (fp32) per tile; tl [B][th][tw][16], tr [B][th][wr][16] (stride-(4,1) tile features)
+int sa_hitnet_tile_init(const void* tl, int tls, const void* tr, int trs, int B, int th, int tw, int wr, int D,
+                        void* cmin, int cs, float* dinit, hipStream_t stream);
+// hyp [P][16] fp32 = [d_init, 0, 0, desc[0..12]]
+int sa_hitnet_hyp_init(const float* dinit, const void* desc, int ds, long P, float* hyp, hipStream_t stream);
+// local warped L1 cost (48 ch) + fp16 hypothesis copy (16 ch) -> out [ncand*B][H/4][W/4][64]
+int sa_hitnet_warp_cost(const void* el, int els, const void* er, int ers, int B, int H, int W, int C,
+                        const float* hyp, int ncand, void* out, hipStream_t stream);
+// refine (cand + delta) and keep the most confident of ncand candidates -> out [P][16]
+int sa_hitnet_select(const float* cand, int ncand, long P, const float* delta, int dstr, float* out,
+                     hipStream_t stream);
+// slanted-plane 2x upsampling of tile hypotheses [B][th][tw][16] -> [B][2th][2tw][16]
+int sa_hitnet_upsample(const float* h, int B, int th, int tw, float* out, hipStream_t stream);
+// level-0 tiles -> full-resolution disparity [B][4th][4tw]
+int sa_hitnet_expand(const float* h, int B, int th, int tw, float* disp, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

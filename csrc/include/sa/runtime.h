@@ -138,7 +138,8 @@ class ConvLayer {
   void build3d(DeviceArena& arena, const WeightStore& ws, const std::string& wname, const std::vector<ChanSeg>& in_segs,
                ConvSpec spec, const std::string& bn_name = "", float bn_eps = 1e-5f);
   // ConvTranspose2d/3d(k=4, s=2, p=1) (weight [Cin][Cout][4][4](4), optional bias / BN fold) as a
-  // 3x3(x3) conv producing 4 (8) parity classes scattered by the epilogue (SaConvArgs.up)
+  // 3x3(x3) conv producing 4 (8) parity classes scattered by the epilogue (SaConvArgs.up);
+  // ConvTranspose2d(k=2, s=2) weights ([Cin][Cout][2][2]) become a 1x1 conv with the same scatter.
   void build_deconv(DeviceArena& arena, const WeightStore& ws, const std::string& wname, bool is3d,
                     const std::vector<ChanSeg>& in_segs, const std::string& bn_name = "", float bn_eps = 1e-5f);
   // Build from explicit host arrays (used by the native random-init path and tests).

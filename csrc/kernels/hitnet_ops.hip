@@ -1,0 +1,266 @@
+// HITNet tile-hypothesis kernels (SURVEY.md §2.2 M3, §2.6 "cost volume L1 + argmin", "slanted-plane
+// upsample / hypothesis select").  Oracle: stereoalgorithms_amd/models/hitnet.py.
+//
+// Hypotheses are fp32 [n][th][tw][16] = [d, dx, dy, p0..p12] (d in level pixels); the conv layers that
+// refine them consume an fp16 copy written next to the local cost features (one 64-channel source).
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include "sa/kernels.h"
+
+namespace {
+typedef _Float16 f16;
+typedef f16 half8 __attribute__((ext_vector_type(8)));
+typedef float float4_ __attribute__((ext_vector_type(4)));
+
+inline int grid_for(long work, int block = 256) {
+  long g = (work + block - 1) / block;
+  if (g > 16384) g = 16384;
+  return g < 1 ? 1 : (int)g;
+}
+
+__device__ __forceinline__ void load16(const f16* p, float* v) {
+  const half8 a = *reinterpret_cast<const half8*>(p);
+  const half8 b = *reinterpret_cast<const half8*>(p + 8);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    v[j] = (float)a[j];
+    v[8 + j] = (float)b[j];
+  }
+}
+
+// Tile initialisation: cost(x, d) = sum_c |tl(x) - tr(4x - d)|, argmin over d in [0, D) (first
+// minimum), invalid right columns excluded.  One thread per tile; the 16-channel left tile feature
+// lives in registers, right features stream through L1/L2 (adjacent tiles read overlapping rows).
+__global__ void __launch_bounds__(256) tile_init_kernel(const f16* __restrict__ tl, int tls, const f16* __restrict__ tr,
+                                                        int trs, int B, int th, int tw, int wr, int D,
+                                                        f16* __restrict__ cmin, int cs, float* __restrict__ dinit) {
+  const long P = (long)B * th * tw;
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
+    const int x = (int)(p % tw);
+    const long row = p / tw;  // n * th + y
+    float l[16];
+    load16(tl + p * tls, l);
+    const f16* rrow = tr + row * (long)wr * trs;
+    float best = 3.0e38f;
+    int bd = 0;
+    const int dmax = min(D, 4 * x + 1);  // j = 4x - d >= 0
+    for (int d = 0; d < dmax; ++d) {
+      const int j = 4 * x - d;
+      if (j >= wr) continue;
+      float r[16];
+      load16(rrow + (long)j * trs, r);
+      float c = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) c += fabsf(l[k] - r[k]);
+      if (c < best) {
+        best = c;
+        bd = d;
+      }
+    }
+    half8 o = {0, 0, 0, 0, 0, 0, 0, 0};
+    o[0] = (f16)best;
+    *reinterpret_cast<half8*>(cmin + p * cs) = o;
+    dinit[p] = (float)bd;
+  }
+}
+
+// hyp = [d_init, 0, 0, desc[0..12]]
+__global__ void hyp_init_kernel(const float* __restrict__ dinit, const f16* __restrict__ desc, int ds, long P,
+                                float* __restrict__ hyp) {
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
+    float h[16];
+    h[0] = dinit[p];
+    h[1] = h[2] = 0.f;
+    float dv[16];
+    load16(desc + p * ds, dv);
+#pragma unroll
+    for (int k = 0; k < 13; ++k) h[3 + k] = dv[k];
+    float4_* o = reinterpret_cast<float4_*>(hyp + p * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = float4_{h[4 * q], h[4 * q + 1], h[4 * q + 2], h[4 * q + 3]};
+  }
+}
+
+// Local cost of candidate n (image n % B): for the 16 tile pixels (u, v) and shifts s in {-1,0,1}:
+// sum_c |el(4y+v, 4x+u) - er_lin(4y+v, 4x+u - (d + dx(u-1.5) + dy(v-1.5) + s))|  (zero outside)
+// -> out[n][y][x][s*16 + v*4 + u]; channels 48..63 = fp16 copy of the hypothesis.
+template <int C>
+__global__ void __launch_bounds__(256) warp_cost_kernel(const f16* __restrict__ el, int els, const f16* __restrict__ er,
+                                                        int ers, int B, int H, int W, const float* __restrict__ hyp,
+                                                        int ncand, int th, int tw, f16* __restrict__ out) {
+  const long P = (long)ncand * B * th * tw;
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
+    const int x = (int)(p % tw);
+    const int y = (int)((p / tw) % th);
+    const int n = (int)(p / ((long)tw * th));
+    const int img = n % B;
+    const float* h = hyp + p * 16;
+    const float d = h[0], sx = h[1], sy = h[2];
+    f16 res[64];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int py = 4 * y + v;
+      const f16* lrow = el + ((long)img * H + py) * W * els;
+      const f16* rrow = er + ((long)img * H + py) * W * ers;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int px = 4 * x + u;
+        float lv[C];
+#pragma unroll
+        for (int c0 = 0; c0 < C; c0 += 8) {
+          const half8 a = *reinterpret_cast<const half8*>(lrow + (long)px * els + c0);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) lv[c0 + j] = (float)a[j];
+        }
+        const float dp = d + sx * ((float)u - 1.5f) + sy * ((float)v - 1.5f);
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const float xr = (float)px - (dp + (float)(s - 1));
+          const float x0f = floorf(xr);
+          const float a = xr - x0f;
+          const int x0 = (int)x0f;
+          float cost = 0.f;
+          const bool ok0 = x0 >= 0 && x0 <= W - 1, ok1 = x0 + 1 >= 0 && x0 + 1 <= W - 1;
+#pragma unroll
+          for (int c0 = 0; c0 < C; c0 += 8) {
+            half8 r0 = {0, 0, 0, 0, 0, 0, 0, 0}, r1 = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (ok0) r0 = *reinterpret_cast<const half8*>(rrow + (long)x0 * ers + c0);
+            if (ok1) r1 = *reinterpret_cast<const half8*>(rrow + (long)(x0 + 1) * ers + c0);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) cost += fabsf(lv[c0 + j] - ((1.f - a) * (float)r0[j] + a * (float)r1[j]));
+          }
+          res[s * 16 + v * 4 + u] = (f16)cost;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) res[48 + k] = (f16)h[k];
+    half8* o = reinterpret_cast<half8*>(out + p * 64);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      half8 t;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] = res[q * 8 + j];
+      o[q] = t;
+    }
+  }
+}
+
+// h' = cand + delta[:16] (d clamped >= 0), conf = delta[16]; keep the first candidate with the
+// strictly highest confidence.  cand / delta: [ncand][B][th][tw][...]
+__global__ void select_kernel(const float* __restrict__ cand, int ncand, long P, const float* __restrict__ delta,
+                              int dstr, float* __restrict__ out) {
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
+    int best = 0;
+    float bc = -3.0e38f;
+    for (int k = 0; k < ncand; ++k) {
+      const float c = delta[((long)k * P + p) * dstr + 16];
+      if (k == 0 || c > bc) {
+        bc = c;
+        best = k;
+      }
+    }
+    const float* h = cand + ((long)best * P + p) * 16;
+    const float* dl = delta + ((long)best * P + p) * dstr;
+    float r[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r[k] = h[k] + dl[k];
+    r[0] = fmaxf(r[0], 0.f);
+    float4_* o = reinterpret_cast<float4_*>(out + p * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = float4_{r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]};
+  }
+}
+
+// slanted-plane 2x upsampling: fine tile (2i+a, 2j+b) of coarse tile (i, j):
+// d' = 2 (d + dx (2b-1) + dy (2a-1)), slopes and descriptor copied
+__global__ void upsample_kernel(const float* __restrict__ h, int B, int th, int tw, float* __restrict__ out) {
+  const int TH = 2 * th, TW = 2 * tw;
+  const long P = (long)B * TH * TW;
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
+    const int X = (int)(p % TW);
+    const int Y = (int)((p / TW) % TH);
+    const int n = (int)(p / ((long)TW * TH));
+    const float* s = h + (((long)n * th + Y / 2) * tw + X / 2) * 16;
+    float r[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r[k] = s[k];
+    r[0] = 2.f * (s[0] + s[1] * (float)(2 * (X & 1) - 1) + s[2] * (float)(2 * (Y & 1) - 1));
+    float4_* o = reinterpret_cast<float4_*>(out + p * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = float4_{r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]};
+  }
+}
+
+// full-resolution disparity from level-0 tiles: max(0, d + dx (u-1.5) + dy (v-1.5))
+__global__ void expand_kernel(const float* __restrict__ h, int B, int th, int tw, float* __restrict__ disp) {
+  const int H = 4 * th, W = 4 * tw;
+  const long P = (long)B * H * W;
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
+    const int x = (int)(p % W);
+    const int y = (int)((p / W) % H);
+    const int n = (int)(p / ((long)W * H));
+    const float* s = h + (((long)n * th + y / 4) * tw + x / 4) * 16;
+    const float d = s[0] + s[1] * ((float)(x & 3) - 1.5f) + s[2] * ((float)(y & 3) - 1.5f);
+    disp[p] = fmaxf(d, 0.f);
+  }
+}
+
+}  // namespace
+
+extern "C" int sa_hitnet_tile_init(const void* tl, int tls, const void* tr, int trs, int B, int th, int tw, int wr,
+                                   int D, void* cmin, int cs, float* dinit, hipStream_t stream) {
+  if (tls % 8 || trs % 8 || cs < 8 || cs % 8) return -2;
+  hipLaunchKernelGGL(tile_init_kernel, dim3(grid_for((long)B * th * tw)), dim3(256), 0, stream, (const f16*)tl, tls,
+                     (const f16*)tr, trs, B, th, tw, wr, D, (f16*)cmin, cs, dinit);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_hitnet_hyp_init(const float* dinit, const void* desc, int ds, long P, float* hyp,
+                                  hipStream_t stream) {
+  if (ds < 16 || ds % 8) return -2;
+  hipLaunchKernelGGL(hyp_init_kernel, dim3(grid_for(P)), dim3(256), 0, stream, dinit, (const f16*)desc, ds, P, hyp);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_hitnet_warp_cost(const void* el, int els, const void* er, int ers, int B, int H, int W, int C,
+                                   const float* hyp, int ncand, void* out, hipStream_t stream) {
+  if (H % 4 || W % 4 || els % 8 || ers % 8) return -2;
+  const int th = H / 4, tw = W / 4;
+  const long P = (long)ncand * B * th * tw;
+  switch (C) {
+    case 16:
+      hipLaunchKernelGGL(warp_cost_kernel<16>, dim3(grid_for(P, 128)), dim3(128), 0, stream, (const f16*)el, els,
+                         (const f16*)er, ers, B, H, W, hyp, ncand, th, tw, (f16*)out);
+      break;
+    case 24:
+      hipLaunchKernelGGL(warp_cost_kernel<24>, dim3(grid_for(P, 128)), dim3(128), 0, stream, (const f16*)el, els,
+                         (const f16*)er, ers, B, H, W, hyp, ncand, th, tw, (f16*)out);
+      break;
+    case 32:
+      hipLaunchKernelGGL(warp_cost_kernel<32>, dim3(grid_for(P, 128)), dim3(128), 0, stream, (const f16*)el, els,
+                         (const f16*)er, ers, B, H, W, hyp, ncand, th, tw, (f16*)out);
+      break;
+    default:
+      return -2;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_hitnet_select(const float* cand, int ncand, long P, const float* delta, int dstr, float* out,
+                                hipStream_t stream) {
+  if (dstr < 17) return -2;
+  hipLaunchKernelGGL(select_kernel, dim3(grid_for(P)), dim3(256), 0, stream, cand, ncand, P, delta, dstr, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_hitnet_upsample(const float* h, int B, int th, int tw, float* out, hipStream_t stream) {
+  hipLaunchKernelGGL(upsample_kernel, dim3(grid_for((long)B * th * tw * 4)), dim3(256), 0, stream, h, B, th, tw, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_hitnet_expand(const float* h, int B, int th, int tw, float* disp, hipStream_t stream) {
+  hipLaunchKernelGGL(expand_kernel, dim3(grid_for((long)B * th * tw * 16)), dim3(256), 0, stream, h, B, th, tw, disp);
+  return (int)hipGetLastError();
+}

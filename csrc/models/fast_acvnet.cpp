@@ -351,6 +351,7 @@ void FastAcvNet::forward(hipStream_t s) {
   stem_conv_.run(s, {img_}, s0_, SA_ACT_RELU6);
   b0dw_.run(s, s0_, b0t_, SA_ACT_RELU6);
   b0pw_.run(s, {b0t_}, x2_);
+  tap(s, "x2", x2_);
   const Tensor* x = &x2_;
   for (const auto& b : blocks_) {
     b.run(s, *x);
@@ -365,32 +366,55 @@ void FastAcvNet::forward(hipStream_t s) {
   up8_1_.run(s, {x8u_}, d4_, SA_ACT_LEAKY);
   up8_2_.run(s, {d4_, x4}, x4c_, SA_ACT_LEAKY);
   conv4_.run(s, {x4c_}, x4u_, SA_ACT_LEAKY);
+  tap(s, "x4", x4);
+  tap(s, "x8", x8);
+  tap(s, "x16", x16);
+  tap(s, "x32", x32);
+  tap(s, "x16u", x16u_);
+  tap(s, "x8u", x8u_);
+  tap(s, "x4u", x4u_);
   // stems
   st2a_.run(s, {img_}, st2t_, SA_ACT_LEAKY);
   st2b_.run(s, {st2t_}, st2_, SA_ACT_RELU);
   st4a_.run(s, {st2_}, st4t_, SA_ACT_LEAKY);
   st4b_.run(s, {st4t_}, st4_, SA_ACT_RELU);
+  tap(s, "stem2", st2_);
+  tap(s, "stem4", st4_);
   const std::vector<Tensor> f0 = {x4u_, st4_};
   const std::vector<Tensor> f0l = {x4u_.slice_n(0, B), st4_.slice_n(0, B)};
   // matching descriptors + normalised correlation volume
   mconv_.run(s, f0, m48_, SA_ACT_LEAKY);
   mdesc_.run(s, {m48_}, match_);
+  tap(s, "match", match_);
   const int D = kMaxDisp / 4;
   check(sa_norm_corr_volume(match_.ptr, 48, match_.slice_n(B, B).ptr, 48, B, h, w, 48, D, cvol_.ptr, 8, s), "corr vol");
   gcorr_.run(s, f0l);
   run_gated(s, corr_stem_, {cvol_}, cost0_, &gcorr_);
+  tap(s, "corr_vol", cvol_);
+  tap(s, "corr_gate", gcorr_.g);
+  tap(s, "cost0", cost0_);
   const Tensor x8l = x8u_.slice_n(0, B), x16l = x16u_.slice_n(0, B);
   hg_att_.run(s, cost0_, x8l, x16l);
+  tap(s, "hga_conv1", hg_att_.v1b);
+  tap(s, "hga_conv2", hg_att_.v2b);
+  tap(s, "hga_agg", hg_att_.ag1);
+  tap(s, "att_weights", hg_att_.out);
   check(sa_topk_disparity(hg_att_.out.ptr, hg_att_.out.stride, B, D, h, w, kTopK, prob_, dsamp_, s), "topk");
   // attention-weighted concatenation volume at the sampled disparities
   cf0_.run(s, f0, cft_, SA_ACT_LEAKY);
   cf1_.run(s, {cft_}, cfeat_);
+  tap_f32(s, "prob", prob_, B, h, w, kTopK);
+  tap_f32(s, "samples", dsamp_, B, h, w, kTopK);
+  tap(s, "concat_feat", cfeat_);
   check(sa_concat_volume(cfeat_.ptr, 16, cfeat_.slice_n(B, B).ptr, 16, prob_, dsamp_, B, h, w, 16, kTopK, cvol2_.ptr,
                          32, s),
         "concat volume");
   gconcat_.run(s, f0l);
   run_gated(s, concat_stem_, {cvol2_}, cost1_, &gconcat_);
   hg_.run(s, cost1_, x8l, x16l);
+  tap(s, "concat_vol", cvol2_);
+  tap(s, "cost1", cost1_);
+  tap(s, "cost", hg_.out);
   check(sa_topk_regress(hg_.out.ptr, hg_.out.stride, dsamp_, B, kTopK, h, w, 2, pred_, s), "regress");
   // spx upsampling
   spx4a_.run(s, f0l, sx4t_, SA_ACT_LEAKY);
@@ -398,6 +422,10 @@ void FastAcvNet::forward(hipStream_t s) {
   spx2c1_.run(s, {sx4_}, sxu_, SA_ACT_LEAKY);
   spx2c2_.run(s, {sxu_, st2_.slice_n(0, B)}, sx2_, SA_ACT_LEAKY);
   spx_.run(s, {sx2_}, spxo_);
+  tap_f32(s, "pred", pred_, B, h, w, 1);
+  tap(s, "spx4", sx4_);
+  tap(s, "spx2", sx2_);
+  tap(s, "spx_logits", spxo_);
   check(sa_spx_upsample(spxo_.ptr, spxo_.stride, pred_, B, h, w, 4, 4.f, disp_, s), "spx upsample");
 }
 

@@ -3,6 +3,7 @@
 #include "sa/engine.h"
 
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -147,6 +148,36 @@ void StereoEngine::set_rectify_maps(const float* ml, const float* mr) {
   if (!rect_maps_) rect_maps_ = (float*)arena_.alloc(2 * n * 4);
   HIP_CHECK(hipMemcpy(rect_maps_, ml, n * 4, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(rect_maps_ + n, mr, n * 4, hipMemcpyHostToDevice));
+}
+
+void StereoEngine::tap(hipStream_t s, const char* name, const Tensor& t) const {
+  if (cfg_.use_graph) return;
+  const char* dir = std::getenv("SA_TAP_DIR");
+  if (!dir || !dir[0]) return;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HIP_CHECK(hipStreamIsCapturing(s, &cs));
+  if (cs != hipStreamCaptureStatusNone) return;
+  HIP_CHECK(hipStreamSynchronize(s));
+  std::vector<char> host(t.nbytes());
+  HIP_CHECK(hipMemcpy(host.data(), t.ptr, host.size(), hipMemcpyDeviceToHost));
+  const std::string path = std::string(dir) + "/" + name + ".sat";
+  FILE* f = std::fopen(path.c_str(), "wb");
+  SA_REQUIRE(f != nullptr, "cannot write tap %s", path.c_str());
+  const int32_t hdr[7] = {t.n, t.d, t.h, t.w, t.c, t.stride, (int32_t)t.dt};
+  std::fwrite(hdr, sizeof(hdr), 1, f);
+  std::fwrite(host.data(), 1, host.size(), f);
+  std::fclose(f);
+}
+
+void StereoEngine::tap_f32(hipStream_t s, const char* name, const float* p, int n, int h, int w, int c) const {
+  Tensor t;
+  t.ptr = const_cast<float*>(p);
+  t.n = n;
+  t.h = h;
+  t.w = w;
+  t.c = t.stride = c;
+  t.dt = DT::F32;
+  tap(s, name, t);
 }
 
 void StereoEngine::frame(hipStream_t s, bool rectify) {

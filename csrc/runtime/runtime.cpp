@@ -267,8 +267,31 @@ void ConvLayer::build_deconv(DeviceArena& arena, const WeightStore& ws, const st
   const HostTensor& wt = ws.get(wname + ".weight");
   const int dims = is3d ? 3 : 2;
   SA_REQUIRE((int)wt.shape.size() == 2 + dims, "%s: expected %d-D transposed-conv weight", wname.c_str(), 2 + dims);
-  for (int k = 0; k < dims; ++k) SA_REQUIRE(wt.shape[2 + k] == 4, "%s: only k=4 s=2 p=1 deconvs", wname.c_str());
   const int ci = (int)wt.shape[0], co = (int)wt.shape[1];
+  if (!is3d && wt.shape[2] == 2 && wt.shape[3] == 2) {
+    // ConvTranspose2d(k=2, s=2, p=0): out[2i + a][2j + b] = sum_ci in[i][j] * Wt[ci][co][a][b] — a 1x1
+    // conv with the 4 parity classes stacked along Cout (class p = 2a + b)
+    SA_REQUIRE(bn.empty(), "%s: BN fold not supported for k=2 deconvs", wname.c_str());
+    std::vector<float> bias(co, 0.f);
+    if (ws.has(wname + ".bias")) bias = ws.get(wname + ".bias").data;
+    std::vector<float> w((size_t)4 * co * ci), b(4 * co);
+    for (int pi = 0; pi < 4; ++pi) {
+      const int pa = pi >> 1, pb = pi & 1;
+      for (int o = 0; o < co; ++o) {
+        b[pi * co + o] = bias[o];
+        for (int i = 0; i < ci; ++i) w[(size_t)(pi * co + o) * ci + i] = wt.data[(((size_t)i * co + o) * 2 + pa) * 2 + pb];
+      }
+    }
+    ConvSpec sp;
+    sp.kh = sp.kw = 1;
+    sp.ph = sp.pw = 0;
+    spec_ = sp;
+    up_ = 2;
+    cout_real_ = co;
+    upload(arena, w, b, 4 * co, ci, in_segs);
+    return;
+  }
+  for (int k = 0; k < dims; ++k) SA_REQUIRE(wt.shape[2 + k] == 4, "%s: only k=4 s=2 p=1 / k=2 s=2 deconvs", wname.c_str());
   std::vector<float> bias(co, 0.f);
   if (ws.has(wname + ".bias")) bias = ws.get(wname + ".bias").data;
   // BN fold on the transposed weight's output channels
