@@ -217,4 +217,41 @@ int sa_reproject_cpu(const float* disp, int h, int w, const double* Q16, float* 
   return 0;
 }
 
+// ---------------------------------------------------------------- calibration tool
+// gray u8 [h][w] -> corners [cols*rows][2] (row-major from the top-left); returns 1 if found
+int sa_find_chessboard(const uint8_t* gray, int h, int w, int cols, int rows, int subpix, double* out) {
+  Mat g(h, w, SA_8UC1, const_cast<uint8_t*>(gray));
+  std::vector<std::array<double, 2>> c;
+  if (!find_chessboard_corners(g, cols, rows, c)) return 0;
+  if (subpix) corner_subpix(g, c, 5, 30, 1e-3);
+  for (size_t i = 0; i < c.size(); ++i) out[2 * i] = c[i][0], out[2 * i + 1] = c[i][1];
+  return 1;
+}
+
+// newline-separated alternating left/right image paths -> calibration handle filled in;
+// rms[3] = left, right, stereo RMS; returns the number of pairs used (< 0 on failure)
+int sa_stereo_calibrate_images(const char* paths, int cols, int rows, double square, int subpix, void* calib,
+                               double* rms) {
+  std::vector<std::string> list;
+  std::string cur;
+  for (const char* q = paths; ; ++q) {
+    if (*q == '\n' || *q == 0) {
+      if (!cur.empty()) list.push_back(cur);
+      cur.clear();
+      if (!*q) break;
+    } else {
+      cur += *q;
+    }
+  }
+  try {
+    StereoCalibReport rep;
+    if (!run_stereo_calibration(list, cols, rows, square, subpix != 0, *static_cast<CalibrationParam*>(calib), &rep))
+      return -1;
+    if (rms) rms[0] = rep.rms_left, rms[1] = rep.rms_right, rms[2] = rep.rms_stereo;
+    return (int)rep.used.size();
+  } catch (const std::exception&) {
+    return -2;
+  }
+}
+
 }  // extern "C"

@@ -100,4 +100,15 @@ double stereo_calibrate(const std::vector<std::vector<std::array<double, 3>>>& o
                         const std::vector<std::vector<std::array<double, 2>>>& img2, CameraCalib& c1,
                         CameraCalib& c2, Mat& R, Mat& T, int max_iters = 100, double eps = 1e-5);
 
+struct StereoCalibReport {
+  std::vector<std::string> used, skipped;  // left image of each pair
+  double rms_left = 0, rms_right = 0, rms_stereo = 0;
+  int width = 0, height = 0;
+  std::vector<std::vector<std::array<double, 2>>> corners_left, corners_right;
+};
+// The whole Stereo_Calibration pipeline over an alternating left/right image list
+// (Stereo_Calibration.cpp:67-182).  Fills every CalibrationParam field incl. ROIs.
+bool run_stereo_calibration(const std::vector<std::string>& images, int cols, int rows, double square, bool subpix,
+                            CalibrationParam& out, StereoCalibReport* report = nullptr);
+
 }  // namespace sa

@@ -56,6 +56,9 @@ def lib():
             "sa_rodrigues_inv": (C.c_int, [_d, _d]),
             "sa_remap_u8_cpu": (C.c_int, [_u8, C.c_int, C.c_int, C.c_int, _f, _u8]),
             "sa_reproject_cpu": (C.c_int, [_f, C.c_int, C.c_int, _d, _f]),
+            "sa_find_chessboard": (C.c_int, [_u8, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _d]),
+            "sa_stereo_calibrate_images": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_double, C.c_int, C.c_void_p,
+                                                     _d]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name, None)
@@ -225,3 +228,24 @@ def reproject(disp: np.ndarray, Q) -> np.ndarray:
     out = np.empty(disp.shape + (3,), np.float32)
     lib().sa_reproject_cpu(_p(disp, _f), disp.shape[0], disp.shape[1], _p(_f64(Q), _d), _p(out, _f))
     return out
+
+
+# ------------------------------------------------------------------ calibration tool
+def find_chessboard(gray: np.ndarray, cols: int = 11, rows: int = 8, subpix: bool = True) -> np.ndarray | None:
+    """Inner chessboard corners [cols*rows, 2] (row-major from the top-left) or None."""
+    g = np.ascontiguousarray(gray, dtype=np.uint8)
+    out = np.zeros((cols * rows, 2), np.float64)
+    ok = lib().sa_find_chessboard(_p(g, _u8), g.shape[0], g.shape[1], cols, rows, int(subpix), _p(out, _d))
+    return out if ok else None
+
+
+def stereo_calibrate_images(paths, cols: int = 11, rows: int = 8, square: float = 25.0, subpix: bool = True):
+    """The Stereo_Calibration pipeline over alternating left/right image paths.
+    Returns (Calibration, used_pairs, (rms_left, rms_right, rms_stereo))."""
+    cal = Calibration()
+    rms = np.zeros(3, np.float64)
+    n = lib().sa_stereo_calibrate_images("\n".join(str(p) for p in paths).encode(), cols, rows, float(square),
+                                        int(subpix), cal._h, _p(rms, _d))
+    if n < 0:
+        raise RuntimeError(f"stereo calibration failed ({n})")
+    return cal, n, tuple(rms.tolist())
