@@ -28,6 +28,9 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import stereoalgorithms_amd  # noqa: E402,F401  (HIP runtime env defaults before torch touches the GPU)
 
 BASELINE_MS = {"raftstereo-sceneflow": 38.0, "raftstereo-realtime": 11.0}  # RTX 3090, README_en.md:139-141
+# the other model families' published RTX 3090 numbers (README_en.md:192-194,244-246,293-295)
+OTHER_MS = {"crestereo-iter2": 12.0, "crestereo-iter5": 23.0, "crestereo-iter10": 42.0, "hitnet-d400": 15.0,
+            "fastacvnet-plus": 12.0}
 
 
 def parse():
@@ -105,7 +108,7 @@ def main():
     extra = {}
     if rank == 0 and not args.no_latency:
         del eng
-        for preset in ("raftstereo-sceneflow", "raftstereo-realtime"):
+        for preset in ("raftstereo-sceneflow", "raftstereo-realtime", *OTHER_MS):
             e1 = NativeStereoEngine(preset, None, H, W, batch=1, device=dev.index, seed=0)
             e1.set_Q(Q)
             l1, r1 = l_np[:1].copy(), r_np[:1].copy()
@@ -121,8 +124,8 @@ def main():
                              "latency_ms_p50": round(float(np.median(ts)), 3),
                              "latency_ms_p99": round(float(np.percentile(ts, 99)), 3),
                              "fps_b1": round(1000.0 / float(ts.mean()), 2),
-                             "baseline_ms_rtx3090": BASELINE_MS[preset],
-                             "speedup_vs_baseline": round(BASELINE_MS[preset] / float(ts.mean()), 3)}
+                             "baseline_ms_rtx3090": {**BASELINE_MS, **OTHER_MS}[preset],
+                             "speedup_vs_baseline": round({**BASELINE_MS, **OTHER_MS}[preset] / float(ts.mean()), 3)}
             e1.close()
     if rank == 0:
         base_fps = 1000.0 / BASELINE_MS[args.model]

@@ -56,18 +56,27 @@ __device__ __forceinline__ void store8(f16* p, const float* v) {
   *reinterpret_cast<half8*>(p) = h;
 }
 
-template <int BM, int BN, int WM, int WN, bool GL = false>
+// Main-loop staging modes
+enum : int {
+  kRegK32 = 0,  // register-staged, BK = 32 (K not a multiple of 64)
+  kDmaK64 = 1,  // global->LDS DMA (global_load_lds_dwordx4), BK = 64 (opt-in, SA_CONV_GLDS=1)
+  kRegK64 = 2,  // register-staged, BK = 64: 8 x 16-B loads in flight per thread, one barrier per 64-deep step
+};
+
+template <int BM, int BN, int WM, int WN, int MODE = kRegK32>
 struct ConvCfg {
-  // GL: global->LDS DMA staging (global_load_lds_dwordx4) with BK = 64; otherwise register
-  // staging with BK = 32 (kept for K not a multiple of 64)
-  static constexpr int BK = GL ? 64 : 32;
+  static constexpr bool GL = MODE == kDmaK64;
+  static constexpr int BK = MODE == kRegK32 ? 32 : 64;
+  static constexpr int KCH = BK / 8;  // 16-byte chunks per row per stage
   static constexpr int TM = BM / WM, TN = BN / WN;
   static constexpr int FM = TM / 16, FN = TN / 16;
-  static constexpr int A_CH = BM * 4, B_CH = BN * 4;  // 16-byte chunks per stage
+  static constexpr int A_CH = BM * KCH, B_CH = BN * KCH;  // 16-byte chunks per stage
   static constexpr int A_PT = (A_CH + 255) / 256, B_PT = (B_CH + 255) / 256;
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   static constexpr int STAGE_BYTES = 2 * (A_BYTES + B_BYTES);
-  static constexpr int CST = BN + 4;  // fp32 C-tile row stride
+  // fp32 C tile, unpadded rows; columns XOR-swizzled in 16-float blocks (cswz) so the MFMA
+  // write-out (4 row groups x 16 lanes) hits 64 distinct banks; aliases the stage buffers
+  static constexpr int CST = BN;
   static constexpr int C_BYTES = BM * CST * 4;
   static constexpr int SMEM = STAGE_BYTES > C_BYTES ? STAGE_BYTES : C_BYTES;
   static_assert(WM * WN == 4, "4 waves per workgroup");
@@ -76,6 +85,17 @@ struct ConvCfg {
 
 // swizzled byte offset of (row, 16B-chunk) inside a [rows][32 halfs] stage buffer
 __device__ __forceinline__ int swz(int row, int c) { return row * 64 + ((c ^ (((row >> 3) & 1) * 3)) << 4); }
+// C-tile column swizzle: 16-float blocks XOR ((row >> 2) & 3) (keeps 8-float chunks contiguous);
+// identity when the tile is narrower than 64 columns
+template <int BN>
+__device__ __forceinline__ int cswz_t(int row, int col) {
+  if constexpr (BN >= 64) return col ^ (((row >> 2) & 3) << 4);
+  else return col;
+}
+#define cswz(row, col) cswz_t<BN>(row, col)
+// [rows][64 halfs] stage buffer (128-B rows): chunk XOR (row>>1)&7 — the 16 rows x one chunk of a
+// ds_read_b128 lane group land in 16 distinct 16-B bank slots
+__device__ __forceinline__ int swz64(int row, int c) { return row * 128 + ((c ^ ((row >> 1) & 7)) << 4); }
 
 // 16 zero bytes in global memory: the source of every padded / out-of-range im2col chunk in the
 // DMA path (a masked-off lane would leave stale LDS behind)
@@ -83,9 +103,9 @@ __device__ __attribute__((aligned(16))) const unsigned char g_zero16[64] = {0};
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-template <int BM, int BN, int WM, int WN, bool GL>
+template <int BM, int BN, int WM, int WN, int MODE>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
-  using C = ConvCfg<BM, BN, WM, WN, GL>;
+  using C = ConvCfg<BM, BN, WM, WN, MODE>;
   __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
 
   const int tid = threadIdx.x;
@@ -113,7 +133,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
   for (int i = 0; i < C::FM; ++i)
 #pragma unroll
     for (int j = 0; j < C::FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (GL) {
+  if constexpr (C::GL) {
     // ---------------- DMA staging: [rows][64 halfs] (128 B) per stage, chunk XOR-swizzled ----------
     // LDS image is lane-linear per wave instruction (q*16 = row*128 + pch*16); the swizzle lives on
     // the SOURCE side: slot q fetches logical chunk lch = pch ^ ((row>>1)&7), so the fragment reads
@@ -222,13 +242,13 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
     __syncthreads();  // all fragment reads done before the epilogue reuses LDS
   } else {
   // ---------------- per-thread A-row precompute ----------------
-  const int cth = tid & 3;  // chunk index this thread loads (constant over k)
+  const int cth = tid % C::KCH;  // chunk index this thread loads (constant over k)
   int a_ih0[C::A_PT], a_iw0[C::A_PT], a_nb[C::A_PT], a_d0[C::A_PT];
   bool a_ok[C::A_PT];
 #pragma unroll
   for (int i = 0; i < C::A_PT; ++i) {
     int q = tid + 256 * i;
-    int row = q >> 2;
+    int row = q / C::KCH;
     int m = m0 + row;
     bool ok = (q < C::A_CH) && (m < M);
     int mm = ok ? m : 0;
@@ -286,9 +306,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
     for (int i = 0; i < C::B_PT; ++i) {
       int q = tid + 256 * i;
       if (q < C::B_CH) {
-        int row = q >> 2;
+        int row = q / C::KCH;
         rb[i] = *reinterpret_cast<const half8*>(wptr + (size_t)(n0 + row) * p.Kpad +
-                                                 (kt0 + kt) * C::BK + (q & 3) * 8);
+                                                 (kt0 + kt) * C::BK + (q % C::KCH) * 8);
       }
     }
     // advance k position by BK for the next tile
@@ -305,12 +325,18 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
 #pragma unroll
     for (int i = 0; i < C::A_PT; ++i) {
       int q = tid + 256 * i;
-      if (q < C::A_CH) *reinterpret_cast<half8*>(sa + swz(q >> 2, q & 3)) = ra[i];
+      if (q < C::A_CH) {
+        if constexpr (C::BK == 64) *reinterpret_cast<half8*>(sa + swz64(q >> 3, q & 7)) = ra[i];
+        else *reinterpret_cast<half8*>(sa + swz(q >> 2, q & 3)) = ra[i];
+      }
     }
 #pragma unroll
     for (int i = 0; i < C::B_PT; ++i) {
       int q = tid + 256 * i;
-      if (q < C::B_CH) *reinterpret_cast<half8*>(sb + swz(q >> 2, q & 3)) = rb[i];
+      if (q < C::B_CH) {
+        if constexpr (C::BK == 64) *reinterpret_cast<half8*>(sb + swz64(q >> 3, q & 7)) = rb[i];
+        else *reinterpret_cast<half8*>(sb + swz(q >> 2, q & 3)) = rb[i];
+      }
     }
   };
 
@@ -328,18 +354,37 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
     if (kt + 1 < nk) load_tile(kt + 1);
     const char* sa = smem + cur * (C::A_BYTES + C::B_BYTES);
     const char* sb = sa + C::A_BYTES;
-    half8 af[C::FM], bf[C::FN];
+    if constexpr (C::BK == 64) {
 #pragma unroll
-    for (int i = 0; i < C::FM; ++i)
-      af[i] = *reinterpret_cast<const half8*>(sa + (wm * C::TM + i * 16) * 64 + foff);
+      for (int kk = 0; kk < 2; ++kk) {
+        half8 af[C::FM], bf[C::FN];
+        const int lc = (lane >> 4) + 4 * kk;
 #pragma unroll
-    for (int j = 0; j < C::FN; ++j)
-      bf[j] = *reinterpret_cast<const half8*>(sb + (wn * C::TN + j * 16) * 64 + foff);
+        for (int i = 0; i < C::FM; ++i)
+          af[i] = *reinterpret_cast<const half8*>(sa + swz64(wm * C::TM + i * 16 + frow, lc));
 #pragma unroll
-    for (int i = 0; i < C::FM; ++i)
+        for (int j = 0; j < C::FN; ++j)
+          bf[j] = *reinterpret_cast<const half8*>(sb + swz64(wn * C::TN + j * 16 + frow, lc));
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int j = 0; j < C::FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      half8 af[C::FM], bf[C::FN];
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i)
+        af[i] = *reinterpret_cast<const half8*>(sa + (wm * C::TM + i * 16) * 64 + foff);
 #pragma unroll
       for (int j = 0; j < C::FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        bf[j] = *reinterpret_cast<const half8*>(sb + (wn * C::TN + j * 16) * 64 + foff);
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
     if (kt + 1 < nk) store_tile(cur ^ 1);
     __syncthreads();
   }
@@ -395,19 +440,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
     }
   }
 
-  // ---------------- epilogue: stage C through LDS ----------------
+  // ---------------- epilogue: stage C through LDS, one TM-row band of waves at a time ----------
   float* ct = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int i = 0; i < C::FM; ++i)
-#pragma unroll
-    for (int j = 0; j < C::FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int row = wm * C::TM + i * 16 + (lane >> 4) * 4 + r;
-        int col = wn * C::TN + j * 16 + (lane & 15);
-        ct[row * C::CST + col] = acc[i][j][r];
-      }
-  __syncthreads();
 
   constexpr int CPR = BN / 8;  // 8-channel chunks per row
   constexpr int RPI = 256 / CPR;  // rows per pass
@@ -443,12 +477,24 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) bias8[j] = (p.bias && j < nvalid) ? p.bias[co + j] : 0.f;
 
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int row = wm * C::TM + i * 16 + (lane >> 4) * 4 + r;
+        int col = wn * C::TN + j * 16 + (lane & 15);
+        ct[row * C::CST + cswz(row, col)] = acc[i][j][r];
+      }
+  __syncthreads();
+
   if (nvalid > 0) {
     for (int row = tid / CPR; row < BM; row += RPI) {
       const int m = m0 + row;
       if (m >= M) break;
       float v[8];
-      const float* cp = ct + row * C::CST + cc * 8;
+      const float* cp = ct + row * C::CST + cswz(row, cc * 8);
       floatx4 c0 = *reinterpret_cast<const floatx4*>(cp);
       floatx4 c1 = *reinterpret_cast<const floatx4*>(cp + 4);
       v[0] = c0[0]; v[1] = c0[1]; v[2] = c0[2]; v[3] = c0[3];
@@ -614,9 +660,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool GL>
+template <int BM, int BN, int WM, int WN, int MODE>
 void launch_kernel(dim3 grid, const SaConvArgs* a, hipStream_t stream) {
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, GL>), grid, dim3(256), 0, stream, *a);
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, MODE>), grid, dim3(256), 0, stream, *a);
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -629,10 +675,16 @@ int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
     return e && e[0] == '1';
   }();
   const bool gl = can_gl && want_gl && a->Kpad % 64 == 0;
+  static const bool k32_only = [] {
+    const char* e = std::getenv("SA_CONV_K32");
+    return e && e[0] == '1';
+  }();
+  // BK = 64 doubles the staging LDS: only for tiles whose C tile needs that LDS anyway (BN >= 64)
+  const bool k64 = BN >= 64 && !gl && !k32_only && a->Kpad % 64 == 0;
   const int M = a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
   const int gx = (M + BM - 1) / BM, gy = (a->Cout + BN - 1) / BN;
   const long tiles = (long)gx * gy;
-  const int nk = a->Kpad / (gl ? 64 : 32);
+  const int nk = a->Kpad / (gl || k64 ? 64 : 32);
   int S = a->splitk;
   if (S == 0) {
     // auto: split the K loop when the tile grid cannot fill 256 CUs (small-M levels of the
@@ -641,7 +693,7 @@ int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
     if (a->ws && a->counters && !a->stats && tiles < 320) {
       S = (int)((640 + tiles - 1) / tiles);
       if (S > 8) S = 8;
-      if (S > nk / 4) S = nk / 4;
+      if (S > nk / (k64 || gl ? 2 : 4)) S = nk / (k64 || gl ? 2 : 4);
       while (S > 1 && ((long)S * tiles * BM * BN > a->ws_floats || tiles > a->n_counters)) --S;
       if (S < 1) S = 1;
     }
@@ -650,8 +702,9 @@ int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
                 tiles > a->n_counters || S > nk))
     return -4;
   dim3 grid(gx, gy, S);
-  if (gl) launch_kernel<BM, BN, WM, WN, true>(grid, a, stream);
-  else launch_kernel<BM, BN, WM, WN, false>(grid, a, stream);
+  if (gl) launch_kernel<BM, BN, WM, WN, kDmaK64>(grid, a, stream);
+  else if (k64) launch_kernel<BM, BN, WM, WN, kRegK64>(grid, a, stream);
+  else launch_kernel<BM, BN, WM, WN, kRegK32>(grid, a, stream);
   return (int)hipGetLastError();
 }
 
