@@ -61,6 +61,9 @@ enum : int {
   kRegK32 = 0,  // register-staged, BK = 32 (K not a multiple of 64)
   kDmaK64 = 1,  // global->LDS DMA (global_load_lds_dwordx4), BK = 64 (opt-in, SA_CONV_GLDS=1)
   kRegK64 = 2,  // register-staged, BK = 64: 8 x 16-B loads in flight per thread, one barrier per 64-deep step
+  kFastK64 = 3,  // kRegK64 when every source's channel count is a multiple of 64: the (tap, source,
+                 // channel) position of a k-step is wave-uniform, so the im2col gather is one
+                 // address add + one validity-bit test per row (per-row tap masks precomputed)
 };
 
 template <int BM, int BN, int WM, int WN, int MODE = kRegK32>
@@ -133,7 +136,126 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
   for (int i = 0; i < C::FM; ++i)
 #pragma unroll
     for (int j = 0; j < C::FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (C::GL) {
+  if constexpr (MODE == kFastK64) {
+    // ---------------- uniform-k im2col, register staged, BK = 64 ----------------
+    constexpr int RPT = C::A_PT;  // A rows per thread: (tid >> 3) + 32 i
+    const int cth = tid & 7;
+    const int KH = p.KH, KW = p.KW;
+    long pixb[RPT];
+    unsigned long long vmask[RPT];
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      const int m = m0 + row;
+      const bool ok = m < M;
+      const int mm = ok ? m : 0;
+      const int img = mm / HWo;
+      const int r = mm - img * HWo;
+      const int oh = r / p.Wo, ow = r - oh * p.Wo;
+      const int n = img / Do, od = img - n * Do;
+      const int ih0 = oh * p.sh - p.ph, iw0 = ow * p.sw - p.pw, id0 = od * sd - p.pd;
+      pixb[i] = (((long)n * Di + id0) * p.H + ih0) * p.W + iw0;
+      unsigned long long mk = 0ull;
+      int t = 0;
+      for (int kd = 0; kd < KD; ++kd)
+        for (int kh = 0; kh < KH; ++kh)
+          for (int kw = 0; kw < KW; ++kw, ++t) {
+            const int dd = id0 + kd, ih = ih0 + kh * p.dh, iw = iw0 + kw * p.dw;
+            if (ok && dd >= 0 && dd < Di && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W) mk |= 1ull << t;
+          }
+      vmask[i] = mk;
+    }
+    // wave-uniform k position: tap (kd, kh, kw), pixel offset of the tap, channel within the tap
+    int kc = kt0 * 64;
+    int tap = kc / p.Cin, ci0 = kc - tap * p.Cin;
+    int kd_ = tap / (KH * KW), kr = tap - kd_ * KH * KW;
+    int kh_ = kr / KW, kw_ = kr - kh_ * KW;
+    long toff = ((long)kd_ * p.H + (long)kh_ * p.dh) * p.W + (long)kw_ * p.dw;
+    const int sb1 = p.src[0].channels;
+    const int sb2 = sb1 + (p.nsrc > 1 ? p.src[1].channels : 0);
+    const int sb3 = sb2 + (p.nsrc > 2 ? p.src[2].channels : 0);
+    const f16* wrow[C::B_PT];
+#pragma unroll
+    for (int j = 0; j < C::B_PT; ++j) {
+      const int row = (tid >> 3) + 32 * j;
+      wrow[j] = reinterpret_cast<const f16*>(p.weight) + (size_t)(n0 + (row < BN ? row : 0)) * p.Kpad + kc + cth * 8;
+    }
+    const half8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
+    half8 ra[RPT], rb[C::B_PT];
+    auto load_tile = [&]() {
+      const int s = (ci0 >= sb1) + (ci0 >= sb2) + (ci0 >= sb3);
+      const int cbase = s == 0 ? 0 : (s == 1 ? sb1 : (s == 2 ? sb2 : sb3));
+      const f16* sp = reinterpret_cast<const f16*>(p.src[s].ptr) + (ci0 - cbase) + cth * 8;
+      const long sst = p.src[s].stride;
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) {
+        const bool v = (vmask[i] >> tap) & 1ull;
+        const f16* a = sp + (pixb[i] + toff) * sst;
+        ra[i] = v ? *reinterpret_cast<const half8*>(a) : zero8;
+      }
+#pragma unroll
+      for (int j = 0; j < C::B_PT; ++j) {
+        if ((tid >> 3) + 32 * j < BN) rb[j] = *reinterpret_cast<const half8*>(wrow[j]);
+        wrow[j] += 64;
+      }
+      // advance the uniform k position by 64 channels
+      ci0 += 64;
+      if (ci0 >= p.Cin) {
+        ci0 = 0;
+        ++tap;
+        ++kw_;
+        toff += p.dw;
+        if (kw_ == KW) {
+          kw_ = 0;
+          toff += (long)p.dh * p.W - (long)KW * p.dw;
+          ++kh_;
+          if (kh_ == KH) {
+            kh_ = 0;
+            toff += (long)p.H * p.W - (long)KH * p.dh * p.W;
+          }
+        }
+      }
+    };
+    auto store_tile = [&](int buf) {
+      char* sa = smem + buf * (C::A_BYTES + C::B_BYTES);
+      char* sb = sa + C::A_BYTES;
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) *reinterpret_cast<half8*>(sa + swz64((tid >> 3) + 32 * i, cth)) = ra[i];
+#pragma unroll
+      for (int j = 0; j < C::B_PT; ++j)
+        if ((tid >> 3) + 32 * j < BN) *reinterpret_cast<half8*>(sb + swz64((tid >> 3) + 32 * j, cth)) = rb[j];
+    };
+    const int frow = lane & 15;
+    if (nk > 0) {
+      load_tile();
+      store_tile(0);
+    }
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) load_tile();
+      const char* sa = smem + cur * (C::A_BYTES + C::B_BYTES);
+      const char* sb = sa + C::A_BYTES;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        half8 af[C::FM], bf[C::FN];
+        const int lc = (lane >> 4) + 4 * kk;
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+          af[i] = *reinterpret_cast<const half8*>(sa + swz64(wm * C::TM + i * 16 + frow, lc));
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j)
+          bf[j] = *reinterpret_cast<const half8*>(sb + swz64(wn * C::TN + j * 16 + frow, lc));
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int j = 0; j < C::FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
+      if (kt + 1 < nk) store_tile(cur ^ 1);
+      __syncthreads();
+    }
+  } else if constexpr (C::GL) {
     // ---------------- DMA staging: [rows][64 halfs] (128 B) per stage, chunk XOR-swizzled ----------
     // LDS image is lane-linear per wave instruction (q*16 = row*128 + pch*16); the swizzle lives on
     // the SOURCE side: slot q fetches logical chunk lch = pch ^ ((row>>1)&7), so the fragment reads
@@ -681,6 +803,15 @@ int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
   }();
   // BK = 64 doubles the staging LDS: only for tiles whose C tile needs that LDS anyway (BN >= 64)
   const bool k64 = BN >= 64 && !gl && !k32_only && a->Kpad % 64 == 0;
+  // uniform-k fast gather: every source a multiple of 64 channels, K unpadded, <= 64 taps
+  const int taps = (a->KD > 0 ? a->KD : 1) * a->KH * a->KW;
+  bool fast = k64 && taps <= 64 && (long)taps * a->Cin == a->Kpad;
+  for (int i = 0; i < a->nsrc; ++i) fast = fast && a->src[i].channels % 64 == 0;
+  static const bool no_fast = [] {
+    const char* e = std::getenv("SA_CONV_NOFAST");
+    return e && e[0] == '1';
+  }();
+  fast = fast && !no_fast;
   const int M = a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
   const int gx = (M + BM - 1) / BM, gy = (a->Cout + BN - 1) / BN;
   const long tiles = (long)gx * gy;
@@ -703,6 +834,7 @@ int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
     return -4;
   dim3 grid(gx, gy, S);
   if (gl) launch_kernel<BM, BN, WM, WN, kDmaK64>(grid, a, stream);
+  else if (fast) launch_kernel<BM, BN, WM, WN, kFastK64>(grid, a, stream);
   else if (k64) launch_kernel<BM, BN, WM, WN, kRegK64>(grid, a, stream);
   else launch_kernel<BM, BN, WM, WN, kRegK32>(grid, a, stream);
   return (int)hipGetLastError();

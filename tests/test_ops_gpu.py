@@ -312,3 +312,42 @@ def test_reproject_matches_Q():
     assert torch.allclose(cloud[0, ..., 0], X, rtol=1e-4, atol=1e-3)
     assert torch.allclose(cloud[0, ..., 2], Z.expand_as(X), rtol=1e-4)
     assert torch.equal(cloud[0, ..., 3:].round().to(torch.uint8), img[0].flip(-1))
+
+
+@pytest.mark.parametrize("srcs,cout,k,stride,dil,splitk", [
+    ((64, 128), 128, 3, 1, 1, 1),
+    ((128, 64, 64), 256, 3, 2, 1, 1),
+    ((64,), 64, 3, 1, 2, 1),
+    ((128,), 96, 5, 1, 1, 1),
+    ((128, 128), 128, 3, 1, 1, 3),
+])
+def test_conv2d_uniform_k_fast_path(srcs, cout, k, stride, dil, splitk):
+    """Every source a multiple of 64 channels: the wave-uniform im2col gather (per-row tap masks,
+    multi-source channel walk, dilation, stride, split-K) equals torch."""
+    O = ops()
+    torch.manual_seed(11)
+    n, h, w = 2, 19, 27
+    xs = [torch.randn(n, c, h, w, device=DEV) for c in srcs]
+    cin = sum(srcs)
+    wt = torch.randn(cout, cin, k, k, device=DEV) / math.sqrt(cin * k * k)
+    pad = dil * (k // 2)
+    ref = F.conv2d(torch.cat(xs, 1).half().float(), wt.half().float(), stride=stride, padding=pad, dilation=dil)
+    wp, kpad, _ = O.pack_conv_weight(wt, [(c, c) for c in srcs])
+    ws = O.splitk_workspace() if splitk != 1 else None
+    out = O.conv2d([nhwc(x).half() for x in xs], wp, kpad, cout, k, k, stride=stride, pad=pad, dil=dil,
+                   splitk=splitk, workspace=ws)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(out), ref) < 2e-3
+
+
+def test_conv3d_uniform_k_fast_path():
+    O = ops()
+    torch.manual_seed(12)
+    x = torch.randn(2, 64, 6, 9, 11, device=DEV).half().float()
+    wt = torch.randn(64, 64, 3, 3, 3, device=DEV) / math.sqrt(64 * 27)
+    for stride in (1, 2):
+        ref = F.conv3d(x, wt, stride=stride, padding=1)
+        wp, kpad, _ = O.pack_conv3d_weight(wt)
+        out = O.conv3d(x.permute(0, 2, 3, 4, 1).contiguous().half(), wp, kpad, 64, 3, stride)
+        torch.cuda.synchronize()
+        assert rel_err(out.permute(0, 4, 1, 2, 3), ref) < 2e-3

@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Micro-benchmark of the implicit-GEMM conv kernel on the RAFT-Stereo hot shapes.
+
+    python3 tools/conv_bench.py [--iters 50] [--shapes zr1,q1,...]
+
+Prints per shape: time per call (hipEvent, averaged), TFLOP/s, and the tile config the launcher chose.
+Env knobs of the kernel (SA_CONV_K32=1, SA_CONV_GLDS=1) select alternative main loops for A/B runs.
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+# name: (N, H, W, Cin, Cout, k, splitk)   splitk 0 = auto (needs workspace), 1 = off
+SHAPES = {
+    "zr1": (1, 120, 160, 384, 256, 3, 0),    # GRU 1/4 z,r at batch 1
+    "q1": (1, 120, 160, 384, 128, 3, 0),     # GRU 1/4 q at batch 1
+    "fh1": (1, 120, 160, 128, 256, 3, 0),    # flow head conv1 at batch 1
+    "enc1": (1, 120, 160, 128, 128, 3, 0),   # motion encoder out conv
+    "zr16": (1, 60, 80, 384, 256, 3, 0),     # GRU 1/8 z,r
+    "zr8": (8, 120, 160, 384, 256, 3, 1),    # GRU 1/4 z,r at batch 8
+    "q8": (8, 120, 160, 384, 128, 3, 1),
+    "fnet": (2, 240, 320, 64, 64, 3, 1),     # feature encoder layer1 at 1/2
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--shapes", default=",".join(SHAPES))
+    a = ap.parse_args()
+    import torch
+    from stereoalgorithms_amd import ops as O
+    torch.manual_seed(0)
+    ws = O.splitk_workspace(1 << 24, 8192)
+    for name in a.shapes.split(","):
+        n, h, w, cin, cout, k, sk = SHAPES[name]
+        x = torch.randn(n, h, w, cin, device="cuda").half()
+        wt = torch.randn(cout, cin, k, k, device="cuda") / (cin * k * k) ** 0.5
+        wp, kpad, _ = O.pack_conv_weight(wt)
+        b = torch.zeros(cout, device="cuda")
+        out = torch.empty(n, h, w, cout, device="cuda", dtype=torch.float16)
+        kw = dict(bias=b, out=out, splitk=sk, workspace=ws if sk != 1 else None)
+        for _ in range(3):
+            O.conv2d(x, wp, kpad, cout, k, k, **kw)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            O.conv2d(x, wp, kpad, cout, k, k, **kw)
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / a.iters * 1e3
+        flop = 2.0 * n * h * w * cout * cin * k * k
+        print(f"{name:6s} M={n * h * w:7d} K={cin * k * k:5d} N={cout:4d}: {us:8.2f} us  {flop / us / 1e6:7.1f} TFLOP/s",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
