@@ -64,6 +64,9 @@ enum : int {
   kFastK64 = 3,  // kRegK64 when every source's channel count is a multiple of 64: the (tap, source,
                  // channel) position of a k-step is wave-uniform, so the im2col gather is one
                  // address add + one validity-bit test per row (per-row tap masks precomputed)
+  kGlds3 = 4,    // kFastK64's uniform-k gather issued as global->LDS DMA into a 3-deep LDS ring:
+                 // 8 waves, one block per CU, counted vmcnt keeps the next stage in flight across
+                 // the (raw) barrier, XCD-aware tile order
 };
 
 template <int BM, int BN, int WM, int WN, int MODE = kRegK32>
@@ -74,15 +77,18 @@ struct ConvCfg {
   static constexpr int TM = BM / WM, TN = BN / WN;
   static constexpr int FM = TM / 16, FN = TN / 16;
   static constexpr int A_CH = BM * KCH, B_CH = BN * KCH;  // 16-byte chunks per stage
-  static constexpr int A_PT = (A_CH + 255) / 256, B_PT = (B_CH + 255) / 256;
+  static constexpr int NW = WM * WN, NT = 64 * NW;  // waves / threads per workgroup
+  static constexpr int A_PT = (A_CH + NT - 1) / NT, B_PT = (B_CH + NT - 1) / NT;
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  static constexpr int STAGE_BYTES = 2 * (A_BYTES + B_BYTES);
+  // kGlds3: three-deep LDS ring; everything else double-buffered
+  static constexpr int NSTAGE = MODE == kGlds3 ? 3 : 2;
+  static constexpr int STAGE_BYTES = NSTAGE * (A_BYTES + B_BYTES);
   // fp32 C tile, unpadded rows; columns XOR-swizzled in 16-float blocks (cswz) so the MFMA
   // write-out (4 row groups x 16 lanes) hits 64 distinct banks; aliases the stage buffers
   static constexpr int CST = BN;
   static constexpr int C_BYTES = BM * CST * 4;
   static constexpr int SMEM = STAGE_BYTES > C_BYTES ? STAGE_BYTES : C_BYTES;
-  static_assert(WM * WN == 4, "4 waves per workgroup");
+  static_assert(WM * WN == 4 || (WM * WN == 8 && MODE == kGlds3), "4 waves (4 or 8 for kGlds3) per workgroup");
   static_assert(TM % 16 == 0 && TN % 16 == 0, "wave tile must be 16-aligned");
 };
 
@@ -106,23 +112,50 @@ __device__ __attribute__((aligned(16))) const unsigned char g_zero16[64] = {0};
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
+#define SA_STR2(x) #x
+#define SA_STR(x) SA_STR2(x)
+// s_waitcnt vmcnt(N) with a compile-time N (the asm string needs a literal)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N <= 16, "vmcnt literal");
+#define SA_VMCNT_CASE(k) \
+  if constexpr (N == k) asm volatile("s_waitcnt vmcnt(" SA_STR(k) ")" ::: "memory");
+  SA_VMCNT_CASE(0) SA_VMCNT_CASE(1) SA_VMCNT_CASE(2) SA_VMCNT_CASE(3) SA_VMCNT_CASE(4) SA_VMCNT_CASE(5)
+  SA_VMCNT_CASE(6) SA_VMCNT_CASE(7) SA_VMCNT_CASE(8) SA_VMCNT_CASE(9) SA_VMCNT_CASE(10) SA_VMCNT_CASE(11)
+  SA_VMCNT_CASE(12) SA_VMCNT_CASE(13) SA_VMCNT_CASE(14) SA_VMCNT_CASE(15) SA_VMCNT_CASE(16)
+#undef SA_VMCNT_CASE
+}
+
 template <int BM, int BN, int WM, int WN, int MODE>
-__global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
+__global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvArgs p) {
   using C = ConvCfg<BM, BN, WM, WN, MODE>;
   __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar LDS bases)
   const int wm = wave / WN, wn = wave % WN;
 
+  constexpr int NT = C::NT;
   const int HWo = p.Ho * p.Wo;
   // 3-D mode (KD > 0): rows enumerate (n, do, oh, ow); 2-D is KD = Di = Do = 1
   const int KD = p.KD > 0 ? p.KD : 1, Di = p.Di > 0 ? p.Di : 1, Do = p.Do > 0 ? p.Do : 1;
   const int sd = p.sd > 0 ? p.sd : 1;
   const int M = p.N * Do * HWo;
-  const int m0 = blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
+  // tile coordinates; kGlds3 walks the (m, n) tiles in an XCD-aware order: consecutive dispatch
+  // ids round-robin over the 8 XCDs, so give each XCD a contiguous run of m-major tiles (neighbour
+  // tiles share input rows through the 3x3 halo, the n tiles of one m share the whole A panel)
+  int bx = blockIdx.x, by = blockIdx.y;
+  if constexpr (MODE == kGlds3) {
+    const int nwg = gridDim.x * gridDim.y;
+    const int bid = blockIdx.y * gridDim.x + blockIdx.x;
+    const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
+    const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    bx = lin / gridDim.y;
+    by = lin - bx * gridDim.y;
+  }
+  const int m0 = bx * BM;
+  const int n0 = by * BN;
   // split-K slice of the K loop handled by this block
   const int S = gridDim.z, z = blockIdx.z;
   const int nk_all = p.Kpad / C::BK;
@@ -255,6 +288,192 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
       if (kt + 1 < nk) store_tile(cur ^ 1);
       __syncthreads();
     }
+  } else if constexpr (MODE == kGlds3) {
+    // ---------------- uniform-k im2col via global->LDS DMA, 3-deep LDS ring, BK = 64 -------------
+    // Stage image per operand: [rows][64 halfs] (128-B rows), lane-linear per wave instruction
+    // (slot q*16 = row*128 + pch*16) with the XOR swizzle on the SOURCE chunk (lch = pch ^
+    // ((row>>1)&7)), read back through the same involution (cdna_hip_programming.md §5.4 rule 21).
+    // Pipeline: stages kt and kt+1 are in flight when iteration kt waits with vmcnt(NA+NB) (= one
+    // stage of DMA left outstanding), crosses a raw s_barrier (so every wave's DMA of stage kt has
+    // landed and every wave finished reading stage kt-1), then issues stage kt+2 into the buffer
+    // stage kt-1 used and runs the MFMAs of stage kt.
+    constexpr int NA = BM * 8 / NT, NB = BN * 8 / NT;  // DMA instructions per thread per stage
+    static_assert(NA * NT == BM * 8 && NB * NT == BN * 8 && NA + NB <= 8, "whole-wave DMA pieces");
+    constexpr int STG = (BM + BN) * 128;
+    const int KH = p.KH, KW = p.KW;
+    int pixb[NA];  // input pixel index of the row's (kd, kh, kw) = 0 tap (32-bit: tensors < 2^31 elements)
+    unsigned long long vmask[NA];
+    int lcho[NA];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int row = (wave * NA + i) * 8 + (lane >> 3);
+      lcho[i] = (((lane & 7) ^ ((row >> 1) & 7)) << 3);
+      const int m = m0 + row;
+      const bool ok = m < M;
+      const int mm = ok ? m : 0;
+      const int img = mm / HWo;
+      const int r = mm - img * HWo;
+      const int oh = r / p.Wo, ow = r - oh * p.Wo;
+      const int n = img / Do, od = img - n * Do;
+      const int ih0 = oh * p.sh - p.ph, iw0 = ow * p.sw - p.pw, id0 = od * sd - p.pd;
+      pixb[i] = ((n * Di + id0) * p.H + ih0) * p.W + iw0;
+      unsigned long long mk = 0ull;
+      int t = 0;
+      for (int kd = 0; kd < KD; ++kd)
+        for (int kh = 0; kh < KH; ++kh)
+          for (int kw = 0; kw < KW; ++kw, ++t) {
+            const int dd = id0 + kd, ih = ih0 + kh * p.dh, iw = iw0 + kw * p.dw;
+            if (ok && dd >= 0 && dd < Di && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W) mk |= 1ull << t;
+          }
+      vmask[i] = mk;
+    }
+    int kc = kt0 * 64;
+    int tap = kc / p.Cin, ci0 = kc - tap * p.Cin;
+    int kd_ = tap / (KH * KW), kr = tap - kd_ * KH * KW;
+    int kh_ = kr / KW, kw_ = kr - kh_ * KW;
+    int toff = (kd_ * p.H + kh_ * p.dh) * p.W + kw_ * p.dw;
+    const int sb1 = p.src[0].channels;
+    const int sb2 = sb1 + (p.nsrc > 1 ? p.src[1].channels : 0);
+    const int sb3 = sb2 + (p.nsrc > 2 ? p.src[2].channels : 0);
+    // source pointers / strides held in registers: indexing the kernarg array per stage would put an
+    // s_load + lgkmcnt(0) (which also waits for the stage's ds_reads) in front of every DMA issue
+    const f16* sp0 = reinterpret_cast<const f16*>(p.src[0].ptr);
+    const f16* sp1 = reinterpret_cast<const f16*>(p.src[p.nsrc > 1 ? 1 : 0].ptr);
+    const f16* sp2 = reinterpret_cast<const f16*>(p.src[p.nsrc > 2 ? 2 : 0].ptr);
+    const f16* sp3 = reinterpret_cast<const f16*>(p.src[p.nsrc > 3 ? 3 : 0].ptr);
+    const int ss0 = p.src[0].stride, ss1 = p.src[p.nsrc > 1 ? 1 : 0].stride;
+    const int ss2 = p.src[p.nsrc > 2 ? 2 : 0].stride, ss3 = p.src[p.nsrc > 3 ? 3 : 0].stride;
+    const f16* wrow[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int row = (wave * NB + j) * 8 + (lane >> 3);
+      const int lch = (lane & 7) ^ ((row >> 1) & 7);
+      wrow[j] = reinterpret_cast<const f16*>(p.weight) + (size_t)(n0 + row) * p.Kpad + kc + lch * 8;
+    }
+    const void* zero_src = g_zero16;
+    auto issue = [&](int buf) {
+      char* sa = smem + buf * STG;
+      char* sb = sa + BM * 128;
+      const f16* sp;
+      int sst;
+      if (ci0 < sb1) { sp = sp0 + ci0; sst = ss0; }
+      else if (ci0 < sb2) { sp = sp1 + (ci0 - sb1); sst = ss1; }
+      else if (ci0 < sb3) { sp = sp2 + (ci0 - sb2); sst = ss2; }
+      else { sp = sp3 + (ci0 - sb3); sst = ss3; }
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const bool v = (vmask[i] >> tap) & 1ull;
+        const f16* ga = sp + ((pixb[i] + toff) * sst + lcho[i]);
+        const void* g = v ? (const void*)ga : zero_src;
+        __builtin_amdgcn_global_load_lds(g, (lds_void_t*)(sa + (wave * NA + i) * 1024), 16, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        __builtin_amdgcn_global_load_lds((const void*)wrow[j], (lds_void_t*)(sb + (wave * NB + j) * 1024), 16, 0, 0);
+        wrow[j] += 64;
+      }
+      ci0 += 64;
+      if (ci0 >= p.Cin) {
+        ci0 = 0;
+        ++tap;
+        ++kw_;
+        toff += p.dw;
+        if (kw_ == KW) {
+          kw_ = 0;
+          toff += p.dh * p.W - KW * p.dw;
+          ++kh_;
+          if (kh_ == KH) {
+            kh_ = 0;
+            toff += p.H * p.W - KH * p.dh * p.W;
+          }
+        }
+      }
+    };
+    const int frow = lane & 15;
+    // fragment reads of one 32-deep half (kk) of the stage in buffer `buf`
+    auto read_half = [&](int buf, int kk, half8* af, half8* bf) {
+      const char* sa = smem + buf * STG;
+      const char* sb = sa + BM * 128;
+      const int lc = (lane >> 4) + 4 * kk;
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) {
+        const int row = wm * C::TM + i * 16 + frow;
+        af[i] = *reinterpret_cast<const half8*>(sa + row * 128 + ((lc ^ ((row >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) {
+        const int row = wn * C::TN + j * 16 + frow;
+        bf[j] = *reinterpret_cast<const half8*>(sb + row * 128 + ((lc ^ ((row >> 1) & 7)) << 4));
+      }
+    };
+    auto mfma_half = [&](const half8* af, const half8* bf) {
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    };
+    // the MFMAs of one half (operands am/bm, already in registers) with the fragment reads of
+    // another half interleaved one read per MFMA: the first MFMA waits only for its own (old)
+    // operands and the reads land under the MFMA stream
+    auto mfma_read = [&](const half8* am, const half8* bm, int buf, int kk, half8* ar, half8* br) {
+      const char* sa = smem + buf * STG;
+      const char* sb = sa + BM * 128;
+      const int lc = (lane >> 4) + 4 * kk;
+#pragma unroll
+      for (int t = 0; t < C::FM * C::FN; ++t) {
+        const int i = t / C::FN, j = t - (t / C::FN) * C::FN;
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(am[i], bm[j], acc[i][j], 0, 0, 0);
+        if (t < C::FM) {
+          const int row = wm * C::TM + t * 16 + frow;
+          ar[t] = *reinterpret_cast<const half8*>(sa + row * 128 + ((lc ^ ((row >> 1) & 7)) << 4));
+        } else if (t < C::FM + C::FN) {
+          const int row = wn * C::TN + (t - C::FM) * 16 + frow;
+          br[t - C::FM] = *reinterpret_cast<const half8*>(sb + row * 128 + ((lc ^ ((row >> 1) & 7)) << 4));
+        }
+      }
+      static_assert(C::FM + C::FN <= C::FM * C::FN, "one read per MFMA slot");
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+#pragma unroll
+      for (int t = 0; t < C::FM + C::FN; ++t) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, C::FM * C::FN - C::FM - C::FN - 1, 0);
+    };
+    // Two phases per 64-deep stage, one barrier: (A) the kk=0 MFMAs of stage kt with the kk=1
+    // fragment reads of stage kt interleaved; (B) retire those reads, wait for stage kt+1's DMA
+    // (stage kt+2 stays in flight), barrier, the kk=1 MFMAs of stage kt with the kk=0 reads of
+    // stage kt+1 interleaved, then refill stage kt's now-free buffer with stage kt+3.  Each
+    // stage's DMA has two k-steps to land; LDS reads always run under MFMAs.
+    half8 a0[C::FM], b0[C::FN], a1[C::FM], b1[C::FN];
+    if (nk > 0) issue(0);
+    if (nk > 1) issue(1);
+    if (nk > 2) issue(2);
+    if (nk > 2) wait_vmcnt<2 * (NA + NB)>();
+    else if (nk > 1) wait_vmcnt<NA + NB>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (nk > 0) read_half(0, 0, a0, b0);
+    int cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      mfma_read(a0, b0, cur, 1, a1, b1);
+      const int nxt = cur == 2 ? 0 : cur + 1;
+      if (kt + 1 < nk) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (kt + 2 < nk) wait_vmcnt<NA + NB>();
+        else wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        mfma_read(a1, b1, nxt, 0, a0, b0);
+        if (kt + 3 < nk) issue(cur);
+      } else {
+        mfma_half(a1, b1);
+      }
+      cur = nxt;
+    }
+    __syncthreads();  // all fragment reads done before the epilogue reuses LDS
   } else if constexpr (C::GL) {
     // ---------------- DMA staging: [rows][64 halfs] (128 B) per stage, chunk XOR-swizzled ----------
     // LDS image is lane-linear per wave instruction (q*16 = row*128 + pch*16); the swizzle lives on
@@ -369,7 +588,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
   bool a_ok[C::A_PT];
 #pragma unroll
   for (int i = 0; i < C::A_PT; ++i) {
-    int q = tid + 256 * i;
+    int q = tid + NT * i;
     int row = q / C::KCH;
     int m = m0 + row;
     bool ok = (q < C::A_CH) && (m < M);
@@ -426,7 +645,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
     // B: packed weights, always in bounds (Cout padded to a multiple of 128)
 #pragma unroll
     for (int i = 0; i < C::B_PT; ++i) {
-      int q = tid + 256 * i;
+      int q = tid + NT * i;
       if (q < C::B_CH) {
         int row = q / C::KCH;
         rb[i] = *reinterpret_cast<const half8*>(wptr + (size_t)(n0 + row) * p.Kpad +
@@ -446,7 +665,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
     char* sb = sa + C::A_BYTES;
 #pragma unroll
     for (int i = 0; i < C::A_PT; ++i) {
-      int q = tid + 256 * i;
+      int q = tid + NT * i;
       if (q < C::A_CH) {
         if constexpr (C::BK == 64) *reinterpret_cast<half8*>(sa + swz64(q >> 3, q & 7)) = ra[i];
         else *reinterpret_cast<half8*>(sa + swz(q >> 2, q & 3)) = ra[i];
@@ -454,7 +673,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
     }
 #pragma unroll
     for (int i = 0; i < C::B_PT; ++i) {
-      int q = tid + 256 * i;
+      int q = tid + NT * i;
       if (q < C::B_CH) {
         if constexpr (C::BK == 64) *reinterpret_cast<half8*>(sb + swz64(q >> 3, q & 7)) = rb[i];
         else *reinterpret_cast<half8*>(sb + swz(q >> 2, q & 3)) = rb[i];
@@ -517,7 +736,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
   // Protocol of cdna_hip_programming.md "Projection GEMM at M = 256" item 2 (agent-scope release
   // by every slice, acquire by the last arriver), valid for any placement of slices over XCDs.
   if (S > 1) {
-    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+    const int tile = by * gridDim.x + bx;
     constexpr int SLAB = BM * BN;
     float* slab = p.ws + ((size_t)tile * S + z) * SLAB;
 #pragma unroll
@@ -525,7 +744,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
 #pragma unroll
       for (int j = 0; j < C::FN; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) slab[((i * C::FN + j) * 4 + r) * 256 + tid] = acc[i][j][r];
+        for (int r = 0; r < 4; ++r) slab[((i * C::FN + j) * 4 + r) * NT + tid] = acc[i][j][r];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int* flag = reinterpret_cast<int*>(smem);
@@ -558,7 +777,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
 #pragma unroll
         for (int j = 0; j < C::FN; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i][j][r] += os[((i * C::FN + j) * 4 + r) * 256 + tid];
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += os[((i * C::FN + j) * 4 + r) * NT + tid];
     }
   }
 
@@ -566,7 +785,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
   float* ct = reinterpret_cast<float*>(smem);
 
   constexpr int CPR = BN / 8;  // 8-channel chunks per row
-  constexpr int RPI = 256 / CPR;  // rows per pass
+  constexpr int RPI = NT / CPR;  // rows per pass
   const int cc = tid % CPR;
   const int co = n0 + cc * 8;
   const bool do_stats = p.stats != nullptr;
@@ -753,7 +972,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
         ssq1[j] += __shfl_xor(ssq1[j], off);
       }
     }
-    constexpr int RG = 4;
+    constexpr int RG = C::NW;
     static_assert(4 * RG * BN * 4 <= C::SMEM, "stats reduction must fit in the staging LDS");
     float* red = reinterpret_cast<float*>(smem);
     __syncthreads();  // everyone finished reading the C tile
@@ -769,7 +988,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
     }
     __syncthreads();
     const bool two = (m_last / HWo) != img_lo;
-    for (int t = tid; t < 4 * BN; t += 256) {
+    for (int t = tid; t < 4 * BN; t += NT) {
       const int q = t / BN, col = t - q * BN;
       const int c = n0 + col;
       if (c >= p.Cout || (q >= 2 && !two)) continue;
@@ -784,7 +1003,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const SaConvArgs p) {
 
 template <int BM, int BN, int WM, int WN, int MODE>
 void launch_kernel(dim3 grid, const SaConvArgs* a, hipStream_t stream) {
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, MODE>), grid, dim3(256), 0, stream, *a);
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, MODE>), grid, dim3(64 * WM * WN), 0, stream, *a);
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -840,11 +1059,71 @@ int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+// kGlds3 launcher (8 waves, 1 block per CU): only for the uniform-k fast gather (every source a
+// multiple of 64 channels, K unpadded, <= 64 taps).  Returns 1 when the shape does not qualify.
+template <int BM, int BN, int WM, int WN>
+int launch_glds3(const SaConvArgs* a, hipStream_t stream, bool forced) {
+  const int taps = (a->KD > 0 ? a->KD : 1) * a->KH * a->KW;
+  bool ok = a->Kpad % 64 == 0 && taps <= 64 && (long)taps * a->Cin == a->Kpad;
+  for (int i = 0; i < a->nsrc; ++i) ok = ok && a->src[i].channels % 64 == 0;
+  if (!ok) return 1;
+  const int M = a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
+  const int gx = (M + BM - 1) / BM, gy = (a->Cout + BN - 1) / BN;
+  const long tiles = (long)gx * gy;
+  const int nk = a->Kpad / 64;
+  int S = a->splitk;
+  if (S == 0) {
+    // auto: one block per CU, so aim for >= ~2 blocks per CU over the 256 CUs
+    S = 1;
+    if (a->ws && a->counters && !a->stats && tiles < 384) {
+      S = (int)((512 + tiles - 1) / tiles);
+      if (S > 8) S = 8;
+      if (S > nk / 3) S = nk / 3;
+      while (S > 1 && ((long)S * tiles * BM * BN > a->ws_floats || tiles > a->n_counters)) --S;
+      if (S < 1) S = 1;
+    }
+  }
+  if (S > 1 && (a->stats || !a->ws || !a->counters || (long)S * tiles * BM * BN > a->ws_floats ||
+                tiles > a->n_counters || S > nk))
+    return forced ? -4 : 1;
+  launch_kernel<BM, BN, WM, WN, kGlds3>(dim3(gx, gy, S), a, stream);
+  return (int)hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
   if (a->Kpad % 32 != 0 || a->Cin % 8 != 0 || a->nsrc < 1 || a->nsrc > 4) return -2;
   int cfg = a->tile_cfg;
+  static const int glds3_mode = [] {  // SA_CONV_GLDS3: 0 = never, 1 = auto (default)
+    const char* e = std::getenv("SA_CONV_GLDS3");
+    return e ? std::atoi(e) : 1;
+  }();
+  if (cfg == 4) {
+    const int r = launch_glds3<256, 128, 4, 2>(a, stream, true);
+    return r == 1 ? -5 : r;
+  }
+  if (cfg == 5) {
+    const int r = launch_glds3<128, 64, 2, 2>(a, stream, true);
+    return r == 1 ? -5 : r;
+  }
+  if (cfg == 6) {
+    const int r = launch_glds3<128, 128, 2, 2>(a, stream, true);
+    return r == 1 ? -5 : r;
+  }
+  if (cfg < 0 && glds3_mode == 1 && a->Cout > 64) {
+    // measured on MI355X (tools/conv_bench.py): 256x128 / 8 waves wins once its grid covers the
+    // chip >= 2x (RAFT batch-8 GRU, flow head, motion encoder); 128x64 / 4 waves (2 blocks per CU)
+    // wins for deep K (GRU convs at any batch) and for grids the register path would split
+    const int M = a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
+    const long tiles256 = (long)((M + 255) / 256) * ((a->Cout + 127) / 128);
+    const long tiles128 = (long)((M + 127) / 128) * ((a->Cout + 63) / 64);
+    int r = 1;
+    if (tiles256 >= 512) r = launch_glds3<256, 128, 4, 2>(a, stream, false);
+    else if (a->Kpad >= 2304 || (tiles128 < 320 && a->ws && a->counters && !a->stats))
+      r = launch_glds3<128, 64, 2, 2>(a, stream, false);
+    if (r != 1) return r;
+  }
   if (cfg < 0) {
     const int M = a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
     if (a->Cout <= 16) cfg = 2;

@@ -15,6 +15,7 @@ FIXTURES = ROOT / "tests" / "fixtures"
 def pytest_configure(config):
     # keep test scratch files (tmp_path) inside the repository's git-ignored build/ directory
     if getattr(config.option, "basetemp", None) is None:
+        (ROOT / "build").mkdir(exist_ok=True)
         config.option.basetemp = str(ROOT / "build" / "pytest-tmp")
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) and the native library")
     config.addinivalue_line("markers", "slow: long-running")

@@ -140,6 +140,66 @@ def test_conv2d_multisource_concat_and_residual():
     assert rel_err(nchw(out), ref) < 2e-3
 
 
+@pytest.mark.parametrize("srcs,cout,k,stride,hw,n,splitk", [
+    ((128, 256), 256, 3, 1, (20, 33), 2, 1),   # GRU z/r shape: two sources, 2 n-tiles
+    ((64,), 64, 3, 1, (17, 23), 1, 1),          # Cout < BN (padded weight rows)
+    ((128,), 128, 3, 2, (31, 40), 2, 1),        # stride 2
+    ((192, 64), 96, 1, 1, (9, 30), 3, 1),       # 1x1, M tail, tiles spanning images
+    ((128, 128, 128), 128, 3, 1, (24, 32), 1, 3),  # three sources + forced split-K
+    ((64,), 128, 7, 1, (12, 12), 1, 1),         # 49 taps
+])
+def test_conv2d_glds3_vs_torch(srcs, cout, k, stride, hw, n, splitk):
+    """8-wave 256x128 global->LDS DMA kernel (3-deep LDS ring, counted vmcnt, XCD-ordered tiles)."""
+    O = ops()
+    torch.manual_seed(11)
+    xs = [torch.randn(n, c, *hw, device=DEV) for c in srcs]
+    cin = sum(srcs)
+    w = torch.randn(cout, cin, k, k, device=DEV) / math.sqrt(cin * k * k)
+    b = torch.randn(cout, device=DEV) * 0.1
+    ref = F.conv2d(torch.cat([x.half().float() for x in xs], 1), w.half().float(), b, stride=stride,
+                   padding=k // 2)
+    ref = F.leaky_relu(ref, 0.1)
+    wp, kpad, _ = O.pack_conv_weight(w)
+    ws = O.splitk_workspace() if splitk != 1 else None
+    for _ in range(2):
+        out = O.conv2d([nhwc(x).half() for x in xs], wp, kpad, cout, k, k, bias=b.contiguous(), stride=stride,
+                       act="leaky", alpha=0.1, tile_cfg=4, splitk=splitk, workspace=ws)
+        torch.cuda.synchronize()
+        assert rel_err(nchw(out), ref) < 2e-3
+
+
+def test_conv2d_glds3_gru_and_stats_epilogues():
+    O = ops()
+    torch.manual_seed(12)
+    n, hd, h, w = 2, 128, 21, 26
+    net = torch.randn(n, hd, h, w, device=DEV).tanh()
+    x = torch.randn(n, 256, h, w, device=DEV)
+    cz, cr = (torch.randn(n, hd, h, w, device=DEV) * 0.5 for _ in range(2))
+    wz, wr = (torch.randn(hd, hd + 256, 3, 3, device=DEV) / math.sqrt((hd + 256) * 9) for _ in range(2))
+    hx = torch.cat([net, x], 1).half().float()
+    z = torch.sigmoid(F.conv2d(hx, wz.half().float(), padding=1) + cz.half().float())
+    r = torch.sigmoid(F.conv2d(hx, wr.half().float(), padding=1) + cr.half().float())
+    net_h = nhwc(net).half()
+    ctx = nhwc(torch.cat([cz, cr], 1)).half()
+    wzr, kpad, _ = O.pack_conv_weight(torch.cat([wz, wr], 0))
+    zb = torch.empty(n, h, w, hd, device=DEV, dtype=torch.float16)
+    rhb = torch.empty_like(zb)
+    O.conv2d([net_h, nhwc(x).half()], wzr, kpad, 2 * hd, 3, 3, out=zb, epi="gru_zr", ctx=ctx, aux=zb,
+             hbuf=net_h, rh=rhb, tile_cfg=4)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(zb), z) < 3e-3
+    assert rel_err(nchw(rhb), r * net.half().float()) < 3e-3
+    w2 = torch.randn(128, 256, 3, 3, device=DEV) / 48
+    wp2, kp2, _ = O.pack_conv_weight(w2)
+    stats = torch.zeros(n, 128, 2, dtype=torch.int64, device=DEV)
+    y = O.conv2d(nhwc(x).half(), wp2, kp2, 128, 3, 3, stats=stats, tile_cfg=4)
+    torch.cuda.synchronize()
+    yr = F.conv2d(x.half().float(), w2.half().float(), padding=1)
+    assert rel_err(nchw(y), yr) < 2e-3
+    assert rel_err(stats[..., 0].double() / 2 ** 24, yr.sum((2, 3))) < 1e-2
+    assert rel_err(stats[..., 1].double() / 2 ** 24, (yr * yr).sum((2, 3))) < 1e-2
+
+
 def test_conv2d_padded_channels_and_output_slice():
     O = ops()
     torch.manual_seed(2)

@@ -22,6 +22,10 @@ SHAPES = {
     "zr8": (8, 120, 160, 384, 256, 3, 1),    # GRU 1/4 z,r at batch 8
     "q8": (8, 120, 160, 384, 128, 3, 1),
     "fnet": (2, 240, 320, 64, 64, 3, 1),     # feature encoder layer1 at 1/2
+    "fh8": (8, 120, 160, 128, 256, 3, 1),    # flow head conv1 at batch 8
+    "enc8": (8, 120, 160, 128, 128, 3, 1),   # motion encoder out conv at batch 8
+    "l1b8": (16, 240, 320, 64, 64, 3, 1),    # feature encoder layer1 at batch 8 (both images)
+    "zr8s": (8, 60, 80, 384, 256, 3, 0),     # GRU 1/8 z,r at batch 8
 }
 
 
@@ -29,6 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--shapes", default=",".join(SHAPES))
+    ap.add_argument("--cfgs", default="-1", help="comma list of tile configs (-1 = launcher's choice, 4 = glds3)")
     a = ap.parse_args()
     import torch
     from stereoalgorithms_amd import ops as O
@@ -41,20 +46,25 @@ def main():
         wp, kpad, _ = O.pack_conv_weight(wt)
         b = torch.zeros(cout, device="cuda")
         out = torch.empty(n, h, w, cout, device="cuda", dtype=torch.float16)
-        kw = dict(bias=b, out=out, splitk=sk, workspace=ws if sk != 1 else None)
-        for _ in range(3):
-            O.conv2d(x, wp, kpad, cout, k, k, **kw)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(a.iters):
-            O.conv2d(x, wp, kpad, cout, k, k, **kw)
-        e1.record()
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) / a.iters * 1e3
-        flop = 2.0 * n * h * w * cout * cin * k * k
-        print(f"{name:6s} M={n * h * w:7d} K={cin * k * k:5d} N={cout:4d}: {us:8.2f} us  {flop / us / 1e6:7.1f} TFLOP/s",
-              flush=True)
+        for cfg in map(int, a.cfgs.split(",")):
+            kw = dict(bias=b, out=out, splitk=sk, workspace=ws if sk != 1 else None, tile_cfg=cfg)
+            try:
+                for _ in range(3):
+                    O.conv2d(x, wp, kpad, cout, k, k, **kw)
+            except RuntimeError as e:
+                print(f"{name:6s} cfg {cfg}: {e}", flush=True)
+                continue
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                O.conv2d(x, wp, kpad, cout, k, k, **kw)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) / a.iters * 1e3
+            flop = 2.0 * n * h * w * cout * cin * k * k
+            print(f"{name:6s} cfg {cfg:2d} M={n * h * w:7d} K={cin * k * k:5d} N={cout:4d}: {us:8.2f} us  "
+                  f"{flop / us / 1e6:7.1f} TFLOP/s", flush=True)
 
 
 if __name__ == "__main__":
