@@ -28,7 +28,9 @@ enum SaEpi {
   SA_EPI_GRU_ZR = 1,    // z = sig(acc+b+cz) -> aux ; r = sig(acc+b+cr) -> rh = r*h
   SA_EPI_GRU_Q = 2,     // q = tanh(acc+b+cq) ; h = (1-z)h + zq  (in place on h)
   SA_EPI_FLOW_ACC = 3,  // fp32 out[m*out_stride + c] += acc*scale + bias for c < min(Cout, out_stride)
-  SA_EPI_STORE_F32 = 4  // y = act(acc*scale + bias) -> fp32
+  SA_EPI_STORE_F32 = 4,  // y = act(acc*scale + bias) -> fp32
+  SA_EPI_PROJ = 5        // y = act(acc*scale + bias) projected onto the taps of a following conv
+                         // (proj_* fields; y itself is stored only when out != NULL)
 };
 
 typedef struct {
@@ -81,9 +83,27 @@ typedef struct {
   // broadcast over depth
   const void* gate;
   int32_t gate_stride;
+  // SA_EPI_PROJ: fuse a following (proj_taps = kh*kw)-tap conv with proj_oc output channels into
+  // this conv's epilogue.  Every output pixel m of an n-tile (slice = n0 / BN) writes
+  //   proj_out[(slice * proj_taps * proj_oc + t * proj_oc + o) * proj_plane + m]
+  //     = sum_{c in tile} y[m][c] * proj_w[(t * proj_oc + o) * Cout + c]
+  // and sa_proj_stencil() sums slices and taps (with the zero padding of the following conv).
+  // proj_taps * proj_oc <= 9; Cout a multiple of the chosen n-tile (64 suffices).
+  const float* proj_w;
+  float* proj_out;
+  int32_t proj_taps, proj_oc;
+  int64_t proj_plane;
 } SaConvArgs;
 
 int sa_conv2d(const SaConvArgs* a, hipStream_t stream);
+// Number of n-tiles (projection slices) sa_conv2d() will use for these args.
+int sa_conv2d_nslices(const SaConvArgs* a);
+// Following-conv stencil of SA_EPI_PROJ: out[n][y][x][o] (fp32, pixel stride out_stride) gets
+// (accumulate ? out + : ) bias[o] + sum_{s < nslices, (ky,kx)} P[s][(ky*kw+kx)*oc + o][n][y+ky-ph][x+kx-pw]
+// (zero outside the image).  Stride-1 'same' convs only.
+int sa_proj_stencil(const float* P, int nslices, long plane, int N, int H, int W, int kh, int kw,
+                    int oc, const float* bias, float* out, int out_stride, int accumulate,
+                    hipStream_t stream);
 
 // ---- normalisation / elementwise ------------------------------------------------------------
 // Instance-norm apply (biased var, eps): y = act(norm(x)); if res: y = act2(resnorm(res) + y)

@@ -126,7 +126,9 @@ __device__ __forceinline__ void wait_vmcnt() {
 #undef SA_VMCNT_CASE
 }
 
-template <int BM, int BN, int WM, int WN, int MODE>
+// PROJ: the SA_EPI_PROJ epilogue is compiled only into its own instantiations -- its registers
+// (hoisted tap weights, 16 partials) would otherwise cost every other conv its occupancy
+template <int BM, int BN, int WM, int WN, int MODE, bool PROJ = false>
 __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvArgs p) {
   using C = ConvCfg<BM, BN, WM, WN, MODE>;
   __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
@@ -788,7 +790,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
   constexpr int RPI = NT / CPR;  // rows per pass
   const int cc = tid % CPR;
   const int co = n0 + cc * 8;
-  const bool do_stats = p.stats != nullptr;
+  const bool do_stats = !PROJ && p.stats != nullptr;
   // Instance-norm statistics: per-thread partial sums for the (at most) two images a BM-row tile
   // can straddle, reduced across the block in LDS, then ONE double atomic per (block, image,
   // channel).  Per-thread atomics to the same N*C addresses serialise at the memory side
@@ -830,6 +832,20 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
       }
   __syncthreads();
 
+  // SA_EPI_PROJ: this thread's 8 channels of the projection taps, hoisted out of the row loop
+  constexpr int kProjMax = PROJ ? 9 : 1;
+  float pw8[kProjMax][8];
+  if (PROJ) {
+    const int np = p.proj_taps * p.proj_oc;
+    // opaque base pointer: keeps the compiler from hoisting these loads above the main loop (72
+    // registers live across it would cost every conv kernel of this template its occupancy)
+    const float* pwb = p.proj_w + co;
+    asm volatile("" : "+v"(pwb));
+#pragma unroll
+    for (int t = 0; t < kProjMax; ++t)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pw8[t][j] = (t < np && j < nvalid) ? pwb[(size_t)t * p.Cout + j] : 0.f;
+  }
   if (nvalid > 0) {
     for (int row = tid / CPR; row < BM; row += RPI) {
       const int m = m0 + row;
@@ -917,6 +933,45 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
             }
           }
         }
+      } else if (PROJ) {
+        // flow-head fusion: project this row's channels onto the taps of the following conv.
+        // The CPR lanes holding one row (consecutive, CPR-aligned) reduce-scatter their 16 tap
+        // partials (taps padded with zeros) with 15 xor shuffles for CPR = 16: afterwards lane cc
+        // holds the totals of taps PF*cc .. PF*cc + PF-1 (PF = 16 / CPR)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], p.act, p.alpha);
+        if (p.out) {
+          f16* op = reinterpret_cast<f16*>(p.out) + (size_t)m * p.out_stride + co;
+          if (full) store8(op, v);
+          else for (int j = 0; j < nvalid; ++j) op[j] = (f16)v[j];
+        }
+        float y[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          y[t] = 0.f;
+          if (t < kProjMax) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) y[t] += v[j] * pw8[t][j];
+          }
+        }
+#pragma unroll
+        for (int k = 16, o = CPR / 2; o >= 1; k >>= 1, o >>= 1) {
+          const bool up = (cc & o) != 0;
+#pragma unroll
+          for (int i = 0; i < k / 2; ++i) {
+            const float give = up ? y[i] : y[i + k / 2];
+            const float keep = up ? y[i + k / 2] : y[i];
+            y[i] = keep + __shfl_xor(give, o);
+          }
+        }
+        constexpr int PF = 16 / CPR;
+        const int np = p.proj_taps * p.proj_oc;
+        float* pout = p.proj_out + (size_t)by * np * p.proj_plane + m;
+#pragma unroll
+        for (int j = 0; j < PF; ++j) {
+          const int t = PF * cc + j;
+          if (t < np) pout[(size_t)t * p.proj_plane] = y[j];
+        }
       } else if (p.epi == SA_EPI_GRU_ZR) {
         const int Hd = p.Cout >> 1;
         float c8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1003,7 +1058,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
 
 template <int BM, int BN, int WM, int WN, int MODE>
 void launch_kernel(dim3 grid, const SaConvArgs* a, hipStream_t stream) {
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, MODE>), grid, dim3(64 * WM * WN), 0, stream, *a);
+  if (a->epi == SA_EPI_PROJ)
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, MODE, true>), grid, dim3(64 * WM * WN), 0, stream, *a);
+  else
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, MODE, false>), grid, dim3(64 * WM * WN), 0, stream, *a);
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -1061,12 +1119,11 @@ int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
 
 // kGlds3 launcher (8 waves, 1 block per CU): only for the uniform-k fast gather (every source a
 // multiple of 64 channels, K unpadded, <= 64 taps).  Returns 1 when the shape does not qualify.
+bool glds3_eligible(const SaConvArgs* a);
+
 template <int BM, int BN, int WM, int WN>
 int launch_glds3(const SaConvArgs* a, hipStream_t stream, bool forced) {
-  const int taps = (a->KD > 0 ? a->KD : 1) * a->KH * a->KW;
-  bool ok = a->Kpad % 64 == 0 && taps <= 64 && (long)taps * a->Cin == a->Kpad;
-  for (int i = 0; i < a->nsrc; ++i) ok = ok && a->src[i].channels % 64 == 0;
-  if (!ok) return 1;
+  if (!glds3_eligible(a)) return 1;
   const int M = a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
   const int gx = (M + BM - 1) / BM, gy = (a->Cout + BN - 1) / BN;
   const long tiles = (long)gx * gy;
@@ -1090,55 +1147,116 @@ int launch_glds3(const SaConvArgs* a, hipStream_t stream, bool forced) {
   return (int)hipGetLastError();
 }
 
-}  // namespace
+// the uniform-k DMA kernels need every source a multiple of 64 channels, K unpadded, <= 64 taps
+bool glds3_eligible(const SaConvArgs* a) {
+  const int taps = (a->KD > 0 ? a->KD : 1) * a->KH * a->KW;
+  bool ok = a->Kpad % 64 == 0 && taps <= 64 && (long)taps * a->Cin == a->Kpad;
+  for (int i = 0; i < a->nsrc; ++i) ok = ok && a->src[i].channels % 64 == 0;
+  return ok;
+}
 
-extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
-  if (a->Kpad % 32 != 0 || a->Cin % 8 != 0 || a->nsrc < 1 || a->nsrc > 4) return -2;
-  int cfg = a->tile_cfg;
+int pick_cfg(const SaConvArgs* a) {
+  if (a->tile_cfg >= 0) return a->tile_cfg;
   static const int glds3_mode = [] {  // SA_CONV_GLDS3: 0 = never, 1 = auto (default)
     const char* e = std::getenv("SA_CONV_GLDS3");
     return e ? std::atoi(e) : 1;
   }();
-  if (cfg == 4) {
-    const int r = launch_glds3<256, 128, 4, 2>(a, stream, true);
-    return r == 1 ? -5 : r;
-  }
-  if (cfg == 5) {
-    const int r = launch_glds3<128, 64, 2, 2>(a, stream, true);
-    return r == 1 ? -5 : r;
-  }
-  if (cfg == 6) {
-    const int r = launch_glds3<128, 128, 2, 2>(a, stream, true);
-    return r == 1 ? -5 : r;
-  }
-  if (cfg < 0 && glds3_mode == 1 && a->Cout > 64) {
+  const int M = a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
+  if (glds3_mode == 1 && a->Cout > 64 && glds3_eligible(a) && (a->splitk <= 1 || a->ws)) {
     // measured on MI355X (tools/conv_bench.py): 256x128 / 8 waves wins once its grid covers the
     // chip >= 2x (RAFT batch-8 GRU, flow head, motion encoder); 128x64 / 4 waves (2 blocks per CU)
     // wins for deep K (GRU convs at any batch) and for grids the register path would split
-    const int M = a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
     const long tiles256 = (long)((M + 255) / 256) * ((a->Cout + 127) / 128);
     const long tiles128 = (long)((M + 127) / 128) * ((a->Cout + 63) / 64);
-    int r = 1;
-    if (tiles256 >= 512) r = launch_glds3<256, 128, 4, 2>(a, stream, false);
-    else if (a->Kpad >= 2304 || (tiles128 < 320 && a->ws && a->counters && !a->stats))
-      r = launch_glds3<128, 64, 2, 2>(a, stream, false);
-    if (r != 1) return r;
+    if (tiles256 >= 512) return 4;
+    if (a->Kpad >= 2304 || (tiles128 < 320 && a->ws && a->counters && !a->stats)) return 5;
   }
-  if (cfg < 0) {
-    const int M = a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
-    if (a->Cout <= 16) cfg = 2;
-    else if (a->Cout <= 64) cfg = 1;
-    else {
-      // prefer the 128x128 tile only when it still fills the chip
-      long tiles128 = (long)((M + 127) / 128) * ((a->Cout + 127) / 128);
-      cfg = tiles128 >= 512 ? 0 : 1;
-    }
+  if (a->Cout <= 16) return 2;
+  if (a->Cout <= 64) return 1;
+  // prefer the 128x128 tile only when it still fills the chip
+  const long tiles128 = (long)((M + 127) / 128) * ((a->Cout + 127) / 128);
+  return tiles128 >= 512 ? 0 : 1;
+}
+
+int cfg_bn(int cfg) {
+  switch (cfg) {
+    case 0: case 4: case 6: return 128;
+    case 1: case 3: case 5: return 64;
+    case 2: return 16;
+    default: return 0;
   }
+}
+
+}  // namespace
+
+extern "C" int sa_conv2d_nslices(const SaConvArgs* a) {
+  const int bn = cfg_bn(pick_cfg(a));
+  return bn > 0 ? (a->Cout + bn - 1) / bn : -3;
+}
+
+extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
+  if (a->Kpad % 32 != 0 || a->Cin % 8 != 0 || a->nsrc < 1 || a->nsrc > 4) return -2;
+  const int cfg = pick_cfg(a);
+  // the projection epilogue reduces whole rows of an n-tile: every tile must be full
+  if (a->epi == SA_EPI_PROJ && (cfg_bn(cfg) == 0 || a->Cout % cfg_bn(cfg) != 0 || !a->proj_w || !a->proj_out ||
+                                a->proj_taps * a->proj_oc > 9 || a->proj_taps * a->proj_oc < 1))
+    return -6;
   switch (cfg) {
     case 0: return launch_cfg<128, 128, 2, 2>(a, stream);
     case 1: return launch_cfg<128, 64, 2, 2>(a, stream);
     case 2: return launch_cfg<256, 16, 4, 1>(a, stream);
     case 3: return launch_cfg<64, 64, 2, 2>(a, stream);
+    case 4: case 5: case 6: {
+      const int r = cfg == 4 ? launch_glds3<256, 128, 4, 2>(a, stream, true)
+                  : cfg == 5 ? launch_glds3<128, 64, 2, 2>(a, stream, true)
+                             : launch_glds3<128, 128, 2, 2>(a, stream, true);
+      return r == 1 ? -5 : r;
+    }
     default: return -3;
   }
+}
+
+// ---------------- SA_EPI_PROJ stencil: the following conv's tap sum ----------------
+namespace {
+__global__ __launch_bounds__(256) void proj_stencil_kernel(const float* __restrict__ P, int nslices, long plane,
+                                                           int N, int H, int W, int kh, int kw, int oc,
+                                                           const float* __restrict__ bias, float* out,
+                                                           int out_stride, int accumulate) {
+  const long M = (long)N * H * W;
+  const long m = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  const int x = (int)(m % W);
+  const long r = m / W;
+  const int y = (int)(r % H);
+  const int ph = kh / 2, pw = kw / 2;
+  const int np = kh * kw * oc;
+  for (int o = 0; o < oc; ++o) {
+    float acc = bias ? bias[o] : 0.f;
+    for (int s = 0; s < nslices; ++s) {
+      const float* ps = P + (size_t)s * np * plane;
+      for (int ky = 0; ky < kh; ++ky) {
+        const int yy = y + ky - ph;
+        if (yy < 0 || yy >= H) continue;
+        for (int kx = 0; kx < kw; ++kx) {
+          const int xx = x + kx - pw;
+          if (xx < 0 || xx >= W) continue;
+          const long q = m + (long)(ky - ph) * W + (kx - pw);
+          acc += ps[(size_t)((ky * kw + kx) * oc + o) * plane + q];
+        }
+      }
+    }
+    float* op = out + m * out_stride + o;
+    *op = accumulate ? *op + acc : acc;
+  }
+}
+}  // namespace
+
+extern "C" int sa_proj_stencil(const float* P, int nslices, long plane, int N, int H, int W, int kh, int kw,
+                               int oc, const float* bias, float* out, int out_stride, int accumulate,
+                               hipStream_t stream) {
+  const long M = (long)N * H * W;
+  if (nslices < 1 || plane < M || oc < 1 || (kh & 1) == 0 || (kw & 1) == 0) return -2;
+  hipLaunchKernelGGL(proj_stencil_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, stream, P, nslices,
+                     plane, N, H, W, kh, kw, oc, bias, out, out_stride, accumulate);
+  return (int)hipGetLastError();
 }

@@ -11,6 +11,7 @@
 namespace {
 typedef _Float16 f16;
 typedef f16 half8 __attribute__((ext_vector_type(8)));
+typedef f16 half4_ __attribute__((ext_vector_type(4)));
 typedef float float4_ __attribute__((ext_vector_type(4)));
 
 inline int grid_for(long work, int block = 256) {
@@ -97,12 +98,15 @@ __global__ void __launch_bounds__(256) warp_cost_kernel(const f16* __restrict__ 
     const int img = n % B;
     const float* h = hyp + p * 16;
     const float d = h[0], sx = h[1], sy = h[2];
-    f16 res[64];
-#pragma unroll
+    f16* orow = out + p * 64;
+    // rows v are a runtime loop (a fully unrolled 4x4x3 body took minutes to compile and spilled);
+    // one row's 3 shifts x 4 columns are stored as three 8-byte groups
+#pragma unroll 1
     for (int v = 0; v < 4; ++v) {
       const int py = 4 * y + v;
       const f16* lrow = el + ((long)img * H + py) * W * els;
       const f16* rrow = er + ((long)img * H + py) * W * ers;
+      float cst[3][4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int px = 4 * x + u;
@@ -130,20 +134,23 @@ __global__ void __launch_bounds__(256) warp_cost_kernel(const f16* __restrict__ 
 #pragma unroll
             for (int j = 0; j < 8; ++j) cost += fabsf(lv[c0 + j] - ((1.f - a) * (float)r0[j] + a * (float)r1[j]));
           }
-          res[s * 16 + v * 4 + u] = (f16)cost;
+          cst[s][u] = cost;
         }
       }
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        half4_ t = {(f16)cst[s][0], (f16)cst[s][1], (f16)cst[s][2], (f16)cst[s][3]};
+        *reinterpret_cast<half4_*>(orow + s * 16 + v * 4) = t;
+      }
     }
+    half8 t0, t1;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) res[48 + k] = (f16)h[k];
-    half8* o = reinterpret_cast<half8*>(out + p * 64);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      half8 t;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) t[j] = res[q * 8 + j];
-      o[q] = t;
+    for (int k = 0; k < 8; ++k) {
+      t0[k] = (f16)h[k];
+      t1[k] = (f16)h[8 + k];
     }
+    reinterpret_cast<half8*>(orow)[6] = t0;
+    reinterpret_cast<half8*>(orow)[7] = t1;
   }
 }
 

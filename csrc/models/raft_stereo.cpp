@@ -15,6 +15,7 @@
 //   reprojection (base class)
 // The entire frame is one hipGraph.
 #include <cmath>
+#include <cstdlib>
 
 #include "blocks.h"
 
@@ -93,6 +94,16 @@ class RaftStereo : public StereoEngine {
   Tensor z_[3], rh_[3];
   Tensor pool_[2], interp_[2];  // pool_[i] = pool2x(net[i]) at level i+1; interp_[i] = interp(net[i+1]) at level i
   Tensor fh_, mask_;
+  // flow-head fusion (SA_EPI_PROJ): conv2's x-channel taps [9][256] fp32, its bias, the per-n-tile
+  // tap planes [<=4][9][M] written by conv1's epilogue
+  float* proj_w_ = nullptr;
+  float* proj_b_ = nullptr;
+  float* proj_p_ = nullptr;
+  // SA_RAFT_FUSE_FH: 0 = off, 1 = on, unset = auto.  Measured in-process on MI355X
+  // (tools/ab_engine.py): batch 8 69.7 vs 70.7 ms/step fused vs unfused, batch 1 25.1 vs 24.3 ms
+  // (the projection instantiation's extra registers cost more than the skipped 256x16 conv there)
+  int fuse_fh_mode_ = std::getenv("SA_RAFT_FUSE_FH") ? std::atoi(std::getenv("SA_RAFT_FUSE_FH")) : -1;
+  bool fuse_fh_ = false;
   float* pyr_ = nullptr;
   float* flow_ = nullptr;
   int lh_[3], lw_[3];
@@ -232,6 +243,14 @@ void RaftStereo::build(WeightSource& src) {
     std::vector<float> wx(w2.data.begin(), w2.data.begin() + 256 * 9);
     std::vector<float> bx = {b2.data[0]};
     fh2_.build_raw(a, wx, bx, 1, 256, {{256, 256}}, s3);
+    // the same taps as [tap][c] for the fused projection
+    std::vector<float> pw(9 * 256);
+    for (int c = 0; c < 256; ++c)
+      for (int t = 0; t < 9; ++t) pw[t * 256 + c] = w2.data[c * 9 + t];
+    proj_w_ = (float*)a.alloc(pw.size() * 4);
+    proj_b_ = (float*)a.alloc(4);
+    HIP_CHECK(hipMemcpy(proj_w_, pw.data(), pw.size() * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(proj_b_, bx.data(), 4, hipMemcpyHostToDevice));
   }
   mask2_.build(a, ws, {u + "mask.2"}, {{256, 256}}, s1, {}, 0.25f);
 
@@ -243,6 +262,8 @@ void RaftStereo::build(WeightSource& src) {
   corflo_ = make_tensor(a, Bn, h0, w0, 128);
   motion_ = make_tensor(a, Bn, h0, w0, 128);
   fh_ = make_tensor(a, Bn, h0, w0, 512);
+  fuse_fh_ = fuse_fh_mode_ > 0 || (fuse_fh_mode_ < 0 && Bn >= 4);
+  if (fuse_fh_) proj_p_ = (float*)a.alloc((size_t)4 * 9 * Bn * h0 * w0 * 4);  // <= 4 n-tiles of 64 channels
   mask_ = make_tensor(a, Bn, h0, w0, round_up(f * f * 9, 8));
   for (int i = 0; i + 1 < rc_.n_gru; ++i) {
     pool_[i] = make_tensor(a, Bn, lh_[i + 1], lw_[i + 1], hd);
@@ -382,14 +403,31 @@ void RaftStereo::forward(hipStream_t s) {
       gru(s, 0, {motion_});
     }
     // flow head (+ mask head on the last iteration), coords1 += delta (x only)
-    if (last) fh1mask_.run(s, {net_[0]}, fh_, SA_ACT_RELU);
-    else fh1_.run(s, {net_[0]}, fh_.slice_c(0, 256), SA_ACT_RELU);
-    {
+    if (last || !fuse_fh_) {
+      if (last) fh1mask_.run(s, {net_[0]}, fh_, SA_ACT_RELU);
+      else fh1_.run(s, {net_[0]}, fh_.slice_c(0, 256), SA_ACT_RELU);
       SaConvArgs fa = fh2_.args({fh_.slice_c(0, 256)}, Tensor{flow_, Bn, h0, w0, 1, 1, DT::F32});
       fa.epi = SA_EPI_FLOW_ACC;
       fh2_.launch(s, fa);
+      if (last) mask2_.run(s, {fh_.slice_c(256, 256)}, mask_);
+    } else {
+      // conv2 (256 -> 1, 3x3) fused into conv1's epilogue: per-pixel tap projections, then a
+      // 9-tap stencil adds bias + taps into the flow; the 256-channel activation never hits memory
+      SaConvArgs pa = fh1_.args({net_[0]}, fh_.slice_c(0, 256));
+      pa.out = nullptr;
+      pa.act = SA_ACT_RELU;
+      pa.epi = SA_EPI_PROJ;
+      pa.proj_w = proj_w_;
+      pa.proj_out = proj_p_;
+      pa.proj_taps = 9;
+      pa.proj_oc = 1;
+      pa.proj_plane = (long)Bn * h0 * w0;
+      const int nsl = sa_conv2d_nslices(&pa);
+      SA_REQUIRE(nsl >= 1 && nsl <= 4, "flow-head projection slices %d", nsl);
+      fh1_.launch(s, pa);
+      check(sa_proj_stencil(proj_p_, nsl, pa.proj_plane, Bn, h0, w0, 3, 3, 1, proj_b_, flow_, 1, 1, s),
+            "flow-head stencil");
     }
-    if (last) mask2_.run(s, {fh_.slice_c(256, 256)}, mask_);
   }
   // convex upsampling; disparity = -flow_up
   check(sa_convex_upsample(mask_.ptr, mask_.stride, flow_, Bn, h0, w0, f, -1.f, disp_, s),

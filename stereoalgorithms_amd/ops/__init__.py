@@ -15,7 +15,7 @@ import torch
 from .. import _native as N
 
 __all__ = [
-    "splitk_workspace", "pack_conv_weight", "conv2d", "instnorm_apply", "avgpool3s2", "avgpool_k", "interp_bilinear",
+    "splitk_workspace", "pack_conv_weight", "conv2d", "proj_stencil", "instnorm_apply", "avgpool3s2", "avgpool_k", "interp_bilinear",
     "corr1d_pyramid", "corr1d_lookup", "convex_upsample", "preprocess", "remap_bgr", "reproject",
     "agcl_corr", "linear_attention", "layernorm", "ew", "interp_flow", "convex_upsample_c",
     "pack_conv3d_weight", "deconv_as_conv_weight", "conv3d", "dwconv3x3", "norm_corr_volume", "topk_disparity",
@@ -38,6 +38,18 @@ def _pix_stride(t: torch.Tensor) -> int:
     s = t.stride(2)
     assert t.stride(1) == w * s and (n == 1 or t.stride(0) == h * w * s), "pixels must be uniformly strided"
     return s
+
+
+def proj_stencil(P, nslices, n, h, w, kh, kw, oc, bias=None, out=None, accumulate=False):
+    """Tap sum of a conv fused into the producer's epilogue (``conv2d(..., epi="proj")``): fp32
+    ``out[n, h, w, oc]`` (+)= bias + sum over slices and taps with zero padding."""
+    if out is None:
+        out = torch.zeros(n, h, w, oc, dtype=torch.float32, device=P.device)
+    assert out.dtype == torch.float32
+    N.check(N.dev().sa_proj_stencil(P.data_ptr(), nslices, P.shape[-1], n, h, w, kh, kw, oc,
+                                    bias.data_ptr() if bias is not None else None, out.data_ptr(),
+                                    _pix_stride(out), int(accumulate), _stream()), "sa_proj_stencil")
+    return out
 
 
 def splitk_workspace(floats: int = 1 << 22, counters: int = 4096, device="cuda"):
@@ -69,8 +81,10 @@ def pack_conv_weight(w: torch.Tensor, segs: Sequence[tuple[int, int]] | None = N
 def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1, act="none",
            act2="none", res=None, out=None, epi="store", scale=1.0, alpha=0.01, stats=None,
            ctx=None, aux=None, hbuf=None, rh=None, tile_cfg=-1, splitk=1, workspace=None, up=0, cout_real=0,
-           gate=None):
-    """NHWC fp16 implicit-GEMM conv.  ``splitk``: 1 = off, 0 = auto, >1 = forced; needs
+           gate=None, proj=None):
+    """NHWC fp16 implicit-GEMM conv.  ``proj = (w2 fp32 [taps*oc, cout], taps, oc)`` with
+    ``epi="proj"``: the epilogue projects the activated output onto the taps of a following conv
+    and the call returns ``(out_or_None, P, nslices)`` for :func:`proj_stencil`.  ``splitk``: 1 = off, 0 = auto, >1 = forced; needs
     ``workspace`` = (fp32 slab tensor, int32 counter tensor zero-initialised).  ``up`` = 2: transposed
     conv, the 4 parity classes (cout = 4 * cout_real) are scattered to a 2x output.  ``gate``: fp16
     NHWC multiplier applied after the activation."""
@@ -100,7 +114,7 @@ def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1
     a.N, a.H, a.W, a.Cin = n, h, w, cin
     a.KH, a.KW, a.sh, a.sw, a.ph, a.pw, a.dh, a.dw = kh, kw, sh, sw, ph, pw, dil, dil
     a.Ho, a.Wo = ho, wo
-    if out is None:
+    if out is None and epi != "proj":
         dt = torch.float32 if epi == "store_f32" else torch.float16
         if up:
             out = torch.empty(n, 2 * ho, 2 * wo, cout_real, dtype=dt, device=xs[0].device)
@@ -112,8 +126,8 @@ def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1
     a.weight = wpacked.data_ptr()
     a.bias = bias.data_ptr() if bias is not None else None
     a.Cout, a.Kpad = cout, kpad
-    a.out = out.data_ptr()
-    a.out_stride = out.stride(2) if out.dim() == 4 else 1
+    a.out = out.data_ptr() if out is not None else None
+    a.out_stride = (out.stride(2) if out.dim() == 4 else 1) if out is not None else 0
     a.epi, a.act, a.act2 = N.EPI[epi], N.ACT[act], N.ACT[act2]
     a.alpha, a.scale = alpha, scale
     if res is not None:
@@ -135,7 +149,18 @@ def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1
         ws, cnt = workspace
         assert ws.dtype == torch.float32 and cnt.dtype == torch.int32
         a.ws, a.counters, a.ws_floats, a.n_counters = ws.data_ptr(), cnt.data_ptr(), ws.numel(), cnt.numel()
+    P = None
+    if epi == "proj":
+        w2, taps, oc = proj
+        assert w2.dtype == torch.float32 and w2.is_contiguous() and w2.shape == (taps * oc, cout)
+        a.tile_cfg = tile_cfg
+        nsl = N.dev().sa_conv2d_nslices(C.byref(a))
+        assert nsl > 0
+        P = torch.empty(nsl, taps * oc, n * ho * wo, dtype=torch.float32, device=xs[0].device)
+        a.proj_w, a.proj_out, a.proj_taps, a.proj_oc, a.proj_plane = w2.data_ptr(), P.data_ptr(), taps, oc, n * ho * wo
     N.check(N.dev().sa_conv2d(C.byref(a), _stream()), "sa_conv2d")
+    if epi == "proj":
+        return out, P, P.shape[0]
     return out
 
 

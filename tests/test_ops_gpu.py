@@ -200,6 +200,31 @@ def test_conv2d_glds3_gru_and_stats_epilogues():
     assert rel_err(stats[..., 1].double() / 2 ** 24, (yr * yr).sum((2, 3))) < 1e-2
 
 
+@pytest.mark.parametrize("n,hw,cfg,oc", [(1, (24, 40), -1, 1), (2, (13, 21), 4, 1), (1, (30, 17), 5, 1),
+                                            (1, (9, 11), 0, 1)])
+def test_conv2d_projection_epilogue_flow_head(n, hw, cfg, oc):
+    """RAFT flow head fused: conv1 (3x3 128->256, ReLU) with the 3x3 256->oc conv2 projected in its
+    epilogue and summed by the stencil == conv2(relu(conv1(x))) (+ the running flow)."""
+    O = ops()
+    torch.manual_seed(21)
+    x = torch.randn(n, 128, *hw, device=DEV)
+    w1 = torch.randn(256, 128, 3, 3, device=DEV) / math.sqrt(128 * 9)
+    b1 = torch.randn(256, device=DEV) * 0.1
+    w2 = torch.randn(oc, 256, 3, 3, device=DEV) / math.sqrt(256 * 9)
+    b2 = torch.randn(oc, device=DEV) * 0.1
+    y1 = F.relu(F.conv2d(x.half().float(), w1.half().float(), b1, padding=1))
+    flow0 = torch.randn(n, *hw, oc, device=DEV)
+    ref = F.conv2d(y1, w2, b2, padding=1).permute(0, 2, 3, 1) + flow0
+    wp, kpad, _ = O.pack_conv_weight(w1)
+    w2p = w2.permute(2, 3, 0, 1).reshape(9 * oc, 256).contiguous()  # [(ky*3+kx)*oc + o][c]
+    _, P, nsl = O.conv2d(nhwc(x).half(), wp, kpad, 256, 3, 3, bias=b1.contiguous(), act="relu", epi="proj",
+                         proj=(w2p, 9, oc), tile_cfg=cfg)
+    out = flow0.clone()
+    O.proj_stencil(P, nsl, n, hw[0], hw[1], 3, 3, oc, bias=b2.contiguous(), out=out, accumulate=True)
+    torch.cuda.synchronize()
+    assert rel_err(out - flow0, ref - flow0) < 3e-3
+
+
 def test_conv2d_padded_channels_and_output_slice():
     O = ops()
     torch.manual_seed(2)
