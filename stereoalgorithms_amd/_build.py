@@ -32,7 +32,7 @@ ABI_LIBS = {"raftstereo_abi.cpp": "libRAFTStereo.so", "hitnet_abi.cpp": "libHitN
 # apps source -> ABI library it links (reference demo executable names)
 APPS = {"raft_stereo_demo.cpp": "libRAFTStereo.so", "HitNet_demo.cpp": "libHitNet.so",
         "crestereo_demo.cpp": "libCREStereo.so", "fastacvnet_plus_demo.cpp": "libFastACVNet_plus.so",
-        "Stereo_Calibration.cpp": "libstereo_host.so"}
+        "Stereo_Calibration.cpp": "libstereo_host.so", "stereo_capture.cpp": "libstereo_host.so"}
 
 COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC / 'include'}", "-Wall", "-Wno-unused-function"]
 

@@ -13,15 +13,18 @@ def _pairs(b, h, w):
     return torch.from_numpy(l).cuda(), torch.from_numpy(r).cuda()
 
 
-@pytest.mark.parametrize("preset,iters,hw", [
-    ("raftstereo-realtime", 7, (96, 160)),
-    ("raftstereo-sceneflow", 6, (96, 128)),
+@pytest.mark.parametrize("preset,iters,hw,fuse", [
+    ("raftstereo-realtime", 7, (96, 160), ""),
+    ("raftstereo-sceneflow", 6, (96, 128), "0"),
+    ("raftstereo-sceneflow", 6, (96, 128), "1"),  # flow head conv2 fused into conv1's epilogue
 ])
-def test_engine_matches_oracle(tmp_path, preset, iters, hw):
+def test_engine_matches_oracle(tmp_path, monkeypatch, preset, iters, hw, fuse):
     from stereoalgorithms_amd.models import raft_stereo as R
     from stereoalgorithms_amd.models.engine import NativeStereoEngine
     from stereoalgorithms_amd.utils.weights import save_model
     h, w = hw
+    if fuse:
+        monkeypatch.setenv("SA_RAFT_FUSE_FH", fuse)
     m = R.build(preset, seed=0)
     path = save_model(m, tmp_path / "w.safetensors", preset)
     left, right = _pairs(2, h, w)

@@ -1,0 +1,84 @@
+"""CPU tests of the capture-side tools: side-by-side splitter (reference
+Stereo_Calibration/process_image.py) and the V4L2 capture app's argument / error handling
+(reference usb_test.py; no camera exists here, so only the paths that need none are exercised)."""
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "tools"))
+
+
+def _host():
+    from stereoalgorithms_amd.utils import hostlib as H
+    try:
+        H.lib()
+    except Exception as e:  # pragma: no cover
+        pytest.skip(f"host library not built: {e}")
+    return H
+
+
+def test_split_stereo_halves(tmp_path):
+    H = _host()
+    import split_stereo
+    src = tmp_path / "raw"
+    src.mkdir()
+    yy, xx = np.mgrid[0:48, 0:128]
+    frames = []
+    for i in range(3):  # smooth gradients (JPEG-friendly), different ramps on the two halves
+        f = np.stack([(xx + 20 * i) % 128, yy * 2 + 10 * i, np.where(xx < 64, 40, 200) + 0 * yy], -1)
+        frames.append(f.astype(np.uint8))
+    for i, f in enumerate(frames):
+        assert H.imwrite(src / f"{i:02d}.png", f)
+    dst = tmp_path / "lr"
+    assert split_stereo.main([str(src), str(dst)]) == 0
+    for i, f in enumerate(frames):
+        l, r = H.imread(dst / f"left{i}.jpg"), H.imread(dst / f"right{i}.jpg")
+        assert l.shape == (48, 64, 3) and r.shape == (48, 64, 3)
+        # JPEG q95 round trip: small error, halves not swapped
+        assert np.abs(l.astype(int) - f[:, :64]).mean() < 3
+        assert np.abs(r.astype(int) - f[:, 64:]).mean() < 3
+        assert np.abs(l.astype(int) - f[:, 64:]).mean() > 30
+
+
+def test_split_pair_exact_and_bad_column():
+    import split_stereo
+    img = np.arange(4 * 10 * 3, dtype=np.uint8).reshape(4, 10, 3)
+    l, r = split_stereo.split_pair(img)
+    assert np.array_equal(np.concatenate([l, r], 1), img) and l.shape[1] == 5
+    l, r = split_stereo.split_pair(img, 3)
+    assert l.shape[1] == 3 and r.shape[1] == 7
+    with pytest.raises(ValueError):
+        split_stereo.split_pair(img, 10)
+
+
+def test_stereo_capture_cli():
+    exe = ROOT / "stereoalgorithms_amd" / "bin" / "stereo_capture"
+    if not exe.exists():
+        pytest.skip("capture app not built")
+    r = subprocess.run([str(exe), "--help"], capture_output=True, text=True, timeout=30)
+    assert r.returncode == 0 and "--device" in r.stdout
+    r = subprocess.run([str(exe), "--device", "/dev/does-not-exist"], capture_output=True, text=True, timeout=30)
+    assert r.returncode == 1 and "cannot open" in r.stderr
+    r = subprocess.run([str(exe), "--bogus"], capture_output=True, text=True, timeout=30)
+    assert r.returncode == 2
+
+
+def test_cmake_configures(tmp_path):
+    """The CMake build (for C++ users, as the reference's) configures; SA_TEST_CMAKE_BUILD=1 also
+    builds every target (~1 min on 8 cores)."""
+    import shutil
+    if not shutil.which("cmake") or not Path("/opt/rocm/llvm/bin/clang++").exists():
+        pytest.skip("cmake / ROCm toolchain not available")
+    b = tmp_path / "cmb"
+    r = subprocess.run(["cmake", "-S", str(ROOT), "-B", str(b)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    if os.environ.get("SA_TEST_CMAKE_BUILD") == "1":
+        r = subprocess.run(["cmake", "--build", str(b), "-j", "8"], capture_output=True, text=True, timeout=1800)
+        assert r.returncode == 0, r.stdout[-3000:]
+        for t in ("libstereo_amd.so", "libRAFTStereo.so", "raft_stereo_demo", "Stereo_Calibration"):
+            assert (b / t).exists()
