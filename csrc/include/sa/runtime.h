@@ -113,6 +113,24 @@ struct ScopedSplitK {
   ~ScopedSplitK();
 };
 
+// ------------------------------------------------------------------ conv tactic selection
+// The MI355X analogue of TensorRT's tactic selection at engine build (common/ONNX2TRT.cpp:111):
+// during the engine's eager tuning pass every distinct conv shape is timed over the tile / split-K
+// candidates of sa_conv2d (outputs redirected to scratch, so in-place epilogues are not disturbed)
+// and the fastest is recorded in a process-wide plan keyed by shape; graph capture and later
+// engines reuse it.  SA_TUNE=0 disables (launcher heuristics only); SA_PLAN_CACHE=<file> persists
+// plans across processes (one "key tile_cfg splitk us" line per shape).
+struct ScopedConvTuning {
+  bool prev;
+  explicit ScopedConvTuning(bool on);
+  ~ScopedConvTuning();
+};
+bool conv_tuning_enabled();
+// Look up (and, inside a ScopedConvTuning(true) scope outside stream capture, tune) the plan for
+// `a`; sets a.tile_cfg / a.splitk when a plan exists.
+void conv_apply_plan(SaConvArgs& a, hipStream_t s);
+size_t conv_plan_entries();
+
 // ------------------------------------------------------------------ conv layers
 // Describes how the conv's (padded) input channels map to the checkpoint's input channels:
 // a list of {real, padded} segments concatenated along channels.

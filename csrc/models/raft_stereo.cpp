@@ -422,6 +422,7 @@ void RaftStereo::forward(hipStream_t s) {
       pa.proj_taps = 9;
       pa.proj_oc = 1;
       pa.proj_plane = (long)Bn * h0 * w0;
+      conv_apply_plan(pa, s);  // the tuned tile fixes the n-tile count (= projection slices)
       const int nsl = sa_conv2d_nslices(&pa);
       SA_REQUIRE(nsl >= 1 && nsl <= 4, "flow-head projection slices %d", nsl);
       fh1_.launch(s, pa);

@@ -133,6 +133,14 @@ void StereoEngine::init() {
   build(src);
   store_.reset();  // host copies no longer needed
   HIP_CHECK(hipDeviceSynchronize());
+  if (conv_tuning_enabled()) {
+    // eager tuning pass: every conv shape of the frame is timed over the launcher's tactics (on
+    // whatever the buffers hold) and the plan is fixed before the frame graph is captured
+    ScopedSplitK sk(&splitk_);
+    ScopedConvTuning tune(true);
+    forward(stream_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
   SA_LOGI("%s: built, %.1f MiB device memory", name(), arena_.bytes() / 1048576.0);
 }
 

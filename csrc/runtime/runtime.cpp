@@ -1,7 +1,10 @@
 // Device arena, safetensors reader, conv weight packing, graph helper.
 #include "sa/runtime.h"
 
+#include <algorithm>
 #include <cmath>
+#include <mutex>
+#include <unordered_map>
 #include <cstring>
 #include <fstream>
 
@@ -423,6 +426,7 @@ SaConvArgs ConvLayer::args(const std::vector<Tensor>& srcs, const Tensor& out) c
 
 void ConvLayer::launch(hipStream_t s, SaConvArgs& a) const {
   if (fault_inject("launch")) throw Error("fault injection: launch");
+  if (a.tile_cfg < 0) conv_apply_plan(a, s);
   int rc = sa_conv2d(&a, s);
   SA_REQUIRE(rc == 0, "sa_conv2d failed rc=%d", rc);
   SA_LAUNCH_CHECK(s);
@@ -461,6 +465,157 @@ void GraphExec::reset() {
   if (graph_) (void)hipGraphDestroy(graph_);
   exec_ = nullptr;
   graph_ = nullptr;
+}
+
+}  // namespace sa
+
+namespace sa {
+
+// ------------------------------------------------------------------ conv tactic selection
+namespace {
+
+struct PlanEntry {
+  int cfg, splitk;
+  float us;
+};
+
+std::mutex g_plan_mu;
+std::unordered_map<std::string, PlanEntry>* g_plan = nullptr;
+thread_local bool g_tuning = false;
+
+std::string plan_file() {
+  const char* e = std::getenv("SA_PLAN_CACHE");
+  return e ? std::string(e) : std::string();
+}
+
+std::unordered_map<std::string, PlanEntry>& plan_map() {  // caller holds g_plan_mu
+  if (!g_plan) {
+    g_plan = new std::unordered_map<std::string, PlanEntry>();
+    const std::string f = plan_file();
+    if (!f.empty()) {
+      std::ifstream in(f);
+      std::string key;
+      PlanEntry e;
+      while (in >> key >> e.cfg >> e.splitk >> e.us) (*g_plan)[key] = e;
+    }
+  }
+  return *g_plan;
+}
+
+std::string plan_key(const SaConvArgs& a) {
+  char buf[512];
+  int n = std::snprintf(buf, sizeof(buf), "gfx950|%d,%d,%d,%d|", a.N, a.H, a.W, a.Cin);
+  for (int i = 0; i < a.nsrc; ++i) n += std::snprintf(buf + n, sizeof(buf) - n, "%d.", a.src[i].channels);
+  std::snprintf(buf + n, sizeof(buf) - n, "|k%dx%dx%d|s%d,%d,%d|p%d,%d,%d|d%d,%d|o%dx%d,%d|D%d,%d|c%d,%d|e%d,%d,%d,%d|w%d",
+                a.KD, a.KH, a.KW, a.sd, a.sh, a.sw, a.pd, a.ph, a.pw, a.dh, a.dw, a.Ho, a.Wo, a.Do, a.Di, a.Cout,
+                a.Kpad, a.epi, a.stats != nullptr, a.up, a.gate != nullptr, a.ws != nullptr && a.counters != nullptr);
+  return buf;
+}
+
+bool env_tune_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("SA_TUNE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
+  // scratch for everything the candidates write (real outputs / in-place state are untouched)
+  const long M = (long)a.N * (a.Do > 0 ? a.Do : 1) * a.Ho * a.Wo;
+  const long Mo = M * (a.up == 2 ? 4 : (a.up == 3 ? 8 : 1));
+  long width = std::max({(long)a.Cout, (long)a.out_stride, (long)a.aux_stride, (long)a.rh_stride, (long)a.h_stride});
+  const size_t out_bytes = (size_t)Mo * width * 4 + 256;
+  const size_t stats_bytes = a.stats ? (size_t)a.N * a.Cout * 2 * sizeof(sa_stat_t) + 256 : 0;
+  const size_t proj_bytes = a.proj_out ? (size_t)4 * std::max(1, a.proj_taps * a.proj_oc) * a.proj_plane * 4 + 256 : 0;
+  char* scratch = nullptr;
+  HIP_CHECK(hipMalloc((void**)&scratch, out_bytes + stats_bytes + proj_bytes));
+  SaConvArgs t = a;
+  if (t.out) t.out = scratch;
+  if (t.epi == SA_EPI_GRU_ZR) t.aux = t.rh = scratch;
+  if (t.epi == SA_EPI_GRU_Q) t.hbuf = scratch;
+  if (t.stats) t.stats = reinterpret_cast<sa_stat_t*>(scratch + out_bytes);
+  if (t.proj_out) t.proj_out = reinterpret_cast<float*>(scratch + out_bytes + stats_bytes);
+  hipEvent_t e0, e1;
+  HIP_CHECK(hipEventCreate(&e0));
+  HIP_CHECK(hipEventCreate(&e1));
+  PlanEntry best{-1, 1, 1e30f};
+  const bool can_split = a.ws && a.counters && !a.stats;
+  for (int cfg = 0; cfg <= 5; ++cfg) {
+    if (cfg == 2 && a.Cout > 32) continue;  // 256x16 tile: narrow outputs only
+    for (int sk : {1, 0}) {
+      if (sk == 0 && !can_split) continue;
+      t.tile_cfg = cfg;
+      t.splitk = sk;
+      if (sa_conv2d(&t, s) != 0) {
+        (void)hipGetLastError();
+        continue;
+      }
+      float best_ms = 1e30f;
+      for (int rep = 0; rep < 3; ++rep) {
+        HIP_CHECK(hipEventRecord(e0, s));
+        HIP_CHECK((hipError_t)sa_conv2d(&t, s));
+        HIP_CHECK(hipEventRecord(e1, s));
+        HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        best_ms = std::min(best_ms, ms);
+      }
+      if (best_ms * 1000.f < best.us) best = PlanEntry{cfg, sk, best_ms * 1000.f};
+    }
+  }
+  HIP_CHECK(hipStreamSynchronize(s));
+  HIP_CHECK(hipEventDestroy(e0));
+  HIP_CHECK(hipEventDestroy(e1));
+  HIP_CHECK(hipFree(scratch));
+  return best;
+}
+
+}  // namespace
+
+ScopedConvTuning::ScopedConvTuning(bool on) : prev(g_tuning) { g_tuning = on; }
+ScopedConvTuning::~ScopedConvTuning() { g_tuning = prev; }
+bool conv_tuning_enabled() { return env_tune_on(); }
+
+size_t conv_plan_entries() {
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  return plan_map().size();
+}
+
+void conv_apply_plan(SaConvArgs& a, hipStream_t s) {
+  if (!env_tune_on()) return;
+  const std::string key = plan_key(a);
+  {
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    auto& m = plan_map();
+    auto it = m.find(key);
+    if (it != m.end()) {
+      if (it->second.cfg >= 0) {
+        a.tile_cfg = it->second.cfg;
+        a.splitk = it->second.splitk;
+      }
+      return;
+    }
+  }
+  if (!g_tuning) return;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HIP_CHECK(hipStreamIsCapturing(s, &cs));
+  if (cs != hipStreamCaptureStatusNone) return;
+  const PlanEntry e = tune_conv(a, s);
+  {
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    plan_map()[key] = e;
+    const std::string f = plan_file();
+    if (!f.empty() && e.cfg >= 0) {
+      std::ofstream out(f, std::ios::app);
+      out << key << ' ' << e.cfg << ' ' << e.splitk << ' ' << e.us << '\n';
+    }
+  }
+  SA_LOGI("conv plan %s -> cfg %d splitk %d (%.1f us)", key.c_str(), e.cfg, e.splitk, e.us);
+  if (e.cfg >= 0) {
+    a.tile_cfg = e.cfg;
+    a.splitk = e.splitk;
+  }
 }
 
 }  // namespace sa

@@ -26,6 +26,11 @@ SHAPES = {
     "enc8": (8, 120, 160, 128, 128, 3, 1),   # motion encoder out conv at batch 8
     "l1b8": (16, 240, 320, 64, 64, 3, 1),    # feature encoder layer1 at batch 8 (both images)
     "zr8s": (8, 60, 80, 384, 256, 3, 0),     # GRU 1/8 z,r at batch 8
+    "mc1": (1, 120, 160, 64, 64, 3, 0),      # motion encoder convc2 / convf2 at batch 1 (auto split)
+    "mc1s1": (1, 120, 160, 64, 64, 3, 1),    # same, no split
+    "cf1": (1, 120, 160, 8, 64, 7, 0),       # motion encoder convf1 (7x7, 2 -> 8 padded channels)
+    "zr32": (1, 30, 40, 256, 256, 3, 0),     # GRU 1/16 z,r at batch 1
+    "zr8l": (1, 60, 80, 384, 256, 3, 0),     # GRU 1/8 z,r at batch 1
 }
 
 
