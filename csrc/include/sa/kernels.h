@@ -143,6 +143,14 @@ int sa_corr1d_lookup(const float* pyr, const float* flow, int B, int H, int W1, 
                      void* flow_out, int flow_stride, int flow_channels, void* flow_out2,
                      int flow_stride2, hipStream_t stream);
 
+// Fused RAFT motion-encoder head: lookup (as sa_corr1d_lookup) -> cor1 = relu(convc1) and
+// flo1 = relu(convf1 7x7 on [flow_x, 0]) as fp16 NHWC (64 channels each), plus [flow_x, 0] into
+// fcopy.  wc: fp32 [levels*(2r+1)][64], wf: fp32 [49][64] (x-channel taps), biases [64].
+int sa_raft_motion_head(const float* pyr, const float* flow, int B, int H, int W1, int W2, int levels,
+                        int radius, const float* wc, const float* bc, const float* wf, const float* bf,
+                        void* cor, int cstride, void* flo, int fstride, void* fcopy, int fcstride,
+                        hipStream_t stream);
+
 // ---- upsampling -----------------------------------------------------------------------------
 // RAFT convex upsampling: mask [B*H*W][9*f*f] fp16 (softmax over the 9), flow fp32 [B*H*W]
 // (x component).  Writes full-res fp32 output = sign * (f * flow) combination.

@@ -136,6 +136,96 @@ __global__ void corr_lookup_kernel(const float* __restrict__ pyr, const float* _
   }
 }
 
+// RAFT-Stereo motion-encoder head fused with the correlation lookup (SURVEY.md §7.2 "corr-lookup +
+// convc1"): for 64 pixels per block, wave l computes pyramid level l's 2r+1 bilinear taps into LDS,
+// then wave q produces output channels [16q, 16q+16) of
+//   cor1 = relu(convc1(corr))      (1x1, levels*(2r+1) -> 64)
+//   flo1 = relu(convf1(flow))      (7x7, 2 -> 64; the y flow is identically 0 in RAFT-Stereo, so only
+//                                   the x-channel taps are applied)
+// and wave 0 also writes the [flow_x, 0] tail of the motion features.  Weights are fp32 [k][64]
+// (k-major, so a wave's 16 outputs of one k are one scalar load); the corr features never leave
+// the chip and three launches per GRU iteration become one.
+__global__ __launch_bounds__(256) void raft_motion_head_kernel(
+    const float* __restrict__ pyr, const float* __restrict__ flow, int total, int H, int W1, int W2,
+    int levels, int radius, long lvl_off1, long lvl_off2, long lvl_off3, const float* __restrict__ wc,
+    const float* __restrict__ bc, const float* __restrict__ wf, const float* __restrict__ bf,
+    f16* __restrict__ cor, int cstride, f16* __restrict__ flo, int fstride, f16* __restrict__ fcopy,
+    int fcstride) {
+  __shared__ float corr_s[64][37];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int q = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const long pix = (long)blockIdx.x * 64 + lane;
+  const bool ok = pix < total;
+  const int ntap = 2 * radius + 1;
+  const int w1 = ok ? (int)(pix % W1) : 0;
+  const float fx = ok ? flow[pix] : 0.f;
+  if (q < levels && ok) {
+    const long off = q == 0 ? 0 : (q == 1 ? lvl_off1 : (q == 2 ? lvl_off2 : lvl_off3));
+    const int Wl = W2 >> q;
+    const float* row = pyr + off + pix * Wl;
+    const float xl = ((float)w1 + fx) / (float)(1 << q) - (float)radius;
+    const float x0f = floorf(xl);
+    const float a = xl - x0f;
+    const int x0 = (int)x0f;
+    float prev = (x0 >= 0 && x0 < Wl) ? row[x0] : 0.f;
+    for (int k = 0; k < ntap; ++k) {
+      const int xi = x0 + k + 1;
+      const float nxt = (xi >= 0 && xi < Wl) ? row[xi] : 0.f;
+      corr_s[lane][q * ntap + k] = (1.f - a) * prev + a * nxt;
+      prev = nxt;
+    }
+  }
+  __syncthreads();
+  if (!ok) return;
+  const int nc = levels * ntap;
+  float acc[16];
+#pragma unroll
+  for (int o = 0; o < 16; ++o) acc[o] = bc[q * 16 + o];
+  for (int k = 0; k < nc; ++k) {
+    const float v = corr_s[lane][k];
+    const float* w = wc + k * 64 + q * 16;
+#pragma unroll
+    for (int o = 0; o < 16; ++o) acc[o] += v * w[o];
+  }
+  half8 h0, h1;
+#pragma unroll
+  for (int o = 0; o < 8; ++o) {
+    h0[o] = (f16)fmaxf(acc[o], 0.f);
+    h1[o] = (f16)fmaxf(acc[8 + o], 0.f);
+  }
+  f16* cp = cor + pix * cstride + q * 16;
+  *reinterpret_cast<half8*>(cp) = h0;
+  *reinterpret_cast<half8*>(cp + 8) = h1;
+
+  const int y = (int)((pix / W1) % H);
+#pragma unroll
+  for (int o = 0; o < 16; ++o) acc[o] = bf[q * 16 + o];
+  for (int ky = 0; ky < 7; ++ky) {
+    const int yy = y + ky - 3;
+    if (yy < 0 || yy >= H) continue;
+    for (int kx = 0; kx < 7; ++kx) {
+      const int xx = w1 + kx - 3;
+      if (xx < 0 || xx >= W1) continue;
+      const float v = flow[pix + (long)(ky - 3) * W1 + (kx - 3)];
+      const float* w = wf + (ky * 7 + kx) * 64 + q * 16;
+#pragma unroll
+      for (int o = 0; o < 16; ++o) acc[o] += v * w[o];
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < 8; ++o) {
+    h0[o] = (f16)fmaxf(acc[o], 0.f);
+    h1[o] = (f16)fmaxf(acc[8 + o], 0.f);
+  }
+  f16* fp = flo + pix * fstride + q * 16;
+  *reinterpret_cast<half8*>(fp) = h0;
+  *reinterpret_cast<half8*>(fp + 8) = h1;
+  if (q == 0 && fcopy) {
+    fcopy[pix * fcstride] = (f16)fx;
+    fcopy[pix * fcstride + 1] = (f16)0.f;
+  }
+}
+
 }  // namespace
 
 extern "C" int sa_corr1d_pyramid(const void* f1, const void* f2, int stride, int B, int H, int W1,
@@ -177,5 +267,25 @@ extern "C" int sa_corr1d_lookup(const float* pyr, const float* flow, int B, int 
                      total, W1, W2, levels, radius, off[1], off[2], off[3], (f16*)out, out_stride,
                      out_channels, (f16*)flow_out, flow_stride, flow_channels, (f16*)flow_out2,
                      flow_stride2);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_raft_motion_head(const float* pyr, const float* flow, int B, int H, int W1, int W2, int levels,
+                                   int radius, const float* wc, const float* bc, const float* wf, const float* bf,
+                                   void* cor, int cstride, void* flo, int fstride, void* fcopy, int fcstride,
+                                   hipStream_t stream) {
+  if (levels < 1 || levels > 4 || levels * (2 * radius + 1) > 36 || cstride % 8 || fstride % 8) return -2;
+  long off[4] = {0, 0, 0, 0};
+  long acc = 0;
+  int Wl = W2;
+  for (int l = 0; l < levels; ++l) {
+    off[l] = acc;
+    acc += (long)B * H * W1 * Wl;
+    Wl >>= 1;
+  }
+  const int total = B * H * W1;
+  hipLaunchKernelGGL(raft_motion_head_kernel, dim3((total + 63) / 64), dim3(256), 0, stream, pyr, flow, total, H, W1,
+                     W2, levels, radius, off[1], off[2], off[3], wc, bc, wf, bf, (f16*)cor, cstride, (f16*)flo,
+                     fstride, (f16*)fcopy, fcstride);
   return (int)hipGetLastError();
 }

@@ -99,6 +99,9 @@ class RaftStereo : public StereoEngine {
   float* proj_w_ = nullptr;
   float* proj_b_ = nullptr;
   float* proj_p_ = nullptr;
+  // fused lookup + convc1 + convf1 (sa_raft_motion_head): fp32 [k][64] weights and biases
+  float *mh_wc_ = nullptr, *mh_bc_ = nullptr, *mh_wf_ = nullptr, *mh_bf_ = nullptr;
+  bool fuse_motion_ = !(std::getenv("SA_RAFT_FUSE_MOTION") && std::getenv("SA_RAFT_FUSE_MOTION")[0] == '0');
   // SA_RAFT_FUSE_FH: 0 = off, 1 = on, unset = auto.  Measured in-process on MI355X
   // (tools/ab_engine.py): batch 8 69.7 vs 70.7 ms/step fused vs unfused, batch 1 25.1 vs 24.3 ms
   // (the projection instantiation's extra registers cost more than the skipped 256x16 conv there)
@@ -210,6 +213,26 @@ void RaftStereo::build(WeightSource& src) {
   convc2_.build(a, ws, {u + "encoder.convc2"}, {{64, 64}}, s3);
   convf1_.build(a, ws, {u + "encoder.convf1"}, {{2, 8}}, s7);
   convf2_.build(a, ws, {u + "encoder.convf2"}, {{64, 64}}, s3);
+  if (cor_planes <= 36) {
+    const HostTensor& wc = ws.get(u + "encoder.convc1.weight");  // [64][cor_planes][1][1]
+    const HostTensor& wf = ws.get(u + "encoder.convf1.weight");  // [64][2][7][7]
+    std::vector<float> hc((size_t)cor_planes * 64), hf(49 * 64);
+    for (int o = 0; o < 64; ++o) {
+      for (int k = 0; k < cor_planes; ++k) hc[(size_t)k * 64 + o] = wc.data[(size_t)o * cor_planes + k];
+      for (int t = 0; t < 49; ++t) hf[(size_t)t * 64 + o] = wf.data[(size_t)o * 98 + t];  // x channel
+    }
+    auto up = [&](const std::vector<float>& v) {
+      float* d = (float*)a.alloc(v.size() * 4);
+      HIP_CHECK(hipMemcpy(d, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+      return d;
+    };
+    mh_wc_ = up(hc);
+    mh_wf_ = up(hf);
+    mh_bc_ = up(ws.get(u + "encoder.convc1.bias").data);
+    mh_bf_ = up(ws.get(u + "encoder.convf1.bias").data);
+  } else {
+    fuse_motion_ = false;
+  }
   mconv_.build(a, ws, {u + "encoder.conv"}, {{128, 128}}, s3);
 
   const char* gnames[3] = {"gru08", "gru16", "gru32"};
@@ -379,19 +402,28 @@ void RaftStereo::forward(hipStream_t s) {
   const int f = 1 << rc_.n_downsample;
   for (int it = 0; it < rc_.iters; ++it) {
     const bool last = it == rc_.iters - 1;
-    check(sa_corr1d_lookup(pyr_, flow_, Bn, h0, w0, w0, rc_.levels, rc_.radius, corr_feat_.ptr,
-                           corr_feat_.stride, corr_feat_.c, flow_feat_.ptr, flow_feat_.stride, 8,
-                           motion_.slice_c(126, 2).ptr, motion_.stride, s),
-          "corr lookup");
+    if (fuse_motion_) {
+      check(sa_raft_motion_head(pyr_, flow_, Bn, h0, w0, w0, rc_.levels, rc_.radius, mh_wc_, mh_bc_, mh_wf_,
+                                mh_bf_, cor1_.ptr, cor1_.stride, flo1_.ptr, flo1_.stride,
+                                motion_.slice_c(126, 2).ptr, motion_.stride, s),
+            "motion head");
+    } else {
+      check(sa_corr1d_lookup(pyr_, flow_, Bn, h0, w0, w0, rc_.levels, rc_.radius, corr_feat_.ptr,
+                             corr_feat_.stride, corr_feat_.c, flow_feat_.ptr, flow_feat_.stride, 8,
+                             motion_.slice_c(126, 2).ptr, motion_.stride, s),
+            "corr lookup");
+    }
     if (rc_.n_gru == 3 && rc_.slow_fast) gru32();
     if (rc_.n_gru >= 2 && rc_.slow_fast) {
       if (rc_.n_gru == 3) gru32();
       gru16();
     }
     // motion encoder
-    convc1_.run(s, {corr_feat_}, cor1_, SA_ACT_RELU);
+    if (!fuse_motion_) {
+      convc1_.run(s, {corr_feat_}, cor1_, SA_ACT_RELU);
+      convf1_.run(s, {flow_feat_}, flo1_, SA_ACT_RELU);
+    }
     convc2_.run(s, {cor1_}, corflo_.slice_c(0, 64), SA_ACT_RELU);
-    convf1_.run(s, {flow_feat_}, flo1_, SA_ACT_RELU);
     convf2_.run(s, {flo1_}, corflo_.slice_c(64, 64), SA_ACT_RELU);
     mconv_.run(s, {corflo_}, motion_.slice_c(0, 126), SA_ACT_RELU);
     if (rc_.n_gru == 3) gru32();

@@ -16,7 +16,7 @@ from .. import _native as N
 
 __all__ = [
     "splitk_workspace", "pack_conv_weight", "conv2d", "proj_stencil", "instnorm_apply", "avgpool3s2", "avgpool_k", "interp_bilinear",
-    "corr1d_pyramid", "corr1d_lookup", "convex_upsample", "preprocess", "remap_bgr", "reproject",
+    "corr1d_pyramid", "corr1d_lookup", "raft_motion_head", "convex_upsample", "preprocess", "remap_bgr", "reproject",
     "agcl_corr", "linear_attention", "layernorm", "ew", "interp_flow", "convex_upsample_c",
     "pack_conv3d_weight", "deconv_as_conv_weight", "conv3d", "dwconv3x3", "norm_corr_volume", "topk_disparity",
     "concat_volume", "topk_regress", "spx_upsample",
@@ -50,6 +50,23 @@ def proj_stencil(P, nslices, n, h, w, kh, kw, oc, bias=None, out=None, accumulat
                                     bias.data_ptr() if bias is not None else None, out.data_ptr(),
                                     _pix_stride(out), int(accumulate), _stream()), "sa_proj_stencil")
     return out
+
+
+def raft_motion_head(pyr_buf, flow, b, h, w1, w2, convc1_w, convc1_b, convf1_w, convf1_b, levels=4, radius=4):
+    """Fused lookup + relu(convc1) + relu(convf1 on [flow_x, 0]): returns (cor1, flo1, flowcopy) fp16
+    NHWC.  ``convc1_w`` [64, L*(2r+1), 1, 1], ``convf1_w`` [64, 2, 7, 7] (torch layouts)."""
+    nc = levels * (2 * radius + 1)
+    wc = convc1_w.reshape(64, nc).t().contiguous().float()
+    wf = convf1_w[:, 0].reshape(64, 49).t().contiguous().float()
+    dev = flow.device
+    cor = torch.empty(b, h, w1, 64, dtype=torch.float16, device=dev)
+    flo = torch.empty(b, h, w1, 64, dtype=torch.float16, device=dev)
+    fc = torch.empty(b, h, w1, 8, dtype=torch.float16, device=dev)
+    N.check(N.dev().sa_raft_motion_head(pyr_buf.data_ptr(), flow.contiguous().data_ptr(), b, h, w1, w2, levels, radius,
+                                        wc.data_ptr(), convc1_b.float().contiguous().data_ptr(), wf.data_ptr(),
+                                        convf1_b.float().contiguous().data_ptr(), cor.data_ptr(), 64, flo.data_ptr(),
+                                        64, fc.data_ptr(), 8, _stream()), "sa_raft_motion_head")
+    return cor, flo, fc[..., :2]
 
 
 def splitk_workspace(floats: int = 1 << 22, counters: int = 4096, device="cuda"):

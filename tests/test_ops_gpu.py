@@ -340,6 +340,34 @@ def test_corr_pyramid_and_lookup_vs_oracle():
     assert feat[..., 36:].abs().max().item() == 0
 
 
+def test_raft_motion_head_vs_torch():
+    """Fused correlation lookup + relu(convc1) + relu(convf1) == the unfused PyTorch composition."""
+    from stereoalgorithms_amd.models.raft_stereo import CorrBlock1D, coords_grid
+    O = ops()
+    torch.manual_seed(9)
+    b, c, h, w = 2, 256, 7, 44
+    f1 = torch.randn(b, c, h, w, device=DEV)
+    f2 = torch.randn(b, c, h, w, device=DEV)
+    buf, _ = O.corr1d_pyramid(nhwc(f1).half(), nhwc(f2).half(), levels=4)
+    flow = torch.randn(b, h, w, device=DEV) * 5 - 2
+    wc = torch.randn(64, 36, 1, 1, device=DEV) / 6
+    bc = torch.randn(64, device=DEV) * 0.1
+    wf = torch.randn(64, 2, 7, 7, device=DEV) / 10
+    bf = torch.randn(64, device=DEV) * 0.1
+    cor, flo, fc = O.raft_motion_head(buf, flow, b, h, w, w, wc, bc, wf, bf)
+    cb = CorrBlock1D(f1.half().float(), f2.half().float(), 4, 4)
+    coords = coords_grid(b, h, w, DEV)
+    coords[:, 0] += flow
+    corr = cb(coords)
+    ref_c = F.relu(F.conv2d(corr, wc, bc))
+    fl2 = torch.stack([flow, torch.zeros_like(flow)], 1)
+    ref_f = F.relu(F.conv2d(fl2, wf, bf, padding=3))
+    torch.cuda.synchronize()
+    assert rel_err(nchw(cor), ref_c) < 3e-3
+    assert rel_err(nchw(flo), ref_f) < 3e-3
+    assert torch.allclose(fc[..., 0].float(), flow, atol=1e-2) and fc[..., 1].abs().max().item() == 0
+
+
 def test_convex_upsample_vs_oracle():
     from stereoalgorithms_amd.models.raft_stereo import RAFTStereo
     O = ops()

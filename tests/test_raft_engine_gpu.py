@@ -17,13 +17,16 @@ def _pairs(b, h, w):
     ("raftstereo-realtime", 7, (96, 160), ""),
     ("raftstereo-sceneflow", 6, (96, 128), "0"),
     ("raftstereo-sceneflow", 6, (96, 128), "1"),  # flow head conv2 fused into conv1's epilogue
+    ("raftstereo-sceneflow", 6, (96, 128), "nomotion"),  # unfused lookup / convc1 / convf1
 ])
 def test_engine_matches_oracle(tmp_path, monkeypatch, preset, iters, hw, fuse):
     from stereoalgorithms_amd.models import raft_stereo as R
     from stereoalgorithms_amd.models.engine import NativeStereoEngine
     from stereoalgorithms_amd.utils.weights import save_model
     h, w = hw
-    if fuse:
+    if fuse == "nomotion":
+        monkeypatch.setenv("SA_RAFT_FUSE_MOTION", "0")
+    elif fuse:
         monkeypatch.setenv("SA_RAFT_FUSE_FH", fuse)
     m = R.build(preset, seed=0)
     path = save_model(m, tmp_path / "w.safetensors", preset)
