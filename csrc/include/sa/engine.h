@@ -92,6 +92,13 @@ class StereoEngine {
   void tap(hipStream_t s, const char* name, const Tensor& t) const;
   void tap_f32(hipStream_t s, const char* name, const float* p, int n, int h, int w, int c) const;
 
+  // Independent branches of a frame run on a second stream: fork() makes the side stream wait for
+  // everything queued on `s` so far and returns it, join() makes `s` wait for the side stream.  Under
+  // capture the two become parallel hipGraph branches.  Convs enqueued on the side stream must run
+  // under ScopedSplitK(&splitk_side_) (split-K slabs / tile counters are per stream).
+  hipStream_t fork(hipStream_t s);
+  void join(hipStream_t s);
+
   void frame(hipStream_t s, bool rectify);  // the captured body
   void launch_frame(hipStream_t s, bool rectify);
 
@@ -111,6 +118,10 @@ class StereoEngine {
   bool have_Q_ = false;
   GraphExec graph_[2];  // [no rectify, rectify]
   SplitKWorkspace splitk_;
+  hipStream_t side_ = nullptr;
+  hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
+  SplitKWorkspace splitk_side_;
+  bool tuning_pass_ = false;  // set during the eager conv-tuning forward (branches serialised)
   uint8_t* pin_in_ = nullptr;
   float* pin_out_ = nullptr;
   long launches_per_frame_ = 0;

@@ -102,6 +102,8 @@ class RaftStereo : public StereoEngine {
   // fused lookup + convc1 + convf1 (sa_raft_motion_head): fp32 [k][64] weights and biases
   float *mh_wc_ = nullptr, *mh_bc_ = nullptr, *mh_wf_ = nullptr, *mh_bf_ = nullptr;
   bool fuse_motion_ = !(std::getenv("SA_RAFT_FUSE_MOTION") && std::getenv("SA_RAFT_FUSE_MOTION")[0] == '0');
+  // SA_RAFT_PARALLEL=0: run the motion encoder and the coarse GRU levels on one stream
+  bool par_ = !(std::getenv("SA_RAFT_PARALLEL") && std::getenv("SA_RAFT_PARALLEL")[0] == '0');
   // SA_RAFT_FUSE_FH: 0 = off, 1 = on, unset = auto.  Measured in-process on MI355X
   // (tools/ab_engine.py): batch 8 69.7 vs 70.7 ms/step fused vs unfused, batch 1 25.1 vs 24.3 ms
   // (the projection instantiation's extra registers cost more than the skipped 256x16 conv there)
@@ -402,32 +404,38 @@ void RaftStereo::forward(hipStream_t s) {
   const int f = 1 << rc_.n_downsample;
   for (int it = 0; it < rc_.iters; ++it) {
     const bool last = it == rc_.iters - 1;
-    if (fuse_motion_) {
-      check(sa_raft_motion_head(pyr_, flow_, Bn, h0, w0, w0, rc_.levels, rc_.radius, mh_wc_, mh_bc_, mh_wf_,
-                                mh_bf_, cor1_.ptr, cor1_.stride, flo1_.ptr, flo1_.stride,
-                                motion_.slice_c(126, 2).ptr, motion_.stride, s),
-            "motion head");
-    } else {
-      check(sa_corr1d_lookup(pyr_, flow_, Bn, h0, w0, w0, rc_.levels, rc_.radius, corr_feat_.ptr,
-                             corr_feat_.stride, corr_feat_.c, flow_feat_.ptr, flow_feat_.stride, 8,
-                             motion_.slice_c(126, 2).ptr, motion_.stride, s),
-            "corr lookup");
+    // The motion encoder (lookup -> convc1/convf1 -> convc2/convf2 -> conv) depends only on the
+    // correlation pyramid and the flow; the coarse GRU levels only on the hidden states.  They run
+    // as two parallel branches of the frame graph and join before the finest GRU.
+    const bool par = par_ && !tuning_pass_;
+    hipStream_t ms = par ? fork(s) : s;
+    {
+      ScopedSplitK sk2(par ? &splitk_side_ : current_splitk());
+      if (fuse_motion_) {
+        check(sa_raft_motion_head(pyr_, flow_, Bn, h0, w0, w0, rc_.levels, rc_.radius, mh_wc_, mh_bc_, mh_wf_,
+                                  mh_bf_, cor1_.ptr, cor1_.stride, flo1_.ptr, flo1_.stride,
+                                  motion_.slice_c(126, 2).ptr, motion_.stride, ms),
+              "motion head");
+      } else {
+        check(sa_corr1d_lookup(pyr_, flow_, Bn, h0, w0, w0, rc_.levels, rc_.radius, corr_feat_.ptr,
+                               corr_feat_.stride, corr_feat_.c, flow_feat_.ptr, flow_feat_.stride, 8,
+                               motion_.slice_c(126, 2).ptr, motion_.stride, ms),
+              "corr lookup");
+        convc1_.run(ms, {corr_feat_}, cor1_, SA_ACT_RELU);
+        convf1_.run(ms, {flow_feat_}, flo1_, SA_ACT_RELU);
+      }
+      convc2_.run(ms, {cor1_}, corflo_.slice_c(0, 64), SA_ACT_RELU);
+      convf2_.run(ms, {flo1_}, corflo_.slice_c(64, 64), SA_ACT_RELU);
+      mconv_.run(ms, {corflo_}, motion_.slice_c(0, 126), SA_ACT_RELU);
     }
     if (rc_.n_gru == 3 && rc_.slow_fast) gru32();
     if (rc_.n_gru >= 2 && rc_.slow_fast) {
       if (rc_.n_gru == 3) gru32();
       gru16();
     }
-    // motion encoder
-    if (!fuse_motion_) {
-      convc1_.run(s, {corr_feat_}, cor1_, SA_ACT_RELU);
-      convf1_.run(s, {flow_feat_}, flo1_, SA_ACT_RELU);
-    }
-    convc2_.run(s, {cor1_}, corflo_.slice_c(0, 64), SA_ACT_RELU);
-    convf2_.run(s, {flo1_}, corflo_.slice_c(64, 64), SA_ACT_RELU);
-    mconv_.run(s, {corflo_}, motion_.slice_c(0, 126), SA_ACT_RELU);
     if (rc_.n_gru == 3) gru32();
     if (rc_.n_gru >= 2) gru16();
+    if (par) join(s);
     if (rc_.n_gru > 1) {
       interp(0);
       gru(s, 0, {motion_, interp_[0]});

@@ -81,6 +81,9 @@ StereoEngine::~StereoEngine() {
   if (pin_out_) (void)hipHostFree(pin_out_);
   if (ev_in_) (void)hipEventDestroy(ev_in_);
   if (ev_out_) (void)hipEventDestroy(ev_out_);
+  if (ev_fork_) (void)hipEventDestroy(ev_fork_);
+  if (ev_join_) (void)hipEventDestroy(ev_join_);
+  if (side_) (void)hipStreamDestroy(side_);
   if (stream_) (void)hipStreamDestroy(stream_);
   arena_.release();
 }
@@ -119,6 +122,9 @@ void StereoEngine::init() {
   HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamDefault));
   HIP_CHECK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
   HIP_CHECK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
+  HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+  HIP_CHECK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
   const size_t img = (size_t)B() * H() * W() * 3;
   in_left_ = (uint8_t*)arena_.alloc(img);
   in_right_ = (uint8_t*)arena_.alloc(img);
@@ -129,6 +135,7 @@ void StereoEngine::init() {
   HIP_CHECK(hipHostMalloc((void**)&pin_in_, 2 * img, hipHostMallocDefault));
   HIP_CHECK(hipHostMalloc((void**)&pin_out_, (size_t)B() * H() * W() * 7 * 4 + 2 * img, hipHostMallocDefault));
   splitk_.alloc(arena_, 16l << 20, 8192);  // 64 MiB of fp32 slabs, 8192 tile counters
+  splitk_side_.alloc(arena_, 16l << 20, 8192);
   WeightSource src{store_.get(), cfg_.weights.empty(), cfg_.seed};
   build(src);
   store_.reset();  // host copies no longer needed
@@ -138,10 +145,23 @@ void StereoEngine::init() {
     // whatever the buffers hold) and the plan is fixed before the frame graph is captured
     ScopedSplitK sk(&splitk_);
     ScopedConvTuning tune(true);
+    tuning_pass_ = true;
     forward(stream_);
+    tuning_pass_ = false;
     HIP_CHECK(hipStreamSynchronize(stream_));
   }
   SA_LOGI("%s: built, %.1f MiB device memory", name(), arena_.bytes() / 1048576.0);
+}
+
+hipStream_t StereoEngine::fork(hipStream_t s) {
+  HIP_CHECK(hipEventRecord(ev_fork_, s));
+  HIP_CHECK(hipStreamWaitEvent(side_, ev_fork_, 0));
+  return side_;
+}
+
+void StereoEngine::join(hipStream_t s) {
+  HIP_CHECK(hipEventRecord(ev_join_, side_));
+  HIP_CHECK(hipStreamWaitEvent(s, ev_join_, 0));
 }
 
 void StereoEngine::set_Q(const float* q16) {
