@@ -333,17 +333,25 @@ void RaftStereo::forward(hipStream_t s) {
   check(sa_preprocess(in_left_, Bn, H(), W(), SA_PRE_SIGNED, img_.ptr, 8, 0, 8, s), "preprocess");
   check(sa_preprocess(in_right_, Bn, H(), W(), SA_PRE_SIGNED, img_.slice_n(Bn, Bn).ptr, 8, 0, 8, s), "preprocess");
 
-  // encoders
-  if (rc_.shared) {
-    cnet_.run(s, sp_, img_);
-    const Tensor& v = cnet_.out();
-    shared_rb_.run(s, sp_, v);
-    shared_conv_.run(s, {shared_rb_.out}, fmap_);
-  } else {
-    cnet_.run(s, sp_, img_.slice_n(0, Bn));
-    fnet_.run(s, sp_, img_);
-    fconv2_.run(s, {fnet_.out()}, fmap_);
-  }
+  // encoders.  The feature branch (fnet -> fmap -> correlation pyramid) and the context branch
+  // (cnet -> levels -> heads) are independent after the shared trunk: parallel graph branches.
+  const int h0 = lh_[0], w0 = lw_[0];
+  const bool par = par_ && !tuning_pass_;
+  auto feature_branch = [&](hipStream_t fs) {
+    ScopedSplitK sk2(par ? &splitk_side_ : current_splitk());
+    if (rc_.shared) {
+      shared_rb_.run(fs, sp_, cnet_.out());
+      shared_conv_.run(fs, {shared_rb_.out}, fmap_);
+    } else {
+      fnet_.run(fs, sp_, img_);
+      fconv2_.run(fs, {fnet_.out()}, fmap_);
+    }
+    check(sa_corr1d_pyramid(fmap_.ptr, fmap_.slice_n(Bn, Bn).ptr, 256, Bn, h0, w0, w0, 256, rc_.levels, pyr_, fs),
+          "corr pyramid");
+  };
+  if (rc_.shared) cnet_.run(s, sp_, img_);  // shared trunk on both images
+  feature_branch(par ? fork(s) : s);
+  if (!rc_.shared) cnet_.run(s, sp_, img_.slice_n(0, Bn));
   Tensor x = cnet_.out().slice_n(0, Bn);
   Tensor lvl_in[3];
   lvl_in[0] = x;
@@ -369,12 +377,7 @@ void RaftStereo::forward(hipStream_t s) {
     head_conv_[i][1].run(s, {hin[1]}, ctxh_[i], SA_ACT_RELU);
     zqr_[i].run(s, {ctxh_[i]}, czrq_[i]);
   }
-
-  // correlation pyramid
-  const int h0 = lh_[0], w0 = lw_[0];
-  check(sa_corr1d_pyramid(fmap_.ptr, fmap_.slice_n(Bn, Bn).ptr, 256, Bn, h0, w0, w0, 256,
-                          rc_.levels, pyr_, s),
-        "corr pyramid");
+  if (par) join(s);
   HIP_CHECK(hipMemsetAsync(flow_, 0, (size_t)Bn * h0 * w0 * 4, s));
 
   auto pool = [&](int i) {  // pool_[i] = pool2x(net[i])
