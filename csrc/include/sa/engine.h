@@ -98,6 +98,10 @@ class StereoEngine {
   // under ScopedSplitK(&splitk_side_) (split-K slabs / tile counters are per stream).
   hipStream_t fork(hipStream_t s);
   void join(hipStream_t s);
+  // General dependency edges for deeper pipelines: record named event i on a stream / make a stream
+  // wait for its latest record (reused across iterations: a wait binds to the record enqueued last).
+  void rec(hipStream_t s, int i);
+  void wait(hipStream_t s, int i);
 
   void frame(hipStream_t s, bool rectify);  // the captured body
   void launch_frame(hipStream_t s, bool rectify);
@@ -121,6 +125,10 @@ class StereoEngine {
   hipStream_t side_ = nullptr;
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
   SplitKWorkspace splitk_side_;
+  hipStream_t side2_ = nullptr;  // third stream for pipelined schedules
+  SplitKWorkspace splitk_side2_;
+  static constexpr int kEvents = 8;
+  hipEvent_t ev_dep_[kEvents] = {};
   bool tuning_pass_ = false;  // set during the eager conv-tuning forward (branches serialised)
   uint8_t* pin_in_ = nullptr;
   float* pin_out_ = nullptr;

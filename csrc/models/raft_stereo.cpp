@@ -104,6 +104,8 @@ class RaftStereo : public StereoEngine {
   bool fuse_motion_ = !(std::getenv("SA_RAFT_FUSE_MOTION") && std::getenv("SA_RAFT_FUSE_MOTION")[0] == '0');
   // SA_RAFT_PARALLEL=0: run the motion encoder and the coarse GRU levels on one stream
   bool par_ = !(std::getenv("SA_RAFT_PARALLEL") && std::getenv("SA_RAFT_PARALLEL")[0] == '0');
+  // SA_RAFT_PIPELINE=0: keep the per-iteration fork/join instead of the cross-iteration pipeline
+  bool pipeline_ = !(std::getenv("SA_RAFT_PIPELINE") && std::getenv("SA_RAFT_PIPELINE")[0] == '0');
   // SA_RAFT_FUSE_FH: 0 = off, 1 = on, unset = auto.  Measured in-process on MI355X
   // (tools/ab_engine.py): batch 8 69.7 vs 70.7 ms/step fused vs unfused, batch 1 25.1 vs 24.3 ms
   // (the projection instantiation's extra registers cost more than the skipped 256x16 conv there)
@@ -380,72 +382,56 @@ void RaftStereo::forward(hipStream_t s) {
   if (par) join(s);
   HIP_CHECK(hipMemsetAsync(flow_, 0, (size_t)Bn * h0 * w0 * 4, s));
 
-  auto pool = [&](int i) {  // pool_[i] = pool2x(net[i])
+  auto pool = [&](hipStream_t st, int i) {  // pool_[i] = pool2x(net[i])
     check(sa_avgpool3s2(net_[i].ptr, net_[i].stride, pool_[i].ptr, pool_[i].stride, Bn, lh_[i],
-                        lw_[i], hd, s),
+                        lw_[i], hd, st),
           "pool2x");
   };
-  auto interp = [&](int i) {  // interp_[i] = interp(net[i+1], net[i])
+  auto interp = [&](hipStream_t st, int i) {  // interp_[i] = interp(net[i+1], net[i])
     check(sa_interp_bilinear(net_[i + 1].ptr, net_[i + 1].stride, interp_[i].ptr, interp_[i].stride,
-                             Bn, lh_[i + 1], lw_[i + 1], hd, lh_[i], lw_[i], 1, 1.f, s),
+                             Bn, lh_[i + 1], lw_[i + 1], hd, lh_[i], lw_[i], 1, 1.f, st),
           "interp");
   };
-  auto gru32 = [&]() {
-    pool(1);
-    gru(s, 2, {pool_[1]});
+  auto gru32 = [&](hipStream_t st) {
+    pool(st, 1);
+    gru(st, 2, {pool_[1]});
   };
-  auto gru16 = [&]() {
-    pool(0);
+  auto gru16 = [&](hipStream_t st) {
+    pool(st, 0);
     if (rc_.n_gru == 3) {
-      interp(1);
-      gru(s, 1, {pool_[0], interp_[1]});
+      interp(st, 1);
+      gru(st, 1, {pool_[0], interp_[1]});
     } else {
-      gru(s, 1, {pool_[0]});
+      gru(st, 1, {pool_[0]});
     }
   };
-
-  const int f = 1 << rc_.n_downsample;
-  for (int it = 0; it < rc_.iters; ++it) {
-    const bool last = it == rc_.iters - 1;
-    // The motion encoder (lookup -> convc1/convf1 -> convc2/convf2 -> conv) depends only on the
-    // correlation pyramid and the flow; the coarse GRU levels only on the hidden states.  They run
-    // as two parallel branches of the frame graph and join before the finest GRU.
-    const bool par = par_ && !tuning_pass_;
-    hipStream_t ms = par ? fork(s) : s;
-    {
-      ScopedSplitK sk2(par ? &splitk_side_ : current_splitk());
-      if (fuse_motion_) {
-        check(sa_raft_motion_head(pyr_, flow_, Bn, h0, w0, w0, rc_.levels, rc_.radius, mh_wc_, mh_bc_, mh_wf_,
-                                  mh_bf_, cor1_.ptr, cor1_.stride, flo1_.ptr, flo1_.stride,
-                                  motion_.slice_c(126, 2).ptr, motion_.stride, ms),
-              "motion head");
-      } else {
-        check(sa_corr1d_lookup(pyr_, flow_, Bn, h0, w0, w0, rc_.levels, rc_.radius, corr_feat_.ptr,
-                               corr_feat_.stride, corr_feat_.c, flow_feat_.ptr, flow_feat_.stride, 8,
-                               motion_.slice_c(126, 2).ptr, motion_.stride, ms),
-              "corr lookup");
-        convc1_.run(ms, {corr_feat_}, cor1_, SA_ACT_RELU);
-        convf1_.run(ms, {flow_feat_}, flo1_, SA_ACT_RELU);
-      }
-      convc2_.run(ms, {cor1_}, corflo_.slice_c(0, 64), SA_ACT_RELU);
-      convf2_.run(ms, {flo1_}, corflo_.slice_c(64, 64), SA_ACT_RELU);
-      mconv_.run(ms, {corflo_}, motion_.slice_c(0, 126), SA_ACT_RELU);
+  // motion encoder: lookup -> convc1/convf1 -> convc2/convf2 -> conv (+ [flow, 0] tail)
+  auto motion = [&](hipStream_t ms) {
+    if (fuse_motion_) {
+      check(sa_raft_motion_head(pyr_, flow_, Bn, h0, w0, w0, rc_.levels, rc_.radius, mh_wc_, mh_bc_, mh_wf_,
+                                mh_bf_, cor1_.ptr, cor1_.stride, flo1_.ptr, flo1_.stride,
+                                motion_.slice_c(126, 2).ptr, motion_.stride, ms),
+            "motion head");
+    } else {
+      check(sa_corr1d_lookup(pyr_, flow_, Bn, h0, w0, w0, rc_.levels, rc_.radius, corr_feat_.ptr,
+                             corr_feat_.stride, corr_feat_.c, flow_feat_.ptr, flow_feat_.stride, 8,
+                             motion_.slice_c(126, 2).ptr, motion_.stride, ms),
+            "corr lookup");
+      convc1_.run(ms, {corr_feat_}, cor1_, SA_ACT_RELU);
+      convf1_.run(ms, {flow_feat_}, flo1_, SA_ACT_RELU);
     }
-    if (rc_.n_gru == 3 && rc_.slow_fast) gru32();
-    if (rc_.n_gru >= 2 && rc_.slow_fast) {
-      if (rc_.n_gru == 3) gru32();
-      gru16();
-    }
-    if (rc_.n_gru == 3) gru32();
-    if (rc_.n_gru >= 2) gru16();
-    if (par) join(s);
+    convc2_.run(ms, {cor1_}, corflo_.slice_c(0, 64), SA_ACT_RELU);
+    convf2_.run(ms, {flo1_}, corflo_.slice_c(64, 64), SA_ACT_RELU);
+    mconv_.run(ms, {corflo_}, motion_.slice_c(0, 126), SA_ACT_RELU);
+  };
+  // finest GRU + flow head (+ mask head on the last iteration), coords1 += delta (x only)
+  auto fine_and_head = [&](bool last) {
     if (rc_.n_gru > 1) {
-      interp(0);
+      interp(s, 0);
       gru(s, 0, {motion_, interp_[0]});
     } else {
       gru(s, 0, {motion_});
     }
-    // flow head (+ mask head on the last iteration), coords1 += delta (x only)
     if (last || !fuse_fh_) {
       if (last) fh1mask_.run(s, {net_[0]}, fh_, SA_ACT_RELU);
       else fh1_.run(s, {net_[0]}, fh_.slice_c(0, 256), SA_ACT_RELU);
@@ -471,6 +457,58 @@ void RaftStereo::forward(hipStream_t s) {
       fh1_.launch(s, pa);
       check(sa_proj_stencil(proj_p_, nsl, pa.proj_plane, Bn, h0, w0, 3, 3, 1, proj_b_, flow_, 1, 1, s),
             "flow-head stencil");
+    }
+  };
+
+  const int f = 1 << rc_.n_downsample;
+  const bool pipe = par && pipeline_ && rc_.n_gru == 3 && !rc_.slow_fast;
+  if (pipe) {
+    // Cross-iteration pipeline on three streams (sceneflow: 3 levels, no slow-fast).  Per iteration t:
+    //   side2: G32(t)  after G16(t-1)   (needs net1(t-1), net2(t-1); overwrites net2 read by G16(t-1))
+    //   side : M(t)    after FH(t-1)    (needs flow(t-1); overwrites motion read by G08(t-1))
+    //   main : G16(t) after G32(t); G08(t) + FH(t) after M(t)
+    // so G32(t) overlaps G08(t-1) + FH(t-1), and M(t) overlaps G16(t).  Events (latest record binds):
+    //   0 = G16 done, 1 = FH done, 2 = G32 done, 3 = M done.
+    rec(s, 0);
+    rec(s, 1);
+    for (int it = 0; it < rc_.iters; ++it) {
+      {
+        ScopedSplitK k2(&splitk_side2_);
+        wait(side2_, 0);
+        gru32(side2_);
+        rec(side2_, 2);
+      }
+      {
+        ScopedSplitK k1(&splitk_side_);
+        wait(side_, 1);
+        motion(side_);
+        rec(side_, 3);
+      }
+      wait(s, 2);
+      gru16(s);
+      rec(s, 0);
+      wait(s, 3);
+      fine_and_head(it == rc_.iters - 1);
+      rec(s, 1);
+    }
+  } else {
+    for (int it = 0; it < rc_.iters; ++it) {
+      // The motion encoder depends only on the correlation pyramid and the flow, the coarse GRU
+      // levels only on the hidden states: two parallel branches that join before the finest GRU.
+      hipStream_t ms = par ? fork(s) : s;
+      {
+        ScopedSplitK sk2(par ? &splitk_side_ : current_splitk());
+        motion(ms);
+      }
+      if (rc_.n_gru == 3 && rc_.slow_fast) gru32(s);
+      if (rc_.n_gru >= 2 && rc_.slow_fast) {
+        if (rc_.n_gru == 3) gru32(s);
+        gru16(s);
+      }
+      if (rc_.n_gru == 3) gru32(s);
+      if (rc_.n_gru >= 2) gru16(s);
+      if (par) join(s);
+      fine_and_head(it == rc_.iters - 1);
     }
   }
   // convex upsampling; disparity = -flow_up

@@ -84,6 +84,9 @@ StereoEngine::~StereoEngine() {
   if (ev_fork_) (void)hipEventDestroy(ev_fork_);
   if (ev_join_) (void)hipEventDestroy(ev_join_);
   if (side_) (void)hipStreamDestroy(side_);
+  if (side2_) (void)hipStreamDestroy(side2_);
+  for (hipEvent_t e : ev_dep_)
+    if (e) (void)hipEventDestroy(e);
   if (stream_) (void)hipStreamDestroy(stream_);
   arena_.release();
 }
@@ -125,6 +128,8 @@ void StereoEngine::init() {
   HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
   HIP_CHECK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
   HIP_CHECK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+  HIP_CHECK(hipStreamCreateWithFlags(&side2_, hipStreamNonBlocking));
+  for (hipEvent_t& e : ev_dep_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   const size_t img = (size_t)B() * H() * W() * 3;
   in_left_ = (uint8_t*)arena_.alloc(img);
   in_right_ = (uint8_t*)arena_.alloc(img);
@@ -136,6 +141,7 @@ void StereoEngine::init() {
   HIP_CHECK(hipHostMalloc((void**)&pin_out_, (size_t)B() * H() * W() * 7 * 4 + 2 * img, hipHostMallocDefault));
   splitk_.alloc(arena_, 16l << 20, 8192);  // 64 MiB of fp32 slabs, 8192 tile counters
   splitk_side_.alloc(arena_, 16l << 20, 8192);
+  splitk_side2_.alloc(arena_, 16l << 20, 8192);
   WeightSource src{store_.get(), cfg_.weights.empty(), cfg_.seed};
   build(src);
   store_.reset();  // host copies no longer needed
@@ -163,6 +169,9 @@ void StereoEngine::join(hipStream_t s) {
   HIP_CHECK(hipEventRecord(ev_join_, side_));
   HIP_CHECK(hipStreamWaitEvent(s, ev_join_, 0));
 }
+
+void StereoEngine::rec(hipStream_t s, int i) { HIP_CHECK(hipEventRecord(ev_dep_[i], s)); }
+void StereoEngine::wait(hipStream_t s, int i) { HIP_CHECK(hipStreamWaitEvent(s, ev_dep_[i], 0)); }
 
 void StereoEngine::set_Q(const float* q16) {
   std::memcpy(Q_, q16, sizeof(Q_));
