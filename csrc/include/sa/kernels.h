@@ -93,6 +93,10 @@ typedef struct {
   float* proj_out;
   int32_t proj_taps, proj_oc;
   int64_t proj_plane;
+  // instance-norm statistics spread over `stats_slots` copies of [N][Cout][2] (block b adds into
+  // copy b % slots): atomics of the thousands of blocks of one image no longer pile onto one row of
+  // addresses.  sa_stats_reduce() folds the copies into copy 0 before the statistics are read.
+  int32_t stats_slots;
 } SaConvArgs;
 
 int sa_conv2d(const SaConvArgs* a, hipStream_t stream);
@@ -118,6 +122,8 @@ typedef struct {
   float eps, alpha;
 } SaNormArgs;
 int sa_instnorm_apply(const SaNormArgs* a, hipStream_t stream);
+// stats[0][i] = sum_r stats[r][i], stats[r>0][i] = 0 for i < count (idempotent)
+int sa_stats_reduce(sa_stat_t* stats, int slots, long count, hipStream_t stream);
 
 // F.avg_pool2d(x, 3, stride=2, padding=1) (count_include_pad) on NHWC fp16
 int sa_avgpool3s2(const void* x, int x_stride, void* out, int out_stride, int N, int H, int W,

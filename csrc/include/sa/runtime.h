@@ -132,6 +132,10 @@ void conv_apply_plan(SaConvArgs& a, hipStream_t s);
 size_t conv_plan_entries();
 
 // ------------------------------------------------------------------ conv layers
+// Copies of every instance-norm statistics buffer the conv epilogues spread their atomics over
+// (SaConvArgs.stats_slots); StatsPool reserves this many, instnorm() folds them (sa_stats_reduce).
+constexpr int kStatSlots = 16;
+
 // Describes how the conv's (padded) input channels map to the checkpoint's input channels:
 // a list of {real, padded} segments concatenated along channels.
 struct ChanSeg {

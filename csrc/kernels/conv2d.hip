@@ -806,10 +806,14 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
   int cur_img = -1;
   const int nvalid = p.Cout - co;  // channels valid in this chunk (may be <=0 or <8)
 
+  // this block's copy of the statistics (stats_slots copies of [N][Cout][2])
+  sa_stat_t* const stats_blk =
+      p.stats_slots > 1 ? p.stats + (size_t)((blockIdx.y * gridDim.x + blockIdx.x) % p.stats_slots) * p.N * p.Cout * 2
+                        : p.stats;
   auto flush_stats = [&](int img) {
     if (img < 0) return;
     for (int j = 0; j < 8 && j < nvalid; ++j) {
-      unsigned long long* sp = reinterpret_cast<unsigned long long*>(p.stats) + ((size_t)img * p.Cout + co + j) * 2;
+      unsigned long long* sp = reinterpret_cast<unsigned long long*>(stats_blk) + ((size_t)img * p.Cout + co + j) * 2;
       atomicAdd(sp, (unsigned long long)__double2ll_rn((double)ssum[j] * SA_STAT_SCALE));
       atomicAdd(sp + 1, (unsigned long long)__double2ll_rn((double)ssq[j] * SA_STAT_SCALE));
       ssum[j] = ssq[j] = 0.f;
@@ -1050,7 +1054,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
       float acc = 0.f;
       for (int r = 0; r < RG; ++r) acc += red[(q * RG + r) * BN + col];
       const int img = img_lo + (q >> 1);
-      atomicAdd(reinterpret_cast<unsigned long long*>(p.stats) + ((size_t)img * p.Cout + c) * 2 + (q & 1),
+      atomicAdd(reinterpret_cast<unsigned long long*>(stats_blk) + ((size_t)img * p.Cout + c) * 2 + (q & 1),
                 (unsigned long long)__double2ll_rn((double)acc * SA_STAT_SCALE));
     }
   }
@@ -1180,8 +1184,8 @@ int pick_cfg(const SaConvArgs* a) {
 
 int cfg_bn(int cfg) {
   switch (cfg) {
-    case 0: case 4: case 6: return 128;
-    case 1: case 3: case 5: return 64;
+    case 0: case 4: case 6: case 7: return 128;
+    case 1: case 3: case 5: case 8: return 64;
     case 2: return 16;
     default: return 0;
   }
@@ -1206,10 +1210,12 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
     case 1: return launch_cfg<128, 64, 2, 2>(a, stream);
     case 2: return launch_cfg<256, 16, 4, 1>(a, stream);
     case 3: return launch_cfg<64, 64, 2, 2>(a, stream);
-    case 4: case 5: case 6: {
+    case 4: case 5: case 6: case 7: case 8: {
       const int r = cfg == 4 ? launch_glds3<256, 128, 4, 2>(a, stream, true)
                   : cfg == 5 ? launch_glds3<128, 64, 2, 2>(a, stream, true)
-                             : launch_glds3<128, 128, 2, 2>(a, stream, true);
+                  : cfg == 6 ? launch_glds3<128, 128, 2, 2>(a, stream, true)
+                  : cfg == 7 ? launch_glds3<128, 128, 2, 4>(a, stream, true)
+                             : launch_glds3<256, 64, 4, 2>(a, stream, true);
       return r == 1 ? -5 : r;
     }
     default: return -3;

@@ -77,6 +77,17 @@ __global__ void instnorm_apply_kernel(const SaNormArgs a) {
   }
 }
 
+__global__ void stats_reduce_kernel(sa_stat_t* stats, int slots, long count) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < count; i += (long)gridDim.x * blockDim.x) {
+    sa_stat_t acc = 0;
+    for (int r = 0; r < slots; ++r) {
+      acc += stats[(size_t)r * count + i];
+      if (r > 0) stats[(size_t)r * count + i] = 0;
+    }
+    stats[i] = acc;
+  }
+}
+
 __global__ void avgpool3s2_kernel(const f16* __restrict__ x, int xs, f16* __restrict__ out, int os,
                                   int N, int H, int W, int C, int Ho, int Wo) {
   const int C8 = C >> 3;
@@ -216,5 +227,14 @@ extern "C" int sa_interp_bilinear(const void* x, int xs, void* out, int os, int 
   long work = (long)N * Ho * Wo * (C / 8);
   hipLaunchKernelGGL(interp_kernel, dim3(grid_for(work)), dim3(256), 0, stream, (const f16*)x, xs,
                      (f16*)out, os, N, H, W, C, Ho, Wo, ac, mul);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_stats_reduce(sa_stat_t* stats, int slots, long count, hipStream_t stream) {
+  if (slots <= 1) return 0;
+  if (count <= 0) return -2;
+  long g = (count + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(stats_reduce_kernel, dim3((unsigned)g), dim3(256), 0, stream, stats, slots, count);
   return (int)hipGetLastError();
 }

@@ -11,6 +11,13 @@ Norm parse_norm(const std::string& s) {
 
 void instnorm(hipStream_t s, const Tensor& x, const sa_stat_t* stats, const Tensor& out, int act,
               const Tensor* res, const sa_stat_t* res_stats, int act2) {
+  // fold the conv epilogues' statistic copies (idempotent: copies r > 0 are cleared)
+  int rc = sa_stats_reduce(const_cast<sa_stat_t*>(stats), kStatSlots, (long)x.n * x.c * 2, s);
+  SA_REQUIRE(rc == 0, "stats reduce failed");
+  if (res_stats) {
+    rc = sa_stats_reduce(const_cast<sa_stat_t*>(res_stats), kStatSlots, (long)x.n * x.c * 2, s);
+    SA_REQUIRE(rc == 0, "stats reduce failed");
+  }
   SaNormArgs a{};
   a.x = x.ptr;
   a.x_stride = x.stride;
@@ -27,7 +34,7 @@ void instnorm(hipStream_t s, const Tensor& x, const sa_stat_t* stats, const Tens
   a.act2 = act2;
   a.eps = 1e-5f;
   a.alpha = 0.01f;
-  int rc = sa_instnorm_apply(&a, s);
+  rc = sa_instnorm_apply(&a, s);
   SA_REQUIRE(rc == 0, "instnorm failed");
   SA_LAUNCH_CHECK(s);
 }

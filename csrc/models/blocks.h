@@ -15,7 +15,7 @@ Norm parse_norm(const std::string& s);
 class StatsPool {
  public:
   sa_stat_t* take(int n, int c) {
-    size_t need = (size_t)n * c * 2;
+    size_t need = (size_t)kStatSlots * n * c * 2;
     reserve_.push_back(need);
     offs_.push_back(total_);
     total_ += need;

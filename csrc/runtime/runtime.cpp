@@ -444,6 +444,7 @@ void ConvLayer::run(hipStream_t s, const std::vector<Tensor>& srcs, const Tensor
     a.act2 = act2;
   }
   a.stats = stats;
+  a.stats_slots = stats ? kStatSlots : 0;
   launch(s, a);
 }
 
@@ -527,7 +528,8 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
   const long Mo = M * (a.up == 2 ? 4 : (a.up == 3 ? 8 : 1));
   long width = std::max({(long)a.Cout, (long)a.out_stride, (long)a.aux_stride, (long)a.rh_stride, (long)a.h_stride});
   const size_t out_bytes = (size_t)Mo * width * 4 + 256;
-  const size_t stats_bytes = a.stats ? (size_t)a.N * a.Cout * 2 * sizeof(sa_stat_t) + 256 : 0;
+  const size_t stats_bytes =
+      a.stats ? (size_t)std::max(1, a.stats_slots) * a.N * a.Cout * 2 * sizeof(sa_stat_t) + 256 : 0;
   const size_t proj_bytes = a.proj_out ? (size_t)4 * std::max(1, a.proj_taps * a.proj_oc) * a.proj_plane * 4 + 256 : 0;
   char* scratch = nullptr;
   HIP_CHECK(hipMalloc((void**)&scratch, out_bytes + stats_bytes + proj_bytes));
@@ -542,8 +544,9 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
   HIP_CHECK(hipEventCreate(&e1));
   PlanEntry best{-1, 1, 1e30f};
   const bool can_split = a.ws && a.counters && !a.stats;
-  for (int cfg = 0; cfg <= 5; ++cfg) {
+  for (int cfg = 0; cfg <= 8; ++cfg) {
     if (cfg == 2 && a.Cout > 32) continue;  // 256x16 tile: narrow outputs only
+    if (cfg == 6) continue;                 // 128x128 / 4 waves: never competitive (conv_bench)
     for (int sk : {1, 0}) {
       if (sk == 0 && !can_split) continue;
       t.tile_cfg = cfg;

@@ -80,7 +80,7 @@ class SaConvArgs(C.Structure):
         ("KD", C.c_int32), ("Di", C.c_int32), ("Do", C.c_int32), ("sd", C.c_int32), ("pd", C.c_int32),
         ("up", C.c_int32), ("cout_real", C.c_int32), ("gate", C.c_void_p), ("gate_stride", C.c_int32),
         ("proj_w", C.c_void_p), ("proj_out", C.c_void_p), ("proj_taps", C.c_int32), ("proj_oc", C.c_int32),
-        ("proj_plane", C.c_int64),
+        ("proj_plane", C.c_int64), ("stats_slots", C.c_int32),
     ]
 
 
@@ -130,6 +130,7 @@ def _declare_dev(lib):
         "sa_conv2d_nslices": (_i, [C.POINTER(SaConvArgs)]),
         "sa_proj_stencil": (_i, [_p, _i, C.c_long, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p]),
         "sa_instnorm_apply": (_i, [C.POINTER(SaNormArgs), _p]),
+        "sa_stats_reduce": (_i, [_p, _i, C.c_long, _p]),
         "sa_avgpool3s2": (_i, [_p, _i, _p, _i, _i, _i, _i, _i, _p]),
         "sa_avgpool_k": (_i, [_p, _i, _p, _i, _i, _i, _i, _i, _i, _p]),
         "sa_interp_bilinear": (_i, [_p, _i, _p, _i, _i, _i, _i, _i, _i, _i, _i, _f, _p]),

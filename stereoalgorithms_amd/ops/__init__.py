@@ -15,7 +15,7 @@ import torch
 from .. import _native as N
 
 __all__ = [
-    "splitk_workspace", "pack_conv_weight", "conv2d", "proj_stencil", "instnorm_apply", "avgpool3s2", "avgpool_k", "interp_bilinear",
+    "splitk_workspace", "pack_conv_weight", "conv2d", "proj_stencil", "stats_reduce", "instnorm_apply", "avgpool3s2", "avgpool_k", "interp_bilinear",
     "corr1d_pyramid", "corr1d_lookup", "raft_motion_head", "convex_upsample", "preprocess", "remap_bgr", "reproject",
     "agcl_corr", "linear_attention", "layernorm", "ew", "interp_flow", "convex_upsample_c",
     "pack_conv3d_weight", "deconv_as_conv_weight", "conv3d", "dwconv3x3", "norm_corr_volume", "topk_disparity",
@@ -38,6 +38,12 @@ def _pix_stride(t: torch.Tensor) -> int:
     s = t.stride(2)
     assert t.stride(1) == w * s and (n == 1 or t.stride(0) == h * w * s), "pixels must be uniformly strided"
     return s
+
+
+def stats_reduce(stats, slots):
+    """Fold ``slots`` copies of instance-norm statistics into copy 0 (copies 1.. are cleared)."""
+    N.check(N.dev().sa_stats_reduce(stats.data_ptr(), slots, stats.numel() // slots, _stream()), "sa_stats_reduce")
+    return stats
 
 
 def proj_stencil(P, nslices, n, h, w, kh, kw, oc, bias=None, out=None, accumulate=False):
@@ -98,7 +104,7 @@ def pack_conv_weight(w: torch.Tensor, segs: Sequence[tuple[int, int]] | None = N
 def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1, act="none",
            act2="none", res=None, out=None, epi="store", scale=1.0, alpha=0.01, stats=None,
            ctx=None, aux=None, hbuf=None, rh=None, tile_cfg=-1, splitk=1, workspace=None, up=0, cout_real=0,
-           gate=None, proj=None):
+           gate=None, proj=None, stats_slots=1):
     """NHWC fp16 implicit-GEMM conv.  ``proj = (w2 fp32 [taps*oc, cout], taps, oc)`` with
     ``epi="proj"``: the epilogue projects the activated output onto the taps of a following conv
     and the call returns ``(out_or_None, P, nslices)`` for :func:`proj_stencil`.  ``splitk``: 1 = off, 0 = auto, >1 = forced; needs
@@ -160,6 +166,7 @@ def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1
     if stats is not None:
         assert stats.dtype == torch.int64  # fixed point, value * 2^24
         a.stats = stats.data_ptr()
+        a.stats_slots = stats_slots
     a.tile_cfg = tile_cfg
     a.splitk = splitk
     if workspace is not None:

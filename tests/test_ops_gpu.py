@@ -299,6 +299,17 @@ def test_conv2d_flow_acc_and_stats():
     assert rel_err(stats[..., 0].double() / 2 ** 24, yr.sum((2, 3))) < 1e-2
     ref2 = F.relu(F.instance_norm(yr))
     assert rel_err(nchw(out), ref2) < 5e-3
+    # slotted statistics (the engine's contention-spreading layout) fold to the same sums
+    st16 = torch.zeros(16, n, 64, 2, dtype=torch.int64, device=DEV)
+    for cfg in (1, 3, 5):
+        st1 = torch.zeros(n, 64, 2, dtype=torch.int64, device=DEV)
+        O.conv2d(nhwc(x).half(), wp2, kp2, 64, 3, 3, stats=st1, tile_cfg=cfg)
+        st16.zero_()
+        O.conv2d(nhwc(x).half(), wp2, kp2, 64, 3, 3, stats=st16, stats_slots=16, tile_cfg=cfg)
+        O.stats_reduce(st16, 16)
+        O.stats_reduce(st16, 16)  # idempotent
+        torch.cuda.synchronize()
+        assert torch.equal(st16[0], st1) and st16[1:].abs().sum().item() == 0
 
 
 def test_pool_interp():

@@ -31,6 +31,7 @@ SHAPES = {
     "cf1": (1, 120, 160, 8, 64, 7, 0),       # motion encoder convf1 (7x7, 2 -> 8 padded channels)
     "zr32": (1, 30, 40, 256, 256, 3, 0),     # GRU 1/16 z,r at batch 1
     "zr8l": (1, 60, 80, 384, 256, 3, 0),     # GRU 1/8 z,r at batch 1
+    "fr8": (16, 480, 640, 64, 64, 3, 1),     # RAFT-SF fnet layer1 at batch 8 (full resolution, both images)
 }
 
 
@@ -39,6 +40,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--cfgs", default="-1", help="comma list of tile configs (-1 = launcher's choice, 4 = glds3)")
+    ap.add_argument("--stats", type=int, default=0, help="fuse instance-norm statistics over N slots (engine: 16)")
     a = ap.parse_args()
     import torch
     from stereoalgorithms_amd import ops as O
@@ -53,6 +55,10 @@ def main():
         out = torch.empty(n, h, w, cout, device="cuda", dtype=torch.float16)
         for cfg in map(int, a.cfgs.split(",")):
             kw = dict(bias=b, out=out, splitk=sk, workspace=ws if sk != 1 else None, tile_cfg=cfg)
+            if a.stats:
+                kw["stats"] = torch.zeros(16, n, cout, 2, dtype=torch.int64, device="cuda")
+                kw["stats_slots"] = a.stats
+                kw["splitk"], kw["workspace"] = 1, None
             try:
                 for _ in range(3):
                     O.conv2d(x, wp, kpad, cout, k, k, **kw)
