@@ -108,6 +108,7 @@ def main():
     extra = {}
     if rank == 0 and not args.no_latency:
         del eng
+        os.environ["SA_STAGE_TIMES"] = "1"  # per-stage device times (event nodes in the frame graph)
         for preset in ("raftstereo-sceneflow", "raftstereo-realtime", *OTHER_MS):
             e1 = NativeStereoEngine(preset, None, H, W, batch=1, device=dev.index, seed=0)
             e1.set_Q(Q)
@@ -125,7 +126,8 @@ def main():
                              "latency_ms_p99": round(float(np.percentile(ts, 99)), 3),
                              "fps_b1": round(1000.0 / float(ts.mean()), 2),
                              "baseline_ms_rtx3090": {**BASELINE_MS, **OTHER_MS}[preset],
-                             "speedup_vs_baseline": round({**BASELINE_MS, **OTHER_MS}[preset] / float(ts.mean()), 3)}
+                             "speedup_vs_baseline": round({**BASELINE_MS, **OTHER_MS}[preset] / float(ts.mean()), 3),
+                             "device_stages_ms": {k: round(v, 3) for k, v in e1.stage_times()}}
             e1.close()
     if rank == 0:
         base_fps = 1000.0 / BASELINE_MS[args.model]

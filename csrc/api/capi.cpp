@@ -86,4 +86,20 @@ const float* sa_engine_aux_output(void* e, int* n) {
 
 void* sa_engine_stream(void* e) { return (void*)static_cast<sa::StereoEngine*>(e)->stream(); }
 
+int sa_engine_stage_times(void* e, float* ms, const char** names, int max) {
+  static thread_local std::vector<std::string> keep;
+  int n = -1;
+  const int rc = guarded([&] {
+    auto st = static_cast<sa::StereoEngine*>(e)->stage_times();
+    keep.clear();
+    for (auto& p : st) keep.push_back(p.first);
+    n = 0;
+    for (size_t i = 0; i < st.size() && (int)i < max; ++i, ++n) {
+      ms[i] = st[i].second;
+      names[i] = keep[i].c_str();
+    }
+  });
+  return rc == 0 ? n : -1;
+}
+
 }  // extern "C"

@@ -21,6 +21,9 @@ int sa_engine_run_host(void* engine, void* left, void* right, float* disp, float
 long long sa_engine_device_bytes(void* engine);
 const float* sa_engine_aux_output(void* engine, int* n);
 void* sa_engine_stream(void* engine);
+// per-stage device times of the last frame (SA_STAGE_TIMES=1): returns the count (<= max), fills
+// ms[i] and names[i] (pointers valid for the engine's lifetime)
+int sa_engine_stage_times(void* engine, float* ms, const char** names, int max);
 
 #ifdef __cplusplus
 }

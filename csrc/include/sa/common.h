@@ -26,6 +26,12 @@ bool debug_sync_enabled();
 // Fault injection for the error paths (SA_FAULT_INJECT=alloc|launch).
 bool fault_inject(const char* what);
 
+// roctx range (rocprofv3 --marker-trace shows it): engine build, tuning pass, frames
+struct TraceRange {
+  explicit TraceRange(const char* name);
+  ~TraceRange();
+};
+
 }  // namespace sa
 
 #define SA_LOG(lvl, ...)                                                        \

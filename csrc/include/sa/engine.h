@@ -76,6 +76,10 @@ class StereoEngine {
     return nullptr;
   }
   long frames_run() const { return launches_per_frame_; }
+  // Per-stage device times of the last frame in ms (SA_STAGE_TIMES=1 at engine creation): events
+  // recorded at stage boundaries of the frame (event nodes of the captured graph).  Each entry is
+  // (stage that ENDS at the mark, ms since the previous mark).  Empty when disabled.
+  std::vector<std::pair<std::string, float>> stage_times() const;
 
  protected:
   explicit StereoEngine(const EngineConfig& cfg);
@@ -103,6 +107,9 @@ class StereoEngine {
   void rec(hipStream_t s, int i);
   void wait(hipStream_t s, int i);
 
+  // stage boundary on the frame's main stream (no-op unless stage timing is on)
+  void stage(hipStream_t s, const char* name);
+
   void frame(hipStream_t s, bool rectify);  // the captured body
   void launch_frame(hipStream_t s, bool rectify);
 
@@ -129,7 +136,12 @@ class StereoEngine {
   SplitKWorkspace splitk_side2_;
   static constexpr int kEvents = 8;
   hipEvent_t ev_dep_[kEvents] = {};
-  bool tuning_pass_ = false;  // set during the eager conv-tuning forward (branches serialised)
+  bool tuning_pass_ = false;
+  static constexpr int kMaxStages = 16;
+  bool stage_on_ = false;
+  int nstage_ = 0;
+  unsigned long long* stage_ts_ = nullptr;  // device wall-clock stamps [kMaxStages]
+  const char* stage_name_[kMaxStages] = {};  // set during the eager conv-tuning forward (branches serialised)
   uint8_t* pin_in_ = nullptr;
   float* pin_out_ = nullptr;
   long launches_per_frame_ = 0;

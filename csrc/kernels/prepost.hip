@@ -229,3 +229,16 @@ extern "C" int sa_convex_upsample(const void* mask, int mask_stride, const float
                      (const f16*)mask, mask_stride, flow, B, H, W, factor, sign, out);
   return (int)hipGetLastError();
 }
+
+// ---- stage timestamps: one wave writes the GPU's constant-rate wall clock (a kernel node of the
+// frame graph, so it runs after everything queued before it on the stream)
+namespace {
+__global__ void stamp_kernel(unsigned long long* buf, int idx) {
+  if (threadIdx.x == 0) buf[idx] = wall_clock64();
+}
+}  // namespace
+
+extern "C" int sa_stamp(unsigned long long* buf, int idx, hipStream_t stream) {
+  hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, stream, buf, idx);
+  return (int)hipGetLastError();
+}

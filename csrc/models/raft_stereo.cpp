@@ -381,6 +381,7 @@ void RaftStereo::forward(hipStream_t s) {
   }
   if (par) join(s);
   HIP_CHECK(hipMemsetAsync(flow_, 0, (size_t)Bn * h0 * w0 * 4, s));
+  stage(s, "encoders+corr");
 
   auto pool = [&](hipStream_t st, int i) {  // pool_[i] = pool2x(net[i])
     check(sa_avgpool3s2(net_[i].ptr, net_[i].stride, pool_[i].ptr, pool_[i].stride, Bn, lh_[i],
@@ -511,6 +512,7 @@ void RaftStereo::forward(hipStream_t s) {
       fine_and_head(it == rc_.iters - 1);
     }
   }
+  stage(s, "gru_iterations");
   // convex upsampling; disparity = -flow_up
   check(sa_convex_upsample(mask_.ptr, mask_.stride, flow_, Bn, h0, w0, f, -1.f, disp_, s),
         "convex upsample");

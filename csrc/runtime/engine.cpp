@@ -87,6 +87,7 @@ StereoEngine::~StereoEngine() {
   if (side2_) (void)hipStreamDestroy(side2_);
   for (hipEvent_t e : ev_dep_)
     if (e) (void)hipEventDestroy(e);
+
   if (stream_) (void)hipStreamDestroy(stream_);
   arena_.release();
 }
@@ -130,6 +131,8 @@ void StereoEngine::init() {
   HIP_CHECK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
   HIP_CHECK(hipStreamCreateWithFlags(&side2_, hipStreamNonBlocking));
   for (hipEvent_t& e : ev_dep_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (const char* st = std::getenv("SA_STAGE_TIMES")) stage_on_ = st[0] == '1';
+  if (stage_on_) stage_ts_ = (unsigned long long*)arena_.alloc(kMaxStages * sizeof(unsigned long long));
   const size_t img = (size_t)B() * H() * W() * 3;
   in_left_ = (uint8_t*)arena_.alloc(img);
   in_right_ = (uint8_t*)arena_.alloc(img);
@@ -143,6 +146,7 @@ void StereoEngine::init() {
   splitk_side_.alloc(arena_, 16l << 20, 8192);
   splitk_side2_.alloc(arena_, 16l << 20, 8192);
   WeightSource src{store_.get(), cfg_.weights.empty(), cfg_.seed};
+  TraceRange tr("engine build");
   build(src);
   store_.reset();  // host copies no longer needed
   HIP_CHECK(hipDeviceSynchronize());
@@ -151,6 +155,7 @@ void StereoEngine::init() {
     // whatever the buffers hold) and the plan is fixed before the frame graph is captured
     ScopedSplitK sk(&splitk_);
     ScopedConvTuning tune(true);
+    TraceRange ttr("conv tactic selection");
     tuning_pass_ = true;
     forward(stream_);
     tuning_pass_ = false;
@@ -217,8 +222,31 @@ void StereoEngine::tap_f32(hipStream_t s, const char* name, const float* p, int 
   tap(s, name, t);
 }
 
+void StereoEngine::stage(hipStream_t s, const char* name) {
+  if (!stage_on_ || tuning_pass_ || nstage_ >= kMaxStages) return;
+  stage_name_[nstage_] = name;
+  const int rc = sa_stamp(stage_ts_, nstage_, s);
+  SA_REQUIRE(rc == 0, "stage stamp failed");
+  ++nstage_;
+}
+
+std::vector<std::pair<std::string, float>> StereoEngine::stage_times() const {
+  std::vector<std::pair<std::string, float>> out;
+  if (!stage_on_ || nstage_ < 2) return out;
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  unsigned long long ts[kMaxStages];
+  HIP_CHECK(hipMemcpy(ts, stage_ts_, nstage_ * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  int khz = 0;
+  HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, cfg_.device));
+  for (int i = 1; i < nstage_; ++i)
+    out.emplace_back(stage_name_[i], khz > 0 ? (float)((double)(ts[i] - ts[i - 1]) / khz) : -1.f);
+  return out;
+}
+
 void StereoEngine::frame(hipStream_t s, bool rectify) {
   ScopedSplitK sk(&splitk_);
+  nstage_ = 0;
+  stage(s, "start");
   if (rectify) {
     SA_REQUIRE(rect_maps_ != nullptr, "rectification requested but no maps set");
     // left images use map 0, right images map 1 (maps laid out [2][H][W][2])
@@ -227,10 +255,13 @@ void StereoEngine::frame(hipStream_t s, bool rectify) {
     rc = sa_remap_bgr(raw_right_, B(), H(), W(), rect_maps_ + (size_t)H() * W() * 2, 1, H(), W(), in_right_, s);
     SA_REQUIRE(rc == 0, "remap failed");
   }
+  if (rectify) stage(s, "rectify");
   forward(s);
+  stage(s, "network");
   if (have_Q_) {
     int rc = sa_reproject(disp_, 1, 1.f, in_left_, B(), H(), W(), Q_, nullptr, cloud_, s);
     SA_REQUIRE(rc == 0, "reproject failed");
+    stage(s, "reproject");
   }
   SA_LAUNCH_CHECK(s);
 }
@@ -245,6 +276,7 @@ void StereoEngine::launch_frame(hipStream_t s, bool rectify) {
     HIP_CHECK(hipEventRecord(ev_in_, s));
     HIP_CHECK(hipStreamWaitEvent(stream_, ev_in_, 0));
   }
+  TraceRange tr("frame");
   if (cfg_.use_graph) {
     if (!g.ready()) g.capture(stream_, [&] { frame(stream_, rectify); });
     g.launch(stream_);

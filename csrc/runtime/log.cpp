@@ -9,6 +9,8 @@
 #include <ctime>
 #include <mutex>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 namespace sa {
 
 static int env_int(const char* name, int dflt) {
@@ -31,6 +33,9 @@ bool fault_inject(const char* what) {
   const char* v = std::getenv("SA_FAULT_INJECT");
   return v && std::strcmp(v, what) == 0;
 }
+
+TraceRange::TraceRange(const char* name) { roctxRangePushA(name); }
+TraceRange::~TraceRange() { roctxRangePop(); }
 
 void log_msg(LogLevel lvl, const char* file, int line, const char* fmt, ...) {
   static std::mutex mu;

@@ -102,7 +102,9 @@ def build(jobs: int | None = None, verbose: bool = False) -> dict:
     dev_objs = [OBJDIR / "dev" / (s.stem + s.suffix + ".o") for s in dev_src]
     if host_objs:
         _link(host_objs, host_lib, True, extra=["-lz"])
-    _link(dev_objs, dev_lib, False, extra=[f"-L{LIBDIR}", "-lstereo_host", "-Wl,-rpath,$ORIGIN"] if host_objs else [])
+    roctx = ["-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]
+    _link(dev_objs, dev_lib, False,
+          extra=([f"-L{LIBDIR}", "-lstereo_host", "-Wl,-rpath,$ORIGIN"] if host_objs else []) + roctx)
     libs = [str(host_lib), str(dev_lib)]
     # reference-compatible per-model C ABI libraries + demo executables (host compiler, link the
     # engine library)

@@ -46,6 +46,16 @@ class NativeStereoEngine:
         except Exception:
             pass
 
+    def stage_times(self) -> list[tuple[str, float]]:
+        """Per-stage device ms of the last frame (engine created with SA_STAGE_TIMES=1), e.g.
+        [("encoders+corr", 1.2), ("gru_iterations", 11.0), ("network", 0.1), ("reproject", 0.05)]."""
+        ms = (C.c_float * 16)()
+        names = (C.c_char_p * 16)()
+        n = self._lib.sa_engine_stage_times(self._h, ms, names, 16)
+        if n < 0:
+            raise RuntimeError(f"stage_times failed: {self._lib.sa_last_error().decode()}")
+        return [(names[i].decode(), float(ms[i])) for i in range(n)]
+
     @property
     def device_bytes(self) -> int:
         return int(self._lib.sa_engine_device_bytes(self._h))

@@ -68,3 +68,19 @@ def test_engine_cloud_and_rectify_roundtrip():
     # host path (reference timed region) agrees with the device path
     dh, ch, _, _ = eng.run_host(left.cpu().numpy(), right.cpu().numpy(), cloud=True)
     assert np.allclose(dh, d0.cpu().numpy(), atol=1e-5)
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_stage_times(monkeypatch, graph):
+    """Per-stage device timers (event nodes inside the captured frame graph, or eager events)."""
+    from stereoalgorithms_amd.models.engine import NativeStereoEngine
+    monkeypatch.setenv("SA_STAGE_TIMES", "1")
+    h, w = 64, 96
+    eng = NativeStereoEngine("raftstereo-sceneflow", None, h, w, batch=1, iters=3, use_graph=graph)
+    left, right = _pairs(1, h, w)
+    for _ in range(2):
+        eng.run(left, right)
+    torch.cuda.synchronize()
+    st = dict(eng.stage_times())
+    assert set(st) >= {"encoders+corr", "gru_iterations", "network"}
+    assert all(v >= 0 for v in st.values()) and st["gru_iterations"] > 0
