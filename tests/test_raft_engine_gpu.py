@@ -84,3 +84,20 @@ def test_stage_times(monkeypatch, graph):
     st = dict(eng.stage_times())
     assert set(st) >= {"encoders+corr", "gru_iterations", "network"}
     assert all(v >= 0 for v in st.values()) and st["gru_iterations"] > 0
+
+
+def test_replay_determinism_race_screen():
+    """Race screen for the multi-stream frame graph: with parallel branches, split-K last-arriver
+    reductions and slotted statistics, repeated replays and an eager (no-graph) run of the same
+    engine configuration must agree bitwise."""
+    from stereoalgorithms_amd.models.engine import NativeStereoEngine
+    h, w = 96, 128
+    left, right = _pairs(2, h, w)
+    eng = NativeStereoEngine("raftstereo-sceneflow", None, h, w, batch=2, iters=4, seed=1)
+    outs = [eng.run(left, right).clone() for _ in range(6)]
+    eager = NativeStereoEngine("raftstereo-sceneflow", None, h, w, batch=2, iters=4, seed=1, use_graph=False)
+    e = eager.run(left, right)
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    assert torch.equal(e, outs[0])
