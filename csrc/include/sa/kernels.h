@@ -100,6 +100,12 @@ typedef struct {
 } SaConvArgs;
 
 int sa_conv2d(const SaConvArgs* a, hipStream_t stream);
+// Direct 3x3 / stride 1 / pad 1 conv, 64 -> 64 channels, weights ([>=64][kpad >= 576] packed fp16)
+// resident in LDS, persistent 2x64-pixel output tiles; bias / act / slotted IN statistics epilogue.
+// Also reachable through sa_conv2d with tile_cfg = 9.
+int sa_conv3x3_c64_direct(const void* x, int xs, const void* w, int kpad, const float* bias, void* out, int os,
+                          int N, int H, int W, int act, float alpha, sa_stat_t* stats, int slots, int max_blocks,
+                          hipStream_t stream);
 // Number of n-tiles (projection slices) sa_conv2d() will use for these args.
 int sa_conv2d_nslices(const SaConvArgs* a);
 // Following-conv stencil of SA_EPI_PROJ: out[n][y][x][o] (fp32, pixel stride out_stride) gets

@@ -1185,7 +1185,7 @@ int pick_cfg(const SaConvArgs* a) {
 int cfg_bn(int cfg) {
   switch (cfg) {
     case 0: case 4: case 6: case 7: return 128;
-    case 1: case 3: case 5: case 8: return 64;
+    case 1: case 3: case 5: case 8: case 9: return 64;
     case 2: return 16;
     default: return 0;
   }
@@ -1210,6 +1210,18 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
     case 1: return launch_cfg<128, 64, 2, 2>(a, stream);
     case 2: return launch_cfg<256, 16, 4, 1>(a, stream);
     case 3: return launch_cfg<64, 64, 2, 2>(a, stream);
+    case 9: {
+      // direct conv: one 64-channel source, 64 outputs, 3x3 / stride 1 / pad 1, plain store epilogue
+      const bool ok = a->nsrc == 1 && a->src[0].channels == 64 && a->Cin == 64 && a->Cout == 64 && a->KH == 3 &&
+                      a->KW == 3 && a->sh == 1 && a->sw == 1 && a->ph == 1 && a->pw == 1 && a->dh == 1 &&
+                      a->dw == 1 && a->KD <= 0 && a->up == 0 && !a->gate && !a->res && a->epi == SA_EPI_STORE &&
+                      a->Kpad >= 576 && a->out_stride % 8 == 0 && a->src[0].stride % 8 == 0 && a->Ho == a->H &&
+                      a->Wo == a->W;
+      if (!ok) return -5;
+      return sa_conv3x3_c64_direct(a->src[0].ptr, a->src[0].stride, a->weight, a->Kpad, a->bias, a->out,
+                                   a->out_stride, a->N, a->H, a->W, a->act, a->alpha, a->stats, a->stats_slots, 0,
+                                   stream);
+    }
     case 4: case 5: case 6: case 7: case 8: {
       const int r = cfg == 4 ? launch_glds3<256, 128, 4, 2>(a, stream, true)
                   : cfg == 5 ? launch_glds3<128, 64, 2, 2>(a, stream, true)

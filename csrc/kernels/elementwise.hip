@@ -37,38 +37,50 @@ __device__ __forceinline__ void st8(f16* p, const float* v) {
   *reinterpret_cast<half8*>(p) = h;
 }
 
-__global__ void instnorm_apply_kernel(const SaNormArgs a) {
+// Per-channel normalisation of one 8-channel group, computed once per thread from the fixed-point
+// sums (mean, rstd), then applied to many pixels of the same image: the statistics cost no longer
+// scales with the tensor size (the per-element version read 128 B of stats per 16 B of data).
+__device__ __forceinline__ void norm8(const sa_stat_t* st, int n, int C, int c, long HW, float eps, float* mean,
+                                      float* rstd) {
+  const double inv = 1.0 / ((double)HW * SA_STAT_SCALE);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const sa_stat_t* s = st + ((long)n * C + c + j) * 2;
+    const double m = (double)s[0] * inv;
+    const double var = (double)s[1] * inv - m * m;
+    mean[j] = (float)m;
+    rstd[j] = rsqrtf((float)(var > 0.0 ? var : 0.0) + eps);
+  }
+}
+
+// grid: (pixel chunks, N); a block's threads tile (pixels x channel groups) of one image, each thread
+// keeps one channel group and walks pixels
+__global__ __launch_bounds__(256) void instnorm_apply_kernel(const SaNormArgs a, int pix_per_block) {
   const int C8 = a.C >> 3;
-  const long total = (long)a.N * a.HW * C8;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
-       i += (long)gridDim.x * blockDim.x) {
-    const int c8 = (int)(i % C8);
-    const long pix = i / C8;
-    const int n = (int)(pix / a.HW);
-    const int c = c8 * 8;
+  const int n = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int c8 = tid % C8;
+  const int lanes_per_c = 256 / C8;  // threads sharing a channel group
+  if (tid >= lanes_per_c * C8) return;
+  const int c = c8 * 8;
+  float mean[8], rstd[8], rmean[8], rrstd[8];
+  norm8(a.stats, n, a.C, c, a.HW, a.eps, mean, rstd);
+  const bool rs = a.res && a.res_stats;
+  if (rs) norm8(a.res_stats, n, a.C, c, a.HW, a.eps, rmean, rrstd);
+  const long p0 = (long)blockIdx.x * pix_per_block;
+  const long p1 = p0 + pix_per_block < a.HW ? p0 + pix_per_block : a.HW;
+  for (long p = p0 + tid / C8; p < p1; p += lanes_per_c) {
+    const long pix = (long)n * a.HW + p;
     float v[8];
     ld8(reinterpret_cast<const f16*>(a.x) + pix * a.x_stride + c, v);
-    const double inv = 1.0 / ((double)a.HW * SA_STAT_SCALE);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const sa_stat_t* s = a.stats + ((long)n * a.C + c + j) * 2;
-      double mean = (double)s[0] * inv;
-      double var = (double)s[1] * inv - mean * mean;
-      float rstd = rsqrtf((float)(var > 0.0 ? var : 0.0) + a.eps);
-      v[j] = act_apply((v[j] - (float)mean) * rstd, a.act, a.alpha);
-    }
+    for (int j = 0; j < 8; ++j) v[j] = act_apply((v[j] - mean[j]) * rstd[j], a.act, a.alpha);
     if (a.res) {
       float r[8];
       ld8(reinterpret_cast<const f16*>(a.res) + pix * a.res_stride + c, r);
-      if (a.res_stats) {
+      if (rs) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const sa_stat_t* s = a.res_stats + ((long)n * a.C + c + j) * 2;
-          double mean = (double)s[0] * inv;
-          double var = (double)s[1] * inv - mean * mean;
-          float rstd = rsqrtf((float)(var > 0.0 ? var : 0.0) + a.eps);
-          r[j] = (r[j] - (float)mean) * rstd;
-        }
+        for (int j = 0; j < 8; ++j) r[j] = (r[j] - rmean[j]) * rrstd[j];
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j] + r[j], a.act2, a.alpha);
@@ -196,8 +208,13 @@ inline int grid_for(long work) {
 
 extern "C" int sa_instnorm_apply(const SaNormArgs* a, hipStream_t stream) {
   if (a->C % 8) return -2;
-  long work = (long)a->N * a->HW * (a->C / 8);
-  hipLaunchKernelGGL(instnorm_apply_kernel, dim3(grid_for(work)), dim3(256), 0, stream, *a);
+  if (a->C > 8 * 256) return -3;
+  // ~8 pixels per thread: enough reuse of the per-thread statistics, enough blocks to fill the chip
+  const int lanes_per_c = 256 / (a->C / 8);
+  const int ppb = lanes_per_c * 8;
+  const long chunks = (a->HW + ppb - 1) / ppb;
+  if (chunks > 2147483647L || a->N > 65535) return -3;
+  hipLaunchKernelGGL(instnorm_apply_kernel, dim3((unsigned)chunks, a->N), dim3(256), 0, stream, *a, ppb);
   return (int)hipGetLastError();
 }
 

@@ -426,8 +426,16 @@ SaConvArgs ConvLayer::args(const std::vector<Tensor>& srcs, const Tensor& out) c
 
 void ConvLayer::launch(hipStream_t s, SaConvArgs& a) const {
   if (fault_inject("launch")) throw Error("fault injection: launch");
-  if (a.tile_cfg < 0) conv_apply_plan(a, s);
+  const bool planned = a.tile_cfg < 0;
+  if (planned) conv_apply_plan(a, s);
   int rc = sa_conv2d(&a, s);
+  if (planned && (rc == -5 || rc == -6) && a.tile_cfg >= 0) {
+    // a plan whose tactic does not apply to these exact args (e.g. a stride / pointer-dependent
+    // eligibility rule): fall back to the launcher's own choice
+    a.tile_cfg = -1;
+    a.splitk = current_splitk() ? 0 : 1;
+    rc = sa_conv2d(&a, s);
+  }
   SA_REQUIRE(rc == 0, "sa_conv2d failed rc=%d", rc);
   SA_LAUNCH_CHECK(s);
 }
@@ -507,9 +515,9 @@ std::string plan_key(const SaConvArgs& a) {
   char buf[512];
   int n = std::snprintf(buf, sizeof(buf), "gfx950|%d,%d,%d,%d|", a.N, a.H, a.W, a.Cin);
   for (int i = 0; i < a.nsrc; ++i) n += std::snprintf(buf + n, sizeof(buf) - n, "%d.", a.src[i].channels);
-  std::snprintf(buf + n, sizeof(buf) - n, "|k%dx%dx%d|s%d,%d,%d|p%d,%d,%d|d%d,%d|o%dx%d|D%d,%d|c%d,%d|e%d,%d,%d,%d|w%d",
+  std::snprintf(buf + n, sizeof(buf) - n, "|k%dx%dx%d|s%d,%d,%d|p%d,%d,%d|d%d,%d|o%dx%d|D%d,%d|c%d,%d|e%d,%d,%d,%d,%d|w%d",
                 a.KD, a.KH, a.KW, a.sd, a.sh, a.sw, a.pd, a.ph, a.pw, a.dh, a.dw, a.Ho, a.Wo, a.Do, a.Di, a.Cout,
-                a.Kpad, a.epi, (int)(a.stats != nullptr), a.up, (int)(a.gate != nullptr),
+                a.Kpad, a.epi, (int)(a.stats != nullptr), a.up, (int)(a.gate != nullptr), (int)(a.res != nullptr),
                 (int)(a.ws != nullptr && a.counters != nullptr));
   return buf;
 }
@@ -544,11 +552,11 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
   HIP_CHECK(hipEventCreate(&e1));
   PlanEntry best{-1, 1, 1e30f};
   const bool can_split = a.ws && a.counters && !a.stats;
-  for (int cfg = 0; cfg <= 8; ++cfg) {
+  for (int cfg = 0; cfg <= 9; ++cfg) {
     if (cfg == 2 && a.Cout > 32) continue;  // 256x16 tile: narrow outputs only
     if (cfg == 6) continue;                 // 128x128 / 4 waves: never competitive (conv_bench)
     for (int sk : {1, 0}) {
-      if (sk == 0 && !can_split) continue;
+      if (sk == 0 && (!can_split || cfg == 9)) continue;
       t.tile_cfg = cfg;
       t.splitk = sk;
       if (sa_conv2d(&t, s) != 0) {

@@ -225,6 +225,34 @@ def test_conv2d_projection_epilogue_flow_head(n, hw, cfg, oc):
     assert rel_err(out - flow0, ref - flow0) < 3e-3
 
 
+@pytest.mark.parametrize("n,hw,act,stats", [(2, (17, 70), "relu", False), (1, (48, 128), "none", True),
+                                             (3, (5, 9), "leaky", True)])
+def test_conv3x3_c64_direct(n, hw, act, stats):
+    """LDS-resident-weight direct conv (tile_cfg 9): tails in both dims, several images per block,
+    slotted statistics folded to the unsplit sums."""
+    O = ops()
+    torch.manual_seed(31)
+    x = torch.randn(n, 64, *hw, device=DEV)
+    w = torch.randn(64, 64, 3, 3, device=DEV) / 24
+    b = torch.randn(64, device=DEV) * 0.1
+    ref = F.conv2d(x.half().float(), w.half().float(), b, padding=1)
+    ref = {"relu": F.relu, "none": lambda t: t, "leaky": lambda t: F.leaky_relu(t, 0.1)}[act](ref)
+    wp, kpad, _ = O.pack_conv_weight(w)
+    kw = {}
+    if stats:
+        st = torch.zeros(16, n, 64, 2, dtype=torch.int64, device=DEV)
+        kw = dict(stats=st, stats_slots=16)
+    out = O.conv2d(nhwc(x).half(), wp, kpad, 64, 3, 3, bias=b.contiguous(), act=act, alpha=0.1, tile_cfg=9, **kw)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(out), ref) < 2e-3
+    if stats:
+        O.stats_reduce(st, 16)
+        torch.cuda.synchronize()
+        y = nchw(out)
+        assert rel_err(st[0, ..., 0].double() / 2 ** 24, y.sum((2, 3))) < 1e-3
+        assert rel_err(st[0, ..., 1].double() / 2 ** 24, (y * y).sum((2, 3))) < 1e-3
+
+
 def test_conv2d_padded_channels_and_output_slice():
     O = ops()
     torch.manual_seed(2)

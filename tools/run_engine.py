@@ -38,6 +38,9 @@ def main():
     dt = (time.perf_counter() - t0) / a.frames * 1e3
     print(f"{a.model} B={a.batch} {a.height}x{a.width}: {dt:.3f} ms/step, {dt / a.batch:.3f} ms/frame, "
           f"mean disp {d.mean().item():.4f}")
+    st = eng.stage_times()
+    if st:
+        print("device stages (ms): " + ", ".join(f"{k} {v:.3f}" for k, v in st))
 
 
 if __name__ == "__main__":
