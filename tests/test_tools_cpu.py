@@ -82,3 +82,16 @@ def test_cmake_configures(tmp_path):
         assert r.returncode == 0, r.stdout[-3000:]
         for t in ("libstereo_amd.so", "libRAFTStereo.so", "raft_stereo_demo", "Stereo_Calibration"):
             assert (b / t).exists()
+
+
+def test_host_sanitizers(tmp_path):
+    """Host code under ASan + UBSan: calibration YAML, rectification, codecs,
+    heat-map, point cloud, chessboard detection and a short stereo calibration on the fixtures."""
+    import shutil
+    if not shutil.which("g++"):
+        pytest.skip("g++ not available")
+    r = subprocess.run(["bash", str(ROOT / "tools" / "sanitize" / "run.sh"), str(tmp_path)], capture_output=True,
+                       text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "host_check ok" in r.stdout
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr
