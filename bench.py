@@ -58,7 +58,10 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        # bounded collectives: a rank that dies or hangs fails the job instead of stalling it
+        from datetime import timedelta
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local),
+                                timeout=timedelta(seconds=int(os.environ.get("SA_DIST_TIMEOUT", "600"))))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local if world > 1 else 0)
