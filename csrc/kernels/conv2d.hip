@@ -112,6 +112,20 @@ __device__ __attribute__((aligned(16))) const unsigned char g_zero16[64] = {0};
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
+// one recursive-halving step of the projection reduce-scatter over K live values: lanes whose bit O
+// is set keep the upper half and receive the partner's copy of it (partner = DPP control CTRL)
+template <int K, int O, int CTRL>
+__device__ __forceinline__ void rs_step(float* y, int cc) {
+  const bool up = (cc & O) != 0;
+#pragma unroll
+  for (int i = 0; i < K / 2; ++i) {
+    const float give = up ? y[i] : y[i + K / 2];
+    const float keep = up ? y[i + K / 2] : y[i];
+    const int g = __builtin_amdgcn_update_dpp(0, __float_as_int(give), CTRL, 0xF, 0xF, false);
+    y[i] = keep + __int_as_float(g);
+  }
+}
+
 #define SA_STR2(x) #x
 #define SA_STR(x) SA_STR2(x)
 // s_waitcnt vmcnt(N) with a compile-time N (the asm string needs a literal)
@@ -958,16 +972,13 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
             for (int j = 0; j < 8; ++j) y[t] += v[j] * pw8[t][j];
           }
         }
-#pragma unroll
-        for (int k = 16, o = CPR / 2; o >= 1; k >>= 1, o >>= 1) {
-          const bool up = (cc & o) != 0;
-#pragma unroll
-          for (int i = 0; i < k / 2; ++i) {
-            const float give = up ? y[i] : y[i + k / 2];
-            const float keep = up ? y[i + k / 2] : y[i];
-            y[i] = keep + __shfl_xor(give, o);
-          }
-        }
+        // partners via DPP (VALU lane permutes, no LDS crossbar): bit 3 = row mirror, bit 2 = half-row
+        // mirror, bits 1 / 0 = quad permutes; each pairs lanes that differ in that bit and agree in
+        // the higher ones, which is all recursive halving needs
+        if constexpr (CPR >= 16) rs_step<16, 8, 0x140>(y, cc);
+        if constexpr (CPR >= 8) rs_step<16 * 8 / CPR, 4, 0x141>(y, cc);
+        if constexpr (CPR >= 4) rs_step<16 * 4 / CPR, 2, 0x4E>(y, cc);
+        if constexpr (CPR >= 2) rs_step<16 * 2 / CPR, 1, 0xB1>(y, cc);
         constexpr int PF = 16 / CPR;
         const int np = p.proj_taps * p.proj_oc;
         float* pout = p.proj_out + (size_t)by * np * p.proj_plane + m;
