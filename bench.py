@@ -5,7 +5,8 @@ Contract (driver): ``python bench.py --gpus N --steps K --warmup W`` (N>1 under 
 One step = every rank runs its shard of stereo pairs (``--per-gpu-batch``, default 8 => 64 pairs on
 8 GPUs, BASELINE.json config 5) through the native engine (one hipGraph per frame batch: preprocess,
 encoders, corr pyramid, 32 ConvGRU iterations, convex upsample, reprojection), fed by an H2D copy
-of the inputs from pinned host memory, then an RCCL all-gather of the disparity maps over xGMI.
+of the inputs from pinned host memory, then an RCCL all-gather of the disparity maps over xGMI
+(issued async on the process group's stream, so step t's gather overlaps step t+1's frame graph).
 K steps are timed between barrier + device synchronize; rank 0 prints ONE JSON line with the
 whole-job FPS (max time over ranks).  Data: synthetic stereo pairs; weights: seeded random init of
 the upstream architecture.
@@ -84,17 +85,21 @@ def main():
     def step():
         left.copy_(left_h, non_blocking=True)
         right.copy_(right_h, non_blocking=True)
-        return dp.step(left, right)
+        # pipelined: the all-gather of step t (RCCL's own stream) overlaps step t+1's frame graph
+        return dp.step_async(left, right)
 
     for _ in range(args.warmup):
         step()
+    dp.flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out = step()
+        pending = step()
+    out = pending.wait()
+    dp.flush()  # every step's collective is complete inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

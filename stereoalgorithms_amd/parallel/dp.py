@@ -27,15 +27,43 @@ def shard_indices_round_robin(total: int, world: int, rank: int) -> list[int]:
     return list(range(rank, total, world))
 
 
+class PendingGather:
+    """Handle of an in-flight disparity all-gather (see DataParallelStereo.step_async)."""
+
+    def __init__(self, out: torch.Tensor, work):
+        self.out, self._work = out, work
+
+    def wait(self) -> torch.Tensor:
+        """Make the current stream wait for the collective; returns the gathered [world*B,H,W] tensor."""
+        if self._work is not None:
+            self._work.wait()
+            self._work = None
+        return self.out
+
+
 @dataclass
 class DataParallelStereo:
-    engine: object  # anything with .run(left, right) -> [B,H,W] and .batch
+    """One rank's view of a DP stereo job.
+
+    ``step`` is the synchronous form (gathered result ordered after this step's frames).  ``step_async``
+    is the pipelined form used by bench.py: the engine writes into one of two persistent send slots, the
+    all-gather is issued with ``async_op=True`` so it runs on the process group's own stream (RCCL's
+    internal HIP stream on GPU) while the NEXT step's frame graph runs on the compute stream, and the
+    compute stream only waits for the collective that last used the slot it is about to overwrite.
+    A gathered buffer stays valid until the step two calls later reuses its slot.
+    """
+    engine: object  # anything with .run(left, right[, out=]) -> [B,H,W] and .batch
     world_size: int = 1
     rank: int = 0
     gather: bool = True
+    slots: int = 2
 
     def __post_init__(self):
         self._out = None
+        self._send: list = [None] * self.slots
+        self._recv: list = [None] * self.slots
+        self._work: list = [None] * self.slots
+        self._i = 0
 
     def step(self, left: torch.Tensor, right: torch.Tensor) -> torch.Tensor:
         """left/right: this rank's shard [B,H,W,3] u8 -> gathered disparity [world*B,H,W]."""
@@ -44,11 +72,49 @@ class DataParallelStereo:
             return disp
         return all_gather_disparity(disp, self.world_size, self._buffer(disp))
 
+    def step_async(self, left: torch.Tensor, right: torch.Tensor) -> PendingGather:
+        """Pipelined step: returns a PendingGather whose wait() yields the gathered disparity."""
+        slot = self._i % self.slots
+        self._i += 1
+        if self._work[slot] is not None:  # WAR: the collective still reading/writing this slot
+            self._work[slot].wait()
+            self._work[slot] = None
+        send = self._send[slot]
+        try:
+            disp = self.engine.run(left, right, out=send) if send is not None else self.engine.run(left, right)
+        except TypeError:  # engines without an ``out=`` argument
+            disp = self.engine.run(left, right)
+            if send is not None:
+                disp = send.copy_(disp)
+        self._send[slot] = disp
+        if self.world_size == 1 or not self.gather:
+            return PendingGather(disp, None)
+        shape = (self.world_size * disp.shape[0],) + tuple(disp.shape[1:])
+        recv = self._recv[slot]
+        if recv is None or recv.shape != shape or recv.device != disp.device:
+            recv = self._recv[slot] = torch.empty(shape, dtype=disp.dtype, device=disp.device)
+        work = _all_gather_async(disp, self.world_size, recv)
+        self._work[slot] = work
+        return PendingGather(recv, work)
+
+    def flush(self):
+        """Order every outstanding collective before the current stream's next work."""
+        for i, w in enumerate(self._work):
+            if w is not None:
+                w.wait()
+                self._work[i] = None
+
     def _buffer(self, disp):
         shape = (self.world_size * disp.shape[0],) + tuple(disp.shape[1:])
         if self._out is None or self._out.shape != shape or self._out.device != disp.device:
             self._out = torch.empty(shape, dtype=disp.dtype, device=disp.device)
         return self._out
+
+
+def _all_gather_async(disp: torch.Tensor, world: int, out: torch.Tensor):
+    if disp.is_cuda:
+        return dist.all_gather_into_tensor(out, disp, async_op=True)
+    return dist.all_gather(list(out.chunk(world, dim=0)), disp, async_op=True)
 
 
 def all_gather_disparity(disp: torch.Tensor, world: int, out: torch.Tensor | None = None) -> torch.Tensor:

@@ -78,3 +78,43 @@ def test_dp_allgather_gloo(world):
     for p in procs:
         p.join(timeout=60)
     assert all(res[r] for r in range(world)), res
+
+
+def _worker_async(rank, world, port, B, H, W, steps, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        eng = FakeEngine(B, H, W)
+        step = dp.DataParallelStereo(eng, world_size=world, rank=rank)
+        ok = True
+        pending = []
+        for t in range(steps):  # keep two steps in flight, check each gathered result a step late
+            g = torch.Generator().manual_seed(100 + t)
+            all_l = torch.randint(0, 255, (world * B, H, W, 3), generator=g, dtype=torch.uint8)
+            all_r = torch.randint(0, 255, (world * B, H, W, 3), generator=g, dtype=torch.uint8)
+            s, e = dp.shard_range(world * B, world, rank)
+            pending.append((step.step_async(all_l[s:e], all_r[s:e]), eng.run(all_l, all_r)))
+            if len(pending) == 2:
+                h, ref = pending.pop(0)
+                ok = ok and torch.equal(h.wait(), ref)
+        for h, ref in pending:
+            ok = ok and torch.equal(h.wait(), ref)
+        step.flush()
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_pipelined_allgather_gloo():
+    """step_async: ping-pong send/recv slots, collective of step t in flight during step t+1."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_async, args=(r, world, port, 2, 6, 8, 5, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert all(res[r] for r in range(world)), res
