@@ -76,7 +76,8 @@ def _link(objs, out: Path, host_only: bool, extra=(), shared: bool = True):
     if host_only:
         cmd = [CXX, *(["-shared"] if shared else []), "-o", str(out), *map(str, objs), *extra]
     else:
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", str(out), *map(str, objs), *extra]
+        cmd = [HIPCC, f"--offload-arch={ARCH}", *(["-shared"] if shared else []), "-o", str(out),
+               *map(str, objs), *extra]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {out}\n{r.stdout}\n{r.stderr}")
@@ -128,6 +129,24 @@ def build(jobs: int | None = None, verbose: bool = False) -> dict:
         libname = lib[3:-3]
         _link([obj], BINDIR / s.stem, True, shared=False,
               extra=[f"-L{LIBDIR}", f"-l{libname}", "-lstereo_host", "-Wl,-rpath,$ORIGIN/../lib"])
+    # native RCCL data parallelism: its own library (Python processes never load a second RCCL next to
+    # torch's) + the C++ multi-GPU bench
+    dsrc = CSRC / "dist" / "dist.cpp"
+    dobj = OBJDIR / "dist" / "dist.cpp.o"
+    r = _compile(dsrc, dobj, False, hmt, verbose)
+    if r:
+        abi_built.append(r)
+    dist_lib = LIBDIR / "libstereo_dist.so"
+    _link([dobj], dist_lib, False, extra=[f"-L{LIBDIR}", "-lstereo_amd", "-L/opt/rocm/lib", "-lrccl",
+                                          "-Wl,-rpath,$ORIGIN", "-Wl,-rpath,/opt/rocm/lib"])
+    libs.append(str(dist_lib))
+    s = ROOT / "apps" / "stereo_bench_dp.cpp"
+    obj = OBJDIR / "apps" / "stereo_bench_dp.o"
+    r = _compile(s, obj, False, hmt, verbose)
+    if r:
+        abi_built.append(r)
+    _link([obj], BINDIR / "stereo_bench_dp", False, shared=False,
+          extra=[f"-L{LIBDIR}", "-lstereo_dist", "-lstereo_amd", "-lstereo_host", "-Wl,-rpath,$ORIGIN/../lib"])
     return {"compiled": built + abi_built, "libs": libs}
 
 

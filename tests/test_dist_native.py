@@ -1,0 +1,67 @@
+"""Native RCCL DP module (csrc/dist/dist.cpp): the GPU-free parts on CPU (TCP bootstrap of the
+ncclUniqueId blob across processes, shard ranges), the RCCL runner on the GPU (world 1 through the
+fork launcher of apps/stereo_bench_dp.cpp; multi-GPU runs are the driver's)."""
+import ctypes as C
+import json
+import multiprocessing as mp
+import os
+import socket
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "stereoalgorithms_amd", "lib", "libstereo_dist.so")
+BIN = os.path.join(ROOT, "stereoalgorithms_amd", "bin", "stereo_bench_dp")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _peer(rank, world, port, q):
+    lib = C.CDLL(LIB, mode=C.RTLD_GLOBAL)
+    buf = (C.c_ubyte * 128)()
+    if rank == 0:
+        for i in range(128):
+            buf[i] = (i * 7 + 3) & 0xFF
+    rc = lib.sa_dist_exchange_blob(rank, world, b"127.0.0.1", port, buf, C.c_size_t(128), 20000)
+    q.put((rank, rc, bytes(buf)))
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="native build missing")
+@pytest.mark.parametrize("world", [2, 4])
+def test_unique_id_bootstrap_tcp(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_peer, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (rc, b) for r, rc, b in (q.get(timeout=60) for _ in procs)}
+    for p in procs:
+        p.join(timeout=30)
+    want = bytes((i * 7 + 3) & 0xFF for i in range(128))
+    assert all(res[r][0] == 0 for r in range(world)), res
+    assert all(res[r][1] == want for r in range(world))
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="native build missing")
+def test_bootstrap_times_out_without_rank0():
+    lib = C.CDLL(LIB, mode=C.RTLD_GLOBAL)
+    buf = (C.c_ubyte * 16)()
+    assert lib.sa_dist_exchange_blob(1, 2, b"127.0.0.1", _free_port(), buf, C.c_size_t(16), 300) == -1
+
+
+@pytest.mark.gpu
+def test_native_dp_bench_world1():
+    env = dict(os.environ, SA_DIST_TIMEOUT="120", SA_DP_GATHER_WORLD1="1")
+    r = subprocess.run([BIN, "--nproc", "1", "--model", "raftstereo-realtime", "--batch", "2", "--steps", "3",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=110, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["n_gpus"] == 1 and rec["finite"] and rec["value"] > 0
