@@ -154,10 +154,11 @@ __global__ __launch_bounds__(256) void raft_motion_head_kernel(
   __shared__ float corr_s[64][37];
   const int tid = threadIdx.x, lane = tid & 63;
   const int q = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const long pix = (long)blockIdx.x * 64 + lane;
-  const bool ok = pix < total;
+  const int pixi = blockIdx.x * 64 + lane;  // total < 2^31 (host-checked): 32-bit index math
+  const long pix = pixi;
+  const bool ok = pixi < total;
   const int ntap = 2 * radius + 1;
-  const int w1 = ok ? (int)(pix % W1) : 0;
+  const int w1 = ok ? pixi % W1 : 0;
   const float fx = ok ? flow[pix] : 0.f;
   if (q < levels && ok) {
     const long off = q == 0 ? 0 : (q == 1 ? lvl_off1 : (q == 2 ? lvl_off2 : lvl_off3));
@@ -181,6 +182,7 @@ __global__ __launch_bounds__(256) void raft_motion_head_kernel(
   float acc[16];
 #pragma unroll
   for (int o = 0; o < 16; ++o) acc[o] = bc[q * 16 + o];
+#pragma unroll 12
   for (int k = 0; k < nc; ++k) {
     const float v = corr_s[lane][k];
     const float* w = wc + k * 64 + q * 16;
@@ -197,20 +199,27 @@ __global__ __launch_bounds__(256) void raft_motion_head_kernel(
   *reinterpret_cast<half8*>(cp) = h0;
   *reinterpret_cast<half8*>(cp + 8) = h1;
 
-  const int y = (int)((pix / W1) % H);
+  const int y = (pixi / W1) % H;
 #pragma unroll
   for (int o = 0; o < 16; ++o) acc[o] = bf[q * 16 + o];
-  for (int ky = 0; ky < 7; ++ky) {
-    const int yy = y + ky - 3;
-    if (yy < 0 || yy >= H) continue;
-    for (int kx = 0; kx < 7; ++kx) {
-      const int xx = w1 + kx - 3;
-      if (xx < 0 || xx >= W1) continue;
-      const float v = flow[pix + (long)(ky - 3) * W1 + (kx - 3)];
-      const float* w = wf + (ky * 7 + kx) * 64 + q * 16;
+  // all 49 taps' loads issued up front (zero outside the image; a masked tap adds exactly 0, so the
+  // accumulation order and result match the per-tap branchy loop), then the FMAs: the loads overlap
+  // instead of paying one global-load latency per tap
+  float fv[49];
 #pragma unroll
-      for (int o = 0; o < 16; ++o) acc[o] += v * w[o];
+  for (int ky = 0; ky < 7; ++ky) {
+    const bool rok = (unsigned)(y + ky - 3) < (unsigned)H;
+#pragma unroll
+    for (int kx = 0; kx < 7; ++kx) {
+      const bool tok = rok && (unsigned)(w1 + kx - 3) < (unsigned)W1;
+      fv[ky * 7 + kx] = tok ? flow[pix + (long)(ky - 3) * W1 + (kx - 3)] : 0.f;
     }
+  }
+#pragma unroll
+  for (int t = 0; t < 49; ++t) {
+    const float* w = wf + t * 64 + q * 16;
+#pragma unroll
+    for (int o = 0; o < 16; ++o) acc[o] += fv[t] * w[o];
   }
 #pragma unroll
   for (int o = 0; o < 8; ++o) {
@@ -283,6 +292,7 @@ extern "C" int sa_raft_motion_head(const float* pyr, const float* flow, int B, i
     acc += (long)B * H * W1 * Wl;
     Wl >>= 1;
   }
+  if ((long)B * H * W1 >= (1L << 31) - 64) return -2;
   const int total = B * H * W1;
   hipLaunchKernelGGL(raft_motion_head_kernel, dim3((total + 63) / 64), dim3(256), 0, stream, pyr, flow, total, H, W1,
                      W2, levels, radius, off[1], off[2], off[3], wc, bc, wf, bf, (f16*)cor, cstride, (f16*)flo,

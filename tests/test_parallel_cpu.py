@@ -80,12 +80,12 @@ def test_dp_allgather_gloo(world):
     assert all(res[r] for r in range(world)), res
 
 
-def _worker_async(rank, world, port, B, H, W, steps, q):
+def _worker_async(rank, world, port, B, H, W, steps, q, gdt=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         eng = FakeEngine(B, H, W)
-        step = dp.DataParallelStereo(eng, world_size=world, rank=rank)
+        step = dp.DataParallelStereo(eng, world_size=world, rank=rank, gather_dtype=gdt)
         ok = True
         pending = []
         for t in range(steps):  # keep two steps in flight, check each gathered result a step late
@@ -93,7 +93,8 @@ def _worker_async(rank, world, port, B, H, W, steps, q):
             all_l = torch.randint(0, 255, (world * B, H, W, 3), generator=g, dtype=torch.uint8)
             all_r = torch.randint(0, 255, (world * B, H, W, 3), generator=g, dtype=torch.uint8)
             s, e = dp.shard_range(world * B, world, rank)
-            pending.append((step.step_async(all_l[s:e], all_r[s:e]), eng.run(all_l, all_r)))
+            ref = eng.run(all_l, all_r)
+            pending.append((step.step_async(all_l[s:e], all_r[s:e]), ref if gdt is None else ref.to(gdt)))
             if len(pending) == 2:
                 h, ref = pending.pop(0)
                 ok = ok and torch.equal(h.wait(), ref)
@@ -105,13 +106,15 @@ def _worker_async(rank, world, port, B, H, W, steps, q):
         dist.destroy_process_group()
 
 
-def test_dp_pipelined_allgather_gloo():
-    """step_async: ping-pong send/recv slots, collective of step t in flight during step t+1."""
+@pytest.mark.parametrize("gdt", [None, torch.float16])
+def test_dp_pipelined_allgather_gloo(gdt):
+    """step_async: ping-pong send/recv slots, collective of step t in flight during step t+1
+    (fp32 gather, and the fp16 gather option)."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_async, args=(r, world, port, 2, 6, 8, 5, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker_async, args=(r, world, port, 2, 6, 8, 5, q, gdt)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in procs)
