@@ -58,10 +58,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # one rank per GPU; more ranks than GPUs only for a gloo rehearsal of the multi-rank path
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         # bounded collectives: a rank that dies or hangs fails the job instead of stalling it
         from datetime import timedelta
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local),
+        backend = os.environ.get("SA_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI
+        dist.init_process_group(backend, rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local) if backend == "nccl" else None,
                                 timeout=timedelta(seconds=int(os.environ.get("SA_DIST_TIMEOUT", "600"))))
     else:
         torch.cuda.set_device(0)

@@ -124,7 +124,7 @@ class DataParallelStereo:
 
 
 def _all_gather_async(disp: torch.Tensor, world: int, out: torch.Tensor):
-    if disp.is_cuda:
+    if disp.is_cuda and dist.get_backend() == "nccl":
         return dist.all_gather_into_tensor(out, disp, async_op=True)
     return dist.all_gather(list(out.chunk(world, dim=0)), disp, async_op=True)
 
@@ -133,7 +133,7 @@ def all_gather_disparity(disp: torch.Tensor, world: int, out: torch.Tensor | Non
     """One all-gather of the whole shard (rank-major), RCCL/xGMI on GPU, gloo on CPU."""
     if out is None:
         out = torch.empty((world * disp.shape[0],) + tuple(disp.shape[1:]), dtype=disp.dtype, device=disp.device)
-    if disp.is_cuda:
+    if disp.is_cuda and dist.get_backend() == "nccl":
         dist.all_gather_into_tensor(out, disp.contiguous())
     else:  # gloo lacks all_gather_into_tensor on older builds
         parts = list(out.chunk(world, dim=0))
