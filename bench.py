@@ -5,7 +5,7 @@ Contract (driver): ``python bench.py --gpus N --steps K --warmup W`` (N>1 under 
 One step = every rank runs its shard of stereo pairs (``--per-gpu-batch``, default 8 => 64 pairs on
 8 GPUs, BASELINE.json config 5) through the native engine (one hipGraph per frame batch: preprocess,
 encoders, corr pyramid, 32 ConvGRU iterations, convex upsample, reprojection), fed by an H2D copy
-of the inputs from pinned host memory, then an RCCL all-gather of the disparity maps over xGMI
+of the inputs from pinned host memory (copy stream, double-buffered, overlapping the previous step), then an RCCL all-gather of the disparity maps over xGMI
 (issued async on the process group's stream, so step t's gather overlaps step t+1's frame graph).
 K steps are timed between barrier + device synchronize; rank 0 prints ONE JSON line with the
 whole-job FPS (max time over ranks).  Data: synthetic stereo pairs; weights: seeded random init of
@@ -83,13 +83,13 @@ def main():
     l_np, r_np = batch_pairs(B, H, W, seed=100 * rank)
     left_h = torch.from_numpy(l_np).pin_memory()
     right_h = torch.from_numpy(r_np).pin_memory()
-    left = torch.empty_like(left_h, device=dev)
-    right = torch.empty_like(right_h, device=dev)
+    from stereoalgorithms_amd.parallel.dp import H2DPrefetcher
+    h2d = H2DPrefetcher([left_h, right_h], dev)
 
     def step():
-        left.copy_(left_h, non_blocking=True)
-        right.copy_(right_h, non_blocking=True)
-        # pipelined: the all-gather of step t (RCCL's own stream) overlaps step t+1's frame graph
+        # every step copies its inputs H2D (copy stream, double-buffered: overlaps the previous step's
+        # frame graph); the all-gather of step t (RCCL's own stream) overlaps step t+1's frame graph
+        left, right = h2d.load([left_h, right_h])
         return dp.step_async(left, right)
 
     for _ in range(args.warmup):

@@ -146,3 +146,42 @@ def gather_to_rank0(disp: torch.Tensor, world: int, rank: int):
     parts = [torch.empty_like(disp) for _ in range(world)] if rank == 0 else None
     dist.gather(disp.contiguous(), parts, dst=0)
     return torch.cat(parts, 0) if rank == 0 else None
+
+
+class H2DPrefetcher:
+    """Double-buffered host->device input staging on a copy stream.
+
+    ``load(host_tensors)`` enqueues the pinned-host -> device copies of the next step on a side stream
+    (the copy engine) and makes the current stream wait for them, so the inputs of step t+1 travel over
+    PCIe while step t's frame graph still runs.  A slot is only overwritten once the compute stream has
+    passed the step that read it (event recorded by the next ``load``).  Every step still copies its
+    own inputs; only the overlap changes.
+    """
+
+    def __init__(self, host_tensors, device, slots: int = 2):
+        self.device = torch.device(device)
+        self.stream = torch.cuda.Stream(self.device)
+        self.slots = slots
+        self.bufs = [[torch.empty_like(h, device=self.device) for h in host_tensors] for _ in range(slots)]
+        self.freed = [None] * slots  # compute-stream event after the step that consumed the slot
+        self._i = 0
+        self._last = None
+
+    def load(self, host_tensors):
+        cs = torch.cuda.current_stream(self.device)
+        if self._last is not None:  # the previous slot is consumed by everything queued so far
+            ev = torch.cuda.Event()
+            ev.record(cs)
+            self.freed[self._last] = ev
+        slot = self._i % self.slots
+        self._i += 1
+        with torch.cuda.stream(self.stream):
+            if self.freed[slot] is not None:
+                self.stream.wait_event(self.freed[slot])
+            for d, h in zip(self.bufs[slot], host_tensors):
+                d.copy_(h, non_blocking=True)
+            ready = torch.cuda.Event()
+            ready.record(self.stream)
+        cs.wait_event(ready)
+        self._last = slot
+        return self.bufs[slot]
