@@ -118,7 +118,9 @@ def main():
     ms_step = dt / args.steps * 1e3
     fps = world * B * args.steps / dt
     extra = {}
-    if rank == 0 and not args.no_latency:
+    # batch-1 latency block: single-process runs only (N = 1 already reports it; in a multi-rank job the
+    # other ranks would sit in process-group teardown while rank 0 builds and tunes seven more engines)
+    if rank == 0 and world == 1 and not args.no_latency:
         del eng
         os.environ["SA_STAGE_TIMES"] = "1"  # per-stage device times (event nodes in the frame graph)
         for preset in ("raftstereo-sceneflow", "raftstereo-realtime", *OTHER_MS):
