@@ -1278,7 +1278,56 @@ __global__ __launch_bounds__(256) void proj_stencil_kernel(const float* __restri
     *op = accumulate ? *op + acc : acc;
   }
 }
+
+// Per-pixel tap projections of a skinny conv: each wave owns 16-row tiles of the [M x C] input, the
+// [16 x C] tap weights stay in registers as B fragments, all A fragments of a tile are loaded before
+// its K/32 chained MFMAs (v_mfma_f32_16x16x32_f16), and each 16 x 16 result is written tap-major.
+__global__ __launch_bounds__(256) void tap_proj_kernel(const f16* __restrict__ x, int xs, long M, int C,
+                                                       const f16* __restrict__ w, int ntaps,
+                                                       float* __restrict__ P, long plane) {
+  const int lane = threadIdx.x & 63;
+  const int r16 = lane & 15, kofs = (lane >> 4) * 8;
+  const int ks = C >> 5;
+  const half8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
+  half8 b[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    b[k] = k < ks ? *reinterpret_cast<const half8*>(w + (size_t)r16 * C + k * 32 + kofs) : zero8;
+  const long ntile = (M + 15) >> 4;
+  const long nw = (long)gridDim.x * 4;
+  for (long t = (long)blockIdx.x * 4 + (threadIdx.x >> 6); t < ntile; t += nw) {
+    const long row = t * 16 + r16;
+    const bool ok = row < M;
+    half8 a[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      a[k] = (ok && k < ks) ? *reinterpret_cast<const half8*>(x + row * xs + k * 32 + kofs) : zero8;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (k < ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[k], b[k], acc, 0, 0, 0);
+    if (r16 < ntaps) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const long m = t * 16 + (lane >> 4) * 4 + r;
+        if (m < M) P[(size_t)r16 * plane + m] = acc[r];
+      }
+    }
+  }
+}
 }  // namespace
+
+extern "C" int sa_tap_proj(const void* x, int xs, long M, int C, const void* w, int ntaps, float* P, long plane,
+                           hipStream_t stream) {
+  if (C % 32 || C > 256 || C < 32 || ntaps < 1 || ntaps > 16 || xs < C || xs % 8 || plane < M || M < 1)
+    return -2;
+  const long ntile = (M + 15) / 16;
+  long blocks = (ntile + 3) / 4;
+  if (blocks > 2048) blocks = 2048;  // grid-stride beyond 8 waves per CU
+  hipLaunchKernelGGL(tap_proj_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (const f16*)x, xs, M, C,
+                     (const f16*)w, ntaps, P, plane);
+  return (int)hipGetLastError();
+}
 
 extern "C" int sa_proj_stencil(const float* P, int nslices, long plane, int N, int H, int W, int kh, int kw,
                                int oc, const float* bias, float* out, int out_stride, int accumulate,

@@ -106,11 +106,18 @@ class RaftStereo : public StereoEngine {
   bool par_ = !(std::getenv("SA_RAFT_PARALLEL") && std::getenv("SA_RAFT_PARALLEL")[0] == '0');
   // SA_RAFT_PIPELINE=0: keep the per-iteration fork/join instead of the cross-iteration pipeline
   bool pipeline_ = !(std::getenv("SA_RAFT_PIPELINE") && std::getenv("SA_RAFT_PIPELINE")[0] == '0');
-  // SA_RAFT_FUSE_FH: 0 = off, 1 = on, unset = auto.  Measured in-process on MI355X
-  // (tools/ab_engine.py): batch 8 69.7 vs 70.7 ms/step fused vs unfused, batch 1 25.1 vs 24.3 ms
-  // (the projection instantiation's extra registers cost more than the skipped 256x16 conv there)
+  // SA_RAFT_FUSE_FH: 0 = off, 1 = on, unset = auto.  With conv2 as a separate tap projection
+  // (sa_tap_proj, below) the unfused head wins at every batch, measured in-process on MI355X
+  // (tools/ab_engine.py): b8 56.6 vs 58.1 ms/step unfused vs fused; b1 tap projection vs the N=1
+  // implicit GEMM 12.0 vs 12.5 ms.  Auto = fused only when the tap projection is disabled and B >= 4.
   int fuse_fh_mode_ = std::getenv("SA_RAFT_FUSE_FH") ? std::atoi(std::getenv("SA_RAFT_FUSE_FH")) : -1;
   bool fuse_fh_ = false;
+  // unfused flow-head conv2 (256 -> 1, 3x3) as tap projection (one MFMA pass over the 256-channel
+  // activation, sa_tap_proj) + 9-tap stencil instead of an N=1 implicit GEMM that re-reads the
+  // activation once per tap.  SA_RAFT_FH2_PROJ=0 restores the implicit GEMM.
+  bool fh2_proj_ = !std::getenv("SA_RAFT_FH2_PROJ") || std::atoi(std::getenv("SA_RAFT_FH2_PROJ")) != 0;
+  void* fh2_w16_ = nullptr;  // fp16 [16][256], taps 9..15 zero
+  float* tap_p_ = nullptr;   // [9][B*h0*w0]
   float* pyr_ = nullptr;
   float* flow_ = nullptr;
   int lh_[3], lw_[3];
@@ -278,6 +285,10 @@ void RaftStereo::build(WeightSource& src) {
     proj_b_ = (float*)a.alloc(4);
     HIP_CHECK(hipMemcpy(proj_w_, pw.data(), pw.size() * 4, hipMemcpyHostToDevice));
     HIP_CHECK(hipMemcpy(proj_b_, bx.data(), 4, hipMemcpyHostToDevice));
+    std::vector<_Float16> w16(16 * 256, (_Float16)0.f);
+    for (int i = 0; i < 9 * 256; ++i) w16[i] = (_Float16)pw[i];
+    fh2_w16_ = a.alloc(w16.size() * 2);
+    HIP_CHECK(hipMemcpy(fh2_w16_, w16.data(), w16.size() * 2, hipMemcpyHostToDevice));
   }
   mask2_.build(a, ws, {u + "mask.2"}, {{256, 256}}, s1, {}, 0.25f);
 
@@ -289,8 +300,9 @@ void RaftStereo::build(WeightSource& src) {
   corflo_ = make_tensor(a, Bn, h0, w0, 128);
   motion_ = make_tensor(a, Bn, h0, w0, 128);
   fh_ = make_tensor(a, Bn, h0, w0, 512);
-  fuse_fh_ = fuse_fh_mode_ > 0 || (fuse_fh_mode_ < 0 && Bn >= 4);
+  fuse_fh_ = fuse_fh_mode_ > 0 || (fuse_fh_mode_ < 0 && !fh2_proj_ && Bn >= 4);
   if (fuse_fh_) proj_p_ = (float*)a.alloc((size_t)4 * 9 * Bn * h0 * w0 * 4);  // <= 4 n-tiles of 64 channels
+  if (fh2_proj_) tap_p_ = (float*)a.alloc((size_t)9 * Bn * h0 * w0 * 4);
   mask_ = make_tensor(a, Bn, h0, w0, round_up(f * f * 9, 8));
   for (int i = 0; i + 1 < rc_.n_gru; ++i) {
     pool_[i] = make_tensor(a, Bn, lh_[i + 1], lw_[i + 1], hd);
@@ -436,9 +448,15 @@ void RaftStereo::forward(hipStream_t s) {
     if (last || !fuse_fh_) {
       if (last) fh1mask_.run(s, {net_[0]}, fh_, SA_ACT_RELU);
       else fh1_.run(s, {net_[0]}, fh_.slice_c(0, 256), SA_ACT_RELU);
-      SaConvArgs fa = fh2_.args({fh_.slice_c(0, 256)}, Tensor{flow_, Bn, h0, w0, 1, 1, DT::F32});
-      fa.epi = SA_EPI_FLOW_ACC;
-      fh2_.launch(s, fa);
+      if (fh2_proj_) {
+        const long M = (long)Bn * h0 * w0;
+        check(sa_tap_proj(fh_.ptr, fh_.stride, M, 256, fh2_w16_, 9, tap_p_, M, s), "flow-head taps");
+        check(sa_proj_stencil(tap_p_, 1, M, Bn, h0, w0, 3, 3, 1, proj_b_, flow_, 1, 1, s), "flow-head stencil");
+      } else {
+        SaConvArgs fa = fh2_.args({fh_.slice_c(0, 256)}, Tensor{flow_, Bn, h0, w0, 1, 1, DT::F32});
+        fa.epi = SA_EPI_FLOW_ACC;
+        fh2_.launch(s, fa);
+      }
       if (last) mask2_.run(s, {fh_.slice_c(256, 256)}, mask_);
     } else {
       // conv2 (256 -> 1, 3x3) fused into conv1's epilogue: per-pixel tap projections, then a

@@ -283,6 +283,11 @@ void StereoEngine::launch_frame(hipStream_t s, bool rectify) {
   } else {
     frame(stream_, rectify);
   }
+  static const bool sync_frame = [] {
+    const char* v = std::getenv("SA_SYNC_FRAME");
+    return v && v[0] == '1';
+  }();
+  if (sync_frame) HIP_CHECK(hipStreamSynchronize(stream_));  // diagnostic: host-ordered hand-off
   if (foreign) {
     HIP_CHECK(hipEventRecord(ev_out_, stream_));
     HIP_CHECK(hipStreamWaitEvent(s, ev_out_, 0));

@@ -129,6 +129,7 @@ def _declare_dev(lib):
         "sa_conv2d": (_i, [C.POINTER(SaConvArgs), _p]),
         "sa_conv2d_nslices": (_i, [C.POINTER(SaConvArgs)]),
         "sa_proj_stencil": (_i, [_p, _i, C.c_long, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p]),
+        "sa_tap_proj": (_i, [_p, _i, C.c_long, _i, _p, _i, _p, C.c_long, _p]),
         "sa_instnorm_apply": (_i, [C.POINTER(SaNormArgs), _p]),
         "sa_stats_reduce": (_i, [_p, _i, C.c_long, _p]),
         "sa_avgpool3s2": (_i, [_p, _i, _p, _i, _i, _i, _i, _i, _p]),

@@ -15,7 +15,7 @@ import torch
 from .. import _native as N
 
 __all__ = [
-    "splitk_workspace", "pack_conv_weight", "conv2d", "proj_stencil", "stats_reduce", "instnorm_apply", "avgpool3s2", "avgpool_k", "interp_bilinear",
+    "splitk_workspace", "pack_conv_weight", "conv2d", "proj_stencil", "tap_proj", "stats_reduce", "instnorm_apply", "avgpool3s2", "avgpool_k", "interp_bilinear",
     "corr1d_pyramid", "corr1d_lookup", "raft_motion_head", "convex_upsample", "preprocess", "remap_bgr", "reproject",
     "agcl_corr", "linear_attention", "layernorm", "ew", "interp_flow", "convex_upsample_c",
     "pack_conv3d_weight", "deconv_as_conv_weight", "conv3d", "dwconv3x3", "norm_corr_volume", "topk_disparity",
@@ -56,6 +56,20 @@ def proj_stencil(P, nslices, n, h, w, kh, kw, oc, bias=None, out=None, accumulat
                                     bias.data_ptr() if bias is not None else None, out.data_ptr(),
                                     _pix_stride(out), int(accumulate), _stream()), "sa_proj_stencil")
     return out
+
+
+def tap_proj(x, w):
+    """Per-pixel tap projections of a skinny conv: fp16 NHWC ``x`` [n,h,w,C] (pixel stride may exceed C),
+    ``w`` [T<=16, C] -> fp32 P [T, n*h*w] with P[t, m] = sum_c x[m, c] * w[t, c]."""
+    n, h, wd, c = x.shape
+    T = w.shape[0]
+    m = n * h * wd
+    w16 = torch.zeros(16, c, dtype=torch.float16, device=x.device)
+    w16[:T] = w.to(torch.float16)
+    P = torch.empty(T, m, dtype=torch.float32, device=x.device)
+    N.check(N.dev().sa_tap_proj(x.data_ptr(), _pix_stride(x), m, c, w16.data_ptr(), T, P.data_ptr(), m, _stream()),
+            "sa_tap_proj")
+    return P
 
 
 def raft_motion_head(pyr_buf, flow, b, h, w1, w2, convc1_w, convc1_b, convf1_w, convf1_b, levels=4, radius=4):

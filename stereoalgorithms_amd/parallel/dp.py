@@ -163,6 +163,10 @@ class H2DPrefetcher:
         self.stream = torch.cuda.Stream(self.device)
         self.slots = slots
         self.bufs = [[torch.empty_like(h, device=self.device) for h in host_tensors] for _ in range(slots)]
+        # The caching allocator hands out blocks whose previous owner may still have work pending on
+        # the allocating (current) stream; the copy stream writes them, so it first waits for that
+        # stream (without this, a recycled block can be overwritten under a not-yet-run read).
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
         self.freed = [None] * slots  # compute-stream event after the step that consumed the slot
         self._i = 0
         self._last = None
