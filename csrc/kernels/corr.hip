@@ -13,6 +13,9 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
 
+#include <cstdint>
+#include <cstdlib>
+
 #include "sa/kernels.h"
 
 namespace {
@@ -235,6 +238,120 @@ __global__ __launch_bounds__(256) void raft_motion_head_kernel(
   }
 }
 
+// MFMA form of the same head.  The block's 64 pixels become a [64 x 96] fp16 A tile in LDS (k < nc:
+// the bilinear correlation taps, wave l gathering level l; nc <= k < nc + 49: the 7x7 flow_x taps, 13
+// per wave; rest zero) and both 1x1 / 7x7 convs are ONE GEMM against a block-diagonal [96 x 128]
+// B (cols 0-63 convc1 on the corr rows, 64-127 convf1 on the flow rows), 6 fp16 B fragments per wave
+// built from the fp32 weights, 24 v_mfma_f32_16x16x32_f16 per wave.  The relu'd fp16 outputs are
+// staged through LDS for 16-B coalesced stores.  Operands are fp16 like every other conv input.
+__global__ __launch_bounds__(256) void raft_motion_head_mfma_kernel(
+    const float* __restrict__ pyr, const float* __restrict__ flow, int total, int H, int W1, int W2,
+    int levels, int radius, long lvl_off1, long lvl_off2, long lvl_off3, const float* __restrict__ wc,
+    const float* __restrict__ bc, const float* __restrict__ wf, const float* __restrict__ bf,
+    f16* __restrict__ cor, int cstride, f16* __restrict__ flo, int fstride, f16* __restrict__ fcopy,
+    int fcstride) {
+  constexpr int KP = 96, AS = KP + 8, CS = 128 + 8;
+  __shared__ __attribute__((aligned(16))) f16 a_s[64 * AS];
+  __shared__ __attribute__((aligned(16))) f16 c_s[64 * CS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int q = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int pixi = blockIdx.x * 64 + lane;
+  const long pix = pixi;
+  const bool ok = pixi < total;
+  const int ntap = 2 * radius + 1, nc = levels * ntap;
+  const int w1 = ok ? pixi % W1 : 0;
+  const int y = ok ? (pixi / W1) % H : 0;
+  const float fx = ok ? flow[pix] : 0.f;
+  f16* arow = a_s + lane * AS;
+  if (q < levels) {
+    const long off = q == 0 ? 0 : (q == 1 ? lvl_off1 : (q == 2 ? lvl_off2 : lvl_off3));
+    const int Wl = W2 >> q;
+    const float* row = pyr + off + pix * Wl;
+    const float xl = ((float)w1 + fx) / (float)(1 << q) - (float)radius;
+    const float x0f = floorf(xl);
+    const float a = xl - x0f;
+    const int x0 = (int)x0f;
+    float prev = (ok && x0 >= 0 && x0 < Wl) ? row[x0] : 0.f;
+    for (int k = 0; k < ntap; ++k) {
+      const int xi = x0 + k + 1;
+      const float nxt = (ok && xi >= 0 && xi < Wl) ? row[xi] : 0.f;
+      arow[q * ntap + k] = (f16)((1.f - a) * prev + a * nxt);
+      prev = nxt;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 13; ++i) {
+    const int t = q * 13 + i;
+    if (t < 49) {
+      const int ky = t / 7, kx = t - ky * 7;
+      const bool tok = ok && (unsigned)(y + ky - 3) < (unsigned)H && (unsigned)(w1 + kx - 3) < (unsigned)W1;
+      arow[nc + t] = (f16)(tok ? flow[pix + (long)(ky - 3) * W1 + (kx - 3)] : 0.f);
+    }
+  }
+  if (q == 3)
+    for (int k = nc + 49; k < KP; ++k) arow[k] = (f16)0.f;
+  __syncthreads();
+
+  const int r16 = lane & 15, kofs = (lane >> 4) * 8;
+  half8 bfr[2][3];
+  float bias[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = 32 * q + 16 * j + r16;
+    bias[j] = n < 64 ? bc[n] : bf[n - 64];
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = ks * 32 + kofs + e;
+        float v = 0.f;
+        if (n < 64) {
+          if (k < nc) v = wc[k * 64 + n];
+        } else if (k >= nc && k < nc + 49) {
+          v = wf[(k - nc) * 64 + (n - 64)];
+        }
+        bfr[j][ks][e] = (f16)v;
+      }
+  }
+  floatx4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const half8 a = *reinterpret_cast<const half8*>(a_s + (16 * i + r16) * AS + ks * 32 + kofs);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bfr[j][ks], acc[i][j], 0, 0, 0);
+    }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * i + (lane >> 4) * 4 + r;
+        const int col = 32 * q + 16 * j + r16;
+        c_s[row * CS + col] = (f16)fmaxf(acc[i][j][r] + bias[j], 0.f);
+      }
+  __syncthreads();
+  for (int c = tid; c < 64 * 16; c += 256) {
+    const int row = c >> 4, ch = (c & 15) * 8;
+    const int p = blockIdx.x * 64 + row;
+    if (p < total) {
+      const half8 v = *reinterpret_cast<const half8*>(c_s + row * CS + ch);
+      if (ch < 64) *reinterpret_cast<half8*>(cor + (long)p * cstride + ch) = v;
+      else *reinterpret_cast<half8*>(flo + (long)p * fstride + (ch - 64)) = v;
+    }
+  }
+  if (q == 0 && ok && fcopy) {
+    fcopy[pix * fcstride] = (f16)fx;
+    fcopy[pix * fcstride + 1] = (f16)0.f;
+  }
+}
+
 }  // namespace
 
 extern "C" int sa_corr1d_pyramid(const void* f1, const void* f2, int stride, int B, int H, int W1,
@@ -294,8 +411,12 @@ extern "C" int sa_raft_motion_head(const float* pyr, const float* flow, int B, i
   }
   if ((long)B * H * W1 >= (1L << 31) - 64) return -2;
   const int total = B * H * W1;
-  hipLaunchKernelGGL(raft_motion_head_kernel, dim3((total + 63) / 64), dim3(256), 0, stream, pyr, flow, total, H, W1,
-                     W2, levels, radius, off[1], off[2], off[3], wc, bc, wf, bf, (f16*)cor, cstride, (f16*)flo,
-                     fstride, (f16*)fcopy, fcstride);
+  // SA_MH_VALU=1: the fp32 VALU kernel (A/B and numerics reference); default the MFMA kernel
+  const char* ve = std::getenv("SA_MH_VALU");  // read per launch (launches are captured once per engine)
+  const bool valu = ve && ve[0] == '1';
+  if (((uintptr_t)cor | (uintptr_t)flo) & 15) return -2;
+  hipLaunchKernelGGL(valu ? raft_motion_head_kernel : raft_motion_head_mfma_kernel, dim3((total + 63) / 64),
+                     dim3(256), 0, stream, pyr, flow, total, H, W1, W2, levels, radius, off[1], off[2], off[3], wc,
+                     bc, wf, bf, (f16*)cor, cstride, (f16*)flo, fstride, (f16*)fcopy, fcstride);
   return (int)hipGetLastError();
 }
