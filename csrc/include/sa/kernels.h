@@ -114,10 +114,11 @@ int sa_conv2d_nslices(const SaConvArgs* a);
 int sa_proj_stencil(const float* P, int nslices, long plane, int N, int H, int W, int kh, int kw,
                     int oc, const float* bias, float* out, int out_stride, int accumulate,
                     hipStream_t stream);
-// Skinny-conv front half (a conv with <= 16 output taps x channels, e.g. RAFT's flow-head conv2
-// 256 -> 1, 3x3): P[t][m] = sum_c x[m][c] * w[t][c] for t < ntaps, as one MFMA GEMM that reads the
-// fp16 input exactly once (the implicit-GEMM conv re-reads it per tap).  x: fp16, pixel stride xs,
-// C % 32 == 0, C <= 256; w: fp16 [16][C] (taps >= ntaps zero).  sa_proj_stencil() then forms the conv.
+// Skinny-conv front half (a conv with <= 32 output taps x channels, e.g. the RAFT / CREStereo flow-head
+// conv2 256 -> 1 or 2, 3x3): P[t][m] = sum_c x[m][c] * w[t][c] for t < ntaps, as one MFMA GEMM that reads
+// the fp16 input exactly once (the implicit-GEMM conv re-reads it per tap).  x: fp16, pixel stride xs,
+// C % 32 == 0, C <= 256; w: fp16 [16][C] (ntaps <= 16) or [32][C], taps >= ntaps zero.
+// sa_proj_stencil() then forms the conv (tap index (ky*kw+kx)*oc + o).
 int sa_tap_proj(const void* x, int xs, long M, int C, const void* w, int ntaps, float* P, long plane,
                 hipStream_t stream);
 

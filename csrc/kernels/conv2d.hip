@@ -1280,8 +1280,9 @@ __global__ __launch_bounds__(256) void proj_stencil_kernel(const float* __restri
 }
 
 // Per-pixel tap projections of a skinny conv: each wave owns 16-row tiles of the [M x C] input, the
-// [16 x C] tap weights stay in registers as B fragments, all A fragments of a tile are loaded before
-// its K/32 chained MFMAs (v_mfma_f32_16x16x32_f16), and each 16 x 16 result is written tap-major.
+// [16*NT x C] tap weights stay in registers as B fragments (NT 16-column tiles), all A fragments of a
+// tile are loaded before its chained MFMAs (v_mfma_f32_16x16x32_f16), and results are written tap-major.
+template <int NT>
 __global__ __launch_bounds__(256) void tap_proj_kernel(const f16* __restrict__ x, int xs, long M, int C,
                                                        const f16* __restrict__ w, int ntaps,
                                                        float* __restrict__ P, long plane) {
@@ -1289,10 +1290,12 @@ __global__ __launch_bounds__(256) void tap_proj_kernel(const f16* __restrict__ x
   const int r16 = lane & 15, kofs = (lane >> 4) * 8;
   const int ks = C >> 5;
   const half8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
-  half8 b[8];
+  half8 b[NT][8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k)
-    b[k] = k < ks ? *reinterpret_cast<const half8*>(w + (size_t)r16 * C + k * 32 + kofs) : zero8;
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      b[j][k] = k < ks ? *reinterpret_cast<const half8*>(w + (size_t)(16 * j + r16) * C + k * 32 + kofs) : zero8;
   const long ntile = (M + 15) >> 4;
   const long nw = (long)gridDim.x * 4;
   for (long t = (long)blockIdx.x * 4 + (threadIdx.x >> 6); t < ntile; t += nw) {
@@ -1302,15 +1305,19 @@ __global__ __launch_bounds__(256) void tap_proj_kernel(const f16* __restrict__ x
 #pragma unroll
     for (int k = 0; k < 8; ++k)
       a[k] = (ok && k < ks) ? *reinterpret_cast<const half8*>(x + row * xs + k * 32 + kofs) : zero8;
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (k < ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[k], b[k], acc, 0, 0, 0);
-    if (r16 < ntaps) {
+    for (int j = 0; j < NT; ++j) {
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const long m = t * 16 + (lane >> 4) * 4 + r;
-        if (m < M) P[(size_t)r16 * plane + m] = acc[r];
+      for (int k = 0; k < 8; ++k)
+        if (k < ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[k], b[j][k], acc, 0, 0, 0);
+      const int tap = 16 * j + r16;
+      if (tap < ntaps) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const long m = t * 16 + (lane >> 4) * 4 + r;
+          if (m < M) P[(size_t)tap * plane + m] = acc[r];
+        }
       }
     }
   }
@@ -1319,13 +1326,17 @@ __global__ __launch_bounds__(256) void tap_proj_kernel(const f16* __restrict__ x
 
 extern "C" int sa_tap_proj(const void* x, int xs, long M, int C, const void* w, int ntaps, float* P, long plane,
                            hipStream_t stream) {
-  if (C % 32 || C > 256 || C < 32 || ntaps < 1 || ntaps > 16 || xs < C || xs % 8 || plane < M || M < 1)
+  if (C % 32 || C > 256 || C < 32 || ntaps < 1 || ntaps > 32 || xs < C || xs % 8 || plane < M || M < 1)
     return -2;
   const long ntile = (M + 15) / 16;
   long blocks = (ntile + 3) / 4;
   if (blocks > 2048) blocks = 2048;  // grid-stride beyond 8 waves per CU
-  hipLaunchKernelGGL(tap_proj_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (const f16*)x, xs, M, C,
-                     (const f16*)w, ntaps, P, plane);
+  if (ntaps <= 16)
+    hipLaunchKernelGGL(tap_proj_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, stream, (const f16*)x, xs, M, C,
+                       (const f16*)w, ntaps, P, plane);
+  else
+    hipLaunchKernelGGL(tap_proj_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, stream, (const f16*)x, xs, M, C,
+                       (const f16*)w, ntaps, P, plane);
   return (int)hipGetLastError();
 }
 

@@ -141,6 +141,11 @@ class CreStereo : public StereoEngine {
   AttnLayer self_, cross_;
   ConvLayer convc1_, convc2_, convf1_, convf2_, mconv_, zr_[2], q_[2], fh1_, fh1mask_, fh2_, mask2_;
   Level lv_[3];  // 0: 1/4, 1: 1/8, 2: 1/16
+  // SA_CRE_FH2_PROJ=0: flow-head conv2 as the N=2 implicit GEMM instead of tap projection + stencil
+  bool fh2_proj_ = !std::getenv("SA_CRE_FH2_PROJ") || std::atoi(std::getenv("SA_CRE_FH2_PROJ")) != 0;
+  void* fh2_w16_ = nullptr;
+  float* fh2_b_ = nullptr;
+  float* tap_p_ = nullptr;
   float *flowup4_ = nullptr, *flowup2_ = nullptr, *pe_ = nullptr;
 };
 
@@ -218,6 +223,21 @@ void CreStereo::build(WeightSource& src) {
   fh1_.build(a, ws, {u + "flow_head.conv1"}, {{128, 128}}, s3);
   fh1mask_.build(a, ws, {u + "flow_head.conv1", u + "mask.0"}, {{128, 128}}, s3);
   fh2_.build(a, ws, {u + "flow_head.conv2"}, {{256, 256}}, s3);
+  {
+    // flow-head conv2 (256 -> 2, 3x3) as an MFMA tap projection + stencil (sa_tap_proj): tap row
+    // (ky*3+kx)*2 + o of a [32][256] fp16 matrix, rows 18..31 zero
+    const HostTensor& w2 = ws.get(u + "flow_head.conv2.weight");  // [2][256][3][3]
+    const HostTensor& b2 = ws.get(u + "flow_head.conv2.bias");
+    std::vector<_Float16> w16(32 * 256, (_Float16)0.f);
+    for (int o = 0; o < 2; ++o)
+      for (int c = 0; c < 256; ++c)
+        for (int t = 0; t < 9; ++t) w16[(size_t)(t * 2 + o) * 256 + c] = (_Float16)w2.data[((size_t)o * 256 + c) * 9 + t];
+    fh2_w16_ = a.alloc(w16.size() * 2);
+    HIP_CHECK(hipMemcpy(fh2_w16_, w16.data(), w16.size() * 2, hipMemcpyHostToDevice));
+    fh2_b_ = (float*)a.alloc(2 * 4);
+    HIP_CHECK(hipMemcpy(fh2_b_, b2.data.data(), 2 * 4, hipMemcpyHostToDevice));
+    tap_p_ = (float*)a.alloc((size_t)18 * B * h4 * w4 * 4);  // largest level (1/4)
+  }
   mask2_.build(a, ws, {u + "mask.2"}, {{256, 256}}, s1, {}, 0.25f);
 
   lv_[0].build(a, B, h4, w4);
@@ -282,9 +302,15 @@ void CreStereo::update(hipStream_t s, Level& L, const Tensor& f1, const Tensor& 
   }
   if (want_mask) fh1mask_.run(s, {L.net}, L.fh, SA_ACT_RELU);
   else fh1_.run(s, {L.net}, L.fh.slice_c(0, 256), SA_ACT_RELU);
-  SaConvArgs fa = fh2_.args({L.fh.slice_c(0, 256)}, Tensor{L.flow, B, L.h, L.w, 2, 2, DT::F32});
-  fa.epi = SA_EPI_FLOW_ACC;
-  fh2_.launch(s, fa);
+  if (fh2_proj_) {
+    const long M = (long)B * L.h * L.w;
+    check(sa_tap_proj(L.fh.ptr, L.fh.stride, M, 256, fh2_w16_, 18, tap_p_, M, s), "flow-head taps");
+    check(sa_proj_stencil(tap_p_, 1, M, B, L.h, L.w, 3, 3, 2, fh2_b_, L.flow, 2, 1, s), "flow-head stencil");
+  } else {
+    SaConvArgs fa = fh2_.args({L.fh.slice_c(0, 256)}, Tensor{L.flow, B, L.h, L.w, 2, 2, DT::F32});
+    fa.epi = SA_EPI_FLOW_ACC;
+    fh2_.launch(s, fa);
+  }
   if (want_mask) mask2_.run(s, {L.fh.slice_c(256, 256)}, L.mask);
 }
 

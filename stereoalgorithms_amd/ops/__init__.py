@@ -60,11 +60,11 @@ def proj_stencil(P, nslices, n, h, w, kh, kw, oc, bias=None, out=None, accumulat
 
 def tap_proj(x, w):
     """Per-pixel tap projections of a skinny conv: fp16 NHWC ``x`` [n,h,w,C] (pixel stride may exceed C),
-    ``w`` [T<=16, C] -> fp32 P [T, n*h*w] with P[t, m] = sum_c x[m, c] * w[t, c]."""
+    ``w`` [T<=32, C] -> fp32 P [T, n*h*w] with P[t, m] = sum_c x[m, c] * w[t, c]."""
     n, h, wd, c = x.shape
     T = w.shape[0]
     m = n * h * wd
-    w16 = torch.zeros(16, c, dtype=torch.float16, device=x.device)
+    w16 = torch.zeros(16 if T <= 16 else 32, c, dtype=torch.float16, device=x.device)
     w16[:T] = w.to(torch.float16)
     P = torch.empty(T, m, dtype=torch.float32, device=x.device)
     N.check(N.dev().sa_tap_proj(x.data_ptr(), _pix_stride(x), m, c, w16.data_ptr(), T, P.data_ptr(), m, _stream()),

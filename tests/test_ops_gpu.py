@@ -225,21 +225,23 @@ def test_conv2d_projection_epilogue_flow_head(n, hw, cfg, oc):
     assert rel_err(out - flow0, ref - flow0) < 3e-3
 
 
-@pytest.mark.parametrize("n,hw,c,xs", [(2, (24, 40), 256, 512), (1, (13, 21), 256, 256), (1, (7, 9), 96, 104)])
-def test_tap_proj_skinny_conv(n, hw, c, xs):
-    """Unfused RAFT flow-head conv2 (3x3 c->1): MFMA tap projection (one pass over the fp16 input, strided
-    pixels) + stencil == F.conv2d in fp32 on the same fp16-rounded operands, added to the running flow."""
+@pytest.mark.parametrize("n,hw,c,xs,oc", [(2, (24, 40), 256, 512, 1), (1, (13, 21), 256, 256, 1),
+                                            (1, (7, 9), 96, 104, 1), (2, (11, 30), 256, 512, 2)])
+def test_tap_proj_skinny_conv(n, hw, c, xs, oc):
+    """Flow-head conv2 (3x3 c->oc; RAFT oc 1, CREStereo oc 2 = 18 taps, two MFMA column tiles): MFMA tap
+    projection (one pass over the fp16 input, strided pixels) + stencil == F.conv2d in fp32 on the same
+    fp16-rounded operands, added to the running flow."""
     O = ops()
     torch.manual_seed(5)
     base = torch.randn(n, *hw, xs, device=DEV).half()
     x = base[..., :c]
-    w2 = torch.randn(1, c, 3, 3, device=DEV) / math.sqrt(c * 9)
-    b2 = torch.randn(1, device=DEV) * 0.1
-    taps = w2[0].permute(1, 2, 0).reshape(9, c)  # [(ky*3+kx)][c]
+    w2 = torch.randn(oc, c, 3, 3, device=DEV) / math.sqrt(c * 9)
+    b2 = torch.randn(oc, device=DEV) * 0.1
+    taps = w2.permute(2, 3, 0, 1).reshape(9 * oc, c)  # [(ky*3+kx)*oc + o][c]
     P = O.tap_proj(x, taps)
-    flow0 = torch.randn(n, *hw, 1, device=DEV)
+    flow0 = torch.randn(n, *hw, oc, device=DEV)
     out = flow0.clone()
-    O.proj_stencil(P, 1, n, hw[0], hw[1], 3, 3, 1, bias=b2.contiguous(), out=out, accumulate=True)
+    O.proj_stencil(P, 1, n, hw[0], hw[1], 3, 3, oc, bias=b2.contiguous(), out=out, accumulate=True)
     torch.cuda.synchronize()
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w2.half().float(), b2, padding=1).permute(0, 2, 3, 1)
     assert rel_err(out - flow0, ref) < 2e-3
