@@ -139,6 +139,8 @@ int sa_instnorm_apply(const SaNormArgs* a, hipStream_t stream);
 int sa_stats_reduce(sa_stat_t* stats, int slots, long count, hipStream_t stream);
 // buf[idx] = wall_clock64() once everything queued before on `stream` has finished
 int sa_stamp(unsigned long long* buf, int idx, hipStream_t stream);
+// zero `bytes` (multiple of 16, 16-B aligned) with vector stores; graph-capturable
+int sa_zero(void* p, size_t bytes, hipStream_t stream);
 
 // F.avg_pool2d(x, 3, stride=2, padding=1) (count_include_pad) on NHWC fp16
 int sa_avgpool3s2(const void* x, int x_stride, void* out, int out_stride, int N, int H, int W,

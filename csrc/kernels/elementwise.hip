@@ -7,11 +7,20 @@
 // pool2x = F.avg_pool2d(x, 3, 2, 1) and interp = F.interpolate(bilinear, align_corners=True)
 // between the multi-level ConvGRUs of RAFT-Stereo.
 #include <hip/hip_runtime.h>
+
+#include <cstdint>
 #include <hip/hip_fp16.h>
 
 #include "sa/kernels.h"
 
 namespace {
+
+// zero fill with 16-B vector stores (a captured hipMemsetAsync of a few MB becomes a chain of small
+// runtime fill kernels: ~20 us each, 18 per RAFT-SF b8 frame for the instance-norm statistics pool)
+__global__ __launch_bounds__(256) void zero16_kernel(uint4* __restrict__ p, long n16) {
+  const uint4 z = {0u, 0u, 0u, 0u};
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long)gridDim.x * 256) p[i] = z;
+}
 typedef _Float16 f16;
 typedef f16 half8 __attribute__((ext_vector_type(8)));
 
@@ -205,6 +214,16 @@ inline int grid_for(long work) {
 }
 
 }  // namespace
+
+extern "C" int sa_zero(void* p, size_t bytes, hipStream_t stream) {
+  if (((uintptr_t)p & 15) || (bytes & 15)) return -2;
+  const long n16 = (long)(bytes >> 4);
+  if (n16 == 0) return 0;
+  long blocks = (n16 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(zero16_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (uint4*)p, n16);
+  return (int)hipGetLastError();
+}
 
 extern "C" int sa_instnorm_apply(const SaNormArgs* a, hipStream_t stream) {
   if (a->C % 8) return -2;
