@@ -115,12 +115,15 @@ __global__ void avgpool3s2_kernel(const f16* __restrict__ x, int xs, f16* __rest
   const long total = (long)N * Ho * Wo * C8;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C8) * 8;
-    long p = i / C8;
-    const int ow = (int)(p % Wo);
-    p /= Wo;
-    const int oh = (int)(p % Ho);
-    const int n = (int)(p / Ho);
+    // 32-bit index decomposition (total < 2^31, host-checked): 64-bit div/mod is a long emulated
+    // sequence per element that outweighed the 8-channel arithmetic
+    const unsigned ii = (unsigned)i;
+    const int c = (int)(ii % (unsigned)C8) * 8;
+    unsigned p = ii / (unsigned)C8;
+    const int ow = (int)(p % (unsigned)Wo);
+    p /= (unsigned)Wo;
+    const int oh = (int)(p % (unsigned)Ho);
+    const int n = (int)(p / (unsigned)Ho);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int dy = -1; dy <= 1; ++dy) {
       int ih = oh * 2 + dy;
@@ -147,12 +150,15 @@ __global__ void avgpoolk_kernel(const f16* __restrict__ x, int xs, f16* __restri
   const float inv = 1.f / (float)(k * k);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C8) * 8;
-    long p = i / C8;
-    const int ow = (int)(p % Wo);
-    p /= Wo;
-    const int oh = (int)(p % Ho);
-    const int n = (int)(p / Ho);
+    // 32-bit index decomposition (total < 2^31, host-checked): 64-bit div/mod is a long emulated
+    // sequence per element that outweighed the 8-channel arithmetic
+    const unsigned ii = (unsigned)i;
+    const int c = (int)(ii % (unsigned)C8) * 8;
+    unsigned p = ii / (unsigned)C8;
+    const int ow = (int)(p % (unsigned)Wo);
+    p /= (unsigned)Wo;
+    const int oh = (int)(p % (unsigned)Ho);
+    const int n = (int)(p / (unsigned)Ho);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int dy = 0; dy < k; ++dy)
       for (int dx = 0; dx < k; ++dx) {
@@ -179,12 +185,15 @@ __global__ void interp_kernel(const f16* __restrict__ x, int xs, f16* __restrict
   const long total = (long)N * Ho * Wo * C8;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C8) * 8;
-    long p = i / C8;
-    const int ow = (int)(p % Wo);
-    p /= Wo;
-    const int oh = (int)(p % Ho);
-    const int n = (int)(p / Ho);
+    // 32-bit index decomposition (total < 2^31, host-checked): 64-bit div/mod is a long emulated
+    // sequence per element that outweighed the 8-channel arithmetic
+    const unsigned ii = (unsigned)i;
+    const int c = (int)(ii % (unsigned)C8) * 8;
+    unsigned p = ii / (unsigned)C8;
+    const int ow = (int)(p % (unsigned)Wo);
+    p /= (unsigned)Wo;
+    const int oh = (int)(p % (unsigned)Ho);
+    const int n = (int)(p / (unsigned)Ho);
     float sy = src_index(oh, H, Ho, ac), sx = src_index(ow, W, Wo, ac);
     int y0 = (int)floorf(sy), x0 = (int)floorf(sx);
     y0 = y0 > H - 1 ? H - 1 : y0;
@@ -242,6 +251,7 @@ extern "C" int sa_avgpool3s2(const void* x, int xs, void* out, int os, int N, in
   if (C % 8) return -2;
   int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   long work = (long)N * Ho * Wo * (C / 8);
+  if (work >= (1L << 31)) return -2;  // 32-bit index math in the kernel
   hipLaunchKernelGGL(avgpool3s2_kernel, dim3(grid_for(work)), dim3(256), 0, stream,
                      (const f16*)x, xs, (f16*)out, os, N, H, W, C, Ho, Wo);
   return (int)hipGetLastError();
@@ -252,6 +262,7 @@ extern "C" int sa_avgpool_k(const void* x, int xs, void* out, int os, int N, int
   if (C % 8) return -2;
   int Ho = H / k, Wo = W / k;
   long work = (long)N * Ho * Wo * (C / 8);
+  if (work >= (1L << 31)) return -2;  // 32-bit index math in the kernel
   hipLaunchKernelGGL(avgpoolk_kernel, dim3(grid_for(work)), dim3(256), 0, stream, (const f16*)x,
                      xs, (f16*)out, os, N, H, W, C, Ho, Wo, k);
   return (int)hipGetLastError();
@@ -261,6 +272,7 @@ extern "C" int sa_interp_bilinear(const void* x, int xs, void* out, int os, int 
                                   int C, int Ho, int Wo, int ac, float mul, hipStream_t stream) {
   if (C % 8) return -2;
   long work = (long)N * Ho * Wo * (C / 8);
+  if (work >= (1L << 31)) return -2;  // 32-bit index math in the kernel
   hipLaunchKernelGGL(interp_kernel, dim3(grid_for(work)), dim3(256), 0, stream, (const f16*)x, xs,
                      (f16*)out, os, N, H, W, C, Ho, Wo, ac, mul);
   return (int)hipGetLastError();
