@@ -1,25 +1,41 @@
 #!/usr/bin/env python3
 """Flagship benchmark: RAFT-Stereo sceneflow 480x640 (32 GRU iterations) throughput on N MI355X.
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W`` (N>1 under torch.distributed.run).
-One step = every rank runs its shard of stereo pairs (``--per-gpu-batch``, default 8 => 64 pairs on
-8 GPUs, BASELINE.json config 5) through the native engine (one hipGraph per frame batch: preprocess,
-encoders, corr pyramid, 32 ConvGRU iterations, convex upsample, reprojection), fed by an H2D copy
-of the inputs from pinned host memory (copy stream, double-buffered, overlapping the previous step), then an RCCL all-gather of the disparity maps over xGMI
-(issued async on the process group's stream, so step t's gather overlaps step t+1's frame graph).
-K steps are timed between barrier + device synchronize; rank 0 prints ONE JSON line with the
-whole-job FPS (max time over ranks).  Data: synthetic stereo pairs; weights: seeded random init of
-the upstream architecture.
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``.  N > 1 works two ways:
 
-Also reported (rank 0, extra fields): batch-1 latency in the reference's timed region (pinned copy,
-H2D, network, reprojection, D2H of disparity + point cloud; RAFTStereo/src/TRTRAFTStereo.cpp:119-146)
-for the sceneflow and realtime presets.
+* under ``torch.distributed.run`` (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set by the launcher):
+  ``--gpus`` must equal WORLD_SIZE, otherwise the run fails loudly;
+* directly (``python bench.py --gpus 8``): the parent process — which never touches the GPU — spawns N
+  fresh rank processes with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set,
+  forwards their output and exits with the first failing rank's code.
+
+Under RCCL (backend ``nccl``) rank r owns GPU LOCAL_RANK; asking for more ranks than visible GPUs exits
+non-zero (no silent oversubscription).  ``SA_DIST_BACKEND=gloo`` is the rehearsal mode (ranks may share a
+GPU, or run on the CPU with ``--device cpu``, which swaps the native engine for the PyTorch oracle so
+the launcher / sharding / gather plumbing is testable without a GPU — that mode is labelled in the JSON
+and is never a performance number).
+
+One step = every rank runs its shard of stereo pairs (``--per-gpu-batch``, default 8 => 64 pairs on 8 GPUs,
+BASELINE.json config 5) through the native engine (one hipGraph per frame batch: preprocess, encoders, corr
+pyramid, 32 ConvGRU iterations, convex upsample), fed by an H2D copy of the inputs from pinned host memory
+(copy stream, double-buffered, overlapping the previous step), then an RCCL all-gather of the disparity maps
+over xGMI (issued async on the process group's stream, so step t's gather overlaps step t+1's frame graph).
+K steps are timed between barrier + device synchronize; rank 0 prints ONE JSON line with the whole-job FPS
+(max time over ranks).  Data: synthetic stereo pairs; weights: seeded random init of the upstream
+architecture.
+
+Also reported (rank 0, extra fields): the all-gather alone (ms per step, measured after the timed region),
+the rank -> device map, the engine's device footprint, and — single-process runs only — batch-1 latency in
+the reference's timed region (pinned copy, H2D, network, reprojection, D2H of disparity + point cloud;
+RAFTStereo/src/TRTRAFTStereo.cpp:119-146) for every model preset.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,9 +48,10 @@ BASELINE_MS = {"raftstereo-sceneflow": 38.0, "raftstereo-realtime": 11.0}  # RTX
 # the other model families' published RTX 3090 numbers (README_en.md:192-194,244-246,293-295)
 OTHER_MS = {"crestereo-iter2": 12.0, "crestereo-iter5": 23.0, "crestereo-iter10": 42.0, "hitnet-d400": 15.0,
             "fastacvnet-plus": 12.0}
+ITERS = {"raftstereo-sceneflow": 32, "raftstereo-realtime": 7}
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
@@ -43,86 +60,216 @@ def parse():
     p.add_argument("--per-gpu-batch", type=int, default=8)
     p.add_argument("--height", type=int, default=480)
     p.add_argument("--width", type=int, default=640)
+    p.add_argument("--iters", type=int, default=-1, help="override GRU iterations (tests only)")
     p.add_argument("--latency-frames", type=int, default=20)
     p.add_argument("--no-latency", action="store_true")
-    return p.parse_args()
+    p.add_argument("--device", choices=("gpu", "cpu"), default="gpu",
+                   help="cpu = PyTorch-oracle rehearsal of the launcher/DP plumbing (gloo only, not a benchmark)")
+    return p.parse_args(argv)
 
 
-def main():
-    args = parse()
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(args, argv) -> int:
+    """Parent of a self-launched N-rank job: spawn, forward output, propagate failure.
+
+    Runs before anything initialises a GPU in this process (torch.cuda.device_count() does not on this
+    image), so the children are fresh processes, never an exec of a GPU-initialised one."""
+    n = args.gpus
+    backend = os.environ.get("SA_DIST_BACKEND", "nccl")
+    if backend == "nccl" and args.device == "gpu":
+        import torch
+        ndev = torch.cuda.device_count()
+        if n > ndev:
+            print(f"bench.py: --gpus {n} but only {ndev} GPU(s) visible; RCCL needs one GPU per rank "
+                  f"(SA_DIST_BACKEND=gloo to rehearse more ranks)", file=sys.stderr, flush=True)
+            return 2
+    port = int(os.environ.get("MASTER_PORT") or _free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=str(port),
+                   SA_BENCH_CHILD="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            code = p.poll()
+            if code is None:
+                continue
+            alive.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                for q in alive:  # one rank failed: the collectives of the others can never complete
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+class OracleEngine:
+    """CPU stand-in with the native engine's ``run`` contract (u8 BGR [B,H,W,3] -> disparity [B,H,W]),
+    backed by the fp32 PyTorch oracle.  Used only by ``--device cpu`` rehearsals of the launcher."""
+
+    def __init__(self, preset, h, w, batch, iters, seed=0):
+        from stereoalgorithms_amd.models import raft_stereo as R
+        self.model = R.build(preset, seed)
+        self.batch, self.height, self.width = batch, h, w
+        self.iters = iters if iters > 0 else R.PRESETS[preset].valid_iters
+        self.device_bytes = 0
+
+    def run(self, left, right, out=None):
+        import torch
+        with torch.no_grad():
+            l = left.flip(-1).permute(0, 3, 1, 2).float()
+            r = right.flip(-1).permute(0, 3, 1, 2).float()
+            _, up = self.model(l, r, iters=self.iters)
+            d = -up[:, 0]
+        if out is not None:
+            return out.copy_(d)
+        return d.contiguous()
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return launch(args, argv)
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per requested GPU",
+              file=sys.stderr, flush=True)
+        return 2
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("SA_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI
+    cpu = args.device == "cpu"
+    if cpu and world > 1 and backend != "gloo":
+        print("bench.py: --device cpu needs SA_DIST_BACKEND=gloo", file=sys.stderr, flush=True)
+        return 2
+
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        # one rank per GPU; more ranks than GPUs only for a gloo rehearsal of the multi-rank path
-        local = local % max(1, torch.cuda.device_count())
-        torch.cuda.set_device(local)
-        # bounded collectives: a rank that dies or hangs fails the job instead of stalling it
-        from datetime import timedelta
-        backend = os.environ.get("SA_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI
-        dist.init_process_group(backend, rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local) if backend == "nccl" else None,
-                                timeout=timedelta(seconds=int(os.environ.get("SA_DIST_TIMEOUT", "600"))))
+    if cpu:
+        dev = torch.device("cpu")
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // world))
     else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+        ndev = torch.cuda.device_count()
+        if backend == "nccl" and local >= ndev:
+            print(f"bench.py: rank {rank} has LOCAL_RANK {local} but only {ndev} GPU(s) are visible",
+                  file=sys.stderr, flush=True)
+            return 2
+        # gloo rehearsal only: more ranks than GPUs share devices round-robin
+        local_dev = local if backend == "nccl" else local % max(1, ndev)
+        torch.cuda.set_device(local_dev)
+        dev = torch.device("cuda", local_dev)
+    if world > 1:
+        from datetime import timedelta
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # bounded collectives: a rank that dies or hangs fails the job instead of stalling it
+        kw = dict(device_id=dev) if (backend == "nccl" and not cpu) else {}
+        dist.init_process_group(backend, rank=rank, world_size=world,
+                                timeout=timedelta(seconds=int(os.environ.get("SA_DIST_TIMEOUT", "600"))), **kw)
+        assert dist.get_world_size() == world and dist.get_rank() == rank
 
-    from stereoalgorithms_amd.models.engine import NativeStereoEngine
-    from stereoalgorithms_amd.parallel.dp import DataParallelStereo
+    from stereoalgorithms_amd.parallel.dp import DataParallelStereo, H2DPrefetcher
     from stereoalgorithms_amd.utils.synthetic import batch_pairs
 
     B, H, W = args.per_gpu_batch, args.height, args.width
     Q = np.array([[1, 0, 0, -W / 2], [0, 1, 0, -H / 2], [0, 0, 0, 500.0], [0, 0, 1 / 60.0, 0]], np.float32)
-    eng = NativeStereoEngine(args.model, None, H, W, batch=B, device=dev.index, seed=0)
-    eng.set_Q(Q)
+    if cpu:
+        eng = OracleEngine(args.model, H, W, B, args.iters, seed=0)
+    else:
+        from stereoalgorithms_amd.models.engine import NativeStereoEngine
+        eng = NativeStereoEngine(args.model, None, H, W, batch=B, iters=args.iters, device=dev.index, seed=0)
+        eng.set_Q(Q)
     dp = DataParallelStereo(eng, world_size=world, rank=rank)
     l_np, r_np = batch_pairs(B, H, W, seed=100 * rank)
-    left_h = torch.from_numpy(l_np).pin_memory()
-    right_h = torch.from_numpy(r_np).pin_memory()
-    from stereoalgorithms_amd.parallel.dp import H2DPrefetcher
-    h2d = H2DPrefetcher([left_h, right_h], dev)
+    left_h, right_h = torch.from_numpy(l_np), torch.from_numpy(r_np)
+    if cpu:
+        def step():
+            return dp.step_async(left_h, right_h)
 
-    def step():
-        # every step copies its inputs H2D (copy stream, double-buffered: overlaps the previous step's
-        # frame graph); the all-gather of step t (RCCL's own stream) overlaps step t+1's frame graph
-        left, right = h2d.load([left_h, right_h])
-        return dp.step_async(left, right)
+        def sync():
+            pass
+    else:
+        left_h, right_h = left_h.pin_memory(), right_h.pin_memory()
+        h2d = H2DPrefetcher([left_h, right_h], dev)
+
+        def step():
+            # every step copies its inputs H2D (copy stream, double-buffered: overlaps the previous step's
+            # frame graph); the all-gather of step t (RCCL's own stream) overlaps step t+1's frame graph
+            left, right = h2d.load([left_h, right_h])
+            return dp.step_async(left, right)
+
+        def sync():
+            torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         step()
     dp.flush()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
+    pending = None
     for _ in range(args.steps):
         pending = step()
     out = pending.wait()
     dp.flush()  # every step's collective is complete inside the timed region
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     dt = time.perf_counter() - t0
+    gather_ms = None
+    ranks = [{"rank": rank, "device": str(dev), "host": socket.gethostname()}]
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
+        # the all-gather alone, outside the timed region (same message as one step's gather)
+        send = out.new_empty((B, H, W))
+        recv = out.new_empty((world * B, H, W))
+        from stereoalgorithms_amd.parallel.dp import all_gather_disparity
+        for _ in range(2):
+            all_gather_disparity(send, world, recv)
+        sync()
+        dist.barrier()
+        reps = 10
+        tg = time.perf_counter()
+        for _ in range(reps):
+            all_gather_disparity(send, world, recv)
+        sync()
+        g = torch.tensor([(time.perf_counter() - tg) / reps * 1e3], device=dev, dtype=torch.float64)
+        dist.all_reduce(g, op=dist.ReduceOp.MAX)
+        gather_ms = round(g.item(), 4)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, ranks[0])
+        ranks = gathered
     assert out.shape == (world * B, H, W) and torch.isfinite(out).all()
 
     ms_step = dt / args.steps * 1e3
     fps = world * B * args.steps / dt
     extra = {}
-    # batch-1 latency block: single-process runs only (N = 1 already reports it; in a multi-rank job the
-    # other ranks would sit in process-group teardown while rank 0 builds and tunes seven more engines)
-    if rank == 0 and world == 1 and not args.no_latency:
+    # batch-1 latency block: single-process GPU runs only (in a multi-rank job the other ranks would sit in
+    # process-group teardown while rank 0 builds and tunes more engines)
+    if rank == 0 and world == 1 and not args.no_latency and not cpu:
+        dev_bytes_b8 = eng.device_bytes
         del eng
         os.environ["SA_STAGE_TIMES"] = "1"  # per-stage device times (event nodes in the frame graph)
+        from stereoalgorithms_amd.models.engine import NativeStereoEngine
         for preset in ("raftstereo-sceneflow", "raftstereo-realtime", *OTHER_MS):
             e1 = NativeStereoEngine(preset, None, H, W, batch=1, device=dev.index, seed=0)
             e1.set_Q(Q)
@@ -135,16 +282,21 @@ def main():
                 e1.run_host(l1, r1, cloud=True)
                 ts.append((time.perf_counter() - t1) * 1e3)
             ts = np.array(ts)
+            base = {**BASELINE_MS, **OTHER_MS}[preset]
             extra[preset] = {"latency_ms_mean": round(float(ts.mean()), 3),
                              "latency_ms_p50": round(float(np.median(ts)), 3),
                              "latency_ms_p99": round(float(np.percentile(ts, 99)), 3),
                              "fps_b1": round(1000.0 / float(ts.mean()), 2),
-                             "baseline_ms_rtx3090": {**BASELINE_MS, **OTHER_MS}[preset],
-                             "speedup_vs_baseline": round({**BASELINE_MS, **OTHER_MS}[preset] / float(ts.mean()), 3),
+                             "baseline_ms_rtx3090": base,
+                             "speedup_vs_baseline": round(base / float(ts.mean()), 3) if base else None,
+                             "device_bytes": e1.device_bytes,
                              "device_stages_ms": {k: round(v, 3) for k, v in e1.stage_times()}}
             e1.close()
+    else:
+        dev_bytes_b8 = eng.device_bytes
     if rank == 0:
         base_fps = 1000.0 / BASELINE_MS[args.model]
+        lat = extra.get(args.model, {}).get("latency_ms_mean")
         rec = {
             "metric": f"{args.model} {H}x{W} throughput (frames/s, whole job)",
             "value": round(fps, 3),
@@ -153,20 +305,33 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
-            "ms_per_frame_per_gpu": round(ms_step / B, 3),
             "higher_is_better": True,
             "scaling": "weak",
+            # throughput (per-GPU batch B) over the reference's batch-1 FPS (1000 / 38 ms); the like-for-like
+            # latency ratio is vs_baseline_latency_b1 (reference ms / our batch-1 ms in its timed region)
             "vs_baseline": round(fps / base_fps, 3),
-            "dtype": "fp16",
+            "vs_baseline_kind": "whole-job throughput vs reference batch-1 FPS (1000/ms)",
+            "vs_baseline_latency_b1": round(BASELINE_MS[args.model] / lat, 3) if lat else None,
+            "dtype": "fp32" if cpu else "fp16",
             "data": "synthetic stereo pairs, seeded random-init weights",
+            "engine": "pytorch-oracle-cpu (plumbing rehearsal, not a benchmark)" if cpu else "native-hip",
             "config": {"model": args.model, "global_batch": world * B, "per_gpu_batch": B,
                        "resolution": f"{H}x{W}", "seq_len": None, "parallelism": f"dp{world}",
-                       "iters": 32 if args.model == "raftstereo-sceneflow" else 7},
+                       "iters": args.iters if args.iters > 0 else ITERS.get(args.model)},
+            "world_size": world,
+            "backend": backend if world > 1 else None,
+            "ranks": ranks,
+            "step_latency_ms": round(ms_step, 3),
+            "ms_per_frame_per_gpu": round(ms_step / B, 3),
+            "allgather_ms": gather_ms,
+            "allgather_bytes_per_rank": B * H * W * 4,
+            "device_bytes": dev_bytes_b8,
             "latency_b1": extra,
         }
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":

@@ -2,6 +2,7 @@
 #include "sa/dist.h"
 
 #include <arpa/inet.h>
+#include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <poll.h>
@@ -84,11 +85,21 @@ void shard_range(long total, int world, int rank, long* start, long* end) {
 int exchange_blob(int rank, int world, const char* addr, int port, void* buf, size_t n, int timeout_ms) {
   if (world <= 1) return 0;
   const auto deadline = Clock::now() + std::chrono::milliseconds(timeout_ms);
+  // MASTER_ADDR may be a hostname (torchrun sets socket.getfqdn()) or a dotted literal: resolve it.
+  // Rank 0 listens on every interface, so whichever address the name resolves to on a peer reaches it.
   sockaddr_in sa{};
   sa.sin_family = AF_INET;
   sa.sin_port = htons((uint16_t)port);
-  if (::inet_pton(AF_INET, addr, &sa.sin_addr) != 1) return -1;
+  if (::inet_pton(AF_INET, addr, &sa.sin_addr) != 1) {
+    addrinfo hints{}, *res = nullptr;
+    hints.ai_family = AF_INET;
+    hints.ai_socktype = SOCK_STREAM;
+    if (::getaddrinfo(addr, nullptr, &hints, &res) != 0 || !res) return -1;
+    sa.sin_addr = ((sockaddr_in*)res->ai_addr)->sin_addr;
+    ::freeaddrinfo(res);
+  }
   if (rank == 0) {
+    sa.sin_addr.s_addr = htonl(INADDR_ANY);
     int ls = ::socket(AF_INET, SOCK_STREAM, 0);
     if (ls < 0) return -1;
     int one = 1;

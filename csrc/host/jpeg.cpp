@@ -7,6 +7,12 @@
 // (RAFTStereo/test/main.cpp:13-14) on its test images.
 // Encoder: baseline 4:2:0 (colour) / grey JPEG with the Annex K tables scaled by libjpeg's
 // quality formula (cv::imwrite default quality 95), ISLOW forward DCT.
+//
+// Attribution: the integer IDCT / forward DCT follow the structure and fixed-point constants of the
+// Independent JPEG Group's jidctint.c / jfdctint.c (libjpeg, Copyright (C) Thomas G. Lane et al.;
+// "this software is based in part on the work of the Independent JPEG Group"), re-derived here so
+// that decoded pixels are bit-exact with the libjpeg-backed cv::imread the reference uses.
+// Every marker field is bounds-checked against its segment (malformed files fail, never overrun).
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -135,7 +141,7 @@ void idct_islow(const int32_t* in /*dequantised, natural order*/, uint8_t* out, 
 struct Huff {
   uint8_t bits[17] = {};
   uint8_t vals[256] = {};
-  int32_t maxcode[18], valptr[17], mincode[17];
+  int32_t maxcode[18] = {}, valptr[17] = {}, mincode[17] = {};
   bool present = false;
   void build() {
     int code = 0, k = 0;
@@ -312,43 +318,57 @@ bool jpeg_decode(const uint8_t* data, size_t size, Image& img, std::string* err)
     if (m == 0xD9) break;
     const int len = u16(p);
     const uint8_t* seg = p + 2;
-    if (p + len > end) return fail("truncated segment");
+    // every field below is read from the file: bound each read by the segment it belongs to
+    if (len < 2 || p + len > end) return fail("truncated segment");
+    const uint8_t* sege = p + len;
     if (m == 0xDB) {
       const uint8_t* q = seg;
-      while (q < p + len) {
+      while (q < sege) {
         const int pq = q[0] >> 4, tq = q[0] & 15;
+        if (pq > 1 || tq > 3) return fail("bad DQT table");
         ++q;
+        if (q + (pq ? 128 : 64) > sege) return fail("truncated DQT");
         for (int i = 0; i < 64; ++i) {
-          qt[tq & 3][kZigzag[i]] = pq ? (uint16_t)u16(q + 2 * i) : q[i];
+          qt[tq][kZigzag[i]] = pq ? (uint16_t)u16(q + 2 * i) : q[i];
         }
         q += pq ? 128 : 64;
       }
     } else if (m == 0xC4) {
       const uint8_t* q = seg;
-      while (q < p + len) {
+      while (q < sege) {
+        if (q + 17 > sege) return fail("truncated DHT");
         const int tc = q[0] >> 4, th = q[0] & 15;
-        Huff& h = tc ? hac[th & 3] : hdc[th & 3];
+        if (tc > 1 || th > 3) return fail("bad DHT table");
+        Huff& h = tc ? hac[th] : hdc[th];
         int tot = 0;
         for (int i = 1; i <= 16; ++i) {
           h.bits[i] = q[i];
           tot += q[i];
         }
+        if (tot > 256 || q + 17 + tot > sege) return fail("bad DHT code counts");
         std::memcpy(h.vals, q + 17, tot);
         h.build();
         q += 17 + tot;
       }
     } else if (m == 0xC0 || m == 0xC1) {
+      if (len < 8) return fail("truncated SOF");
       if (seg[0] != 8) return fail("only 8-bit JPEG supported");
       H = u16(seg + 1);
       W = u16(seg + 3);
       const int nc = seg[5];
+      if (H <= 0 || W <= 0) return fail("bad image size");
+      if (nc != 1 && nc != 3) return fail("only 1- or 3-component JPEG supported");
+      if (8 + 3 * nc > len) return fail("truncated SOF");
       comps.clear();
+      hmax = vmax = 1;
       for (int i = 0; i < nc; ++i) {
         Comp c;
         c.id = seg[6 + 3 * i];
         c.h = seg[7 + 3 * i] >> 4;
         c.v = seg[7 + 3 * i] & 15;
         c.tq = seg[8 + 3 * i];
+        if (c.h < 1 || c.h > 2 || c.v < 1 || c.v > 2) return fail("sampling factors above 2x2 not supported");
+        if (c.tq > 3) return fail("bad quantisation table index");
         hmax = std::max(hmax, c.h);
         vmax = std::max(vmax, c.v);
         comps.push_back(c);
@@ -356,13 +376,16 @@ bool jpeg_decode(const uint8_t* data, size_t size, Image& img, std::string* err)
     } else if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
       return fail("progressive / arithmetic / lossless JPEG not supported");
     } else if (m == 0xDD) {
+      if (len < 4) return fail("truncated DRI");
       restart = u16(seg);
     } else if (m == 0xEE) {
       if (len >= 12 && std::memcmp(seg, "Adobe", 5) == 0) adobe_rgb = seg[11] == 0;
     } else if (m == 0xDA) {
       if (comps.empty()) return fail("SOS before SOF");
+      if (len < 3) return fail("truncated SOS");
       const int ns = seg[0];
-      std::vector<int> sc(ns);
+      if (ns < 1 || ns > (int)comps.size() || 3 + 2 * ns > len) return fail("bad SOS component count");
+      std::vector<int> sc(ns, -1);
       for (int i = 0; i < ns; ++i) {
         const int cid = seg[1 + 2 * i];
         for (size_t k = 0; k < comps.size(); ++k)
@@ -370,7 +393,10 @@ bool jpeg_decode(const uint8_t* data, size_t size, Image& img, std::string* err)
             sc[i] = (int)k;
             comps[k].td = seg[2 + 2 * i] >> 4;
             comps[k].ta = seg[2 + 2 * i] & 15;
+            if (comps[k].td > 3 || comps[k].ta > 3) return fail("bad Huffman table index");
+            if (!hdc[comps[k].td].present || !hac[comps[k].ta].present) return fail("undefined Huffman table");
           }
+        if (sc[i] < 0) return fail("SOS names an unknown component");
       }
       const int mcux = (W + 8 * hmax - 1) / (8 * hmax), mcuy = (H + 8 * vmax - 1) / (8 * vmax);
       for (auto& c : comps) {
@@ -404,6 +430,7 @@ bool jpeg_decode(const uint8_t* data, size_t size, Image& img, std::string* err)
             for (int bx = 0; bx < nbx; ++bx) {
               std::fill(blk, blk + 64, 0);
               const int t = decode_huff(br, hdc[c.td]);
+              if (t > 15) return fail("corrupt DC coefficient");
               const int diff = t ? extend(br.bits(t), t) : 0;
               c.pred += diff;
               blk[0] = c.pred * qt[c.tq][0];

@@ -39,6 +39,7 @@ bool png_decode(const uint8_t* d, size_t n, Image& img, std::string* err) {
     const uint8_t* body = d + p + 8;
     if (p + 12 + len > n) return fail("truncated PNG");
     if (!std::memcmp(type, "IHDR", 4)) {
+      if (len != 13) return fail("bad IHDR");
       W = be32(body);
       H = be32(body + 4);
       depth = body[8];
@@ -54,10 +55,16 @@ bool png_decode(const uint8_t* d, size_t n, Image& img, std::string* err) {
     p += 12 + len;
   }
   if (interlace) return fail("interlaced PNG not supported");
-  if (depth != 8 && depth != 16) return fail("PNG bit depth must be 8 or 16");
+  // header fields come from the file: bound them before any size arithmetic
+  constexpr uint32_t kMaxDim = 1u << 15;
+  if (W == 0 || H == 0 || W > kMaxDim || H > kMaxDim) return fail("PNG dimensions out of range");
+  if (ctype != 0 && ctype != 2 && ctype != 3 && ctype != 4 && ctype != 6) return fail("bad PNG colour type");
+  const bool sub8 = depth == 1 || depth == 2 || depth == 4;
+  if (sub8 ? (ctype != 0 && ctype != 3) : (depth != 8 && !(depth == 16 && ctype != 3)))
+    return fail("unsupported PNG bit depth for this colour type");
   const int spp = ctype == 0 ? 1 : ctype == 2 ? 3 : ctype == 3 ? 1 : ctype == 4 ? 2 : 4;
-  const int bpp = spp * depth / 8;
-  const size_t stride = (size_t)W * bpp;
+  const int bpp = sub8 ? 1 : spp * depth / 8;  // filter unit (bytes), >= 1
+  const size_t stride = sub8 ? ((size_t)W * depth + 7) / 8 : (size_t)W * bpp;  // <= 2^15 * 8 bytes
   std::vector<uint8_t> raw((stride + 1) * H);
   uLongf rl = (uLongf)raw.size();
   if (uncompress(raw.data(), &rl, idat.data(), (uLong)idat.size()) != Z_OK || rl != raw.size())
@@ -88,6 +95,18 @@ bool png_decode(const uint8_t* d, size_t n, Image& img, std::string* err) {
   img.data.assign((size_t)W * H * img.channels, 0);
   const int bs = depth / 8;
   for (size_t i = 0; i < (size_t)W * H; ++i) {
+    if (sub8) {  // packed 1/2/4-bit samples, MSB first, rows byte-aligned
+      const size_t y = i / W, x = i % W;
+      const size_t bit = x * depth;
+      const int v = (px[y * stride + bit / 8] >> (8 - depth - (int)(bit % 8))) & ((1 << depth) - 1);
+      if (ctype == 3) {
+        for (int k = 0; k < 3; ++k)
+          img.data[i * 3 + k] = palette.size() > (size_t)v * 3 + (2 - k) ? palette[v * 3 + (2 - k)] : 0;
+      } else {
+        img.data[i] = (uint8_t)(v * 255 / ((1 << depth) - 1));
+      }
+      continue;
+    }
     const uint8_t* s = &px[i * bpp];
     auto sample = [&](int k) { return s[k * bs]; };  // 16-bit: keep the MSB (cv::imread 8-bit path)
     if (ctype == 3) {

@@ -32,7 +32,8 @@ ABI_LIBS = {"raftstereo_abi.cpp": "libRAFTStereo.so", "hitnet_abi.cpp": "libHitN
 # apps source -> ABI library it links (reference demo executable names)
 APPS = {"raft_stereo_demo.cpp": "libRAFTStereo.so", "HitNet_demo.cpp": "libHitNet.so",
         "crestereo_demo.cpp": "libCREStereo.so", "fastacvnet_plus_demo.cpp": "libFastACVNet_plus.so",
-        "Stereo_Calibration.cpp": "libstereo_host.so", "stereo_capture.cpp": "libstereo_host.so"}
+        "Stereo_Calibration.cpp": "libstereo_host.so", "stereo_capture.cpp": "libstereo_host.so",
+        "abi_check.cpp": "libstereo_host.so"}
 
 COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC / 'include'}", "-Wall", "-Wno-unused-function"]
 
@@ -70,7 +71,11 @@ def _compile(src: Path, obj: Path, host_only: bool, hmt: float, verbose: bool) -
 
 def _link(objs, out: Path, host_only: bool, extra=(), shared: bool = True):
     newest = max(o.stat().st_mtime for o in objs)
-    if out.exists() and out.stat().st_mtime >= newest:
+    # the object set is part of the link's inputs: a deleted / added source relinks too
+    manifest = OBJDIR / "link" / (out.name + ".objs")
+    objset = "\n".join(sorted(map(str, objs))) + "\n" + " ".join(extra)
+    same = manifest.exists() and manifest.read_text() == objset
+    if same and out.exists() and out.stat().st_mtime >= newest:
         return False
     out.parent.mkdir(parents=True, exist_ok=True)
     if host_only:
@@ -81,6 +86,8 @@ def _link(objs, out: Path, host_only: bool, extra=(), shared: bool = True):
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {out}\n{r.stdout}\n{r.stderr}")
+    manifest.parent.mkdir(parents=True, exist_ok=True)
+    manifest.write_text(objset)
     return True
 
 
@@ -128,7 +135,7 @@ def build(jobs: int | None = None, verbose: bool = False) -> dict:
             abi_built.append(r)
         libname = lib[3:-3]
         _link([obj], BINDIR / s.stem, True, shared=False,
-              extra=[f"-L{LIBDIR}", f"-l{libname}", "-lstereo_host", "-Wl,-rpath,$ORIGIN/../lib"])
+              extra=[f"-L{LIBDIR}", f"-l{libname}", "-lstereo_host", "-ldl", "-Wl,-rpath,$ORIGIN/../lib"])
     # native RCCL data parallelism: its own library (Python processes never load a second RCCL next to
     # torch's) + the C++ multi-GPU bench
     dsrc = CSRC / "dist" / "dist.cpp"

@@ -23,23 +23,24 @@ def _free_port():
     return p
 
 
-def _peer(rank, world, port, q):
+def _peer(rank, world, port, q, addr=b"127.0.0.1"):
     lib = C.CDLL(LIB, mode=C.RTLD_GLOBAL)
     buf = (C.c_ubyte * 128)()
     if rank == 0:
         for i in range(128):
             buf[i] = (i * 7 + 3) & 0xFF
-    rc = lib.sa_dist_exchange_blob(rank, world, b"127.0.0.1", port, buf, C.c_size_t(128), 20000)
+    rc = lib.sa_dist_exchange_blob(rank, world, addr, port, buf, C.c_size_t(128), 20000)
     q.put((rank, rc, bytes(buf)))
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="native build missing")
-@pytest.mark.parametrize("world", [2, 4])
-def test_unique_id_bootstrap_tcp(world):
+@pytest.mark.parametrize("world,addr", [(2, b"127.0.0.1"), (4, b"127.0.0.1"), (2, b"localhost")])
+def test_unique_id_bootstrap_tcp(world, addr):
+    """MASTER_ADDR as a dotted literal and as a hostname (torchrun passes socket.getfqdn())."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_peer, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_peer, args=(r, world, port, q, addr)) for r in range(world)]
     for p in procs:
         p.start()
     res = {r: (rc, b) for r, rc, b in (q.get(timeout=60) for _ in procs)}
