@@ -84,6 +84,11 @@ const float* sa_engine_aux_output(void* e, int* n) {
   return static_cast<sa::StereoEngine*>(e)->aux_output(n);
 }
 
+const char* sa_engine_plan_path(void* e) { return static_cast<sa::StereoEngine*>(e)->plan_path().c_str(); }
+long sa_engine_tuned_shapes(void* e) { return static_cast<sa::StereoEngine*>(e)->tuned_shapes(); }
+long sa_conv_tune_count(void) { return sa::conv_tune_count(); }
+void sa_conv_plan_clear(void) { sa::conv_plan_clear(); }
+
 void* sa_engine_stream(void* e) { return (void*)static_cast<sa::StereoEngine*>(e)->stream(); }
 
 int sa_engine_stage_times(void* e, float* ms, const char** names, int max) {

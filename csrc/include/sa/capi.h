@@ -21,6 +21,12 @@ int sa_engine_run_host(void* engine, void* left, void* right, float* disp, float
 long long sa_engine_device_bytes(void* engine);
 const float* sa_engine_aux_output(void* engine, int* n);
 void* sa_engine_stream(void* engine);
+// tuned-plan cache: the engine's plan file ("" = none), the conv shapes it had to time at build,
+// the process-wide count of timed shapes, and a reset of the in-process plan (tests)
+const char* sa_engine_plan_path(void* engine);
+long sa_engine_tuned_shapes(void* engine);
+long sa_conv_tune_count(void);
+void sa_conv_plan_clear(void);
 // per-stage device times of the last frame (SA_STAGE_TIMES=1): returns the count (<= max), fills
 // ms[i] and names[i] (pointers valid for the engine's lifetime)
 int sa_engine_stage_times(void* engine, float* ms, const char** names, int max);

@@ -70,6 +70,9 @@ class StereoEngine {
 
   hipStream_t stream() const { return stream_; }
   size_t device_bytes() const { return arena_.bytes(); }
+  // tuned-plan file used by this engine ("" = none) and how many conv shapes it had to time
+  const std::string& plan_path() const { return plan_path_; }
+  long tuned_shapes() const { return tuned_shapes_; }
   // low-resolution flow / auxiliary output (RAFT "diff" = coords1 - coords0), may be null
   virtual const float* aux_output(int* n) const {
     *n = 0;
@@ -128,6 +131,9 @@ class StereoEngine {
   float Q_[16];
   bool have_Q_ = false;
   GraphExec graph_[2];  // [no rectify, rectify]
+  std::string default_plan_path() const;
+  std::string plan_path_;
+  long tuned_shapes_ = 0;
   SplitKWorkspace splitk_;
   hipStream_t side_ = nullptr;
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;

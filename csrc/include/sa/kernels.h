@@ -108,6 +108,9 @@ int sa_conv3x3_c64_direct(const void* x, int xs, const void* w, int kpad, const 
                           hipStream_t stream);
 // Number of n-tiles (projection slices) sa_conv2d() will use for these args.
 int sa_conv2d_nslices(const SaConvArgs* a);
+// split-K footprint of the calling thread's last successful sa_conv2d launch: slab floats and tile
+// counters it used (0, 0 when it did not split)
+void sa_conv2d_last_split(long* ws_floats, long* tiles);
 // Following-conv stencil of SA_EPI_PROJ: out[n][y][x][o] (fp32, pixel stride out_stride) gets
 // (accumulate ? out + : ) bias[o] + sum_{s < nslices, (ky,kx)} P[s][(ky*kw+kx)*oc + o][n][y+ky-ph][x+kx-pw]
 // (zero outside the image).  Stride-1 'same' convs only.

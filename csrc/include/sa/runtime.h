@@ -28,13 +28,16 @@ class DeviceArena {
   // Allocations are individually hipMalloc'd (so ASan-like tooling sees bounds) and freed
   // together; sizes are rounded to 256 B.
   void* alloc(size_t bytes);
+  void free(void* p);  // one allocation of this arena
   size_t bytes() const { return total_; }
   void release();
 
  private:
   std::vector<void*> ptrs_;
+  std::vector<size_t> sizes_;
   size_t total_ = 0;
 };
+
 
 // ------------------------------------------------------------------ tensors
 enum class DT { F16 = 0, F32 = 1, U8 = 2 };
@@ -67,6 +70,34 @@ struct Tensor {
 
 Tensor make_tensor(DeviceArena& a, int n, int h, int w, int c, DT dt = DT::F16, int stride = -1);
 Tensor make_volume(DeviceArena& a, int n, int d, int h, int w, int c, DT dt = DT::F16, int stride = -1);
+
+// ------------------------------------------------------------------ activation memory planner
+// Liveness-based placement of the activations of a straight-line run (a chain of encoder blocks):
+// each tensor is declared with the step that defines it and the last step that reads it; commit()
+// packs all of them into ONE allocation (greedy best-fit by size over address intervals of tensors
+// whose lifetimes overlap) and patches their pointers.  Tensors must not need zero-initialised
+// padding (they share bytes with dead tensors) and must only be touched inside their interval.
+class ActPlan {
+ public:
+  static constexpr int kForever = 1 << 30;
+  void def(Tensor* t, int n, int h, int w, int c, DT dt = DT::F16);  // defined at the current step
+  void use(const Tensor* t);    // read at the current step (extends the lifetime)
+  void keep(const Tensor* t);   // live past the run (outputs)
+  void next() { ++step_; }
+  int step() const { return step_; }
+  size_t commit(DeviceArena& a);  // returns the bytes of the shared allocation
+  size_t naive_bytes() const;     // what one allocation per tensor would take
+ private:
+  struct Item {
+    Tensor* t;
+    size_t bytes;
+    int first, last;
+    size_t off = 0;
+  };
+  Item* find(const Tensor* t);
+  std::vector<Item> items_;
+  int step_ = 0;
+};
 
 // ------------------------------------------------------------------ host weights
 struct HostTensor {
@@ -104,7 +135,10 @@ struct SplitKWorkspace {
   int32_t* counters = nullptr;
   int64_t ws_floats = 0;
   int32_t n_counters = 0;
-  void alloc(DeviceArena& a, int64_t floats, int32_t counters);
+  // high-water mark of what launches under this workspace actually used (ConvLayer::launch)
+  mutable int64_t max_floats = 0;
+  mutable int32_t max_counters = 0;
+  void alloc(DeviceArena& a, int64_t floats, int32_t counters);  // (re)allocates
 };
 const SplitKWorkspace* current_splitk();
 struct ScopedSplitK {
@@ -130,6 +164,18 @@ bool conv_tuning_enabled();
 // `a`; sets a.tile_cfg / a.splitk when a plan exists.
 void conv_apply_plan(SaConvArgs& a, hipStream_t s);
 size_t conv_plan_entries();
+long conv_tune_count();     // shapes tuned (timed) in this process
+void conv_plan_clear();     // drop the in-process plan (tests: prove a plan file is used)
+void conv_plan_set_arch(const std::string& gcn_arch_name);  // plan keys carry the device's arch
+const std::string& conv_plan_arch();
+int conv_plan_load(const std::string& file);  // merge a plan file; returns entries added, -1 if absent
+int conv_plan_save(const std::string& file, const std::vector<std::string>& keys);
+// collects every plan key consulted by conv_apply_plan in this thread (the engine's own shapes)
+struct ScopedPlanCollect {
+  std::vector<std::string>* prev;
+  explicit ScopedPlanCollect(std::vector<std::string>* keys);
+  ~ScopedPlanCollect();
+};
 
 // ------------------------------------------------------------------ conv layers
 // Copies of every instance-norm statistics buffer the conv epilogues spread their atomics over

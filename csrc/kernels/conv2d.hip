@@ -1079,6 +1079,12 @@ void launch_kernel(dim3 grid, const SaConvArgs* a, hipStream_t stream) {
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, MODE, false>), grid, dim3(64 * WM * WN), 0, stream, *a);
 }
 
+thread_local long g_split_floats = 0, g_split_tiles = 0;
+inline void note_split(int S, long tiles, long tile_floats) {
+  g_split_floats = S > 1 ? (long)S * tiles * tile_floats : 0;
+  g_split_tiles = S > 1 ? tiles : 0;
+}
+
 template <int BM, int BN, int WM, int WN>
 int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
   // DMA path (opt-in, SA_CONV_GLDS=1): measured 14% slower than register staging on the RAFT-SF
@@ -1125,6 +1131,7 @@ int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
                 tiles > a->n_counters || S > nk))
     return -4;
   dim3 grid(gx, gy, S);
+  note_split(S, tiles, BM * BN);
   if (gl) launch_kernel<BM, BN, WM, WN, kDmaK64>(grid, a, stream);
   else if (fast) launch_kernel<BM, BN, WM, WN, kFastK64>(grid, a, stream);
   else if (k64) launch_kernel<BM, BN, WM, WN, kRegK64>(grid, a, stream);
@@ -1158,6 +1165,7 @@ int launch_glds3(const SaConvArgs* a, hipStream_t stream, bool forced) {
   if (S > 1 && (a->stats || !a->ws || !a->counters || (long)S * tiles * BM * BN > a->ws_floats ||
                 tiles > a->n_counters || S > nk))
     return forced ? -4 : 1;
+  note_split(S, tiles, BM * BN);
   launch_kernel<BM, BN, WM, WN, kGlds3>(dim3(gx, gy, S), a, stream);
   return (int)hipGetLastError();
 }
@@ -1204,6 +1212,11 @@ int cfg_bn(int cfg) {
 
 }  // namespace
 
+extern "C" void sa_conv2d_last_split(long* ws_floats, long* tiles) {
+  *ws_floats = g_split_floats;
+  *tiles = g_split_tiles;
+}
+
 extern "C" int sa_conv2d_nslices(const SaConvArgs* a) {
   const int bn = cfg_bn(pick_cfg(a));
   return bn > 0 ? (a->Cout + bn - 1) / bn : -3;
@@ -1229,6 +1242,7 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
                       a->Kpad >= 576 && a->out_stride % 8 == 0 && a->src[0].stride % 8 == 0 && a->Ho == a->H &&
                       a->Wo == a->W;
       if (!ok) return -5;
+      note_split(1, 0, 0);
       return sa_conv3x3_c64_direct(a->src[0].ptr, a->src[0].stride, a->weight, a->Kpad, a->bias, a->out,
                                    a->out_stride, a->N, a->H, a->W, a->act, a->alpha, a->stats, a->stats_slots, 0,
                                    stream);

@@ -40,7 +40,8 @@ void instnorm(hipStream_t s, const Tensor& x, const sa_stat_t* stats, const Tens
 }
 
 void ResBlock::build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std::string& p,
-                     int in_planes, int planes, int stride, Norm nrm, int N, int H, int W) {
+                     int in_planes, int planes, int stride, Norm nrm, int N, int H, int W, ActPlan* plan,
+                     const Tensor* x) {
   norm = nrm;
   has_down = !(stride == 1 && in_planes == planes);
   src.conv(p + ".conv1", planes, in_planes, 3, 3);
@@ -67,11 +68,28 @@ void ResBlock::build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std
   }
   const int Ho = c1.out_h(H), Wo = c1.out_w(W);
   if (norm == Norm::Instance) {
-    y1 = make_tensor(a, N, Ho, Wo, planes);
-    y2 = make_tensor(a, N, Ho, Wo, planes);
     st1 = sp.take(N, planes);
     st2 = sp.take(N, planes);
     if (has_down) std_ = sp.take(N, planes);
+  }
+  if (plan) {
+    // lifetimes in run() order (see below); x is the block input (tracked only if the plan owns it)
+    if (norm == Norm::Instance) {
+      plan->use(x), plan->def(&y1, N, Ho, Wo, planes), plan->next();                   // c1(x) -> y1
+      plan->use(&y1), plan->def(&a1, N, Ho, Wo, planes), plan->next();                 // IN -> a1
+      plan->use(&a1), plan->def(&y2, N, Ho, Wo, planes), plan->next();                 // c2(a1) -> y2
+      if (has_down) plan->use(x), plan->def(&yd, N, Ho, Wo, planes), plan->next();     // down(x) -> yd
+      plan->use(&y2), plan->use(has_down ? &yd : x), plan->def(&out, N, Ho, Wo, planes), plan->next();
+    } else {
+      plan->use(x), plan->def(&a1, N, Ho, Wo, planes), plan->next();                   // c1(x) -> a1
+      if (has_down) plan->use(x), plan->def(&yd, N, Ho, Wo, planes), plan->next();     // down(x) -> yd
+      plan->use(&a1), plan->use(has_down ? &yd : x), plan->def(&out, N, Ho, Wo, planes), plan->next();
+    }
+    return;
+  }
+  if (norm == Norm::Instance) {
+    y1 = make_tensor(a, N, Ho, Wo, planes);
+    y2 = make_tensor(a, N, Ho, Wo, planes);
   }
   a1 = make_tensor(a, N, Ho, Wo, planes);
   if (has_down) yd = make_tensor(a, N, Ho, Wo, planes);
@@ -110,23 +128,32 @@ void Trunk::build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std::s
   conv1.build(a, *src.ws, {p + ".conv1"}, {{3, 8}}, sp7,
               norm == Norm::Batch ? std::vector<std::string>{p + ".norm1"} : std::vector<std::string>{});
   int h = conv1.out_h(H), w = conv1.out_w(W);
+  // the trunk's activations go through a liveness plan: at most ~3 full-resolution tensors are alive
+  // at once (batch 8 RAFT-Stereo sceneflow: several GB less than one buffer per tensor)
+  ActPlan plan;
   if (norm == Norm::Instance) {
-    c1y = make_tensor(a, N, h, w, 64);
     c1st = sp.take(N, 64);
+    plan.def(&c1y, N, h, w, 64), plan.next();                      // conv1(img) -> c1y
+    plan.use(&c1y), plan.def(&c1a, N, h, w, 64), plan.next();      // IN -> c1a
+  } else {
+    plan.def(&c1a, N, h, w, 64), plan.next();                      // conv1(img) -> c1a
   }
-  c1a = make_tensor(a, N, h, w, 64);
   const int dims[3] = {64, 96, 128};
   int inp = 64;
-  layers.resize(6);
+  layers.resize(6);  // sized up front: the plan holds pointers into the blocks
+  const Tensor* x = &c1a;
   for (int l = 0; l < 3; ++l)
     for (int b = 0; b < 2; ++b) {
       ResBlock& rb = layers[l * 2 + b];
       rb.build(a, src, sp, p + ".layer" + std::to_string(l + 1) + "." + std::to_string(b), inp, dims[l],
-               b == 0 ? strides[l] : 1, norm, N, h, w);
+               b == 0 ? strides[l] : 1, norm, N, h, w, &plan, x);
+      x = &rb.out;
       h = rb.out.h;
       w = rb.out.w;
       inp = dims[l];
     }
+  plan.keep(&layers.back().out);
+  plan.commit(a);
 }
 
 void Trunk::run(hipStream_t s, const StatsPool& sp, const Tensor& img) const {

@@ -56,8 +56,11 @@ struct ResBlock {
   Norm norm = Norm::None;
   Tensor y1, a1, y2, yd, out;
   sa_stat_t *st1 = nullptr, *st2 = nullptr, *std_ = nullptr;  // StatsPool handles
+  // plan != nullptr: the block's activations are declared in `plan` (lifetimes in run() order, x =
+  // the block input) instead of being allocated; the caller commits the plan
   void build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std::string& prefix, int in_planes,
-             int planes, int stride, Norm norm, int N, int H, int W);
+             int planes, int stride, Norm norm, int N, int H, int W, ActPlan* plan = nullptr,
+             const Tensor* x = nullptr);
   void run(hipStream_t s, const StatsPool& sp, const Tensor& x) const;
 };
 

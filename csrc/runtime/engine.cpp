@@ -6,6 +6,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <cerrno>
+#include <sys/stat.h>
 
 namespace sa {
 
@@ -151,17 +153,82 @@ void StereoEngine::init() {
   store_.reset();  // host copies no longer needed
   HIP_CHECK(hipDeviceSynchronize());
   if (conv_tuning_enabled()) {
-    // eager tuning pass: every conv shape of the frame is timed over the launcher's tactics (on
-    // whatever the buffers hold) and the plan is fixed before the frame graph is captured
-    ScopedSplitK sk(&splitk_);
-    ScopedConvTuning tune(true);
-    TraceRange ttr("conv tactic selection");
-    tuning_pass_ = true;
-    forward(stream_);
-    tuning_pass_ = false;
-    HIP_CHECK(hipStreamSynchronize(stream_));
+    hipDeviceProp_t prop;
+    HIP_CHECK(hipGetDeviceProperties(&prop, cfg_.device));
+    conv_plan_set_arch(prop.gcnArchName);
+    // tuned-plan cache next to the model, the analogue of the reference's "<stem>_batch=1.engine"
+    // (RAFTStereo/src/TRTRAFTStereo.cpp:25-46): a second Initialize of the same model / shape / device
+    // arch skips tactic timing entirely
+    plan_path_ = default_plan_path();
+    if (!plan_path_.empty()) {
+      const int n = conv_plan_load(plan_path_);
+      if (n >= 0) SA_LOGI("tactic plan %s: %d entries loaded", plan_path_.c_str(), n);
+    }
+    const long tuned0 = conv_tune_count();
+    std::vector<std::string> keys;
+    {
+      // eager tuning pass: every conv shape of the frame is timed over the launcher's tactics (on
+      // whatever the buffers hold) and the plan is fixed before the frame graph is captured
+      ScopedSplitK sk(&splitk_);
+      ScopedConvTuning tune(true);
+      ScopedPlanCollect collect(&keys);
+      TraceRange ttr("conv tactic selection");
+      tuning_pass_ = true;
+      forward(stream_);
+      tuning_pass_ = false;
+      HIP_CHECK(hipStreamSynchronize(stream_));
+    }
+    tuned_shapes_ = conv_tune_count() - tuned0;
+    if (!plan_path_.empty() && tuned_shapes_ > 0) {
+      if (conv_plan_save(plan_path_, keys) == 0) SA_LOGI("tactic plan saved to %s", plan_path_.c_str());
+      else SA_LOGW("could not write tactic plan %s", plan_path_.c_str());
+    }
+    // right-size the split-K workspaces to what the tuned plan actually launches (every stream's
+    // workspace serves a subset of the same convs, so the pass's high-water mark bounds each)
+    const int64_t fl = splitk_.max_floats;
+    const int32_t nc = splitk_.max_counters;
+    HIP_CHECK(hipDeviceSynchronize());
+    splitk_.alloc(arena_, fl, nc);
+    splitk_side_.alloc(arena_, fl, nc);
+    splitk_side2_.alloc(arena_, fl, nc);
   }
   SA_LOGI("%s: built, %.1f MiB device memory", name(), arena_.bytes() / 1048576.0);
+}
+
+std::string StereoEngine::default_plan_path() const {
+  // SA_PLAN_CACHE=<file> (process-wide plan file, appended), SA_PLAN_CACHE=0 / SA_PLAN_DIR="" disable
+  if (const char* e = std::getenv("SA_PLAN_CACHE")) {
+    (void)e;
+    return std::string();
+  }
+  std::string dir, stem;
+  if (!cfg_.weights.empty()) {
+    const size_t slash = cfg_.weights.find_last_of('/');
+    dir = slash == std::string::npos ? "." : cfg_.weights.substr(0, slash);
+    stem = cfg_.weights.substr(slash == std::string::npos ? 0 : slash + 1);
+    const size_t dot = stem.rfind('.');
+    if (dot != std::string::npos) stem = stem.substr(0, dot);
+  } else {
+    stem = cfg_.model + "_seed" + std::to_string(cfg_.seed);
+  }
+  if (const char* d = std::getenv("SA_PLAN_DIR")) {
+    if (!d[0]) return std::string();
+    dir = d;
+  } else if (dir.empty()) {
+    const char* xdg = std::getenv("XDG_CACHE_HOME");
+    const char* home = std::getenv("HOME");
+    if (xdg && xdg[0]) dir = std::string(xdg) + "/stereoalgorithms_amd";
+    else if (home && home[0]) dir = std::string(home) + "/.cache/stereoalgorithms_amd";
+    else return std::string();
+  }
+  for (size_t i = 1; i <= dir.size(); ++i)  // mkdir -p
+    if (i == dir.size() || dir[i] == '/') {
+      const std::string part = dir.substr(0, i);
+      if (::mkdir(part.c_str(), 0755) != 0 && errno != EEXIST) return std::string();
+    }
+  char tail[160];
+  std::snprintf(tail, sizeof(tail), "_b%d_%dx%d_it%d_%s.plan", B(), H(), W(), cfg_.iters, conv_plan_arch().c_str());
+  return dir + "/" + stem + tail;
 }
 
 hipStream_t StereoEngine::fork(hipStream_t s) {

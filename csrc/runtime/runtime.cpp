@@ -23,14 +23,96 @@ void* DeviceArena::alloc(size_t bytes) {
   HIP_CHECK(hipMalloc(&p, bytes));
   HIP_CHECK(hipMemset(p, 0, bytes));
   ptrs_.push_back(p);
+  sizes_.push_back(bytes);
   total_ += bytes;
   return p;
+}
+
+void DeviceArena::free(void* p) {
+  auto it = std::find(ptrs_.begin(), ptrs_.end(), p);
+  SA_REQUIRE(it != ptrs_.end(), "arena free of a foreign pointer");
+  const size_t i = (size_t)(it - ptrs_.begin());
+  HIP_CHECK(hipFree(p));
+  total_ -= sizes_[i];
+  ptrs_.erase(it);
+  sizes_.erase(sizes_.begin() + (long)i);
 }
 
 void DeviceArena::release() {
   for (void* p : ptrs_) (void)hipFree(p);
   ptrs_.clear();
+  sizes_.clear();
   total_ = 0;
+}
+
+// ------------------------------------------------------------------ activation planner
+ActPlan::Item* ActPlan::find(const Tensor* t) {
+  for (Item& it : items_)
+    if (it.t == t) return &it;
+  return nullptr;
+}
+
+void ActPlan::def(Tensor* t, int n, int h, int w, int c, DT dt) {
+  SA_REQUIRE(!find(t), "tensor defined twice in an activation plan");
+  t->n = n;
+  t->d = 1;
+  t->h = h;
+  t->w = w;
+  t->c = c;
+  t->stride = c;
+  t->dt = dt;
+  t->ptr = nullptr;
+  items_.push_back(Item{t, (t->nbytes() + 255) & ~(size_t)255, step_, step_});
+}
+
+void ActPlan::use(const Tensor* t) {
+  Item* it = find(t);
+  if (it) it->last = std::max(it->last, step_);  // tensors from outside the plan are not tracked
+}
+
+void ActPlan::keep(const Tensor* t) {
+  Item* it = find(t);
+  SA_REQUIRE(it, "keep() of a tensor outside the plan");
+  it->last = kForever;
+}
+
+size_t ActPlan::naive_bytes() const {
+  size_t s = 0;
+  for (const Item& it : items_) s += it.bytes;
+  return s;
+}
+
+size_t ActPlan::commit(DeviceArena& a) {
+  if (items_.empty()) return 0;
+  std::vector<Item*> order;
+  for (Item& it : items_) order.push_back(&it);
+  std::stable_sort(order.begin(), order.end(), [](const Item* x, const Item* y) { return x->bytes > y->bytes; });
+  std::vector<Item*> placed;
+  size_t total = 0;
+  for (Item* it : order) {
+    // address intervals already taken by tensors alive at the same time, sorted by offset
+    std::vector<std::pair<size_t, size_t>> busy;
+    for (const Item* q : placed)
+      if (q->first <= it->last && it->first <= q->last) busy.push_back({q->off, q->off + q->bytes});
+    std::sort(busy.begin(), busy.end());
+    size_t best = SIZE_MAX, best_gap = SIZE_MAX, cur = 0;
+    for (const auto& b : busy) {  // smallest gap that fits (best fit), else the end
+      if (b.first > cur && b.first - cur >= it->bytes && b.first - cur < best_gap) {
+        best = cur;
+        best_gap = b.first - cur;
+      }
+      cur = std::max(cur, b.second);
+    }
+    if (best == SIZE_MAX) best = cur;
+    it->off = best;
+    total = std::max(total, best + it->bytes);
+    placed.push_back(it);
+  }
+  char* base = (char*)a.alloc(total);
+  for (Item& it : items_) it.t->ptr = base + it.off;
+  SA_LOGI("activation plan: %zu tensors, %.1f MiB planned vs %.1f MiB unplanned", items_.size(),
+          total / 1048576.0, naive_bytes() / 1048576.0);
+  return total;
 }
 
 Tensor make_volume(DeviceArena& a, int n, int d, int h, int w, int c, DT dt, int stride) {
@@ -438,6 +520,13 @@ void ConvLayer::launch(hipStream_t s, SaConvArgs& a) const {
   }
   SA_REQUIRE(rc == 0, "sa_conv2d failed rc=%d", rc);
   SA_LAUNCH_CHECK(s);
+  if (const SplitKWorkspace* sk = current_splitk()) {
+    // record what this launch's split actually needs (engine right-sizes the workspaces after tuning)
+    long fl = 0, tiles = 0;
+    sa_conv2d_last_split(&fl, &tiles);
+    sk->max_floats = std::max<int64_t>(sk->max_floats, fl);
+    sk->max_counters = std::max<int32_t>(sk->max_counters, (int32_t)tiles);
+  }
 }
 
 void ConvLayer::run(hipStream_t s, const std::vector<Tensor>& srcs, const Tensor& out, int act,
@@ -462,6 +551,10 @@ ScopedSplitK::ScopedSplitK(const SplitKWorkspace* w) : prev(g_splitk) { g_splitk
 ScopedSplitK::~ScopedSplitK() { g_splitk = prev; }
 
 void SplitKWorkspace::alloc(DeviceArena& a, int64_t floats, int32_t ncnt) {
+  if (ws) a.free(ws);
+  if (counters) a.free(counters);
+  floats = std::max<int64_t>(floats, 64);
+  ncnt = std::max<int32_t>(ncnt, 64);
   ws = (float*)a.alloc((size_t)floats * 4);
   counters = (int32_t*)a.alloc((size_t)ncnt * 4);
   HIP_CHECK(hipMemset(counters, 0, (size_t)ncnt * 4));
@@ -491,29 +584,35 @@ struct PlanEntry {
 std::mutex g_plan_mu;
 std::unordered_map<std::string, PlanEntry>* g_plan = nullptr;
 thread_local bool g_tuning = false;
+thread_local std::vector<std::string>* g_plan_collect = nullptr;  // keys consulted by the engine being built
+std::string g_arch = "gfx950";  // device gcnArchName (base name), set by conv_plan_set_arch
+long g_tuned = 0;               // shapes tuned in this process (sa_conv_tune_count)
 
 std::string plan_file() {
   const char* e = std::getenv("SA_PLAN_CACHE");
-  return e ? std::string(e) : std::string();
+  if (!e || !e[0] || (e[0] == '0' && !e[1])) return std::string();
+  return std::string(e);
+}
+
+void load_plan_file(std::unordered_map<std::string, PlanEntry>& m, const std::string& f) {
+  std::ifstream in(f);
+  std::string key;
+  PlanEntry e;
+  while (in >> key >> e.cfg >> e.splitk >> e.us) m[key] = e;
 }
 
 std::unordered_map<std::string, PlanEntry>& plan_map() {  // caller holds g_plan_mu
   if (!g_plan) {
     g_plan = new std::unordered_map<std::string, PlanEntry>();
     const std::string f = plan_file();
-    if (!f.empty()) {
-      std::ifstream in(f);
-      std::string key;
-      PlanEntry e;
-      while (in >> key >> e.cfg >> e.splitk >> e.us) (*g_plan)[key] = e;
-    }
+    if (!f.empty()) load_plan_file(*g_plan, f);
   }
   return *g_plan;
 }
 
 std::string plan_key(const SaConvArgs& a) {
   char buf[512];
-  int n = std::snprintf(buf, sizeof(buf), "gfx950|%d,%d,%d,%d|", a.N, a.H, a.W, a.Cin);
+  int n = std::snprintf(buf, sizeof(buf), "%s|%d,%d,%d,%d|", g_arch.c_str(), a.N, a.H, a.W, a.Cin);
   for (int i = 0; i < a.nsrc; ++i) n += std::snprintf(buf + n, sizeof(buf) - n, "%d.", a.src[i].channels);
   std::snprintf(buf + n, sizeof(buf) - n, "|k%dx%dx%d|s%d,%d,%d|p%d,%d,%d|d%d,%d|o%dx%d|D%d,%d|c%d,%d|e%d,%d,%d,%d,%d|w%d",
                 a.KD, a.KH, a.KW, a.sd, a.sh, a.sw, a.pd, a.ph, a.pw, a.dh, a.dw, a.Ho, a.Wo, a.Do, a.Di, a.Cout,
@@ -594,9 +693,64 @@ size_t conv_plan_entries() {
   return plan_map().size();
 }
 
+long conv_tune_count() {
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  return g_tuned;
+}
+
+void conv_plan_clear() {
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  if (g_plan) g_plan->clear();
+}
+
+void conv_plan_set_arch(const std::string& arch) {
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  g_arch = arch.substr(0, arch.find(':'));  // "gfx950:sramecc+:xnack-" -> "gfx950"
+  if (g_arch.empty()) g_arch = "unknown";
+}
+
+const std::string& conv_plan_arch() { return g_arch; }
+
+ScopedPlanCollect::ScopedPlanCollect(std::vector<std::string>* keys) : prev(g_plan_collect) { g_plan_collect = keys; }
+ScopedPlanCollect::~ScopedPlanCollect() { g_plan_collect = prev; }
+
+int conv_plan_load(const std::string& file) {
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  auto& m = plan_map();
+  const size_t before = m.size();
+  std::ifstream in(file);
+  if (!in.good()) return -1;
+  load_plan_file(m, file);
+  return (int)(m.size() - before);
+}
+
+int conv_plan_save(const std::string& file, const std::vector<std::string>& keys) {
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  auto& m = plan_map();
+  const std::string tmp = file + ".tmp";
+  {
+    std::ofstream out(tmp);
+    if (!out.good()) return -1;
+    int n = 0;
+    std::vector<std::string> seen;
+    for (const std::string& k : keys) {
+      auto it = m.find(k);
+      if (it == m.end() || it->second.cfg < 0 || std::find(seen.begin(), seen.end(), k) != seen.end()) continue;
+      seen.push_back(k);
+      out << k << ' ' << it->second.cfg << ' ' << it->second.splitk << ' ' << it->second.us << '\n';
+      ++n;
+    }
+    if (!out.good()) return -1;
+  }
+  // atomic replace: concurrent engines (one per rank) never see a half-written plan
+  if (std::rename(tmp.c_str(), file.c_str()) != 0) return -1;
+  return 0;
+}
+
 void conv_apply_plan(SaConvArgs& a, hipStream_t s) {
   if (!env_tune_on()) return;
   const std::string key = plan_key(a);
+  if (g_plan_collect) g_plan_collect->push_back(key);
   {
     std::lock_guard<std::mutex> lk(g_plan_mu);
     auto& m = plan_map();
@@ -617,6 +771,7 @@ void conv_apply_plan(SaConvArgs& a, hipStream_t s) {
   {
     std::lock_guard<std::mutex> lk(g_plan_mu);
     plan_map()[key] = e;
+    ++g_tuned;
     const std::string f = plan_file();
     if (!f.empty() && e.cfg >= 0) {
       std::ofstream out(f, std::ios::app);

@@ -166,6 +166,10 @@ def _declare_dev(lib):
         "sa_engine_device_bytes": (C.c_longlong, [_p]),
         "sa_engine_aux_output": (_p, [_p, C.POINTER(_i)]),
         "sa_engine_stream": (_p, [_p]),
+        "sa_engine_plan_path": (C.c_char_p, [_p]),
+        "sa_engine_tuned_shapes": (C.c_long, [_p]),
+        "sa_conv_tune_count": (C.c_long, []),
+        "sa_conv_plan_clear": (None, []),
         "sa_engine_stage_times": (_i, [_p, C.POINTER(C.c_float), C.POINTER(C.c_char_p), _i]),
     }
     for name, (res, args) in sig.items():

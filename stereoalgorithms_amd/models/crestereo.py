@@ -335,3 +335,21 @@ def build(preset: str = "crestereo-iter5", seed: int = 0) -> CREStereo:
     m = CREStereo(iters=PRESETS[preset]).eval()
     randomize_norm_stats(m, seed)
     return m
+
+
+def scale_heads(m: CREStereo, flow_gain: float = 4.0, flow_bias: float = -0.3, mask_gain: float = 6.0,
+                seed: int = 0) -> CREStereo:
+    """Well-scaled flow / mask heads for full-configuration numerics tests (see raft_stereo.scale_heads):
+    the cascade then produces disparities of several pixels with spatial structure, so the AGCL windows,
+    the deformable offsets and the convex upsampling are exercised away from zero flow."""
+    g = torch.Generator().manual_seed(seed + 11)
+    ub = m.update_block
+    with torch.no_grad():
+        c2 = ub.flow_head.conv2
+        c2.weight.mul_(flow_gain)
+        c2.bias.zero_()
+        c2.bias[0] = flow_bias
+        mk = ub.mask[2]
+        mk.weight.mul_(mask_gain)
+        mk.bias.copy_(0.5 * torch.randn(mk.bias.shape, generator=g))
+    return m

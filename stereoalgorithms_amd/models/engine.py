@@ -60,6 +60,16 @@ class NativeStereoEngine:
     def device_bytes(self) -> int:
         return int(self._lib.sa_engine_device_bytes(self._h))
 
+    @property
+    def plan_path(self) -> str:
+        """Tuned-plan cache file of this engine ('' when disabled: SA_PLAN_CACHE set, SA_PLAN_DIR='')."""
+        return self._lib.sa_engine_plan_path(self._h).decode()
+
+    @property
+    def tuned_shapes(self) -> int:
+        """Conv shapes this engine had to time at build (0 when its plan file covered everything)."""
+        return int(self._lib.sa_engine_tuned_shapes(self._h))
+
     def set_Q(self, Q):
         q = np.ascontiguousarray(np.asarray(Q, dtype=np.float32).reshape(16))
         N.check(self._lib.sa_engine_set_q(self._h, q.ctypes.data_as(C.c_void_p)), "set_Q")

@@ -158,7 +158,7 @@ def _t(taps, name):
     return t[:, 0].permute(0, 3, 1, 2).contiguous() if t.shape[1] == 1 else t.permute(0, 4, 1, 2, 3).contiguous()
 
 
-@pytest.mark.parametrize("hw,batch", [((96, 128), 1), ((128, 192), 2)])
+@pytest.mark.parametrize("hw,batch", [((96, 128), 1), ((128, 192), 2), ((480, 640), 1)])
 def test_engine_chain_vs_oracle(tmp_path, hw, batch):
     """Every stage of the oracle is fed the engine's own (tapped) inputs: the top-24 / top-2 selections
     are discontinuous, so an end-to-end comparison of random-init networks is dominated by legitimate

@@ -1,0 +1,65 @@
+"""Tuned-plan cache next to the model (the analogue of the reference's
+"<onnx stem>_batch=1.engine", /root/reference/RAFTStereo/src/TRTRAFTStereo.cpp:25-46): the first engine
+of a model / shape / device arch times its conv tactics and writes the plan; a second Initialize reads it
+and times nothing.  Also pins the activation planner's footprint reduction."""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_second_initialize_skips_tuning(tmp_path, monkeypatch):
+    from stereoalgorithms_amd import _native as N
+    from stereoalgorithms_amd.models.engine import NativeStereoEngine
+    from stereoalgorithms_amd.models import raft_stereo as R
+    from stereoalgorithms_amd.utils.weights import save_model
+    monkeypatch.delenv("SA_PLAN_CACHE", raising=False)
+    monkeypatch.delenv("SA_PLAN_DIR", raising=False)
+    w = save_model(R.build("raftstereo-realtime", seed=5), tmp_path / "rt.safetensors", "raftstereo-realtime")
+    lib = N.require_native()
+    lib.sa_conv_plan_clear()
+    e1 = NativeStereoEngine("", str(w), 96, 160, batch=2, iters=3)
+    path = e1.plan_path
+    assert path.startswith(str(tmp_path)) and path.endswith(".plan"), path
+    assert "rt_b2_96x160" in os.path.basename(path) and "gfx" in os.path.basename(path)
+    assert os.path.exists(path) and e1.tuned_shapes > 0
+    entries = open(path).read().splitlines()
+    assert len(entries) >= e1.tuned_shapes
+    d1 = e1.run(*_pairs(2, 96, 160)).clone()
+    e1.close()
+    lib.sa_conv_plan_clear()  # forget the in-process plan: only the file can supply it now
+    before = lib.sa_conv_tune_count()
+    e2 = NativeStereoEngine("", str(w), 96, 160, batch=2, iters=3)
+    assert e2.tuned_shapes == 0 and lib.sa_conv_tune_count() == before
+    d2 = e2.run(*_pairs(2, 96, 160))
+    torch.cuda.synchronize()
+    assert torch.equal(d1, d2)  # same tactics => bitwise identical
+    # a different shape gets its own file
+    e3 = NativeStereoEngine("", str(w), 96, 192, batch=2, iters=3)
+    assert e3.plan_path != path and e3.tuned_shapes > 0
+
+
+def test_plan_cache_disabled(tmp_path, monkeypatch):
+    from stereoalgorithms_amd.models.engine import NativeStereoEngine
+    monkeypatch.delenv("SA_PLAN_CACHE", raising=False)
+    monkeypatch.setenv("SA_PLAN_DIR", "")
+    e = NativeStereoEngine("raftstereo-realtime", None, 64, 96, batch=1, iters=2)
+    assert e.plan_path == ""
+
+
+def _pairs(b, h, w):
+    from stereoalgorithms_amd.utils.synthetic import batch_pairs
+    l, r = batch_pairs(b, h, w, seed=3)
+    return torch.from_numpy(l).cuda(), torch.from_numpy(r).cuda()
+
+
+def test_activation_plan_footprint():
+    """b8 RAFT-Stereo sceneflow at 480x640: the encoders' activations are liveness-planned and the split-K
+    workspaces sized from the tuned plan (round 1 held 13.25 GB)."""
+    from stereoalgorithms_amd.models.engine import NativeStereoEngine
+    e = NativeStereoEngine("raftstereo-sceneflow", None, 480, 640, batch=8, iters=2)
+    gb = e.device_bytes / 1e9
+    print(f"b8 sceneflow device bytes {gb:.2f} GB")
+    assert gb < 6.0
