@@ -25,6 +25,7 @@ namespace {
 typedef _Float16 f16;
 typedef f16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ float act_apply(float v, int act, float alpha) {
   switch (act) {
@@ -67,29 +68,39 @@ enum : int {
   kGlds3 = 4,    // kFastK64's uniform-k gather issued as global->LDS DMA into a 3-deep LDS ring:
                  // 8 waves, one block per CU, counted vmcnt keeps the next stage in flight across
                  // the (raw) barrier, XCD-aware tile order
+  kWide = 5,     // wide tiles (256x256 / 512x128) for the big RAFT GRU / flow-head GEMMs: the same
+                 // uniform-k DMA gather in BK = 32 stages through a 4-deep LDS ring (3 stages in
+                 // flight), v_mfma_f32_32x32x16_f16 on a 128x64 wave tile (8 waves), one raw barrier
+                 // per stage, fragment reads software-pipelined at k16 granularity; epilogue in two
+                 // row bands (the fp32 C tile is staged through LDS one band at a time)
 };
 
 template <int BM, int BN, int WM, int WN, int MODE = kRegK32>
 struct ConvCfg {
   static constexpr bool GL = MODE == kDmaK64;
-  static constexpr int BK = MODE == kRegK32 ? 32 : 64;
+  static constexpr bool WIDE = MODE == kWide;
+  static constexpr int BK = (MODE == kRegK32 || WIDE) ? 32 : 64;
   static constexpr int KCH = BK / 8;  // 16-byte chunks per row per stage
   static constexpr int TM = BM / WM, TN = BN / WN;
-  static constexpr int FM = TM / 16, FN = TN / 16;
+  // 16x16 fragment repeats (kWide keeps its own 32x32 accumulators: a 1x1 placeholder here)
+  static constexpr int FM = WIDE ? 1 : TM / 16, FN = WIDE ? 1 : TN / 16;
   static constexpr int A_CH = BM * KCH, B_CH = BN * KCH;  // 16-byte chunks per stage
   static constexpr int NW = WM * WN, NT = 64 * NW;  // waves / threads per workgroup
   static constexpr int A_PT = (A_CH + NT - 1) / NT, B_PT = (B_CH + NT - 1) / NT;
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  // kGlds3: three-deep LDS ring; everything else double-buffered
-  static constexpr int NSTAGE = MODE == kGlds3 ? 3 : 2;
+  // kGlds3: three-deep LDS ring; kWide: four-deep; everything else double-buffered
+  static constexpr int NSTAGE = MODE == kGlds3 ? 3 : (WIDE ? 4 : 2);
   static constexpr int STAGE_BYTES = NSTAGE * (A_BYTES + B_BYTES);
   // fp32 C tile, unpadded rows; columns XOR-swizzled in 16-float blocks (cswz) so the MFMA
-  // write-out (4 row groups x 16 lanes) hits 64 distinct banks; aliases the stage buffers
+  // write-out (4 row groups x 16 lanes) hits 64 distinct banks; aliases the stage buffers.
+  // kWide stages it in bands of CROWS rows (128 KB of fp32 per band)
   static constexpr int CST = BN;
-  static constexpr int C_BYTES = BM * CST * 4;
+  static constexpr int CROWS = WIDE ? (32768 / BN < BM ? 32768 / BN : BM) : BM;
+  static constexpr int C_BYTES = CROWS * CST * 4;
   static constexpr int SMEM = STAGE_BYTES > C_BYTES ? STAGE_BYTES : C_BYTES;
-  static_assert(WM * WN == 4 || (WM * WN == 8 && MODE == kGlds3), "4 waves (4 or 8 for kGlds3) per workgroup");
+  static_assert(WM * WN == 4 || (WM * WN == 8 && (MODE == kGlds3 || WIDE)), "4 waves (8 for kGlds3; 4 or 8 for kWide) per workgroup");
   static_assert(TM % 16 == 0 && TN % 16 == 0, "wave tile must be 16-aligned");
+  static_assert(!WIDE || (TM == 128 && (TN == 64 || TN == 128)), "kWide: 128x64 or 128x128 wave tiles");
 };
 
 // swizzled byte offset of (row, 16B-chunk) inside a [rows][32 halfs] stage buffer
@@ -131,12 +142,15 @@ __device__ __forceinline__ void rs_step(float* y, int cc) {
 // s_waitcnt vmcnt(N) with a compile-time N (the asm string needs a literal)
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N <= 16, "vmcnt literal");
+  static_assert(N >= 0 && N <= 32, "vmcnt literal");
 #define SA_VMCNT_CASE(k) \
   if constexpr (N == k) asm volatile("s_waitcnt vmcnt(" SA_STR(k) ")" ::: "memory");
   SA_VMCNT_CASE(0) SA_VMCNT_CASE(1) SA_VMCNT_CASE(2) SA_VMCNT_CASE(3) SA_VMCNT_CASE(4) SA_VMCNT_CASE(5)
   SA_VMCNT_CASE(6) SA_VMCNT_CASE(7) SA_VMCNT_CASE(8) SA_VMCNT_CASE(9) SA_VMCNT_CASE(10) SA_VMCNT_CASE(11)
-  SA_VMCNT_CASE(12) SA_VMCNT_CASE(13) SA_VMCNT_CASE(14) SA_VMCNT_CASE(15) SA_VMCNT_CASE(16)
+  SA_VMCNT_CASE(12) SA_VMCNT_CASE(13) SA_VMCNT_CASE(14) SA_VMCNT_CASE(15) SA_VMCNT_CASE(16) SA_VMCNT_CASE(17)
+  SA_VMCNT_CASE(18) SA_VMCNT_CASE(19) SA_VMCNT_CASE(20) SA_VMCNT_CASE(21) SA_VMCNT_CASE(22) SA_VMCNT_CASE(23)
+  SA_VMCNT_CASE(24) SA_VMCNT_CASE(25) SA_VMCNT_CASE(26) SA_VMCNT_CASE(27) SA_VMCNT_CASE(28) SA_VMCNT_CASE(29)
+  SA_VMCNT_CASE(30) SA_VMCNT_CASE(31) SA_VMCNT_CASE(32)
 #undef SA_VMCNT_CASE
 }
 
@@ -162,7 +176,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
   // ids round-robin over the 8 XCDs, so give each XCD a contiguous run of m-major tiles (neighbour
   // tiles share input rows through the 3x3 halo, the n tiles of one m share the whole A panel)
   int bx = blockIdx.x, by = blockIdx.y;
-  if constexpr (MODE == kGlds3) {
+  if constexpr (MODE == kGlds3 || MODE == kWide) {
     const int nwg = gridDim.x * gridDim.y;
     const int bid = blockIdx.y * gridDim.x + blockIdx.x;
     const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
@@ -185,6 +199,17 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
   for (int i = 0; i < C::FM; ++i)
 #pragma unroll
     for (int j = 0; j < C::FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // kWide: 4 x (2 or 4) blocks of 32x32 per wave (C/D: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5))
+  constexpr int WFM = C::WIDE ? 4 : 1, WFN = C::WIDE ? C::TN / 32 : 1;
+  floatx16 acc32[WFM][WFN];
+  if constexpr (C::WIDE) {
+#pragma unroll
+    for (int i = 0; i < WFM; ++i)
+#pragma unroll
+      for (int j = 0; j < WFN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc32[i][j][r] = 0.f;
+  }
   if constexpr (MODE == kFastK64) {
     // ---------------- uniform-k im2col, register staged, BK = 64 ----------------
     constexpr int RPT = C::A_PT;  // A rows per thread: (tid >> 3) + 32 i
@@ -490,6 +515,203 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
       cur = nxt;
     }
     __syncthreads();  // all fragment reads done before the epilogue reuses LDS
+  } else if constexpr (MODE == kWide) {
+    // ---------------- wide tile: uniform-k DMA gather, BK = 32, 4-deep LDS ring, 32x32x16 MFMA ----------
+    // Stage image per operand: [rows][32 halfs] (64-B rows), lane-linear per wave instruction (16 rows x 4
+    // chunks per 1 KB DMA piece) with the chunk XOR ((row >> 2) & 3) applied on the SOURCE side and on
+    // the fragment reads (same involution; cdna_hip_programming.md §5.4 rule 21): the 16 lanes of each
+    // ds_read_b128 group then hit 16 distinct 16-B bank slots.
+    // Schedule of stage t (buffer t % 4; stages t+1..t+3 in flight at its start):
+    //   [A] MFMAs of k16 half 0 (fragments X) + fragment reads of half 1 (-> Y)
+    //   lgkmcnt(0); vmcnt(<= 2 stages); raw s_barrier   -- stage t+1 has landed for every wave and every
+    //                                                     wave is done reading buffer t % 4
+    //   DMA of stage t+4 into buffer t % 4
+    //   [B] MFMAs of half 1 (Y) + fragment reads of stage t+1 half 0 (-> X)
+    // so every stage has three stages of MFMA work to land and LDS reads always run under MFMAs.
+    constexpr int NA = BM * 4 / NT, NB = BN * 4 / NT;  // 1-KB DMA pieces per thread per stage
+    static_assert(NA * NT == BM * 4 && NB * NT == BN * 4 && NA >= 1 && NB >= 1, "whole-wave DMA pieces");
+    constexpr int NAB = NA + NB;
+    constexpr int STG = (BM + BN) * 64;
+    static_assert(4 * STG <= C::SMEM, "ring fits");
+    const int KH = p.KH, KW = p.KW;
+    int pixb[NA];
+    unsigned long long vmask[NA];
+    int lcho[NA];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int row = (wave * NA + i) * 16 + (lane >> 2);
+      lcho[i] = (((lane & 3) ^ ((row >> 2) & 3)) << 3);
+      const int m = m0 + row;
+      const bool ok = m < M;
+      const int mm = ok ? m : 0;
+      const int img = mm / HWo;
+      const int r = mm - img * HWo;
+      const int oh = r / p.Wo, ow = r - oh * p.Wo;
+      const int n = img / Do, od = img - n * Do;
+      const int ih0 = oh * p.sh - p.ph, iw0 = ow * p.sw - p.pw, id0 = od * sd - p.pd;
+      pixb[i] = ((n * Di + id0) * p.H + ih0) * p.W + iw0;
+      unsigned long long mk = 0ull;
+      int t = 0;
+      for (int kd = 0; kd < KD; ++kd)
+        for (int kh = 0; kh < KH; ++kh)
+          for (int kw = 0; kw < KW; ++kw, ++t) {
+            const int dd = id0 + kd, ih = ih0 + kh * p.dh, iw = iw0 + kw * p.dw;
+            if (ok && dd >= 0 && dd < Di && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W) mk |= 1ull << t;
+          }
+      vmask[i] = mk;
+    }
+    // K loop in channel-chunk-major order: for each 32-channel chunk, all KD*KH*KW taps.  Consecutive
+    // stages then re-read the same input pixels shifted by one tap (L1 / L2 reuse distance of one stage);
+    // tap-major order streams a whole tile's A panel between two uses and thrashes the XCD's L2 once 32
+    // CUs each hold a different 256-row panel.  (kWide is never split: kt0 = 0.)
+    const int taps_all = KD * KH * KW;
+    int tap = 0, ci0 = 0, kh_ = 0, kw_ = 0;
+    int toff = 0;
+    const int sb1 = p.src[0].channels;
+    const int sb2 = sb1 + (p.nsrc > 1 ? p.src[1].channels : 0);
+    const int sb3 = sb2 + (p.nsrc > 2 ? p.src[2].channels : 0);
+    const f16* sp0 = reinterpret_cast<const f16*>(p.src[0].ptr);
+    const f16* sp1 = reinterpret_cast<const f16*>(p.src[p.nsrc > 1 ? 1 : 0].ptr);
+    const f16* sp2 = reinterpret_cast<const f16*>(p.src[p.nsrc > 2 ? 2 : 0].ptr);
+    const f16* sp3 = reinterpret_cast<const f16*>(p.src[p.nsrc > 3 ? 3 : 0].ptr);
+    const int ss0 = p.src[0].stride, ss1 = p.src[p.nsrc > 1 ? 1 : 0].stride;
+    const int ss2 = p.src[p.nsrc > 2 ? 2 : 0].stride, ss3 = p.src[p.nsrc > 3 ? 3 : 0].stride;
+    // weight rows past the packed Cout (a multiple of 128, ConvLayer::upload) re-read the last packed row:
+    // those output columns are never stored (nvalid), and a finite row keeps them finite
+    const int cout_pad = (p.Cout + 127) & ~127;
+    const f16* wrow[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int row = (wave * NB + j) * 16 + (lane >> 2);
+      const int lch = (lane & 3) ^ ((row >> 2) & 3);
+      const int wr = n0 + row < cout_pad ? n0 + row : cout_pad - 1;
+      wrow[j] = reinterpret_cast<const f16*>(p.weight) + (size_t)wr * p.Kpad + lch * 8;
+    }
+    const void* zero_src = g_zero16;
+    auto issue = [&](int buf) {
+      char* sa = smem + buf * STG;
+      char* sb = sa + BM * 64;
+      const f16* sp;
+      int sst;
+      if (ci0 < sb1) { sp = sp0 + ci0; sst = ss0; }
+      else if (ci0 < sb2) { sp = sp1 + (ci0 - sb1); sst = ss1; }
+      else if (ci0 < sb3) { sp = sp2 + (ci0 - sb2); sst = ss2; }
+      else { sp = sp3 + (ci0 - sb3); sst = ss3; }
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const bool v = (vmask[i] >> tap) & 1ull;
+        const f16* ga = sp + ((pixb[i] + toff) * sst + lcho[i]);
+        __builtin_amdgcn_global_load_lds(v ? (const void*)ga : zero_src, (lds_void_t*)(sa + (wave * NA + i) * 1024), 16, 0, 0);
+      }
+      const int koff = tap * p.Cin + ci0;  // packed K order is (tap, channel)
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        // (explicit void* source: a conditional or typed source makes the host pass drop the kernel stub)
+        __builtin_amdgcn_global_load_lds((const void*)(wrow[j] + koff), (lds_void_t*)(sb + (wave * NB + j) * 1024), 16, 0, 0);
+      // next tap; after the last tap the next 32-channel chunk
+      ++tap;
+      ++kw_;
+      toff += p.dw;
+      if (kw_ == KW) {
+        kw_ = 0;
+        toff += p.dh * p.W - KW * p.dw;
+        ++kh_;
+        if (kh_ == KH) {
+          kh_ = 0;
+          toff += p.H * p.W - KH * p.dh * p.W;
+        }
+      }
+      if (tap == taps_all) {
+        tap = 0;
+        toff = 0;
+        ci0 += 32;
+      }
+    };
+    // 32x32x16 fragments of k16 half h of the stage in `buf`: lane = (r, hl) holds row r, k = 16h + 8hl..+7
+    const int fr = lane & 31, fh = lane >> 5;
+    auto frag = [&](const char* base, int row, int h) {
+      return *reinterpret_cast<const half8*>(base + row * 64 + (((2 * h + fh) ^ ((row >> 2) & 3)) << 4));
+    };
+    auto read = [&](int buf, int h, half8* a, half8* b) {
+      const char* sa = smem + buf * STG;
+      const char* sb = sa + BM * 64;
+#pragma unroll
+      for (int i = 0; i < WFM; ++i) a[i] = frag(sa, wm * 128 + i * 32 + fr, h);
+#pragma unroll
+      for (int j = 0; j < WFN; ++j) b[j] = frag(sb, wn * C::TN + j * 32 + fr, h);
+    };
+    // 8 MFMAs on (a, b) with the 6 fragment reads of (buf, h) interleaved, one per MFMA slot.
+    // SA_EXP_* (tools/exp_build.sh, timing experiments only -- results are garbage): NOMFMA drops the
+    // MFMAs (operands kept live), NOLDSREAD the fragment reads, NODMA the in-loop DMA, NOBAR the barrier
+    auto mfma_read = [&](const half8* a, const half8* b, int buf, int h, half8* ar, half8* br) {
+      const char* sa = smem + buf * STG;
+      const char* sb = sa + BM * 64;
+#pragma unroll
+      for (int t = 0; t < WFM * WFN; ++t) {
+        const int i = t / WFN, j = t % WFN;
+#ifdef SA_EXP_NOMFMA
+        asm volatile("" ::"v"(a[i]), "v"(b[j]));
+#else
+        acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc32[i][j], 0, 0, 0);
+#endif
+#ifndef SA_EXP_NOLDSREAD
+        if (t < WFM) ar[t] = frag(sa, wm * 128 + t * 32 + fr, h);
+        else if (t < WFM + WFN) br[t - WFM] = frag(sb, wn * C::TN + (t - WFM) * 32 + fr, h);
+#endif
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+#pragma unroll
+      for (int t = 0; t < WFM + WFN; ++t) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, WFM * WFN - WFM - WFN - 1, 0);
+    };
+    auto mfma_only = [&](const half8* a, const half8* b) {
+#pragma unroll
+      for (int t = 0; t < WFM * WFN; ++t) {
+        const int i = t / WFN, j = t % WFN;
+        acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc32[i][j], 0, 0, 0);
+      }
+    };
+    half8 xa[WFM], xb[WFN], ya[WFM], yb[WFN];
+    // prologue: stages 0..3 in flight, wait for stage 0
+    if (nk > 0) issue(0);
+    if (nk > 1) issue(1);
+    if (nk > 2) issue(2);
+    if (nk > 3) issue(3);
+    if (nk > 3) wait_vmcnt<3 * NAB>();
+    else if (nk > 2) wait_vmcnt<2 * NAB>();
+    else if (nk > 1) wait_vmcnt<NAB>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (nk > 0) read(0, 0, xa, xb);
+    // the last stage is peeled so the loop body has one control path for the accumulators (a branch
+    // around the MFMAs makes the compiler copy all 128 of them at the merge)
+    for (int kt = 0; kt < nk - 1; ++kt) {
+      const int cur = kt & 3;
+      mfma_read(xa, xb, cur, 1, ya, yb);  // [A]
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // stage kt+1 must have landed; stages issued beyond it may stay in flight
+      const int ahead = (nk - 1 < kt + 3 ? nk - 1 : kt + 3) - (kt + 1);
+      if (ahead >= 2) wait_vmcnt<2 * NAB>();
+      else if (ahead == 1) wait_vmcnt<NAB>();
+      else wait_vmcnt<0>();
+#ifndef SA_EXP_NOBAR
+      __builtin_amdgcn_s_barrier();
+#endif
+      asm volatile("" ::: "memory");
+#ifndef SA_EXP_NODMA
+      if (kt + 4 < nk) issue(cur);
+#endif
+      mfma_read(ya, yb, (kt + 1) & 3, 0, xa, xb);  // [B]
+    }
+    if (nk > 0) {
+      mfma_read(xa, xb, (nk - 1) & 3, 1, ya, yb);
+      mfma_only(ya, yb);
+    }
+    __syncthreads();  // all fragment reads done before the epilogue reuses LDS
   } else if constexpr (C::GL) {
     // ---------------- DMA staging: [rows][64 halfs] (128 B) per stage, chunk XOR-swizzled ----------
     // LDS image is lane-linear per wave instruction (q*16 = row*128 + pch*16); the swizzle lives on
@@ -751,7 +973,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
   // ---------------- split-K: partial slabs + last-arriver reduction ----------------
   // Protocol of cdna_hip_programming.md "Projection GEMM at M = 256" item 2 (agent-scope release
   // by every slice, acquire by the last arriver), valid for any placement of slices over XCDs.
-  if (S > 1) {
+  if (!C::WIDE && S > 1) {  // (kWide is always launched unsplit)
     const int tile = by * gridDim.x + bx;
     constexpr int SLAB = BM * BN;
     float* slab = p.ws + ((size_t)tile * S + z) * SLAB;
@@ -838,17 +1060,19 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
 #pragma unroll
   for (int j = 0; j < 8; ++j) bias8[j] = (p.bias && j < nvalid) ? p.bias[co + j] : 0.f;
 
+  if constexpr (!C::WIDE) {
 #pragma unroll
-  for (int i = 0; i < C::FM; ++i)
+    for (int i = 0; i < C::FM; ++i)
 #pragma unroll
-    for (int j = 0; j < C::FN; ++j)
+      for (int j = 0; j < C::FN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int row = wm * C::TM + i * 16 + (lane >> 4) * 4 + r;
-        int col = wn * C::TN + j * 16 + (lane & 15);
-        ct[row * C::CST + cswz(row, col)] = acc[i][j][r];
-      }
-  __syncthreads();
+        for (int r = 0; r < 4; ++r) {
+          int row = wm * C::TM + i * 16 + (lane >> 4) * 4 + r;
+          int col = wn * C::TN + j * 16 + (lane & 15);
+          ct[row * C::CST + cswz(row, col)] = acc[i][j][r];
+        }
+    __syncthreads();
+  }
 
   // SA_EPI_PROJ: this thread's 8 channels of the projection taps, hoisted out of the row loop
   constexpr int kProjMax = PROJ ? 9 : 1;
@@ -864,12 +1088,14 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
 #pragma unroll
       for (int j = 0; j < 8; ++j) pw8[t][j] = (t < np && j < nvalid) ? pwb[(size_t)t * p.Cout + j] : 0.f;
   }
-  if (nvalid > 0) {
-    for (int row = tid / CPR; row < BM; row += RPI) {
+  // rows [r0, r1) of the tile, their C values staged in LDS at row - cbase
+  auto epi_rows = [&](const int r0, const int r1, const int cbase) {
+    for (int row = r0 + tid / CPR; row < r1; row += RPI) {
       const int m = m0 + row;
       if (m >= M) break;
       float v[8];
-      const float* cp = ct + row * C::CST + cswz(row, cc * 8);
+      const int crow = row - cbase;
+      const float* cp = ct + crow * C::CST + cswz(crow, cc * 8);
       floatx4 c0 = *reinterpret_cast<const floatx4*>(cp);
       floatx4 c1 = *reinterpret_cast<const floatx4*>(cp + 4);
       v[0] = c0[0]; v[1] = c0[1]; v[2] = c0[2]; v[3] = c0[3];
@@ -1024,6 +1250,30 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
         }
       }
     }
+  };
+  if constexpr (C::WIDE) {
+    // two row bands: the waves owning a band's rows stage their 32x32 accumulators, everyone stores
+#pragma unroll
+    for (int band = 0; band < BM / C::CROWS; ++band) {
+      const int b0 = band * C::CROWS;
+      if (wm * 128 >= b0 && wm * 128 < b0 + C::CROWS) {
+#pragma unroll
+        for (int i = 0; i < WFM; ++i)
+#pragma unroll
+          for (int j = 0; j < WFN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) - b0;
+              const int col = wn * C::TN + j * 32 + (lane & 31);
+              ct[row * C::CST + cswz(row, col)] = acc32[i][j][r];
+            }
+      }
+      __syncthreads();
+      if (nvalid > 0) epi_rows(b0, b0 + C::CROWS, b0);
+      __syncthreads();  // band consumed before the next one overwrites the staging LDS
+    }
+  } else {
+    if (nvalid > 0) epi_rows(0, BM, 0);
   }
   if (do_stats) {
     if (!block_reduce) {
@@ -1170,6 +1420,19 @@ int launch_glds3(const SaConvArgs* a, hipStream_t stream, bool forced) {
   return (int)hipGetLastError();
 }
 
+// kWide launcher (8 waves, 1 block per CU, never split): uniform-k gather, no projection epilogue.
+// Returns 1 when the shape does not qualify.
+template <int BM, int BN, int WM, int WN>
+int launch_wide(const SaConvArgs* a, hipStream_t stream) {
+  if (!glds3_eligible(a) || a->epi == SA_EPI_PROJ || a->splitk > 1) return 1;
+  const int M = a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
+  const int gx = (M + BM - 1) / BM, gy = (a->Cout + BN - 1) / BN;
+  note_split(1, 0, 0);
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, kWide, false>), dim3(gx, gy, 1), dim3(64 * WM * WN), 0,
+                     stream, *a);
+  return (int)hipGetLastError();
+}
+
 // the uniform-k DMA kernels need every source a multiple of 64 channels, K unpadded, <= 64 taps
 bool glds3_eligible(const SaConvArgs* a) {
   const int taps = (a->KD > 0 ? a->KD : 1) * a->KH * a->KW;
@@ -1203,7 +1466,8 @@ int pick_cfg(const SaConvArgs* a) {
 
 int cfg_bn(int cfg) {
   switch (cfg) {
-    case 0: case 4: case 6: case 7: return 128;
+    case 10: case 12: return 256;
+    case 0: case 4: case 6: case 7: case 11: case 13: return 128;
     case 1: case 3: case 5: case 8: case 9: return 64;
     case 2: return 16;
     default: return 0;
@@ -1253,6 +1517,15 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
                   : cfg == 6 ? launch_glds3<128, 128, 2, 2>(a, stream, true)
                   : cfg == 7 ? launch_glds3<128, 128, 2, 4>(a, stream, true)
                              : launch_glds3<256, 64, 4, 2>(a, stream, true);
+      return r == 1 ? -5 : r;
+    }
+    case 10: case 11: case 12: case 13: {
+      // 10 / 11: 8 waves of 128x64 (2 per SIMD); 12 / 13: 4 waves of 128x128 (1 per SIMD, 512-VGPR budget,
+      // a third less LDS read traffic per MFMA)
+      const int r = cfg == 10 ? launch_wide<256, 256, 2, 4>(a, stream)
+                  : cfg == 11 ? launch_wide<512, 128, 4, 2>(a, stream)
+                  : cfg == 12 ? launch_wide<256, 256, 2, 2>(a, stream)
+                              : launch_wide<512, 128, 4, 1>(a, stream);
       return r == 1 ? -5 : r;
     }
     default: return -3;

@@ -651,11 +651,15 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
   HIP_CHECK(hipEventCreate(&e1));
   PlanEntry best{-1, 1, 1e30f};
   const bool can_split = a.ws && a.counters && !a.stats;
-  for (int cfg = 0; cfg <= 9; ++cfg) {
+  // (cfgs 12 / 13, the 4-wave wide tiles, lose everywhere on MI355X (tools/conv_bench.py): not timed)
+  for (int cfg = 0; cfg <= 11; ++cfg) {
     if (cfg == 2 && a.Cout > 32) continue;  // 256x16 tile: narrow outputs only
     if (cfg == 6) continue;                 // 128x128 / 4 waves: never competitive (conv_bench)
+    // wide tiles (one block per CU, never split): only where their grid still covers the chip
+    if ((cfg == 10 || cfg == 12) && (a.Cout <= 128 || ((M + 255) / 256) * ((a.Cout + 255) / 256) < 256)) continue;
+    if ((cfg == 11 || cfg == 13) && ((M + 511) / 512) * ((a.Cout + 127) / 128) < 256) continue;
     for (int sk : {1, 0}) {
-      if (sk == 0 && (!can_split || cfg == 9)) continue;
+      if (sk == 0 && (!can_split || cfg >= 9)) continue;
       t.tile_cfg = cfg;
       t.splitk = sk;
       if (sa_conv2d(&t, s) != 0) {

@@ -33,7 +33,10 @@ def dev():
     global _dev
     if _dev is None:
         import torch  # noqa: F401  (bind to torch's HIP runtime)
-        _dev = _load("libstereo_amd.so")
+        # SA_NATIVE_LIB: an alternative build of the device library (kernel A/B experiments, e.g.
+        # tools/exp_build.sh variants); it must export the same C API
+        alt = os.environ.get("SA_NATIVE_LIB")
+        _dev = C.CDLL(alt, mode=C.RTLD_GLOBAL) if alt else _load("libstereo_amd.so")
         _declare_dev(_dev)
     return _dev
 

@@ -1,26 +1,43 @@
-"""HITNet PyTorch oracle (fp32, NCHW), preset ``hitnet-d400``.
+"""HITNet PyTorch oracle (fp32, NCHW), presets ``hitnet-d400`` and ``hitnet-xl``.
 
-Reference pin: HitNet/src/HitNet.cpp:13-17,69-78 — one 6-channel input ``input`` [1,6,480,640] =
+Reference pins: HitNet/src/HitNet.cpp:13-17,69-78 — one 6-channel input ``input`` [1,6,480,640] =
 [left RGB; right RGB] / 255 (HitNet_preprocess.cu:19-51), output ``reference_output_disparity`` H*W
 positive disparity; the benchmarked export is ``middlebury_d400`` (HitNet/test/main.cpp:9,
-README_en.md:171,192), i.e. a maximum disparity of 400 px at full resolution.  The reference only ships
-that I/O contract (the network is a PINTO TF->ONNX export), so this is a re-implementation of the
-published architecture (Tankovich et al., "HITNet: Hierarchical Iterative Tile Refinement Network for
-Real-time Stereo Matching", CVPR 2021) with our own parameter names:
+README_en.md:171,192, max disparity 400 px at full resolution); README_en.md:171 also lists
+``flyingthings_finalpass_xl`` (no latency published, README_en.md:192-194).  The reference ships only that
+I/O contract (the networks are PINTO TF->ONNX exports of the authors' saved models, not in the repo and
+not downloadable here), so this is a re-implementation of the published architecture (Tankovich et al.,
+"HITNet: Hierarchical Iterative Tile Refinement Network for Real-time Stereo Matching", CVPR 2021, §3)
+with our own parameter names.  Parity with the upstream weights is therefore unpinned.
 
-  * U-Net feature extractor, 5 levels (1 .. 1/16), channels 16,16,24,24,32, LeakyReLU(0.2); strided
-    2x2 convs down, 2x2 transposed convs up, skip concatenation + 1x1 merge + 3x3 conv.
-  * Tile hypotheses on levels 0..3: a 4x4/stride-4 tile embedding of the left features and the same
-    conv at stride (4,1) on the right; L1 matching cost over every integer disparity of the level
-    (400 >> l), argmin -> d_init; descriptor p = MLP(cost, tile feature) (13 channels).
-    A hypothesis is h = [d, dx, dy, p] (16 channels), d in level-l pixels.
-  * Propagation coarse -> fine: level 3 refines its own init; levels 2..0 refine two candidates
-    (the slanted-plane upsampled hypothesis of the coarser level and the level's own init).  Each
-    candidate gets a local cost: the 4x4 tile pixels warped into the right features along x at
-    d + dx*u + dy*v (+-1 shifts), L1 over channels -> 48 features; [cost, h] -> 1x1 conv + two
-    dilated residual blocks + 3x3 conv -> (delta h, confidence).  The refined candidate with the highest
-    confidence wins (hard selection, inference-mode HITNet).
-  * Final slanted-plane expansion of the level-0 tiles to full resolution.
+Architecture (paper section in brackets):
+
+  * Feature extractor [§3.1]: U-Net, 5 levels e_0 .. e_4 at 1 .. 1/16, LeakyReLU(0.2); strided 2x2 convs
+    down, 2x2 transposed convs up, skip concatenation + 1x1 merge + 3x3 conv.  Channels (16,16,24,24,32)
+    for d400, (32,32,48,48,64) for XL.
+  * Initialisation [§3.2] on levels 0..3 (4x4 tiles, so the tile grids are 1/4 .. 1/32 of the input; a
+    480x640 input has no integral 1/64 grid, which pins the coarsest hypothesis level to 3): a 4x4 /
+    stride-4 tile embedding of the left features and the same conv at stride (4,1) on the right; L1 cost of
+    the 16-channel tile features over every integer disparity of the level (maxdisp >> l), argmin -> d_init;
+    descriptor p = MLP(cost, tile feature) (13 channels).  A hypothesis is h = [d, dx, dy, p] (16 channels),
+    d in level-l pixels, slanted plane d + dx * u + dy * v over the tile.
+  * Propagation [§3.3], coarse -> fine: level 3 refines its own init; levels 2..0 refine TWO candidates
+    jointly, the slanted-plane 2x upsampling of the coarser level's winner and the level's own init.  Each
+    candidate gets a local cost from warping: the 16 tile pixels of the left features against the right
+    features sampled (linear interpolation along x, zeros outside) at the candidate's plane disparity and
+    at +-1, L1 over channels -> 48 costs.  The update network sees all candidates at once
+    ([cost_k, h_k] for every k concatenated), 1x1 conv -> residual blocks with a dilation schedule ->
+    3x3 conv -> per candidate (delta h_k, confidence w_k); the refined candidate with the highest confidence
+    wins (inference-mode HITNet: argmax of the confidences).
+  * Final refinement [§3.3, the propagation steps below the tile resolution]: the level-0 winner is split
+    into 2x2 tiles (plane evaluated at each sub-tile centre) and refined once more with the same warping
+    cost (4 pixels x 3 shifts) and a residual update network (one hypothesis, no init), then split into
+    1x1 tiles (per pixel, full resolution) and refined again (1 pixel x 3 shifts).  Output = max(d, 0).
+
+Choices not fixed by the published description (documented deviations, all shared by the native engine):
+update-network width 32 (XL 64); residual dilations (1, 2, 4) per level (XL (1, 2, 4, 8, 1)); refinement
+widths 32 / 16 (XL 48 / 24) with dilations (1, 2) / (1, 1); XL max disparity 320; the local cost uses the
+level's full feature vector (paper: learned tile features of the same width).
 
 This module is the numerics oracle for csrc/models/hitnet.cpp and the source of seeded random weights.
 """
@@ -30,8 +47,12 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-PRESETS = {"hitnet-d400": dict(maxdisp=400)}
-CH = [16, 16, 24, 24, 32]
+PRESETS = {
+    "hitnet-d400": dict(maxdisp=400, ch=(16, 16, 24, 24, 32), width=32, dils=(1, 2, 4),
+                        refine=((32, (1, 2)), (16, (1, 1)))),
+    "hitnet-xl": dict(maxdisp=320, ch=(32, 32, 48, 48, 64), width=64, dils=(1, 2, 4, 8, 1),
+                      refine=((48, (1, 2)), (24, (1, 1)))),
+}
 HYP_LEVELS = 4  # tile hypotheses on feature levels 0..3
 SLOPE = 0.2
 
@@ -54,14 +75,14 @@ class UpBlock(nn.Module):
 
 
 class FeatureUNet(nn.Module):
-    def __init__(self):
+    def __init__(self, ch):
         super().__init__()
-        down = [nn.ModuleList([nn.Conv2d(3, CH[0], 3, 1, 1), nn.Conv2d(CH[0], CH[0], 3, 1, 1)])]
+        down = [nn.ModuleList([nn.Conv2d(3, ch[0], 3, 1, 1), nn.Conv2d(ch[0], ch[0], 3, 1, 1)])]
         for l in range(1, 5):
-            down.append(nn.ModuleList([nn.Conv2d(CH[l - 1], CH[l], 2, 2), nn.Conv2d(CH[l], CH[l], 3, 1, 1),
-                                       nn.Conv2d(CH[l], CH[l], 3, 1, 1)]))
+            down.append(nn.ModuleList([nn.Conv2d(ch[l - 1], ch[l], 2, 2), nn.Conv2d(ch[l], ch[l], 3, 1, 1),
+                                       nn.Conv2d(ch[l], ch[l], 3, 1, 1)]))
         self.down = nn.ModuleList(down)
-        self.up = nn.ModuleList([UpBlock(CH[l + 1], CH[l]) for l in range(4)])
+        self.up = nn.ModuleList([UpBlock(ch[l + 1], ch[l]) for l in range(4)])
 
     def forward(self, x):
         d = []
@@ -118,38 +139,58 @@ class ResBlock(nn.Module):
         return lrelu(x + self.conv2(lrelu(self.conv1(x))))
 
 
-class Propagation(nn.Module):
-    def __init__(self, dils=(1, 2)):
-        super().__init__()
-        self.inp = nn.Conv2d(64, 32, 1)
-        self.res = nn.ModuleList([ResBlock(32, d) for d in dils])
-        self.out = nn.Conv2d(32, 17, 3, 1, 1)
+def cost_channels(t: int) -> int:
+    return 3 * t * t
 
-    def forward(self, cost, h):
-        x = lrelu(self.inp(torch.cat((cost, h), 1)))
+
+class UpdateNet(nn.Module):
+    """Joint update of ``ncand`` hypotheses of tile size ``t``: input [cost_k (3 t^2), h_k (16)] for every
+    candidate k, output per candidate 16 deltas (+ a confidence when ncand > 1, or always for levels)."""
+
+    def __init__(self, t: int, ncand: int, width: int, dils, conf: bool = True):
+        super().__init__()
+        self.t, self.ncand, self.conf = t, ncand, conf
+        self.cin = cost_channels(t) + 16
+        self.nout = 17 if conf else 16
+        self.inp = nn.Conv2d(ncand * self.cin, width, 1)
+        self.res = nn.ModuleList([ResBlock(width, d) for d in dils])
+        self.out = nn.Conv2d(width, ncand * self.nout, 3, 1, 1)
+
+    def forward(self, costs, hyps):
+        """costs/hyps: lists over candidates of [B,3t^2,h,w] / [B,16,h,w] -> (refined list, confidences)."""
+        x = torch.cat([torch.cat((c, h), 1) for c, h in zip(costs, hyps)], 1)
+        x = lrelu(self.inp(x))
         for r in self.res:
             x = r(x)
         y = self.out(x)
-        hn = h + y[:, :16]
-        hn = torch.cat((hn[:, :1].clamp_min(0), hn[:, 1:]), 1)
-        return hn, y[:, 16:17]
+        outs, confs = [], []
+        for k, h in enumerate(hyps):
+            yk = y[:, k * self.nout:(k + 1) * self.nout]
+            hn = h + yk[:, :16]
+            outs.append(torch.cat((hn[:, :1].clamp_min(0), hn[:, 1:]), 1))
+            confs.append(yk[:, 16:17] if self.conf else None)
+        return outs, confs
 
 
-def tile_offsets(device):
-    """(u, v) pixel offsets of the 16 tile pixels relative to the tile centre, channel k = v*4 + u."""
-    r = torch.arange(4, device=device, dtype=torch.float32) - 1.5
+def tile_offsets(t: int, device):
+    """(u, v) pixel offsets of the t*t tile pixels relative to the tile centre, channel k = v*t + u."""
+    r = torch.arange(t, device=device, dtype=torch.float32) - (t - 1) / 2.0
     v, u = torch.meshgrid(r, r, indexing="ij")
-    return u.reshape(16), v.reshape(16)
+    return u.reshape(t * t), v.reshape(t * t)
 
 
-def warp_cost(el, er, h):
-    """Local L1 cost of each tile's 16 pixels at the plane disparity (+-1): [B,48,h,w], channel s*16 + v*4 + u."""
+def plane_pixels(h, t: int):
+    """Per-pixel plane disparity of t x t tiles: [B,1,t*th,t*tw]."""
+    u, v = tile_offsets(t, h.device)
+    d = h[:, 0:1] + h[:, 1:2] * u.view(1, -1, 1, 1) + h[:, 2:3] * v.view(1, -1, 1, 1)  # [B,t*t,th,tw]
+    return F.pixel_shuffle(d, t) if t > 1 else d
+
+
+def warp_cost(el, er, h, t: int = 4):
+    """Local L1 cost of each tile's t*t pixels at the plane disparity (+-1): [B,3t^2,th,tw],
+    channel s*t^2 + v*t + u."""
     b, c, H, W = el.shape
-    th, tw = h.shape[-2:]
-    u, v = tile_offsets(el.device)
-    # per-pixel plane disparity at full level resolution
-    d = h[:, 0:1] + h[:, 1:2] * u.view(1, 16, 1, 1) + h[:, 2:3] * v.view(1, 16, 1, 1)  # [B,16,th,tw]
-    dpix = F.pixel_shuffle(d, 4)  # [B,1,H,W]: channel v*4+u -> pixel (4y+v, 4x+u)
+    dpix = plane_pixels(h, t)  # [B,1,H,W]
     xs = torch.arange(W, device=el.device, dtype=torch.float32).view(1, 1, 1, W)
     out = []
     for s in (-1.0, 0.0, 1.0):
@@ -157,18 +198,18 @@ def warp_cost(el, er, h):
         x0 = torch.floor(xr)
         a = xr - x0
         acc = torch.zeros(b, c, H, W, device=el.device)
-        for t, wt in ((0, 1 - a), (1, a)):
-            xi = x0 + t
+        for k, wt in ((0, 1 - a), (1, a)):
+            xi = x0 + k
             ok = (xi >= 0) & (xi <= W - 1)
             g = torch.gather(er, 3, xi.clamp(0, W - 1).long().expand(b, c, H, W))
             acc = acc + g * (wt * ok)
         cost = (el - acc).abs().sum(1, keepdim=True)  # [B,1,H,W]
-        out.append(F.pixel_unshuffle(cost, 4))  # [B,16,th,tw]
+        out.append(F.pixel_unshuffle(cost, t) if t > 1 else cost)  # [B,t*t,th,tw]
     return torch.cat(out, 1)
 
 
 def upsample_hyp(h):
-    """Slanted-plane 2x upsampling of tile hypotheses to the next finer level."""
+    """Slanted-plane 2x upsampling of tile hypotheses to the next finer feature level (d doubles)."""
     b, c, th, tw = h.shape
     up = F.interpolate(h, scale_factor=2, mode="nearest")
     oy = (torch.arange(2 * th, device=h.device) % 2 * 2 - 1).float().view(1, 1, 2 * th, 1)
@@ -177,19 +218,49 @@ def upsample_hyp(h):
     return torch.cat((d, up[:, 1:]), 1)
 
 
-def expand_final(h):
-    u, v = tile_offsets(h.device)
-    d = h[:, 0:1] + h[:, 1:2] * u.view(1, 16, 1, 1) + h[:, 2:3] * v.view(1, 16, 1, 1)
-    return F.pixel_shuffle(d, 4)[:, 0].clamp_min(0)
+def split_hyp(h, t: int):
+    """Split t x t tiles into (t/2) x (t/2) tiles of the same level: the plane is evaluated at each sub-tile
+    centre (offsets +-t/4 pixels), slopes and descriptor copied."""
+    b, c, th, tw = h.shape
+    up = F.interpolate(h, scale_factor=2, mode="nearest")
+    q = t / 4.0
+    oy = ((torch.arange(2 * th, device=h.device) % 2) * 2 - 1).float().view(1, 1, 2 * th, 1) * q
+    ox = ((torch.arange(2 * tw, device=h.device) % 2) * 2 - 1).float().view(1, 1, 1, 2 * tw) * q
+    d = up[:, 0:1] + up[:, 1:2] * ox + up[:, 2:3] * oy
+    return torch.cat((d, up[:, 1:]), 1)
+
+
+def expand_final(h, t: int = 1):
+    """Disparity map from tile hypotheses of size t (plane evaluated per pixel), clamped at 0."""
+    return plane_pixels(h, t)[:, 0].clamp_min(0)
 
 
 class HITNet(nn.Module):
-    def __init__(self, maxdisp=400):
+    def __init__(self, maxdisp=400, ch=(16, 16, 24, 24, 32), width=32, dils=(1, 2, 4),
+                 refine=((32, (1, 2)), (16, (1, 1)))):
         super().__init__()
-        self.maxdisp = maxdisp
-        self.feature = FeatureUNet()
-        self.init = nn.ModuleList([TileInit(CH[l]) for l in range(HYP_LEVELS)])
-        self.prop = nn.ModuleList([Propagation() for _ in range(HYP_LEVELS)])
+        self.maxdisp, self.ch = maxdisp, ch
+        self.feature = FeatureUNet(ch)
+        self.init = nn.ModuleList([TileInit(ch[l]) for l in range(HYP_LEVELS)])
+        self.prop = nn.ModuleList([UpdateNet(4, 1 if l == HYP_LEVELS - 1 else 2, width, dils)
+                                   for l in range(HYP_LEVELS)])
+        self.refine = nn.ModuleList([UpdateNet(t, 1, w, d, conf=False) for t, (w, d) in zip((2, 1), refine)])
+
+    def levels(self, el, er):
+        """Tile hypotheses coarse -> fine; returns the per-level winners (index = level)."""
+        hyps = [None] * HYP_LEVELS
+        h = None
+        for l in range(HYP_LEVELS - 1, -1, -1):
+            hi = self.init[l](el[l], er[l], self.maxdisp >> l)
+            cands = [hi] if h is None else [upsample_hyp(h), hi]
+            outs, confs = self.prop[l]([warp_cost(el[l], er[l], c) for c in cands], cands)
+            best, conf = outs[0], confs[0]
+            for o, cf in zip(outs[1:], confs[1:]):  # strictly greater wins: ties keep the upsampled candidate
+                take = cf > conf
+                best = torch.where(take, o, best)
+                conf = torch.where(take, cf, conf)
+            hyps[l] = h = best
+        return hyps
 
     def forward(self, x6):
         """x6: [B,6,H,W] = [left RGB; right RGB] / 255 -> disparity [B,H,W]."""
@@ -197,21 +268,11 @@ class HITNet(nn.Module):
         e = self.feature(torch.cat((x6[:, :3], x6[:, 3:]), 0))
         el = [t[:b] for t in e]
         er = [t[b:] for t in e]
-        h = None
-        for l in range(HYP_LEVELS - 1, -1, -1):
-            hi = self.init[l](el[l], er[l], self.maxdisp >> l)
-            cands = [hi] if h is None else [upsample_hyp(h), hi]
-            best, conf = None, None
-            for c in cands:
-                hn, cf = self.prop[l](warp_cost(el[l], er[l], c), c)
-                if best is None:
-                    best, conf = hn, cf
-                else:  # strictly greater wins: ties keep the earlier (upsampled) candidate
-                    take = cf > conf
-                    best = torch.where(take, hn, best)
-                    conf = torch.where(take, cf, conf)
-            h = best
-        return expand_final(h)
+        h = self.levels(el, er)[0]
+        for t, net in zip((2, 1), self.refine):
+            h = split_hyp(h, 2 * t)
+            (h,), _ = net([warp_cost(el[0], er[0], h, t)], [h])
+        return expand_final(h, 1)
 
 
 def build(preset: str = "hitnet-d400", seed: int = 0) -> HITNet:

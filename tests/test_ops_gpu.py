@@ -148,8 +148,13 @@ def test_conv2d_multisource_concat_and_residual():
     ((128, 128, 128), 128, 3, 1, (24, 32), 1, 3),  # three sources + forced split-K
     ((64,), 128, 7, 1, (12, 12), 1, 1),         # 49 taps
 ])
-def test_conv2d_glds3_vs_torch(srcs, cout, k, stride, hw, n, splitk):
-    """8-wave 256x128 global->LDS DMA kernel (3-deep LDS ring, counted vmcnt, XCD-ordered tiles)."""
+@pytest.mark.parametrize("cfg", [4, 10, 11, 12, 13])
+def test_conv2d_glds3_vs_torch(srcs, cout, k, stride, hw, n, splitk, cfg):
+    """8-wave global->LDS DMA kernels: 256x128 (cfg 4: 3-deep LDS ring, counted vmcnt, XCD-ordered
+    tiles) and the wide tiles 256x256 / 512x128 (cfg 10 / 11: BK 32 4-deep ring, 32x32x16 MFMA,
+    two-band epilogue; never split)."""
+    if cfg >= 10 and splitk != 1:
+        pytest.skip("wide tiles are never split")
     O = ops()
     torch.manual_seed(11)
     xs = [torch.randn(n, c, *hw, device=DEV) for c in srcs]
@@ -163,12 +168,13 @@ def test_conv2d_glds3_vs_torch(srcs, cout, k, stride, hw, n, splitk):
     ws = O.splitk_workspace() if splitk != 1 else None
     for _ in range(2):
         out = O.conv2d([nhwc(x).half() for x in xs], wp, kpad, cout, k, k, bias=b.contiguous(), stride=stride,
-                       act="leaky", alpha=0.1, tile_cfg=4, splitk=splitk, workspace=ws)
+                       act="leaky", alpha=0.1, tile_cfg=cfg, splitk=splitk, workspace=ws)
         torch.cuda.synchronize()
         assert rel_err(nchw(out), ref) < 2e-3
 
 
-def test_conv2d_glds3_gru_and_stats_epilogues():
+@pytest.mark.parametrize("cfg", [4, 10, 11, 12, 13])
+def test_conv2d_glds3_gru_and_stats_epilogues(cfg):
     O = ops()
     torch.manual_seed(12)
     n, hd, h, w = 2, 128, 21, 26
@@ -185,14 +191,14 @@ def test_conv2d_glds3_gru_and_stats_epilogues():
     zb = torch.empty(n, h, w, hd, device=DEV, dtype=torch.float16)
     rhb = torch.empty_like(zb)
     O.conv2d([net_h, nhwc(x).half()], wzr, kpad, 2 * hd, 3, 3, out=zb, epi="gru_zr", ctx=ctx, aux=zb,
-             hbuf=net_h, rh=rhb, tile_cfg=4)
+             hbuf=net_h, rh=rhb, tile_cfg=cfg)
     torch.cuda.synchronize()
     assert rel_err(nchw(zb), z) < 3e-3
     assert rel_err(nchw(rhb), r * net.half().float()) < 3e-3
     w2 = torch.randn(128, 256, 3, 3, device=DEV) / 48
     wp2, kp2, _ = O.pack_conv_weight(w2)
     stats = torch.zeros(n, 128, 2, dtype=torch.int64, device=DEV)
-    y = O.conv2d(nhwc(x).half(), wp2, kp2, 128, 3, 3, stats=stats, tile_cfg=4)
+    y = O.conv2d(nhwc(x).half(), wp2, kp2, 128, 3, 3, stats=stats, tile_cfg=cfg)
     torch.cuda.synchronize()
     yr = F.conv2d(x.half().float(), w2.half().float(), padding=1)
     assert rel_err(nchw(y), yr) < 2e-3

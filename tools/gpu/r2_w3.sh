@@ -1,0 +1,7 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_ops_gpu.py -k "glds3" -q --timeout 100 --timeout-method thread > gpurun_out/wide_ops.log 2>&1
+rc=$?; tail -3 gpurun_out/wide_ops.log
+if [ $rc -ne 0 ]; then grep -E "^E |FAIL" gpurun_out/wide_ops.log | head -20; exit $rc; fi
+timeout -k 10 200 python -u tools/conv_bench.py --iters 30 --shapes zr8,q8,fh8,enc8,zr8s,zr1,q1 --cfgs 4,7,10,12,13 > gpurun_out/cb.log 2>&1; grep cfg gpurun_out/cb.log
