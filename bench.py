@@ -47,7 +47,7 @@ import stereoalgorithms_amd  # noqa: E402,F401  (HIP runtime env defaults before
 BASELINE_MS = {"raftstereo-sceneflow": 38.0, "raftstereo-realtime": 11.0}  # RTX 3090, README_en.md:139-141
 # the other model families' published RTX 3090 numbers (README_en.md:192-194,244-246,293-295)
 OTHER_MS = {"crestereo-iter2": 12.0, "crestereo-iter5": 23.0, "crestereo-iter10": 42.0, "hitnet-d400": 15.0,
-            "fastacvnet-plus": 12.0}
+            "hitnet-xl": None, "fastacvnet-plus": 12.0}  # flyingthings_finalpass_xl: no published latency
 ITERS = {"raftstereo-sceneflow": 32, "raftstereo-realtime": 7}
 
 

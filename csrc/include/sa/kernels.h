@@ -271,16 +271,20 @@ int sa_hitnet_tile_init(const void* tl, int tls, const void* tr, int trs, int B,
                         void* cmin, int cs, float* dinit, hipStream_t stream);
 // hyp [P][16] fp32 = [d_init, 0, 0, desc[0..12]]
 int sa_hitnet_hyp_init(const float* dinit, const void* desc, int ds, long P, float* hyp, hipStream_t stream);
-// local warped L1 cost (48 ch) + fp16 hypothesis copy (16 ch) -> out [ncand*B][H/4][W/4][64]
-int sa_hitnet_warp_cost(const void* el, int els, const void* er, int ers, int B, int H, int W, int C,
-                        const float* hyp, int ncand, void* out, hipStream_t stream);
-// refine (cand + delta) and keep the most confident of ncand candidates -> out [P][16]
-int sa_hitnet_select(const float* cand, int ncand, long P, const float* delta, int dstr, float* out,
-                     hipStream_t stream);
-// slanted-plane 2x upsampling of tile hypotheses [B][th][tw][16] -> [B][2th][2tw][16]
+// local warped L1 cost of T x T tiles (T = 4, 2, 1: 3*T*T costs) + fp16 hypothesis copy (16 ch): candidate k
+// of tile q -> out[q][k*ccand ...] (row stride ostride); hyp [ncand][B*th*tw][16], th = H/T
+int sa_hitnet_warp_cost(const void* el, int els, const void* er, int ers, int B, int H, int W, int C, int T,
+                        const float* hyp, int ncand, void* out, int ostride, int ccand, hipStream_t stream);
+// refine (cand + delta, delta block of candidate k at channel k*dcand of a stride-dstr row) and, with
+// confidences (channel 16 of each block), keep the most confident of ncand candidates -> out [P][16]
+int sa_hitnet_select(const float* cand, int ncand, long P, const float* delta, int dstr, int dcand, int has_conf,
+                     float* out, hipStream_t stream);
+// slanted-plane 2x upsampling of tile hypotheses to the next finer level [B][th][tw][16] -> [B][2th][2tw][16]
 int sa_hitnet_upsample(const float* h, int B, int th, int tw, float* out, hipStream_t stream);
-// level-0 tiles -> full-resolution disparity [B][4th][4tw]
-int sa_hitnet_expand(const float* h, int B, int th, int tw, float* disp, hipStream_t stream);
+// split T x T tiles (T = 4, 2) into T/2 x T/2 tiles of the same level -> [B][2th][2tw][16]
+int sa_hitnet_split(const float* h, int B, int th, int tw, int T, float* out, hipStream_t stream);
+// disparity [B][T th][T tw] from tiles of size T (plane evaluated per pixel, clamped at 0)
+int sa_hitnet_expand(const float* h, int B, int th, int tw, int T, float* disp, hipStream_t stream);
 
 #ifdef __cplusplus
 }

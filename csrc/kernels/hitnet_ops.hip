@@ -83,41 +83,46 @@ __global__ void hyp_init_kernel(const float* __restrict__ dinit, const f16* __re
   }
 }
 
-// Local cost of candidate n (image n % B): for the 16 tile pixels (u, v) and shifts s in {-1,0,1}:
-// sum_c |el(4y+v, 4x+u) - er_lin(4y+v, 4x+u - (d + dx(u-1.5) + dy(v-1.5) + s))|  (zero outside)
-// -> out[n][y][x][s*16 + v*4 + u]; channels 48..63 = fp16 copy of the hypothesis.
-template <int C>
-__global__ void __launch_bounds__(256) warp_cost_kernel(const f16* __restrict__ el, int els, const f16* __restrict__ er,
+// Local cost of candidate k of tile q (image q / (th*tw)) at tile size T: for the T*T tile pixels (u, v) and
+// shifts s in {-1,0,1}:  sum_c |el(Ty+v, Tx+u) - er_lin(Ty+v, Tx+u - (d + dx(u-(T-1)/2) + dy(v-(T-1)/2) + s))|
+// (linear interpolation along x, zero outside) -> out[q][k*ccand + s*T*T + v*T + u]; the next 16 channels
+// are an fp16 copy of the hypothesis.  Candidates of one tile sit side by side in the channel dimension,
+// the layout the joint update network reads (one multi-candidate source).
+template <int C, int T>
+__global__ void __launch_bounds__(128) warp_cost_kernel(const f16* __restrict__ el, int els, const f16* __restrict__ er,
                                                         int ers, int B, int H, int W, const float* __restrict__ hyp,
-                                                        int ncand, int th, int tw, f16* __restrict__ out) {
-  const long P = (long)ncand * B * th * tw;
+                                                        int ncand, int th, int tw, f16* __restrict__ out, int ostride,
+                                                        int ccand) {
+  const long Q = (long)B * th * tw;
+  const long P = (long)ncand * Q;
+  constexpr float c0 = (T - 1) * 0.5f;
   for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
-    const int x = (int)(p % tw);
-    const int y = (int)((p / tw) % th);
-    const int n = (int)(p / ((long)tw * th));
-    const int img = n % B;
+    const int k = (int)(p / Q);
+    const long q = p - (long)k * Q;
+    const int x = (int)(q % tw);
+    const int y = (int)((q / tw) % th);
+    const int img = (int)(q / ((long)tw * th));
     const float* h = hyp + p * 16;
     const float d = h[0], sx = h[1], sy = h[2];
-    f16* orow = out + p * 64;
-    // rows v are a runtime loop (a fully unrolled 4x4x3 body took minutes to compile and spilled);
-    // one row's 3 shifts x 4 columns are stored as three 8-byte groups
+    f16* orow = out + q * ostride + (long)k * ccand;
+    // rows v are a runtime loop (a fully unrolled 4x4x3 body took minutes to compile and spilled)
 #pragma unroll 1
-    for (int v = 0; v < 4; ++v) {
-      const int py = 4 * y + v;
+    for (int v = 0; v < T; ++v) {
+      const int py = T * y + v;
       const f16* lrow = el + ((long)img * H + py) * W * els;
       const f16* rrow = er + ((long)img * H + py) * W * ers;
-      float cst[3][4];
+      float cst[3][T];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int px = 4 * x + u;
+      for (int u = 0; u < T; ++u) {
+        const int px = T * x + u;
         float lv[C];
 #pragma unroll
-        for (int c0 = 0; c0 < C; c0 += 8) {
-          const half8 a = *reinterpret_cast<const half8*>(lrow + (long)px * els + c0);
+        for (int cc = 0; cc < C; cc += 8) {
+          const half8 a = *reinterpret_cast<const half8*>(lrow + (long)px * els + cc);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) lv[c0 + j] = (float)a[j];
+          for (int j = 0; j < 8; ++j) lv[cc + j] = (float)a[j];
         }
-        const float dp = d + sx * ((float)u - 1.5f) + sy * ((float)v - 1.5f);
+        const float dp = d + sx * ((float)u - c0) + sy * ((float)v - c0);
 #pragma unroll
         for (int s = 0; s < 3; ++s) {
           const float xr = (float)px - (dp + (float)(s - 1));
@@ -127,49 +132,45 @@ __global__ void __launch_bounds__(256) warp_cost_kernel(const f16* __restrict__ 
           float cost = 0.f;
           const bool ok0 = x0 >= 0 && x0 <= W - 1, ok1 = x0 + 1 >= 0 && x0 + 1 <= W - 1;
 #pragma unroll
-          for (int c0 = 0; c0 < C; c0 += 8) {
+          for (int cc = 0; cc < C; cc += 8) {
             half8 r0 = {0, 0, 0, 0, 0, 0, 0, 0}, r1 = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (ok0) r0 = *reinterpret_cast<const half8*>(rrow + (long)x0 * ers + c0);
-            if (ok1) r1 = *reinterpret_cast<const half8*>(rrow + (long)(x0 + 1) * ers + c0);
+            if (ok0) r0 = *reinterpret_cast<const half8*>(rrow + (long)x0 * ers + cc);
+            if (ok1) r1 = *reinterpret_cast<const half8*>(rrow + (long)(x0 + 1) * ers + cc);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) cost += fabsf(lv[c0 + j] - ((1.f - a) * (float)r0[j] + a * (float)r1[j]));
+            for (int j = 0; j < 8; ++j) cost += fabsf(lv[cc + j] - ((1.f - a) * (float)r0[j] + a * (float)r1[j]));
           }
           cst[s][u] = cost;
         }
       }
 #pragma unroll
-      for (int s = 0; s < 3; ++s) {
-        half4_ t = {(f16)cst[s][0], (f16)cst[s][1], (f16)cst[s][2], (f16)cst[s][3]};
-        *reinterpret_cast<half4_*>(orow + s * 16 + v * 4) = t;
-      }
-    }
-    half8 t0, t1;
+      for (int s = 0; s < 3; ++s)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      t0[k] = (f16)h[k];
-      t1[k] = (f16)h[8 + k];
+        for (int u = 0; u < T; ++u) orow[s * T * T + v * T + u] = (f16)cst[s][u];
     }
-    reinterpret_cast<half8*>(orow)[6] = t0;
-    reinterpret_cast<half8*>(orow)[7] = t1;
+    f16* hc = orow + 3 * T * T;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) hc[j] = (f16)h[j];
   }
 }
 
-// h' = cand + delta[:16] (d clamped >= 0), conf = delta[16]; keep the first candidate with the
-// strictly highest confidence.  cand / delta: [ncand][B][th][tw][...]
+// h' = cand + delta[:16] (d clamped >= 0); with confidences (delta channel 16 of each candidate block)
+// keep the first candidate with the strictly highest one.  cand [ncand][P][16]; delta [P][dstr] with
+// candidate k's block at channel k * dcand.
 __global__ void select_kernel(const float* __restrict__ cand, int ncand, long P, const float* __restrict__ delta,
-                              int dstr, float* __restrict__ out) {
+                              int dstr, int dcand, int has_conf, float* __restrict__ out) {
   for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
     int best = 0;
     float bc = -3.0e38f;
-    for (int k = 0; k < ncand; ++k) {
-      const float c = delta[((long)k * P + p) * dstr + 16];
-      if (k == 0 || c > bc) {
-        bc = c;
-        best = k;
+    if (has_conf)
+      for (int k = 0; k < ncand; ++k) {
+        const float c = delta[p * dstr + k * dcand + 16];
+        if (k == 0 || c > bc) {
+          bc = c;
+          best = k;
+        }
       }
-    }
     const float* h = cand + ((long)best * P + p) * 16;
-    const float* dl = delta + ((long)best * P + p) * dstr;
+    const float* dl = delta + p * dstr + best * dcand;
     float r[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) r[k] = h[k] + dl[k];
@@ -180,8 +181,8 @@ __global__ void select_kernel(const float* __restrict__ cand, int ncand, long P,
   }
 }
 
-// slanted-plane 2x upsampling: fine tile (2i+a, 2j+b) of coarse tile (i, j):
-// d' = 2 (d + dx (2b-1) + dy (2a-1)), slopes and descriptor copied
+// slanted-plane 2x upsampling to the next finer feature level: fine tile (2i+a, 2j+b) of coarse tile
+// (i, j): d' = 2 (d + dx (2b-1) + dy (2a-1)), slopes and descriptor copied
 __global__ void upsample_kernel(const float* __restrict__ h, int B, int th, int tw, float* __restrict__ out) {
   const int TH = 2 * th, TW = 2 * tw;
   const long P = (long)B * TH * TW;
@@ -200,16 +201,37 @@ __global__ void upsample_kernel(const float* __restrict__ h, int B, int th, int 
   }
 }
 
-// full-resolution disparity from level-0 tiles: max(0, d + dx (u-1.5) + dy (v-1.5))
-__global__ void expand_kernel(const float* __restrict__ h, int B, int th, int tw, float* __restrict__ disp) {
-  const int H = 4 * th, W = 4 * tw;
+// split T x T tiles into (T/2) x (T/2) tiles of the same level: sub-tile (2i+a, 2j+b) evaluates the plane
+// at its centre, offset ((2b-1) T/4, (2a-1) T/4) pixels from the parent's; slopes and descriptor copied
+__global__ void split_kernel(const float* __restrict__ h, int B, int th, int tw, float q4, float* __restrict__ out) {
+  const int TH = 2 * th, TW = 2 * tw;
+  const long P = (long)B * TH * TW;
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
+    const int X = (int)(p % TW);
+    const int Y = (int)((p / TW) % TH);
+    const int n = (int)(p / ((long)TW * TH));
+    const float* s = h + (((long)n * th + Y / 2) * tw + X / 2) * 16;
+    float r[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r[k] = s[k];
+    r[0] = s[0] + s[1] * ((float)(2 * (X & 1) - 1) * q4) + s[2] * ((float)(2 * (Y & 1) - 1) * q4);
+    float4_* o = reinterpret_cast<float4_*>(out + p * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = float4_{r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]};
+  }
+}
+
+// disparity from tiles of size T: max(0, d + dx (u-(T-1)/2) + dy (v-(T-1)/2)) per pixel
+__global__ void expand_kernel(const float* __restrict__ h, int B, int th, int tw, int T, float* __restrict__ disp) {
+  const int H = T * th, W = T * tw;
   const long P = (long)B * H * W;
+  const float c0 = (T - 1) * 0.5f;
   for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
     const int x = (int)(p % W);
     const int y = (int)((p / W) % H);
     const int n = (int)(p / ((long)W * H));
-    const float* s = h + (((long)n * th + y / 4) * tw + x / 4) * 16;
-    const float d = s[0] + s[1] * ((float)(x & 3) - 1.5f) + s[2] * ((float)(y & 3) - 1.5f);
+    const float* s = h + (((long)n * th + y / T) * tw + x / T) * 16;
+    const float d = s[0] + s[1] * ((float)(x % T) - c0) + s[2] * ((float)(y % T) - c0);
     disp[p] = fmaxf(d, 0.f);
   }
 }
@@ -231,23 +253,21 @@ extern "C" int sa_hitnet_hyp_init(const float* dinit, const void* desc, int ds, 
   return (int)hipGetLastError();
 }
 
-extern "C" int sa_hitnet_warp_cost(const void* el, int els, const void* er, int ers, int B, int H, int W, int C,
-                                   const float* hyp, int ncand, void* out, hipStream_t stream) {
-  if (H % 4 || W % 4 || els % 8 || ers % 8) return -2;
-  const int th = H / 4, tw = W / 4;
-  const long P = (long)ncand * B * th * tw;
-  switch (C) {
-    case 16:
-      hipLaunchKernelGGL(warp_cost_kernel<16>, dim3(grid_for(P, 128)), dim3(128), 0, stream, (const f16*)el, els,
-                         (const f16*)er, ers, B, H, W, hyp, ncand, th, tw, (f16*)out);
+template <int C>
+int launch_warp(int T, dim3 g, const f16* el, int els, const f16* er, int ers, int B, int H, int W, const float* hyp,
+                int ncand, int th, int tw, f16* out, int ostride, int ccand, hipStream_t stream) {
+  switch (T) {
+    case 4:
+      hipLaunchKernelGGL((warp_cost_kernel<C, 4>), g, dim3(128), 0, stream, el, els, er, ers, B, H, W, hyp, ncand, th, tw,
+                         out, ostride, ccand);
       break;
-    case 24:
-      hipLaunchKernelGGL(warp_cost_kernel<24>, dim3(grid_for(P, 128)), dim3(128), 0, stream, (const f16*)el, els,
-                         (const f16*)er, ers, B, H, W, hyp, ncand, th, tw, (f16*)out);
+    case 2:
+      hipLaunchKernelGGL((warp_cost_kernel<C, 2>), g, dim3(128), 0, stream, el, els, er, ers, B, H, W, hyp, ncand, th, tw,
+                         out, ostride, ccand);
       break;
-    case 32:
-      hipLaunchKernelGGL(warp_cost_kernel<32>, dim3(grid_for(P, 128)), dim3(128), 0, stream, (const f16*)el, els,
-                         (const f16*)er, ers, B, H, W, hyp, ncand, th, tw, (f16*)out);
+    case 1:
+      hipLaunchKernelGGL((warp_cost_kernel<C, 1>), g, dim3(128), 0, stream, el, els, er, ers, B, H, W, hyp, ncand, th, tw,
+                         out, ostride, ccand);
       break;
     default:
       return -2;
@@ -255,10 +275,28 @@ extern "C" int sa_hitnet_warp_cost(const void* el, int els, const void* er, int 
   return (int)hipGetLastError();
 }
 
-extern "C" int sa_hitnet_select(const float* cand, int ncand, long P, const float* delta, int dstr, float* out,
-                                hipStream_t stream) {
-  if (dstr < 17) return -2;
-  hipLaunchKernelGGL(select_kernel, dim3(grid_for(P)), dim3(256), 0, stream, cand, ncand, P, delta, dstr, out);
+extern "C" int sa_hitnet_warp_cost(const void* el, int els, const void* er, int ers, int B, int H, int W, int C, int T,
+                                   const float* hyp, int ncand, void* out, int ostride, int ccand, hipStream_t stream) {
+  if (T < 1 || H % T || W % T || els % 8 || ers % 8 || ccand < 3 * T * T + 16 || ostride < ncand * ccand) return -2;
+  const int th = H / T, tw = W / T;
+  const dim3 g(grid_for((long)ncand * B * th * tw, 128));
+  const f16 *l = (const f16*)el, *r = (const f16*)er;
+  f16* o = (f16*)out;
+  switch (C) {
+    case 16: return launch_warp<16>(T, g, l, els, r, ers, B, H, W, hyp, ncand, th, tw, o, ostride, ccand, stream);
+    case 24: return launch_warp<24>(T, g, l, els, r, ers, B, H, W, hyp, ncand, th, tw, o, ostride, ccand, stream);
+    case 32: return launch_warp<32>(T, g, l, els, r, ers, B, H, W, hyp, ncand, th, tw, o, ostride, ccand, stream);
+    case 48: return launch_warp<48>(T, g, l, els, r, ers, B, H, W, hyp, ncand, th, tw, o, ostride, ccand, stream);
+    case 64: return launch_warp<64>(T, g, l, els, r, ers, B, H, W, hyp, ncand, th, tw, o, ostride, ccand, stream);
+    default: return -2;
+  }
+}
+
+extern "C" int sa_hitnet_select(const float* cand, int ncand, long P, const float* delta, int dstr, int dcand,
+                                int has_conf, float* out, hipStream_t stream) {
+  if (dcand < (has_conf ? 17 : 16) || dstr < ncand * dcand) return -2;
+  hipLaunchKernelGGL(select_kernel, dim3(grid_for(P)), dim3(256), 0, stream, cand, ncand, P, delta, dstr, dcand,
+                     has_conf, out);
   return (int)hipGetLastError();
 }
 
@@ -267,7 +305,16 @@ extern "C" int sa_hitnet_upsample(const float* h, int B, int th, int tw, float* 
   return (int)hipGetLastError();
 }
 
-extern "C" int sa_hitnet_expand(const float* h, int B, int th, int tw, float* disp, hipStream_t stream) {
-  hipLaunchKernelGGL(expand_kernel, dim3(grid_for((long)B * th * tw * 16)), dim3(256), 0, stream, h, B, th, tw, disp);
+extern "C" int sa_hitnet_split(const float* h, int B, int th, int tw, int T, float* out, hipStream_t stream) {
+  if (T != 4 && T != 2) return -2;
+  hipLaunchKernelGGL(split_kernel, dim3(grid_for((long)B * th * tw * 4)), dim3(256), 0, stream, h, B, th, tw,
+                     T * 0.25f, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_hitnet_expand(const float* h, int B, int th, int tw, int T, float* disp, hipStream_t stream) {
+  if (T < 1) return -2;
+  hipLaunchKernelGGL(expand_kernel, dim3(grid_for((long)B * th * tw * T * T)), dim3(256), 0, stream, h, B, th, tw, T,
+                     disp);
   return (int)hipGetLastError();
 }

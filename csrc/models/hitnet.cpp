@@ -1,4 +1,4 @@
-// HITNet (preset hitnet-d400) as a native op graph.
+// HITNet (presets hitnet-d400, hitnet-xl) as a native op graph.
 //
 // Reference pins: one 6-channel input = [L RGB; R RGB] / 255
 // (HitNet/src/HitNet_preprocess.cu:19-51, HitNet.cpp:78), output H*W positive disparity
@@ -7,17 +7,34 @@
 //
 // Layout: both images run the U-Net as one 2B batch (NHWC fp16, every conv an MFMA implicit GEMM with
 // fused bias + LeakyReLU(0.2); the 2x2 transposed convs are 1x1 convs whose epilogue scatters the 4
-// parity classes).  Tile hypotheses are fp32; the per-level refinement nets see [local cost | fp16
-// hypothesis copy] as one 64-channel source written by the warp kernel, and both candidates of a level
-// run as one 2B batch through the shared refinement weights.
+// parity classes).  Tile hypotheses are fp32; each update network sees [local cost | fp16 hypothesis
+// copy] of all its candidates side by side as one multi-candidate source written by the warp kernel
+// (joint update, per-candidate deltas + confidences, argmax selection); the level-0 winner is then split
+// into 2x2 and 1x1 tiles and refined twice more on the full-resolution features.
 #include "blocks.h"
 
 namespace sa {
 namespace {
 
 constexpr int kLevels = 5, kHypLevels = 4;
-constexpr int kCh[kLevels] = {16, 16, 24, 24, 32};
 constexpr float kSlope = 0.2f;
+
+// Presets (stereoalgorithms_amd/models/hitnet.py PRESETS; the oracle's docstring lists which numbers the
+// published description fixes and which are our choices)
+struct HitCfg {
+  int maxdisp;
+  int ch[kLevels];
+  int width;                 // level update networks
+  std::vector<int> dils;     // residual-block dilations of the level update networks
+  int rwidth[2];             // final refinement (2x2 tiles, 1x1 tiles)
+  std::vector<int> rdils[2];
+};
+
+HitCfg preset(const std::string& name) {
+  if (name == "hitnet-d400" || name == "hitnet") return HitCfg{400, {16, 16, 24, 24, 32}, 32, {1, 2, 4}, {32, 16}, {{1, 2}, {1, 1}}};
+  if (name == "hitnet-xl") return HitCfg{320, {32, 32, 48, 48, 64}, 64, {1, 2, 4, 8, 1}, {48, 24}, {{1, 2}, {1, 1}}};
+  throw Error("unknown HITNet preset " + name);
+}
 
 static void check(int rc, const char* what) { SA_REQUIRE(rc == 0, "%s failed (rc=%d)", what, rc); }
 
@@ -30,41 +47,59 @@ ConvSpec spec(int k, int s = 1, int pad = -1, int dil = 1) {
   return sp;
 }
 
-struct PropNet {
-  ConvLayer inp, r1a, r1b, r2a, r2b, out;
+// Joint update of ncand hypotheses of tile size t (oracle: hitnet.UpdateNet): x = [cost_k (3t^2), h_k (16)]
+// per candidate k (each block padded to 8 channels) -> 1x1 conv -> residual blocks -> 3x3 conv -> per
+// candidate 16 deltas (+ a confidence when conf).
+struct UpdateNet {
+  int t = 4, ncand = 1, nout = 17, cin = 64, cin_pad = 64;
+  ConvLayer inp, out;
+  std::vector<ConvLayer> c1, c2;
+  std::vector<int> dils;
   Tensor x, a, b, c, delta;
-  void build(DeviceArena& ar, WeightSource& src, const std::string& p, int N, int th, int tw) {
-    src.conv(p + ".inp", 32, 64, 1, 1);
-    inp.build(ar, *src.ws, {p + ".inp"}, {{64, 64}}, spec(1, 1, 0));
-    const int dils[2] = {1, 2};
-    ConvLayer* L[2][2] = {{&r1a, &r1b}, {&r2a, &r2b}};
-    for (int i = 0; i < 2; ++i)
-      for (int j = 0; j < 2; ++j) {
-        const std::string n = p + ".res." + std::to_string(i) + ".conv" + std::to_string(j + 1);
-        src.conv(n, 32, 32, 3, 3);
-        L[i][j]->build(ar, *src.ws, {n}, {{32, 32}}, spec(3, 1, -1, dils[i]));
-      }
-    src.conv(p + ".out", 17, 32, 3, 3);
-    out.build(ar, *src.ws, {p + ".out"}, {{32, 32}}, spec(3));
-    x = make_tensor(ar, N, th, tw, 64);
-    a = make_tensor(ar, N, th, tw, 32);
-    b = make_tensor(ar, N, th, tw, 32);
-    c = make_tensor(ar, N, th, tw, 32);
-    delta = make_tensor(ar, N, th, tw, 17, DT::F32, 24);
+  void build(DeviceArena& ar, WeightSource& src, const std::string& p, int t_, int ncand_, int width,
+             const std::vector<int>& dils_, bool conf, int N, int th, int tw) {
+    t = t_;
+    ncand = ncand_;
+    nout = conf ? 17 : 16;
+    cin = 3 * t * t + 16;
+    cin_pad = round_up(cin, 8);
+    dils = dils_;
+    src.conv(p + ".inp", width, ncand * cin, 1, 1);
+    std::vector<ChanSeg> segs(ncand, ChanSeg{cin, cin_pad});
+    inp.build(ar, *src.ws, {p + ".inp"}, segs, spec(1, 1, 0));
+    c1.resize(dils.size());
+    c2.resize(dils.size());
+    for (size_t i = 0; i < dils.size(); ++i) {
+      const std::string n = p + ".res." + std::to_string(i) + ".conv";
+      src.conv(n + "1", width, width, 3, 3);
+      src.conv(n + "2", width, width, 3, 3);
+      c1[i].build(ar, *src.ws, {n + "1"}, {{width, width}}, spec(3, 1, -1, dils[i]));
+      c2[i].build(ar, *src.ws, {n + "2"}, {{width, width}}, spec(3, 1, -1, dils[i]));
+    }
+    src.conv(p + ".out", ncand * nout, width, 3, 3);
+    out.build(ar, *src.ws, {p + ".out"}, {{width, width}}, spec(3));
+    x = make_tensor(ar, N, th, tw, ncand * cin_pad);
+    a = make_tensor(ar, N, th, tw, width);
+    b = make_tensor(ar, N, th, tw, width);
+    c = make_tensor(ar, N, th, tw, width);
+    delta = make_tensor(ar, N, th, tw, ncand * nout, DT::F32, round_up(ncand * nout, 8));
   }
   void run(hipStream_t s) const {
     inp.run(s, {x}, a, SA_ACT_LEAKY, nullptr, SA_ACT_NONE, nullptr, kSlope);
-    r1a.run(s, {a}, b, SA_ACT_LEAKY, nullptr, SA_ACT_NONE, nullptr, kSlope);
-    r1b.run(s, {b}, c, SA_ACT_NONE, &a, SA_ACT_LEAKY, nullptr, kSlope);
-    r2a.run(s, {c}, b, SA_ACT_LEAKY, nullptr, SA_ACT_NONE, nullptr, kSlope);
-    r2b.run(s, {b}, a, SA_ACT_NONE, &c, SA_ACT_LEAKY, nullptr, kSlope);
-    out.run(s, {a}, delta);
+    const Tensor* cur = &a;
+    const Tensor* nxt = &c;
+    for (size_t i = 0; i < dils.size(); ++i) {
+      c1[i].run(s, {*cur}, b, SA_ACT_LEAKY, nullptr, SA_ACT_NONE, nullptr, kSlope);
+      c2[i].run(s, {b}, *nxt, SA_ACT_NONE, cur, SA_ACT_LEAKY, nullptr, kSlope);
+      std::swap(cur, nxt);
+    }
+    out.run(s, {*cur}, delta);
   }
 };
 
 class HitNet : public StereoEngine {
  public:
-  explicit HitNet(const EngineConfig& cfg) : StereoEngine(cfg) {}
+  explicit HitNet(const EngineConfig& cfg) : StereoEngine(cfg), hc_(preset(cfg.model)) {}
   const char* name() const override { return "HitNet"; }
 
  protected:
@@ -72,7 +107,7 @@ class HitNet : public StereoEngine {
   void forward(hipStream_t s) override;
 
  private:
-  int maxdisp_ = 400;
+  HitCfg hc_;
   Tensor img_;
   std::vector<ConvLayer> down_[kLevels];
   std::vector<Tensor> dt_[kLevels];  // per-conv outputs of the down path (last = d_l)
@@ -85,13 +120,20 @@ class HitNet : public StereoEngine {
     float* cand = nullptr;  // [ncand][B][th][tw][16]
     float* hyp = nullptr;   // selected [B][th][tw][16]
     int th = 0, tw = 0, wr = 0, ncand = 1;
-    PropNet prop;
+    UpdateNet prop;
   } lv_[kHypLevels];
+  struct Refine {  // final refinement at tile size t (2, then 1) on the level-0 features
+    int t = 2, th = 0, tw = 0;
+    float* cand = nullptr;  // split of the previous stage's hypotheses [B][th][tw][16]
+    float* hyp = nullptr;
+    UpdateNet net;
+  } rf_[2];
 };
 
 void HitNet::build(WeightSource& src) {
   DeviceArena& a = arena_;
   const int B = this->B(), N2 = 2 * B;
+  const int* kCh = hc_.ch;
   SA_REQUIRE(H() % 32 == 0 && W() % 32 == 0, "HITNet needs H, W multiples of 32");
   img_ = make_tensor(a, N2, H(), W(), 8);
   // ---- U-Net down path
@@ -156,7 +198,18 @@ void HitNet::build(WeightSource& src) {
     L.dinit = (float*)a.alloc(P * 4);
     L.cand = (float*)a.alloc(P * L.ncand * 16 * 4);
     L.hyp = (float*)a.alloc(P * 16 * 4);
-    L.prop.build(a, src, "prop." + std::to_string(l), L.ncand * B, L.th, L.tw);
+    L.prop.build(a, src, "prop." + std::to_string(l), 4, L.ncand, hc_.width, hc_.dils, true, B, L.th, L.tw);
+  }
+  // ---- final refinement: 2x2 tiles (half resolution) then per pixel, on e_0
+  for (int j = 0; j < 2; ++j) {
+    Refine& R = rf_[j];
+    R.t = j == 0 ? 2 : 1;
+    R.th = H() / R.t;
+    R.tw = W() / R.t;
+    const size_t P = (size_t)B * R.th * R.tw;
+    R.cand = (float*)a.alloc(P * 16 * 4);
+    R.hyp = (float*)a.alloc(P * 16 * 4);
+    R.net.build(a, src, "refine." + std::to_string(j), R.t, 1, hc_.rwidth[j], hc_.rdils[j], false, B, R.th, R.tw);
   }
 }
 
@@ -184,7 +237,7 @@ void HitNet::forward(hipStream_t s) {
     L.tile_r.run(s, {er}, L.tr);
     tap(s, ("tl" + std::to_string(l)).c_str(), L.tl);
     tap(s, ("tr" + std::to_string(l)).c_str(), L.tr);
-    check(sa_hitnet_tile_init(L.tl.ptr, L.tl.stride, L.tr.ptr, L.tr.stride, B, L.th, L.tw, L.wr, maxdisp_ >> l,
+    check(sa_hitnet_tile_init(L.tl.ptr, L.tl.stride, L.tr.ptr, L.tr.stride, B, L.th, L.tw, L.wr, hc_.maxdisp >> l,
                               L.cmin.ptr, L.cmin.stride, L.dinit, s),
           "tile init");
     L.desc.run(s, {L.cmin, L.tl}, L.dsc, SA_ACT_LEAKY, nullptr, SA_ACT_NONE, nullptr, kSlope);
@@ -195,18 +248,42 @@ void HitNet::forward(hipStream_t s) {
       const Lvl& C = lv_[l + 1];
       check(sa_hitnet_upsample(C.hyp, B, C.th, C.tw, L.cand, s), "hyp upsample");
     }
-    check(sa_hitnet_warp_cost(el.ptr, el.stride, er.ptr, er.stride, B, e_[l].h, e_[l].w, kCh[l], L.cand, L.ncand,
-                              L.prop.x.ptr, s),
+    const UpdateNet& U = L.prop;
+    check(sa_hitnet_warp_cost(el.ptr, el.stride, er.ptr, er.stride, B, e_[l].h, e_[l].w, hc_.ch[l], 4, L.cand,
+                              L.ncand, U.x.ptr, U.x.stride, U.cin_pad, s),
           "warp cost");
-    L.prop.run(s);
-    check(sa_hitnet_select(L.cand, L.ncand, P, (const float*)L.prop.delta.ptr, L.prop.delta.stride, L.hyp, s),
+    U.run(s);
+    check(sa_hitnet_select(L.cand, L.ncand, P, (const float*)U.delta.ptr, U.delta.stride, U.nout, 1, L.hyp, s),
           "select");
     tap_f32(s, ("cand" + std::to_string(l)).c_str(), L.cand, L.ncand * B, L.th, L.tw, 16);
-    tap(s, ("cost" + std::to_string(l)).c_str(), L.prop.x);
-    tap(s, ("delta" + std::to_string(l)).c_str(), L.prop.delta);
+    tap(s, ("cost" + std::to_string(l)).c_str(), U.x);
+    tap(s, ("delta" + std::to_string(l)).c_str(), U.delta);
     tap_f32(s, ("hyp" + std::to_string(l)).c_str(), L.hyp, B, L.th, L.tw, 16);
   }
-  check(sa_hitnet_expand(lv_[0].hyp, B, lv_[0].th, lv_[0].tw, disp_, s), "expand");
+  // final refinement on the level-0 (full-resolution) features
+  const Tensor e0l = e_[0].slice_n(0, B), e0r = e_[0].slice_n(B, B);
+  const float* prev = lv_[0].hyp;
+  int pth = lv_[0].th, ptw = lv_[0].tw, pt = 4;
+  for (int j = 0; j < 2; ++j) {
+    const Refine& R = rf_[j];
+    const long P = (long)B * R.th * R.tw;
+    check(sa_hitnet_split(prev, B, pth, ptw, pt, R.cand, s), "hyp split");
+    const UpdateNet& U = R.net;
+    check(sa_hitnet_warp_cost(e0l.ptr, e0l.stride, e0r.ptr, e0r.stride, B, H(), W(), hc_.ch[0], R.t, R.cand, 1,
+                              U.x.ptr, U.x.stride, U.cin_pad, s),
+          "warp cost");
+    U.run(s);
+    check(sa_hitnet_select(R.cand, 1, P, (const float*)U.delta.ptr, U.delta.stride, U.nout, 0, R.hyp, s), "refine");
+    tap_f32(s, ("rcand" + std::to_string(j)).c_str(), R.cand, B, R.th, R.tw, 16);
+    tap(s, ("rcost" + std::to_string(j)).c_str(), U.x);
+    tap(s, ("rdelta" + std::to_string(j)).c_str(), U.delta);
+    tap_f32(s, ("rhyp" + std::to_string(j)).c_str(), R.hyp, B, R.th, R.tw, 16);
+    prev = R.hyp;
+    pth = R.th;
+    ptw = R.tw;
+    pt = R.t;
+  }
+  check(sa_hitnet_expand(prev, B, pth, ptw, 1, disp_, s), "expand");
 }
 
 }  // namespace

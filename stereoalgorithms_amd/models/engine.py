@@ -16,7 +16,7 @@ from .. import _native as N
 MODEL_PRESETS = (
     "raftstereo-sceneflow", "raftstereo-realtime",
     "crestereo-iter2", "crestereo-iter5", "crestereo-iter10",
-    "hitnet-d400", "fastacvnet-plus",
+    "hitnet-d400", "hitnet-xl", "fastacvnet-plus",
 )
 
 

@@ -21,17 +21,18 @@ def nchw(t):  # tap [n, 1, h, w, c] -> [n, c, h, w] on the GPU
     return t[:, 0].permute(0, 3, 1, 2).contiguous().to(DEV)
 
 
-@pytest.fixture(scope="module")
-def run(tmp_path_factory):
+@pytest.fixture(scope="module", params=["hitnet-d400", "hitnet-xl"])
+def run(request, tmp_path_factory):
     from stereoalgorithms_amd.models import hitnet as HN
     from stereoalgorithms_amd.models.engine import NativeStereoEngine
     from stereoalgorithms_amd.utils.synthetic import batch_pairs
     from stereoalgorithms_amd.utils.taps import load_taps
     from stereoalgorithms_amd.utils.weights import save_model
-    d = tmp_path_factory.mktemp("hitnet")
+    preset = request.param
+    d = tmp_path_factory.mktemp(preset)
     B, H, W = 2, 128, 192
-    m = HN.build("hitnet-d400", seed=0)
-    path = save_model(m, d / "hitnet.safetensors", "hitnet-d400")
+    m = HN.build(preset, seed=0)
+    path = save_model(m, d / "hitnet.safetensors", preset)
     l, r = batch_pairs(B, H, W, seed=7)
     left, right = torch.from_numpy(l).to(DEV), torch.from_numpy(r).to(DEV)
     os.environ["SA_TAP_DIR"] = str(d)
@@ -46,7 +47,7 @@ def run(tmp_path_factory):
     disp_g = graph.run(left, right)
     torch.cuda.synchronize()
     x6 = torch.cat([t.flip(-1).permute(0, 3, 1, 2).float() / 255.0 for t in (left, right)], 1)
-    return dict(m=m.to(DEV), taps=taps, disp=disp, disp_graph=disp_g, x6=x6, B=B)
+    return dict(m=m.to(DEV), taps=taps, disp=disp, disp_graph=disp_g, x6=x6, B=B, preset=preset)
 
 
 def test_features(run):
@@ -57,6 +58,15 @@ def test_features(run):
         assert rel_err(nchw(taps[f"e{l}"]), e[l]) < 3e-3, l
 
 
+def _cand_blocks(x, ncand, cin, cpad):
+    """[B, ncand*cpad, h, w] joint layout -> list over candidates of (cost [B, cin-16], h [B, 16])."""
+    out = []
+    for k in range(ncand):
+        blk = x[:, k * cpad:k * cpad + cin]
+        out.append((blk[:, :cin - 16], blk[:, cin - 16:]))
+    return out
+
+
 def test_levels_chain(run):
     from stereoalgorithms_amd.models import hitnet as HN
     m, taps, B = run["m"], run["taps"], run["B"]
@@ -65,12 +75,13 @@ def test_levels_chain(run):
         el, er = e[:B], e[B:]
         cand = nchw(taps[f"cand{l}"])  # [ncand*B, 16, th, tw]
         ncand = cand.shape[0] // B
+        cands = [cand[k * B:(k + 1) * B] for k in range(ncand)]
         tl_e, tr_e = nchw(taps[f"tl{l}"]), nchw(taps[f"tr{l}"])
         with torch.no_grad():
             tl, tr = m.init[l].tiles(el, er)
             assert rel_err(tl_e, tl) < 3e-3 and rel_err(tr_e, tr) < 3e-3
             hi = m.init[l].hypothesis(tl_e, tr_e, m.maxdisp >> l)  # argmin on the engine's tile features
-        init_e = cand[(ncand - 1) * B:]
+        init_e = cands[-1]
         same = (init_e[:, 0] == hi[:, 0])
         # fp32 sums of the same fp16 operands in a different order: only exact near-ties may differ
         assert same.float().mean().item() > 0.98, f"level {l}: d_init agreement {same.float().mean().item():.3f}"
@@ -78,26 +89,29 @@ def test_levels_chain(run):
         assert rel_err(init_e[msk], hi[msk]) < 5e-3
         if ncand > 1:  # slot 0 = slanted-plane upsampling of the coarser selected hypothesis
             up = HN.upsample_hyp(nchw(taps[f"hyp{l + 1}"]))
-            assert rel_err(cand[:B], up) < 1e-6
-        cost_t = nchw(taps[f"cost{l}"])  # [ncand*B, 64, th, tw]
+            assert rel_err(cands[0], up) < 1e-6
+        net = m.prop[l]
+        blocks = _cand_blocks(nchw(taps[f"cost{l}"]), ncand, net.cin, (net.cin + 7) // 8 * 8)
         with torch.no_grad():
-            ref_cost = torch.cat([HN.warp_cost(el, er, cand[k * B:(k + 1) * B]) for k in range(ncand)], 0)
-        assert rel_err(cost_t[:, :48], ref_cost) < 3e-3
-        assert rel_err(cost_t[:, 48:], cand) < 2e-3
-        delta = nchw(taps[f"delta{l}"])  # [ncand*B, 17, th, tw] raw refinement output
-        with torch.no_grad():
-            hn, conf = m.prop[l](cost_t[:, :48].float(), cand)
-        assert rel_err(delta[:, 16:17], conf) < 5e-3
-        # hn clamps d at 0, so compare the slope / descriptor channels directly and d via the clamp
-        assert rel_err(delta[:, 1:16], (hn - cand)[:, 1:16]) < 5e-3
-        assert rel_err((cand[:, :1] + delta[:, :1]).clamp_min(0), hn[:, :1]) < 5e-3
+            for k, (cst, hc) in enumerate(blocks):
+                assert rel_err(cst, HN.warp_cost(el, er, cands[k])) < 3e-3
+                assert rel_err(hc, cands[k]) < 2e-3
+            outs, confs = net([c.float() for c, _ in blocks], cands)
+        delta = nchw(taps[f"delta{l}"])  # [B, ncand*17 (+pad), th, tw] raw update output
+        for k in range(ncand):
+            dk = delta[:, k * 17:(k + 1) * 17]
+            assert rel_err(dk[:, 16:17], confs[k]) < 5e-3
+            # outs clamp d at 0: compare slopes / descriptor directly and d via the clamp
+            assert rel_err(dk[:, 1:16], (outs[k] - cands[k])[:, 1:16]) < 5e-3
+            assert rel_err((cands[k][:, :1] + dk[:, :1]).clamp_min(0), outs[k][:, :1]) < 5e-3
         # selection from the engine's own deltas
         hyp = nchw(taps[f"hyp{l}"])
         best, bc = None, None
         for k in range(ncand):
-            h = cand[k * B:(k + 1) * B] + delta[k * B:(k + 1) * B, :16]
+            dk = delta[:, k * 17:(k + 1) * 17]
+            h = cands[k] + dk[:, :16]
             h = torch.cat((h[:, :1].clamp_min(0), h[:, 1:]), 1)
-            c = delta[k * B:(k + 1) * B, 16:17]
+            c = dk[:, 16:17]
             if best is None:
                 best, bc = h, c
             else:
@@ -106,9 +120,34 @@ def test_levels_chain(run):
         assert rel_err(hyp, best) < 1e-6
 
 
+def test_refinement_chain(run):
+    """Final refinement: split of the previous winner into 2x2 / 1x1 tiles, warped cost on e_0, update."""
+    from stereoalgorithms_amd.models import hitnet as HN
+    m, taps, B = run["m"], run["taps"], run["B"]
+    e = nchw(taps["e0"])
+    el, er = e[:B], e[B:]
+    prev, pt = nchw(taps["hyp0"]), 4
+    for j, t in enumerate((2, 1)):
+        cand = nchw(taps[f"rcand{j}"])
+        assert rel_err(cand, HN.split_hyp(prev, pt)) < 1e-6
+        net = m.refine[j]
+        ((cst, hc),) = _cand_blocks(nchw(taps[f"rcost{j}"]), 1, net.cin, (net.cin + 7) // 8 * 8)
+        with torch.no_grad():
+            assert rel_err(cst, HN.warp_cost(el, er, cand, t)) < 3e-3
+            assert rel_err(hc, cand) < 2e-3
+            (out,), _ = net([cst.float()], [cand])
+        delta = nchw(taps[f"rdelta{j}"])[:, :16]
+        assert rel_err(delta[:, 1:16], (out - cand)[:, 1:16]) < 5e-3
+        hyp = nchw(taps[f"rhyp{j}"])
+        ref = cand + delta
+        ref = torch.cat((ref[:, :1].clamp_min(0), ref[:, 1:]), 1)
+        assert rel_err(hyp, ref) < 1e-6
+        prev, pt = hyp, t
+
+
 def test_final_expand_and_graph(run):
     from stereoalgorithms_amd.models import hitnet as HN
-    ref = HN.expand_final(nchw(run["taps"]["hyp0"]))
+    ref = HN.expand_final(nchw(run["taps"]["rhyp1"]), 1)
     assert rel_err(run["disp"], ref) < 1e-6
     assert torch.equal(run["disp"], run["disp_graph"])
     assert torch.isfinite(run["disp"]).all() and run["disp"].min().item() >= 0

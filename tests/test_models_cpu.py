@@ -50,3 +50,34 @@ def test_crestereo_oracle_shape(preset):
     with torch.no_grad():
         d = m(torch.rand(1, 3, 64, 64) * 255, torch.rand(1, 3, 64, 64) * 255)
     assert d.shape[0] == 1 and d.shape[-2:] == (64, 64) and torch.isfinite(d).all()
+
+
+@pytest.mark.parametrize("preset", ["hitnet-d400", "hitnet-xl"])
+def test_hitnet_oracle_shapes_and_names(preset, tmp_path):
+    """HITNet v2 oracle: both presets run, produce non-negative full-resolution disparity, and the
+    state_dict holds the names the native engine loads (csrc/models/hitnet.cpp)."""
+    from stereoalgorithms_amd.models import hitnet as HN
+    m = HN.build(preset, seed=0)
+    with torch.no_grad():
+        d = m(torch.rand(1, 6, 64, 96))
+    assert d.shape == (1, 64, 96) and (d >= 0).all()
+    sd = m.state_dict()
+    for k in ("prop.3.inp.weight", "prop.0.inp.weight", "prop.0.out.weight", "refine.0.inp.weight",
+              "refine.1.out.weight", "prop.0.res.0.conv1.weight", "init.3.tile.weight", "feature.up.0.deconv.weight"):
+        assert k in sd, k
+    cfg = HN.PRESETS[preset]
+    # coarsest level: one candidate (64 inputs); finer levels: two candidates jointly (128 -> 2 x 17 outputs)
+    assert sd["prop.3.inp.weight"].shape[1] == 64 and sd["prop.0.inp.weight"].shape[1] == 128
+    assert sd["prop.0.out.weight"].shape[0] == 34 and sd["refine.1.out.weight"].shape[0] == 16
+    assert len([k for k in sd if k.startswith("prop.0.res.") and k.endswith("conv1.weight")]) == len(cfg["dils"])
+
+
+def test_hitnet_plane_split_consistency():
+    """Splitting a tile hypothesis evaluates the same slanted plane at every pixel."""
+    from stereoalgorithms_amd.models import hitnet as HN
+    torch.manual_seed(0)
+    h = torch.randn(2, 16, 3, 5)
+    for t in (4, 2):
+        a = HN.plane_pixels(h, t)
+        b = HN.plane_pixels(HN.split_hyp(h, t), t // 2)
+        assert torch.allclose(a, b, atol=1e-5)
