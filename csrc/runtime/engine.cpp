@@ -121,11 +121,16 @@ void StereoEngine::init() {
   HIP_CHECK(hipSetDevice(cfg_.device));
   if (const char* e = std::getenv("SA_NO_GRAPH"))
     if (e[0] == '1') cfg_.use_graph = false;  // debugging: eager launches (with SA_DEBUG_SYNC=1)
-  // A blocking stream (like the reference's cudaStreamCreate, TRTRAFTStereo.cpp:85): frames are
-  // implicitly ordered after work already queued on the legacy default stream by the host
-  // program (observed: a graph replayed on a non-blocking stream while torch kernels were still
-  // in flight on the default stream faulted).
-  HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamDefault));
+  // Non-blocking engine stream: every dependency on caller work is explicit (launch_frame records an event
+  // on the caller's stream and the engine stream waits on it, and the reverse after the frame), so the frame
+  // never implicitly serialises with the legacy null stream.  Round 1 used a blocking stream to dodge a fault
+  // it could not explain; at HEAD the engine's replay screens pass with either kind
+  // (tools/graph_repro/engine_matrix.sh).  SA_ENGINE_STREAM_BLOCKING=1 restores the blocking stream.
+  static const bool blocking = [] {
+    const char* e = std::getenv("SA_ENGINE_STREAM_BLOCKING");
+    return e && e[0] == '1';
+  }();
+  HIP_CHECK(hipStreamCreateWithFlags(&stream_, blocking ? hipStreamDefault : hipStreamNonBlocking));
   HIP_CHECK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
   HIP_CHECK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
   HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));

@@ -58,9 +58,3 @@ void log_msg(LogLevel lvl, const char* file, int line, const char* fmt, ...) {
 }
 
 }  // namespace sa
-
-// See stereoalgorithms_amd/__init__.py: disable ROCm's graph packet-capture path before the HIP
-// runtime initialises (runs when libstereo_amd.so is loaded, i.e. before main() of the demos).
-__attribute__((constructor)) static void sa_runtime_env_defaults() {
-  setenv("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0", 0);
-}

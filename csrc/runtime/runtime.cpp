@@ -7,6 +7,7 @@
 #include <unordered_map>
 #include <cstring>
 #include <fstream>
+#include <unistd.h>
 
 #include "sa/json.h"
 
@@ -731,7 +732,8 @@ int conv_plan_load(const std::string& file) {
 int conv_plan_save(const std::string& file, const std::vector<std::string>& keys) {
   std::lock_guard<std::mutex> lk(g_plan_mu);
   auto& m = plan_map();
-  const std::string tmp = file + ".tmp";
+  // per-process temporary + atomic rename: ranks of a DP job writing the same plan never interleave
+  const std::string tmp = file + ".tmp." + std::to_string((long)::getpid());
   {
     std::ofstream out(tmp);
     if (!out.good()) return -1;

@@ -11,14 +11,13 @@ Layers:
 """
 import os as _os
 
-# ROCm's graph "packet capture" fast path (AQL packets + kernel arguments pre-baked at
-# instantiation) corrupted replays of our captured frames when other HIP work (torch kernels
-# loading new code objects) ran between replays: garbage disparities and, downstream, illegal
-# memory accesses (reproduced by tests/test_raft_engine_gpu.py::test_engine_cloud_and_rectify_roundtrip;
-# DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 makes it pass).  The runtime reads the flag once at HIP
-# initialisation, so it is set here, before torch initialises the device, and by a load-time
-# constructor in libstereo_amd.so for the C/C++ entry points.
-_os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+# Round 1 forced DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 after corrupted frame replays were seen with ROCm's graph
+# packet-capture path.  Round 2 could not reproduce any corruption at HEAD: neither a standalone program with
+# the engine's graph shape and torch-like work between replays (tools/graph_repro/graph_capture_repro.hip) nor
+# the engine's own replay screens under packet capture on / off x blocking / non-blocking engine stream
+# (tools/graph_repro/engine_matrix.sh; profiles/graph_repro_r02.log), and frame latency is identical either
+# way, so the runtime default is used again.  Set DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 in the environment to
+# force the old behaviour.
 _os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 __version__ = "0.1.0"

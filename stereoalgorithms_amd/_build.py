@@ -154,6 +154,17 @@ def build(jobs: int | None = None, verbose: bool = False) -> dict:
         abi_built.append(r)
     _link([obj], BINDIR / "stereo_bench_dp", False, shared=False,
           extra=[f"-L{LIBDIR}", "-lstereo_dist", "-lstereo_amd", "-lstereo_host", "-Wl,-rpath,$ORIGIN/../lib"])
+    # standalone HIP diagnostics (tools/graph_repro: graph-replay stability without the engine)
+    gdir = ROOT / "tools" / "graph_repro"
+    for src, out, extra in (("graph_capture_repro.hip", "graph_capture_repro", []),
+                            ("other_kernel.hip", "other_kernel.hsaco", ["--genco"])):
+        s, o = gdir / src, BINDIR / out
+        if not o.exists() or o.stat().st_mtime < s.stat().st_mtime:
+            r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-O2", *extra, "-o", str(o), str(s)],
+                               capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"compile failed: {s}\n{r.stderr}")
+            abi_built.append(str(s.relative_to(ROOT)))
     return {"compiled": built + abi_built, "libs": libs}
 
 
