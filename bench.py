@@ -173,7 +173,12 @@ def main(argv=None) -> int:
         local_dev = local if backend == "nccl" else local % max(1, ndev)
         torch.cuda.set_device(local_dev)
         dev = torch.device("cuda", local_dev)
-    if world > 1:
+    # SA_DP_GATHER_WORLD1=1: a world-1 RCCL process group that still runs every step's all-gather, so the
+    # H2D-copy / all-gather / frame-graph overlap of the multi-GPU path can be traced on one GPU
+    force_gather = world == 1 and os.environ.get("SA_DP_GATHER_WORLD1") == "1" and not cpu
+    if force_gather:
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    if world > 1 or force_gather:
         from datetime import timedelta
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # bounded collectives: a rank that dies or hangs fails the job instead of stalling it
@@ -193,7 +198,7 @@ def main(argv=None) -> int:
         from stereoalgorithms_amd.models.engine import NativeStereoEngine
         eng = NativeStereoEngine(args.model, None, H, W, batch=B, iters=args.iters, device=dev.index, seed=0)
         eng.set_Q(Q)
-    dp = DataParallelStereo(eng, world_size=world, rank=rank)
+    dp = DataParallelStereo(eng, world_size=world, rank=rank, force_gather=force_gather)
     l_np, r_np = batch_pairs(B, H, W, seed=100 * rank)
     left_h, right_h = torch.from_numpy(l_np), torch.from_numpy(r_np)
     if cpu:
@@ -338,7 +343,7 @@ def main(argv=None) -> int:
             "latency_b1": extra,
         }
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if world > 1 or force_gather:
         dist.destroy_process_group()
     return 0
 

@@ -104,8 +104,13 @@ class RaftStereo : public StereoEngine {
   bool fuse_motion_ = !(std::getenv("SA_RAFT_FUSE_MOTION") && std::getenv("SA_RAFT_FUSE_MOTION")[0] == '0');
   // SA_RAFT_PARALLEL=0: run the motion encoder and the coarse GRU levels on one stream
   bool par_ = !(std::getenv("SA_RAFT_PARALLEL") && std::getenv("SA_RAFT_PARALLEL")[0] == '0');
-  // SA_RAFT_PIPELINE=0: keep the per-iteration fork/join instead of the cross-iteration pipeline
-  bool pipeline_ = !(std::getenv("SA_RAFT_PIPELINE") && std::getenv("SA_RAFT_PIPELINE")[0] == '0');
+  // Cross-iteration pipeline on a third stream: worth ~1.3 ms at batch 1 (small grids leave CUs idle), nothing
+  // at batch 8 (56.19 vs 56.17 ms/step in-process, tools/ab_engine.py), where the big GEMMs fill the chip —
+  // and there a third engine stream pushes the data-parallel step (copy stream + RCCL stream + torch
+  // stream) past the 4 hardware queues per process: the H2D prefetch stopped overlapping the frame graph
+  // (0 % vs 95.5 % concurrent, profiles/dp_overlap_r02.txt).  Auto = on below batch 4;
+  // SA_RAFT_PIPELINE=0/1 forces it.
+  int pipeline_mode_ = std::getenv("SA_RAFT_PIPELINE") ? std::atoi(std::getenv("SA_RAFT_PIPELINE")) : -1;
   // SA_RAFT_FUSE_FH: 0 = off, 1 = on, unset = auto.  With conv2 as a separate tap projection
   // (sa_tap_proj, below) the unfused head wins at every batch, measured in-process on MI355X
   // (tools/ab_engine.py): b8 56.6 vs 58.1 ms/step unfused vs fused; b1 tap projection vs the N=1
@@ -480,7 +485,8 @@ void RaftStereo::forward(hipStream_t s) {
   };
 
   const int f = 1 << rc_.n_downsample;
-  const bool pipe = par && pipeline_ && rc_.n_gru == 3 && !rc_.slow_fast;
+  const bool pipeline = pipeline_mode_ >= 0 ? pipeline_mode_ != 0 : Bn < 4;
+  const bool pipe = par && pipeline && rc_.n_gru == 3 && !rc_.slow_fast;
   if (pipe) {
     // Cross-iteration pipeline on three streams (sceneflow: 3 levels, no slow-fast).  Per iteration t:
     //   side2: G32(t)  after G16(t-1)   (needs net1(t-1), net2(t-1); overwrites net2 read by G16(t-1))

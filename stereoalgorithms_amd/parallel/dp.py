@@ -61,6 +61,7 @@ class DataParallelStereo:
     gather: bool = True
     slots: int = 2
     gather_dtype: torch.dtype | None = None
+    force_gather: bool = False  # run the collective even at world size 1 (overlap traces on one GPU)
 
     def __post_init__(self):
         self._out = None
@@ -94,7 +95,7 @@ class DataParallelStereo:
             if send is not None:
                 disp = send.copy_(disp)
         self._send[slot] = disp
-        if self.world_size == 1 or not self.gather:
+        if not self.gather or (self.world_size == 1 and not self.force_gather):
             return PendingGather(disp, None)
         if self.gather_dtype is not None and disp.dtype != self.gather_dtype:
             c = self._cast[slot]
