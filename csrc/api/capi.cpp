@@ -86,7 +86,9 @@ const float* sa_engine_aux_output(void* e, int* n) {
 
 const char* sa_engine_plan_path(void* e) { return static_cast<sa::StereoEngine*>(e)->plan_path().c_str(); }
 long sa_engine_tuned_shapes(void* e) { return static_cast<sa::StereoEngine*>(e)->tuned_shapes(); }
+long sa_engine_nonzero_splitk_counters(void* e) { return static_cast<sa::StereoEngine*>(e)->nonzero_splitk_counters(); }
 long sa_conv_tune_count(void) { return sa::conv_tune_count(); }
+long sa_conv_tune_rejects(void) { return sa::conv_tune_rejects(); }
 void sa_conv_plan_clear(void) { sa::conv_plan_clear(); }
 
 void* sa_engine_stream(void* e) { return (void*)static_cast<sa::StereoEngine*>(e)->stream(); }

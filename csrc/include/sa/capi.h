@@ -25,7 +25,9 @@ void* sa_engine_stream(void* engine);
 // the process-wide count of timed shapes, and a reset of the in-process plan (tests)
 const char* sa_engine_plan_path(void* engine);
 long sa_engine_tuned_shapes(void* engine);
+long sa_engine_nonzero_splitk_counters(void* engine);
 long sa_conv_tune_count(void);
+long sa_conv_tune_rejects(void);
 void sa_conv_plan_clear(void);
 // per-stage device times of the last frame (SA_STAGE_TIMES=1): returns the count (<= max), fills
 // ms[i] and names[i] (pointers valid for the engine's lifetime)

@@ -73,6 +73,9 @@ class StereoEngine {
   // tuned-plan file used by this engine ("" = none) and how many conv shapes it had to time
   const std::string& plan_path() const { return plan_path_; }
   long tuned_shapes() const { return tuned_shapes_; }
+  // diagnostic: split-K tile counters that are not zero (every split conv's last arriver resets its
+  // tiles' counters, so a non-zero one after a completed frame means two launches raced on them)
+  long nonzero_splitk_counters();
   // low-resolution flow / auxiliary output (RAFT "diff" = coords1 - coords0), may be null
   virtual const float* aux_output(int* n) const {
     *n = 0;

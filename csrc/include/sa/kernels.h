@@ -140,9 +140,13 @@ typedef struct {
 int sa_instnorm_apply(const SaNormArgs* a, hipStream_t stream);
 // stats[0][i] = sum_r stats[r][i], stats[r>0][i] = 0 for i < count (idempotent)
 int sa_stats_reduce(sa_stat_t* stats, int slots, long count, hipStream_t stream);
+// res[0] = max |a - b| (NaN / inf -> +inf), res[1] = max |b| over n fp16 (f32 = 0) or fp32 elements, as float
+// bits merged with atomicMax: the caller zeroes res first.
+int sa_absdiff_max(const void* a, const void* b, long n, int f32, unsigned* res, hipStream_t stream);
 // buf[idx] = wall_clock64() once everything queued before on `stream` has finished
 int sa_stamp(unsigned long long* buf, int idx, hipStream_t stream);
-// zero `bytes` (multiple of 16, 16-B aligned) with vector stores; graph-capturable
+// zero `bytes` with a kernel (16-B vector stores when p / bytes are 16-B multiples, else 4-B stores; p and bytes
+// must be 4-B multiples); graph-capturable, and unlike a hipMemsetAsync node it is an ordinary kernel node
 int sa_zero(void* p, size_t bytes, hipStream_t stream);
 
 // F.avg_pool2d(x, 3, stride=2, padding=1) (count_include_pad) on NHWC fp16

@@ -140,6 +140,11 @@ struct SplitKWorkspace {
   mutable int32_t max_counters = 0;
   void alloc(DeviceArena& a, int64_t floats, int32_t counters);  // (re)allocates
 };
+// Zero device memory inside a frame.  Always a kernel node (sa_zero): hipMemsetAsync nodes in a graph replayed
+// with packet capture on a non-blocking stream were seen executing out of order with the kernels around them
+// (tools/diag/replay_stress.py, tools/graph_repro/overlap_repro.hip).  SA_ZERO_MEMSET=1 restores the memset
+// node for that A/B.
+void device_zero(void* p, size_t bytes, hipStream_t s);
 const SplitKWorkspace* current_splitk();
 struct ScopedSplitK {
   const SplitKWorkspace* prev;
@@ -165,6 +170,7 @@ bool conv_tuning_enabled();
 void conv_apply_plan(SaConvArgs& a, hipStream_t s);
 size_t conv_plan_entries();
 long conv_tune_count();     // shapes tuned (timed) in this process
+long conv_tune_rejects();   // tactic candidates rejected by the tuner's output verification
 void conv_plan_clear();     // drop the in-process plan (tests: prove a plan file is used)
 void conv_plan_set_arch(const std::string& gcn_arch_name);  // plan keys carry the device's arch
 const std::string& conv_plan_arch();

@@ -21,6 +21,9 @@ __global__ __launch_bounds__(256) void zero16_kernel(uint4* __restrict__ p, long
   const uint4 z = {0u, 0u, 0u, 0u};
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long)gridDim.x * 256) p[i] = z;
 }
+__global__ __launch_bounds__(256) void zero4_kernel(unsigned* __restrict__ p, long n4) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) p[i] = 0u;
+}
 typedef _Float16 f16;
 typedef f16 half8 __attribute__((ext_vector_type(8)));
 
@@ -215,6 +218,32 @@ __global__ void interp_kernel(const f16* __restrict__ x, int xs, f16* __restrict
   }
 }
 
+// max |a - b| and max |b| over n elements (fp16 or fp32), as float bits in res[0] / res[1] (non-negative
+// floats order like their unsigned bit patterns, so a vector atomicMax merges blocks).  A NaN / inf
+// difference counts as +inf.  Used by the conv tactic tuner to reject a candidate whose output disagrees
+// with the reference candidate's.
+__global__ void absdiff_max_kernel(const void* __restrict__ a, const void* __restrict__ b, long n, int f32,
+                                   unsigned* __restrict__ res) {
+  float md = 0.f, mb = 0.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float x = f32 ? ((const float*)a)[i] : (float)((const f16*)a)[i];
+    const float y = f32 ? ((const float*)b)[i] : (float)((const f16*)b)[i];
+    float d = fabsf(x - y);
+    if (!(d <= 3.0e38f)) d = INFINITY;  // NaN or inf
+    md = fmaxf(md, d);
+    const float ay = fabsf(y);
+    if (ay <= 3.0e38f) mb = fmaxf(mb, ay);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    md = fmaxf(md, __shfl_xor(md, o));
+    mb = fmaxf(mb, __shfl_xor(mb, o));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(res, __float_as_uint(md));
+    atomicMax(res + 1, __float_as_uint(mb));
+  }
+}
+
 inline int grid_for(long work) {
   long g = (work + 255) / 256;
   if (g > 8192) g = 8192;
@@ -225,7 +254,15 @@ inline int grid_for(long work) {
 }  // namespace
 
 extern "C" int sa_zero(void* p, size_t bytes, hipStream_t stream) {
-  if (((uintptr_t)p & 15) || (bytes & 15)) return -2;
+  if (((uintptr_t)p & 3) || (bytes & 3)) return -2;
+  if (((uintptr_t)p & 15) || (bytes & 15)) {  // 4-byte granularity (fp32 / int buffers of any length)
+    const long n4 = (long)(bytes >> 2);
+    if (n4 == 0) return 0;
+    long blocks = (n4 + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(zero4_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (unsigned*)p, n4);
+    return (int)hipGetLastError();
+  }
   const long n16 = (long)(bytes >> 4);
   if (n16 == 0) return 0;
   long blocks = (n16 + 255) / 256;
@@ -275,6 +312,12 @@ extern "C" int sa_interp_bilinear(const void* x, int xs, void* out, int os, int 
   if (work >= (1L << 31)) return -2;  // 32-bit index math in the kernel
   hipLaunchKernelGGL(interp_kernel, dim3(grid_for(work)), dim3(256), 0, stream, (const f16*)x, xs,
                      (f16*)out, os, N, H, W, C, Ho, Wo, ac, mul);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_absdiff_max(const void* a, const void* b, long n, int f32, unsigned* res, hipStream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(absdiff_max_kernel, dim3(grid_for(n)), dim3(256), 0, stream, a, b, n, f32, res);
   return (int)hipGetLastError();
 }
 

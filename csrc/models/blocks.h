@@ -30,16 +30,7 @@ class StatsPool {
     size_t idx = (size_t)handle - 1;
     return base_ + offs_[idx];
   }
-  void zero(hipStream_t s) const {
-    const size_t bytes = std::max<size_t>(total_, 1) * sizeof(sa_stat_t);
-    const char* mz = std::getenv("SA_ZERO_MEMSET");  // A/B: 1 = runtime memset (fill kernels)
-    if (mz && mz[0] == '1') {
-      HIP_CHECK(hipMemsetAsync(base_, 0, bytes, s));
-      return;
-    }
-    if (sa_zero(base_, bytes & ~(size_t)15, s) != 0) HIP_CHECK(hipErrorInvalidValue);
-    if (bytes & 15) HIP_CHECK(hipMemsetAsync((char*)base_ + (bytes & ~(size_t)15), 0, bytes & 15, s));
-  }
+  void zero(hipStream_t s) const { device_zero(base_, std::max<size_t>(total_, 1) * sizeof(sa_stat_t), s); }
 
  private:
   std::vector<size_t> reserve_, offs_;

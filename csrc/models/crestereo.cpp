@@ -374,7 +374,7 @@ void CreStereo::forward(hipStream_t s) {
   const Tensor c16r{cross2_.ptr, B, L16.h, L16.w, 256, 256, DT::F16};
 
   // RUM 1/16
-  HIP_CHECK(hipMemsetAsync(L16.flow, 0, (size_t)B * L16.h * L16.w * 2 * 4, s));
+  device_zero(L16.flow, (size_t)B * L16.h * L16.w * 2 * 4, s);
   const int n_coarse = iters_ / 2;
   for (int it = 0; it < n_coarse; ++it)
     update(s, L16, c16l, c16r, &off16_, it % 2 == 1, false, it == n_coarse - 1);
@@ -382,7 +382,7 @@ void CreStereo::forward(hipStream_t s) {
     check(sa_convex_upsample_c(L16.mask.ptr, L16.mask.stride, L16.flow, 2, B, L16.h, L16.w, 4, 1.f, flowup4_, 2, s),
           "convex16");
   } else {
-    HIP_CHECK(hipMemsetAsync(flowup4_, 0, (size_t)B * h4 * w4 * 2 * 4, s));
+    device_zero(flowup4_, (size_t)B * h4 * w4 * 2 * 4, s);
   }
   check(sa_interp_flow(flowup4_, L8.flow, B, h4, w4, 2, L8.h, L8.w, -(float)L8.h / (float)h4, s), "interp8");
   // RUM 1/8

@@ -397,7 +397,7 @@ void RaftStereo::forward(hipStream_t s) {
     zqr_[i].run(s, {ctxh_[i]}, czrq_[i]);
   }
   if (par) join(s);
-  HIP_CHECK(hipMemsetAsync(flow_, 0, (size_t)Bn * h0 * w0 * 4, s));
+  device_zero(flow_, (size_t)Bn * h0 * w0 * 4, s);
   stage(s, "encoders+corr");
 
   auto pool = [&](hipStream_t st, int i) {  // pool_[i] = pool2x(net[i])

@@ -123,9 +123,10 @@ void StereoEngine::init() {
     if (e[0] == '1') cfg_.use_graph = false;  // debugging: eager launches (with SA_DEBUG_SYNC=1)
   // Non-blocking engine stream: every dependency on caller work is explicit (launch_frame records an event
   // on the caller's stream and the engine stream waits on it, and the reverse after the frame), so the frame
-  // never implicitly serialises with the legacy null stream.  Round 1 used a blocking stream to dodge a fault
-  // it could not explain; at HEAD the engine's replay screens pass with either kind
-  // (tools/graph_repro/engine_matrix.sh).  SA_ENGINE_STREAM_BLOCKING=1 restores the blocking stream.
+  // never implicitly serialises with the legacy null stream.  Round 1 used a blocking stream to dodge replay
+  // corruption it could not explain; its cause was the hipMemsetAsync nodes in the frame graph (replays with
+  // packet capture on a non-blocking stream diverged, profiles/graph_replay_memset_r02.md).  Frames now zero
+  // memory with kernel nodes only (device_zero).  SA_ENGINE_STREAM_BLOCKING=1 restores the blocking stream.
   static const bool blocking = [] {
     const char* e = std::getenv("SA_ENGINE_STREAM_BLOCKING");
     return e && e[0] == '1';
@@ -198,6 +199,18 @@ void StereoEngine::init() {
     splitk_side2_.alloc(arena_, fl, nc);
   }
   SA_LOGI("%s: built, %.1f MiB device memory", name(), arena_.bytes() / 1048576.0);
+}
+
+long StereoEngine::nonzero_splitk_counters() {
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  long bad = 0;
+  for (const SplitKWorkspace* w : {&splitk_, &splitk_side_, &splitk_side2_}) {
+    if (!w->counters || w->n_counters <= 0) continue;
+    std::vector<int32_t> h((size_t)w->n_counters);
+    HIP_CHECK(hipMemcpy(h.data(), w->counters, h.size() * 4, hipMemcpyDeviceToHost));
+    for (int32_t v : h) bad += v != 0;
+  }
+  return bad;
 }
 
 std::string StereoEngine::default_plan_path() const {

@@ -546,6 +546,20 @@ void ConvLayer::run(hipStream_t s, const std::vector<Tensor>& srcs, const Tensor
   launch(s, a);
 }
 
+void device_zero(void* p, size_t bytes, hipStream_t s) {
+  static const bool memset_node = [] {
+    const char* e = std::getenv("SA_ZERO_MEMSET");
+    return e && e[0] == '1';
+  }();
+  if (bytes == 0) return;
+  if (memset_node) {
+    HIP_CHECK(hipMemsetAsync(p, 0, bytes, s));
+    return;
+  }
+  SA_REQUIRE(sa_zero(p, bytes, s) == 0, "device_zero: %zu bytes at %p (needs 4-byte multiples)", bytes, p);
+  SA_LAUNCH_CHECK(s);
+}
+
 static thread_local const SplitKWorkspace* g_splitk = nullptr;
 const SplitKWorkspace* current_splitk() { return g_splitk; }
 ScopedSplitK::ScopedSplitK(const SplitKWorkspace* w) : prev(g_splitk) { g_splitk = w; }
@@ -588,6 +602,7 @@ thread_local bool g_tuning = false;
 thread_local std::vector<std::string>* g_plan_collect = nullptr;  // keys consulted by the engine being built
 std::string g_arch = "gfx950";  // device gcnArchName (base name), set by conv_plan_set_arch
 long g_tuned = 0;               // shapes tuned in this process (sa_conv_tune_count)
+long g_rejected = 0;            // tactic candidates rejected by output verification (sa_conv_tune_rejects)
 
 std::string plan_file() {
   const char* e = std::getenv("SA_PLAN_CACHE");
@@ -640,11 +655,31 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
       a.stats ? (size_t)std::max(1, a.stats_slots) * a.N * a.Cout * 2 * sizeof(sa_stat_t) + 256 : 0;
   const size_t proj_bytes = a.proj_out ? (size_t)4 * std::max(1, a.proj_taps * a.proj_oc) * a.proj_plane * 4 + 256 : 0;
   char* scratch = nullptr;
-  HIP_CHECK(hipMalloc((void**)&scratch, out_bytes + stats_bytes + proj_bytes));
+  const size_t all_bytes = out_bytes + stats_bytes + proj_bytes;
+  HIP_CHECK(hipMalloc((void**)&scratch, all_bytes));
   SaConvArgs t = a;
   if (t.out) t.out = scratch;
-  if (t.epi == SA_EPI_GRU_ZR) t.aux = t.rh = scratch;
+  if (t.epi == SA_EPI_GRU_ZR) {  // z and r*h (fp16) in disjoint halves, so both can be verified
+    t.aux = scratch;
+    t.rh = scratch + (((size_t)Mo * width * 2 + 255) & ~(size_t)255);
+  }
   if (t.epi == SA_EPI_GRU_Q) t.hbuf = scratch;
+  // Tactic verification: every candidate's output (from zeroed scratch, so in-place epilogues start from
+  // the same state) is compared with the first candidate's; one that disagrees is logged and never chosen.
+  // SA_TUNE_VERIFY=0 skips it.
+  static const bool verify = [] {
+    const char* e = std::getenv("SA_TUNE_VERIFY");
+    return !(e && e[0] == '0');
+  }();
+  const bool out_f32 = t.epi == SA_EPI_STORE_F32 || t.epi == SA_EPI_FLOW_ACC;
+  char* ref = nullptr;
+  unsigned* res = nullptr;
+  if (verify) {
+    HIP_CHECK(hipMalloc((void**)&ref, all_bytes));
+    HIP_CHECK(hipMalloc((void**)&res, 2 * sizeof(unsigned)));
+  }
+  bool have_ref = false;
+  int ref_cfg = -1, ref_sk = 0;
   if (t.stats) t.stats = reinterpret_cast<sa_stat_t*>(scratch + out_bytes);
   if (t.proj_out) t.proj_out = reinterpret_cast<float*>(scratch + out_bytes + stats_bytes);
   hipEvent_t e0, e1;
@@ -667,6 +702,38 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
         (void)hipGetLastError();
         continue;
       }
+      if (verify) {
+        HIP_CHECK(hipMemsetAsync(scratch, 0, all_bytes, s));
+        HIP_CHECK((hipError_t)sa_conv2d(&t, s));
+        if (!have_ref) {
+          HIP_CHECK(hipMemcpyAsync(ref, scratch, all_bytes, hipMemcpyDeviceToDevice, s));
+          have_ref = true;
+          ref_cfg = cfg;
+          ref_sk = sk;
+        } else {
+          HIP_CHECK(hipMemsetAsync(res, 0, 2 * sizeof(unsigned), s));
+          HIP_CHECK((hipError_t)sa_absdiff_max(scratch, ref, (long)(out_bytes / (out_f32 ? 4 : 2)), out_f32 ? 1 : 0,
+                                               res, s));
+          if (proj_bytes)
+            HIP_CHECK((hipError_t)sa_absdiff_max(scratch + out_bytes + stats_bytes, ref + out_bytes + stats_bytes,
+                                                 (long)(proj_bytes / 4), 1, res, s));
+          unsigned h[2];
+          HIP_CHECK(hipMemcpyAsync(h, res, sizeof(h), hipMemcpyDeviceToHost, s));
+          HIP_CHECK(hipStreamSynchronize(s));
+          float md, mb;
+          std::memcpy(&md, &h[0], 4);
+          std::memcpy(&mb, &h[1], 4);
+          if (!(md <= 3e-2f * mb + 1e-2f)) {
+            {
+              std::lock_guard<std::mutex> lk(g_plan_mu);
+              ++g_rejected;
+            }
+            SA_LOGW("conv tactic cfg %d splitk %d rejected: max |diff| %g vs cfg %d splitk %d (max |ref| %g) for %s",
+                    cfg, sk, md, ref_cfg, ref_sk, mb, plan_key(a).c_str());
+            continue;
+          }
+        }
+      }
       float best_ms = 1e30f;
       for (int rep = 0; rep < 3; ++rep) {
         HIP_CHECK(hipEventRecord(e0, s));
@@ -684,6 +751,8 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
   HIP_CHECK(hipEventDestroy(e0));
   HIP_CHECK(hipEventDestroy(e1));
   HIP_CHECK(hipFree(scratch));
+  if (ref) HIP_CHECK(hipFree(ref));
+  if (res) HIP_CHECK(hipFree(res));
   return best;
 }
 
@@ -701,6 +770,11 @@ size_t conv_plan_entries() {
 long conv_tune_count() {
   std::lock_guard<std::mutex> lk(g_plan_mu);
   return g_tuned;
+}
+
+long conv_tune_rejects() {
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  return g_rejected;
 }
 
 void conv_plan_clear() {

@@ -171,7 +171,9 @@ def _declare_dev(lib):
         "sa_engine_stream": (_p, [_p]),
         "sa_engine_plan_path": (C.c_char_p, [_p]),
         "sa_engine_tuned_shapes": (C.c_long, [_p]),
+        "sa_engine_nonzero_splitk_counters": (C.c_long, [_p]),
         "sa_conv_tune_count": (C.c_long, []),
+        "sa_conv_tune_rejects": (C.c_long, []),
         "sa_conv_plan_clear": (None, []),
         "sa_engine_stage_times": (_i, [_p, C.POINTER(C.c_float), C.POINTER(C.c_char_p), _i]),
     }

@@ -70,6 +70,10 @@ class NativeStereoEngine:
         """Conv shapes this engine had to time at build (0 when its plan file covered everything)."""
         return int(self._lib.sa_engine_tuned_shapes(self._h))
 
+    def nonzero_splitk_counters(self) -> int:
+        """Diagnostic: split-K tile counters left non-zero (0 after every correctly ordered frame)."""
+        return int(self._lib.sa_engine_nonzero_splitk_counters(self._h))
+
     def set_Q(self, Q):
         q = np.ascontiguousarray(np.asarray(Q, dtype=np.float32).reshape(16))
         N.check(self._lib.sa_engine_set_q(self._h, q.ctypes.data_as(C.c_void_p)), "set_Q")
