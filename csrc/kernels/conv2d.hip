@@ -156,12 +156,23 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 // PROJ: the SA_EPI_PROJ epilogue is compiled only into its own instantiations -- its registers
 // (hoisted tap weights, 16 partials) would otherwise cost every other conv its occupancy
-template <int BM, int BN, int WM, int WN, int MODE, bool PROJ = false>
-__global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvArgs p) {
+// One (tile, k-range) work item of the implicit GEMM: the output tile (bx, by) over k-steps [kt0, kt0 + nk).
+// S > 1: this item is contributor z of the S items of tile `ctr`; it writes its partial sums to its slab and
+// the last contributor to arrive (counter ctr) sums the S contributors' slabs in contributor order and runs
+// the epilogue.  Grid mode (skG == 0): contributor c's slab is slab_base + c.  Stream-K (skG = G blocks over
+// skI k-steps): contributor c is block b = slab_base + c, and since only a block's first and last segments
+// can be partial tiles its slab is 2b (the segment starts the block's range) or 2b + 1, so 2G slabs cover
+// any tile count.  Called once per block (grid tiling / split-K) or once per segment of a stream-K block.
+template <int BM, int BN, int WM, int WN, int MODE, bool PROJ>
+__device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const int bx, const int by, const int kt0,
+                                          const int nk, const int S, const int z, const int slab_base,
+                                          const int ctr, const int skG, const long skI) {
   using C = ConvCfg<BM, BN, WM, WN, MODE>;
-  __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
 
-  const int tid = threadIdx.x;
+  // opaque per call: in the stream-K segment loop nothing lane-dependent is hoisted out of the loop (it would
+  // stay live across the main loop)
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar LDS bases)
   const int wm = wave / WN, wn = wave % WN;
@@ -172,25 +183,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
   const int KD = p.KD > 0 ? p.KD : 1, Di = p.Di > 0 ? p.Di : 1, Do = p.Do > 0 ? p.Do : 1;
   const int sd = p.sd > 0 ? p.sd : 1;
   const int M = p.N * Do * HWo;
-  // tile coordinates; kGlds3 walks the (m, n) tiles in an XCD-aware order: consecutive dispatch
-  // ids round-robin over the 8 XCDs, so give each XCD a contiguous run of m-major tiles (neighbour
-  // tiles share input rows through the 3x3 halo, the n tiles of one m share the whole A panel)
-  int bx = blockIdx.x, by = blockIdx.y;
-  if constexpr (MODE == kGlds3 || MODE == kWide) {
-    const int nwg = gridDim.x * gridDim.y;
-    const int bid = blockIdx.y * gridDim.x + blockIdx.x;
-    const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
-    const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-    bx = lin / gridDim.y;
-    by = lin - bx * gridDim.y;
-  }
   const int m0 = bx * BM;
   const int n0 = by * BN;
-  // split-K slice of the K loop handled by this block
-  const int S = gridDim.z, z = blockIdx.z;
-  const int nk_all = p.Kpad / C::BK;
-  const int kt0 = (int)((long)z * nk_all / S);
-  const int nk = (int)((long)(z + 1) * nk_all / S) - kt0;
   const int khw = p.KH * p.KW;
   const int taps = KD * khw;
 
@@ -974,9 +968,15 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
   // Protocol of cdna_hip_programming.md "Projection GEMM at M = 256" item 2 (agent-scope release
   // by every slice, acquire by the last arriver), valid for any placement of slices over XCDs.
   if (!C::WIDE && S > 1) {  // (kWide is always launched unsplit)
-    const int tile = by * gridDim.x + bx;
+    const int tile = ctr;
     constexpr int SLAB = BM * BN;
-    float* slab = p.ws + ((size_t)tile * S + z) * SLAB;
+    auto slab_of = [&](int c) -> size_t {
+      if (skG == 0) return (size_t)slab_base + c;
+      const int b = slab_base + c;
+      const int first_tile = (int)((long)b * skI / skG / (p.Kpad / C::BK));
+      return 2 * (size_t)b + (first_tile == ctr ? 0 : 1);
+    };
+    float* slab = p.ws + slab_of(z) * SLAB;
 #pragma unroll
     for (int i = 0; i < C::FM; ++i)
 #pragma unroll
@@ -1009,7 +1009,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
 #pragma unroll
       for (int j = 0; j < C::FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
     for (int sl = 0; sl < S; ++sl) {
-      const float* os = p.ws + ((size_t)tile * S + sl) * SLAB;
+      const float* os = p.ws + slab_of(sl) * SLAB;
 #pragma unroll
       for (int i = 0; i < C::FM; ++i)
 #pragma unroll
@@ -1321,6 +1321,73 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
   }
 }
 
+// Grid tiling (+ split-K over gridDim.z), or stream-K for the DMA-ring family (p.splitk == -1, grid (G, 1, 1)):
+// the T x nk_all k-steps of all tiles are cut into G equal contiguous ranges, block b walks its range as
+// (tile, k-range) segments (a segment ends at a tile or range boundary), and tiles whose k-steps span several
+// blocks are finished by the last contributor (conv_tile's split-K path, 2G partial slabs).
+// Every block does the same amount of MFMA work whatever T is, so grids of 150 or 600 tiles no longer leave
+// CUs idle in the last wave (Osama et al., "Stream-K", PPoPP'23).
+template <int BM, int BN, int WM, int WN, int MODE, bool PROJ = false>
+__global__ __launch_bounds__(64 * WM * WN) void conv_igemm_streamk_kernel(const SaConvArgs p) {
+  static_assert(MODE == kGlds3, "stream-K is built for the DMA-ring family");
+  using C = ConvCfg<BM, BN, WM, WN, MODE>;
+  __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
+  const int nk_all = p.Kpad / C::BK;
+  const int M = p.N * (p.Do > 0 ? p.Do : 1) * p.Ho * p.Wo;
+  const int gy = (p.Cout + BN - 1) / BN;
+  const long T = (long)((M + BM - 1) / BM) * gy;
+  const long I = T * nk_all;
+  const int G = gridDim.x;
+  // XCD-major logical block id: consecutive ranges (which share tiles and A panels) on one XCD's L2
+  const int b = (G & 7) ? (int)blockIdx.x : (int)((blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3));
+  long it = (long)b * I / G;
+  const long end = (long)(b + 1) * I / G;
+  // the argument block is re-read through an opaque pointer per segment: otherwise every kernarg load of the
+  // tile body is hoisted out of this loop and the live SGPRs spill
+  // (p is the kernel's only explicit argument: it sits at offset 0 of the kernarg segment.  Taking &p instead
+  // would give the address of a private copy.)
+  typedef const __attribute__((address_space(4))) SaConvArgs* kernarg_ptr;  // constant (kernarg) address space
+  kernarg_ptr pp = (kernarg_ptr)__builtin_amdgcn_kernarg_segment_ptr();
+  while (it < end) {
+    const int t = (int)(it / nk_all);
+    const int kb = (int)(it - (long)t * nk_all);
+    const int ke = (int)((long)nk_all < kb + (end - it) ? nk_all : kb + (end - it));
+    // contributors of tile t: the blocks whose ranges meet [t * nk_all, (t + 1) * nk_all)
+    const int bf = (int)((((long)t * nk_all + 1) * G + I - 1) / I) - 1;
+    const int bl = (int)((((long)(t + 1) * nk_all) * G + I - 1) / I) - 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("" : "+s"(pp));
+    conv_tile<BM, BN, WM, WN, MODE, PROJ>(*(const SaConvArgs*)pp, smem, t / gy, t % gy, kb, ke - kb, bl - bf + 1, b - bf, bf, t, G, I);
+    it += ke - kb;
+    __syncthreads();  // the next segment's DMA reuses the LDS this segment's epilogue read
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int MODE, bool PROJ = false>
+__global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvArgs p) {
+  using C = ConvCfg<BM, BN, WM, WN, MODE>;
+  __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
+  const int nk_all = p.Kpad / C::BK;
+  // grid tiling; kGlds3 / kWide walk the (m, n) tiles in an XCD-aware order: consecutive dispatch ids
+  // round-robin over the 8 XCDs, so give each XCD a contiguous run of m-major tiles (neighbour tiles share
+  // input rows through the 3x3 halo, the n tiles of one m share the whole A panel)
+  int bx = blockIdx.x, by = blockIdx.y;
+  if constexpr (MODE == kGlds3 || MODE == kWide) {
+    const int nwg = gridDim.x * gridDim.y;
+    const int bid = blockIdx.y * gridDim.x + blockIdx.x;
+    const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
+    const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    bx = lin / gridDim.y;
+    by = lin - bx * gridDim.y;
+  }
+  // split-K slice of the K loop handled by this block
+  const int S = gridDim.z, z = blockIdx.z;
+  const int kt0 = (int)((long)z * nk_all / S);
+  const int nk = (int)((long)(z + 1) * nk_all / S) - kt0;
+  const int tile = by * gridDim.x + bx;
+  conv_tile<BM, BN, WM, WN, MODE, PROJ>(p, smem, bx, by, kt0, nk, S, z, tile * S, tile, 0, 0);
+}
+
 template <int BM, int BN, int WM, int WN, int MODE>
 void launch_kernel(dim3 grid, const SaConvArgs* a, hipStream_t stream) {
   if (a->epi == SA_EPI_PROJ)
@@ -1333,6 +1400,18 @@ thread_local long g_split_floats = 0, g_split_tiles = 0;
 inline void note_split(int S, long tiles, long tile_floats) {
   g_split_floats = S > 1 ? (long)S * tiles * tile_floats : 0;
   g_split_tiles = S > 1 ? tiles : 0;
+}
+
+// CUs of the current device (stream-K grids are sized to one or two waves of blocks over them)
+int device_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -1364,6 +1443,7 @@ int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
   const int gx = (M + BM - 1) / BM, gy = (a->Cout + BN - 1) / BN;
   const long tiles = (long)gx * gy;
   const int nk = a->Kpad / (gl || k64 ? 64 : 32);
+  if (a->splitk < 0) return -4;  // stream-K exists for the DMA-ring (kGlds3) family only
   int S = a->splitk;
   if (S == 0) {
     // auto: split the K loop when the tile grid cannot fill 256 CUs (small-M levels of the
@@ -1400,6 +1480,28 @@ int launch_glds3(const SaConvArgs* a, hipStream_t stream, bool forced) {
   const int gx = (M + BM - 1) / BM, gy = (a->Cout + BN - 1) / BN;
   const long tiles = (long)gx * gy;
   const int nk = a->Kpad / 64;
+  if (a->splitk == -1) {
+    // stream-K: G resident blocks (LDS / waves per CU), 2G partial slabs, T tile counters
+    using C = ConvCfg<BM, BN, WM, WN, kGlds3>;
+    int per_cu = 163840 / C::SMEM;
+    if (per_cu > 8 / C::NW) per_cu = 8 / C::NW;  // <= 2 waves per SIMD
+    if (per_cu < 1) per_cu = 1;
+    long G = (long)device_cus() * per_cu;
+    if (G > tiles * nk) G = tiles * nk;
+    const long slabs = 2 * G;
+    if (a->stats || !a->ws || !a->counters || slabs * BM * BN > a->ws_floats || tiles > a->n_counters ||
+        tiles * nk * (long)G >= (1L << 62))
+      return forced ? -4 : 1;
+    g_split_floats = slabs * BM * BN;
+    g_split_tiles = tiles;
+    if (a->epi == SA_EPI_PROJ)
+      hipLaunchKernelGGL((conv_igemm_streamk_kernel<BM, BN, WM, WN, kGlds3, true>), dim3((unsigned)G), dim3(C::NT), 0,
+                         stream, *a);
+    else
+      hipLaunchKernelGGL((conv_igemm_streamk_kernel<BM, BN, WM, WN, kGlds3, false>), dim3((unsigned)G), dim3(C::NT),
+                         0, stream, *a);
+    return (int)hipGetLastError();
+  }
   int S = a->splitk;
   if (S == 0) {
     // auto: one block per CU, so aim for >= ~2 blocks per CU over the 256 CUs

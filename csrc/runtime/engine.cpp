@@ -150,9 +150,11 @@ void StereoEngine::init() {
   cloud_ = (float*)arena_.alloc((size_t)B() * H() * W() * 6 * 4);
   HIP_CHECK(hipHostMalloc((void**)&pin_in_, 2 * img, hipHostMallocDefault));
   HIP_CHECK(hipHostMalloc((void**)&pin_out_, (size_t)B() * H() * W() * 7 * 4 + 2 * img, hipHostMallocDefault));
-  splitk_.alloc(arena_, 16l << 20, 8192);  // 64 MiB of fp32 slabs, 8192 tile counters
-  splitk_side_.alloc(arena_, 16l << 20, 8192);
-  splitk_side2_.alloc(arena_, 16l << 20, 8192);
+  // generous split-K / stream-K workspaces for the tuning pass (128 MiB of fp32 slabs, 8192 tile counters);
+  // right-sized to the tuned plan's high-water mark afterwards
+  splitk_.alloc(arena_, 32l << 20, 8192);
+  splitk_side_.alloc(arena_, 32l << 20, 8192);
+  splitk_side2_.alloc(arena_, 32l << 20, 8192);
   WeightSource src{store_.get(), cfg_.weights.empty(), cfg_.seed};
   TraceRange tr("engine build");
   build(src);

@@ -694,8 +694,9 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
     // wide tiles (one block per CU, never split): only where their grid still covers the chip
     if ((cfg == 10 || cfg == 12) && (a.Cout <= 128 || ((M + 255) / 256) * ((a.Cout + 255) / 256) < 256)) continue;
     if ((cfg == 11 || cfg == 13) && ((M + 511) / 512) * ((a.Cout + 127) / 128) < 256) continue;
-    for (int sk : {1, 0}) {
+    for (int sk : {1, 0, -1}) {
       if (sk == 0 && (!can_split || cfg >= 9)) continue;
+      if (sk == -1 && (!can_split || cfg < 4 || cfg > 8)) continue;  // stream-K: DMA-ring family only
       t.tile_cfg = cfg;
       t.splitk = sk;
       if (sa_conv2d(&t, s) != 0) {

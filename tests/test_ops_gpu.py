@@ -173,6 +173,63 @@ def test_conv2d_glds3_vs_torch(srcs, cout, k, stride, hw, n, splitk, cfg):
         assert rel_err(nchw(out), ref) < 2e-3
 
 
+@pytest.mark.parametrize("srcs,cout,k,hw,n", [
+    ((128, 128, 128), 256, 3, (120, 160), 1),  # RAFT-SF 1/4 GRU z/r at batch 1 (150 tiles of 256x128 < 256 CUs)
+    ((128, 256), 256, 3, (60, 80), 2),         # multi-tile stream-K ranges, tiles spanning images
+    ((64,), 128, 3, (17, 23), 1),              # fewer k-steps than blocks (G capped), M tail
+    ((192, 64), 96, 1, (9, 30), 3),            # 1x1, Cout < BN
+])
+@pytest.mark.parametrize("cfg", [4, 5, 7, 8])
+def test_conv2d_streamk_vs_torch(srcs, cout, k, hw, n, cfg):
+    """Stream-K (splitk = -1): G resident blocks share the T x nk k-steps equally, partial tiles are finished
+    by the last contributor.  Repeated launches must be bitwise identical (fixed-order reduction, counters
+    reset by the last arriver) and match torch."""
+    O = ops()
+    torch.manual_seed(13)
+    xs = [torch.randn(n, c, *hw, device=DEV) for c in srcs]
+    cin = sum(srcs)
+    w = torch.randn(cout, cin, k, k, device=DEV) / math.sqrt(cin * k * k)
+    b = torch.randn(cout, device=DEV) * 0.1
+    ref = F.conv2d(torch.cat([x.half().float() for x in xs], 1), w.half().float(), b, padding=k // 2)
+    ref = F.leaky_relu(ref, 0.1)
+    wp, kpad, _ = O.pack_conv_weight(w)
+    ws = O.splitk_workspace(1 << 25, 8192)
+    outs = []
+    for _ in range(3):
+        out = O.conv2d([nhwc(x).half() for x in xs], wp, kpad, cout, k, k, bias=b.contiguous(), act="leaky",
+                       alpha=0.1, tile_cfg=cfg, splitk=-1, workspace=ws)
+        torch.cuda.synchronize()
+        outs.append(out.clone())
+        assert rel_err(nchw(out), ref) < 2e-3
+    assert all(torch.equal(o, outs[0]) for o in outs)
+    assert int(ws[1].abs().sum()) == 0, "tile counters not reset"
+
+
+def test_conv2d_streamk_gru_zr_epilogue():
+    """Stream-K with the fused ConvGRU z / r*h epilogue (the RAFT b1 hot conv)."""
+    O = ops()
+    torch.manual_seed(14)
+    n, hd, h, w = 1, 128, 60, 80
+    net = torch.randn(n, hd, h, w, device=DEV).tanh()
+    x = torch.randn(n, 256, h, w, device=DEV)
+    cz, cr = (torch.randn(n, hd, h, w, device=DEV) * 0.5 for _ in range(2))
+    wz, wr = (torch.randn(hd, hd + 256, 3, 3, device=DEV) / math.sqrt((hd + 256) * 9) for _ in range(2))
+    hx = torch.cat([net, x], 1).half().float()
+    z = torch.sigmoid(F.conv2d(hx, wz.half().float(), padding=1) + cz.half().float())
+    r = torch.sigmoid(F.conv2d(hx, wr.half().float(), padding=1) + cr.half().float())
+    net_h = nhwc(net).half()
+    ctx = nhwc(torch.cat([cz, cr], 1)).half()
+    wzr, kpad, _ = O.pack_conv_weight(torch.cat([wz, wr], 0))
+    zb = torch.empty(n, h, w, hd, device=DEV, dtype=torch.float16)
+    rhb = torch.empty_like(zb)
+    ws = O.splitk_workspace(1 << 25, 8192)
+    O.conv2d([net_h, nhwc(x).half()], wzr, kpad, 2 * hd, 3, 3, out=zb, epi="gru_zr", ctx=ctx, aux=zb,
+             hbuf=net_h, rh=rhb, tile_cfg=4, splitk=-1, workspace=ws)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(zb), z) < 3e-3
+    assert rel_err(nchw(rhb), r * net.half().float()) < 3e-3
+
+
 @pytest.mark.parametrize("cfg", [4, 10, 11, 12, 13])
 def test_conv2d_glds3_gru_and_stats_epilogues(cfg):
     O = ops()

@@ -40,12 +40,14 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--cfgs", default="-1", help="comma list of tile configs (-1 = launcher's choice, 4 = glds3)")
+    ap.add_argument("--splits", default="", help="comma list of split-K modes (0 = auto, 1 = off, >1 forced, -1 = stream-K); "
+                    "default: the shape's own setting")
     ap.add_argument("--stats", type=int, default=0, help="fuse instance-norm statistics over N slots (engine: 16)")
     a = ap.parse_args()
     import torch
     from stereoalgorithms_amd import ops as O
     torch.manual_seed(0)
-    ws = O.splitk_workspace(1 << 24, 8192)
+    ws = O.splitk_workspace(1 << 25, 8192)
     for name in a.shapes.split(","):
         n, h, w, cin, cout, k, sk = SHAPES[name]
         x = torch.randn(n, h, w, cin, device="cuda").half()
@@ -53,7 +55,9 @@ def main():
         wp, kpad, _ = O.pack_conv_weight(wt)
         b = torch.zeros(cout, device="cuda")
         out = torch.empty(n, h, w, cout, device="cuda", dtype=torch.float16)
-        for cfg in map(int, a.cfgs.split(",")):
+        combos = [(cfg, sp) for cfg in map(int, a.cfgs.split(","))
+                  for sp in (map(int, a.splits.split(",")) if a.splits else [sk])]
+        for cfg, sk in combos:
             kw = dict(bias=b, out=out, splitk=sk, workspace=ws if sk != 1 else None, tile_cfg=cfg)
             if a.stats:
                 kw["stats"] = torch.zeros(16, n, cout, 2, dtype=torch.int64, device="cuda")
@@ -63,7 +67,7 @@ def main():
                 for _ in range(3):
                     O.conv2d(x, wp, kpad, cout, k, k, **kw)
             except RuntimeError as e:
-                print(f"{name:6s} cfg {cfg}: {e}", flush=True)
+                print(f"{name:6s} cfg {cfg} split {sk}: {e}", flush=True)
                 continue
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -74,7 +78,7 @@ def main():
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) / a.iters * 1e3
             flop = 2.0 * n * h * w * cout * cin * k * k
-            print(f"{name:6s} cfg {cfg:2d} M={n * h * w:7d} K={cin * k * k:5d} N={cout:4d}: {us:8.2f} us  "
+            print(f"{name:6s} cfg {cfg:2d} split {sk} M={n * h * w:7d} K={cin * k * k:5d} N={cout:4d}: {us:8.2f} us  "
                   f"{flop / us / 1e6:7.1f} TFLOP/s", flush=True)
 
 
