@@ -73,7 +73,11 @@ enum : int {
                  // flight), v_mfma_f32_32x32x16_f16 on a 128x64 wave tile (8 waves), one raw barrier
                  // per stage, fragment reads software-pipelined at k16 granularity; epilogue in two
                  // row bands (the fp32 C tile is staged through LDS one band at a time)
+  kGldsDeep = 6,  // kGlds3 with the LDS ring as deep as 160 KB allows (up to 8 stages, NSTAGE - 1 in
+                  // flight): for the small-M / deep-K convs of the coarse GRU levels and the motion
+                  // encoder, whose k-steps wait on DMA latency rather than on the MFMAs
 };
+__host__ __device__ constexpr bool is_glds(int mode) { return mode == kGlds3 || mode == kGldsDeep; }
 
 template <int BM, int BN, int WM, int WN, int MODE = kRegK32>
 struct ConvCfg {
@@ -88,8 +92,10 @@ struct ConvCfg {
   static constexpr int NW = WM * WN, NT = 64 * NW;  // waves / threads per workgroup
   static constexpr int A_PT = (A_CH + NT - 1) / NT, B_PT = (B_CH + NT - 1) / NT;
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  // kGlds3: three-deep LDS ring; kWide: four-deep; everything else double-buffered
-  static constexpr int NSTAGE = MODE == kGlds3 ? 3 : (WIDE ? 4 : 2);
+  // kGlds3: three-deep LDS ring; kGldsDeep: as deep as 160 KB allows (<= 8); kWide: four-deep; everything
+  // else double-buffered
+  static constexpr int DEEP_NS = 163840 / (A_BYTES + B_BYTES) < 8 ? 163840 / (A_BYTES + B_BYTES) : 8;
+  static constexpr int NSTAGE = MODE == kGlds3 ? 3 : MODE == kGldsDeep ? DEEP_NS : (WIDE ? 4 : 2);
   static constexpr int STAGE_BYTES = NSTAGE * (A_BYTES + B_BYTES);
   // fp32 C tile, unpadded rows; columns XOR-swizzled in 16-float blocks (cswz) so the MFMA
   // write-out (4 row groups x 16 lanes) hits 64 distinct banks; aliases the stage buffers.
@@ -98,7 +104,8 @@ struct ConvCfg {
   static constexpr int CROWS = WIDE ? (32768 / BN < BM ? 32768 / BN : BM) : BM;
   static constexpr int C_BYTES = CROWS * CST * 4;
   static constexpr int SMEM = STAGE_BYTES > C_BYTES ? STAGE_BYTES : C_BYTES;
-  static_assert(WM * WN == 4 || (WM * WN == 8 && (MODE == kGlds3 || WIDE)), "4 waves (8 for kGlds3; 4 or 8 for kWide) per workgroup");
+  static_assert(WM * WN == 4 || (WM * WN == 8 && (is_glds(MODE) || WIDE)), "4 waves (8 for kGlds3; 4 or 8 for kWide) per workgroup");
+  static_assert(!is_glds(MODE) || NSTAGE >= 3, "DMA rings keep at least one stage in flight across the barrier");
   static_assert(TM % 16 == 0 && TN % 16 == 0, "wave tile must be 16-aligned");
   static_assert(!WIDE || (TM == 128 && (TN == 64 || TN == 128)), "kWide: 128x64 or 128x128 wave tiles");
 };
@@ -152,6 +159,18 @@ __device__ __forceinline__ void wait_vmcnt() {
   SA_VMCNT_CASE(24) SA_VMCNT_CASE(25) SA_VMCNT_CASE(26) SA_VMCNT_CASE(27) SA_VMCNT_CASE(28) SA_VMCNT_CASE(29)
   SA_VMCNT_CASE(30) SA_VMCNT_CASE(31) SA_VMCNT_CASE(32)
 #undef SA_VMCNT_CASE
+}
+
+// s_waitcnt vmcnt(s * PER) for a wave-uniform s in [0, K]: "at most s stages of PER DMA instructions each are
+// still in flight"
+template <int PER, int K>
+__device__ __forceinline__ void wait_stages(int s) {
+  if constexpr (K <= 0) {
+    wait_vmcnt<0>();
+  } else {
+    if (s >= K) wait_vmcnt<K * PER>();
+    else wait_stages<PER, K - 1>(s);
+  }
 }
 
 // PROJ: the SA_EPI_PROJ epilogue is compiled only into its own instantiations -- its registers
@@ -323,7 +342,7 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
       if (kt + 1 < nk) store_tile(cur ^ 1);
       __syncthreads();
     }
-  } else if constexpr (MODE == kGlds3) {
+  } else if constexpr (is_glds(MODE)) {
     // ---------------- uniform-k im2col via global->LDS DMA, 3-deep LDS ring, BK = 64 -------------
     // Stage image per operand: [rows][64 halfs] (128-B rows), lane-linear per wave instruction
     // (slot q*16 = row*128 + pch*16) with the XOR swizzle on the SOURCE chunk (lch = pch ^
@@ -481,28 +500,30 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
     // (stage kt+2 stays in flight), barrier, the kk=1 MFMAs of stage kt with the kk=0 reads of
     // stage kt+1 interleaved, then refill stage kt's now-free buffer with stage kt+3.  Each
     // stage's DMA has two k-steps to land; LDS reads always run under MFMAs.
+    // Generalised to an NS-deep ring (kGldsDeep): the prologue issues NS stages, iteration kt waits for
+    // stage kt + 1 with min(nk - kt - 2, NS - 2) later stages still in flight and refills stage kt's buffer
+    // with stage kt + NS.
+    constexpr int NS = C::NSTAGE;
+    static_assert((NS - 1) * (NA + NB) <= 32, "vmcnt literal range");
     half8 a0[C::FM], b0[C::FN], a1[C::FM], b1[C::FN];
-    if (nk > 0) issue(0);
-    if (nk > 1) issue(1);
-    if (nk > 2) issue(2);
-    if (nk > 2) wait_vmcnt<2 * (NA + NB)>();
-    else if (nk > 1) wait_vmcnt<NA + NB>();
-    else wait_vmcnt<0>();
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      if (nk > s) issue(s);
+    wait_stages<NA + NB, NS - 1>(nk < NS ? nk - 1 : NS - 1);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (nk > 0) read_half(0, 0, a0, b0);
     int cur = 0;
     for (int kt = 0; kt < nk; ++kt) {
       mfma_read(a0, b0, cur, 1, a1, b1);
-      const int nxt = cur == 2 ? 0 : cur + 1;
+      const int nxt = cur == NS - 1 ? 0 : cur + 1;
       if (kt + 1 < nk) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (kt + 2 < nk) wait_vmcnt<NA + NB>();
-        else wait_vmcnt<0>();
+        wait_stages<NA + NB, NS - 2>(nk - kt - 2 < NS - 2 ? nk - kt - 2 : NS - 2);
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         mfma_read(a1, b1, nxt, 0, a0, b0);
-        if (kt + 3 < nk) issue(cur);
+        if (kt + NS < nk) issue(cur);
       } else {
         mfma_half(a1, b1);
       }
@@ -1372,7 +1393,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
   // round-robin over the 8 XCDs, so give each XCD a contiguous run of m-major tiles (neighbour tiles share
   // input rows through the 3x3 halo, the n tiles of one m share the whole A panel)
   int bx = blockIdx.x, by = blockIdx.y;
-  if constexpr (MODE == kGlds3 || MODE == kWide) {
+  if constexpr (is_glds(MODE) || MODE == kWide) {
     const int nwg = gridDim.x * gridDim.y;
     const int bid = blockIdx.y * gridDim.x + blockIdx.x;
     const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
@@ -1473,14 +1494,16 @@ int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
 // multiple of 64 channels, K unpadded, <= 64 taps).  Returns 1 when the shape does not qualify.
 bool glds3_eligible(const SaConvArgs* a);
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int MODE = kGlds3>
 int launch_glds3(const SaConvArgs* a, hipStream_t stream, bool forced) {
   if (!glds3_eligible(a)) return 1;
   const int M = a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
   const int gx = (M + BM - 1) / BM, gy = (a->Cout + BN - 1) / BN;
   const long tiles = (long)gx * gy;
   const int nk = a->Kpad / 64;
-  if (a->splitk == -1) {
+  if constexpr (MODE != kGlds3) {
+    if (a->splitk == -1) return forced ? -4 : 1;  // stream-K: 3-deep ring only
+  } else if (a->splitk == -1) {
     // stream-K: G resident blocks (LDS / waves per CU), 2G partial slabs, T tile counters
     using C = ConvCfg<BM, BN, WM, WN, kGlds3>;
     int per_cu = 163840 / C::SMEM;
@@ -1518,7 +1541,7 @@ int launch_glds3(const SaConvArgs* a, hipStream_t stream, bool forced) {
                 tiles > a->n_counters || S > nk))
     return forced ? -4 : 1;
   note_split(S, tiles, BM * BN);
-  launch_kernel<BM, BN, WM, WN, kGlds3>(dim3(gx, gy, S), a, stream);
+  launch_kernel<BM, BN, WM, WN, MODE>(dim3(gx, gy, S), a, stream);
   return (int)hipGetLastError();
 }
 
@@ -1569,8 +1592,8 @@ int pick_cfg(const SaConvArgs* a) {
 int cfg_bn(int cfg) {
   switch (cfg) {
     case 10: case 12: return 256;
-    case 0: case 4: case 6: case 7: case 11: case 13: return 128;
-    case 1: case 3: case 5: case 8: case 9: return 64;
+    case 0: case 4: case 6: case 7: case 11: case 13: case 15: return 128;
+    case 1: case 3: case 5: case 8: case 9: case 14: case 16: case 17: return 64;
     case 2: return 16;
     default: return 0;
   }
@@ -1619,6 +1642,15 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
                   : cfg == 6 ? launch_glds3<128, 128, 2, 2>(a, stream, true)
                   : cfg == 7 ? launch_glds3<128, 128, 2, 4>(a, stream, true)
                              : launch_glds3<256, 64, 4, 2>(a, stream, true);
+      return r == 1 ? -5 : r;
+    }
+    case 14: case 15: case 16: case 17: {
+      // deep DMA rings (kGldsDeep): 128x64 / 4 waves (6 stages), 128x128 / 8 waves (5), 64x64 / 4 waves (8),
+      // 256x64 / 8 waves (4); one block per CU
+      const int r = cfg == 14 ? launch_glds3<128, 64, 2, 2, kGldsDeep>(a, stream, true)
+                  : cfg == 15 ? launch_glds3<128, 128, 2, 4, kGldsDeep>(a, stream, true)
+                  : cfg == 16 ? launch_glds3<64, 64, 2, 2, kGldsDeep>(a, stream, true)
+                              : launch_glds3<256, 64, 4, 2, kGldsDeep>(a, stream, true);
       return r == 1 ? -5 : r;
     }
     case 10: case 11: case 12: case 13: {

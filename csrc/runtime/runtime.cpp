@@ -687,8 +687,10 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
   HIP_CHECK(hipEventCreate(&e1));
   PlanEntry best{-1, 1, 1e30f};
   const bool can_split = a.ws && a.counters && !a.stats;
-  // (cfgs 12 / 13, the 4-wave wide tiles, lose everywhere on MI355X (tools/conv_bench.py): not timed)
-  for (int cfg = 0; cfg <= 11; ++cfg) {
+  // (cfgs 12 / 13, the 4-wave wide tiles, lose everywhere on MI355X (tools/conv_bench.py): not timed;
+  // 14-17 are the deep DMA rings)
+  for (int cfg = 0; cfg <= 17; ++cfg) {
+    if (cfg == 12 || cfg == 13) continue;
     if (cfg == 2 && a.Cout > 32) continue;  // 256x16 tile: narrow outputs only
     if (cfg == 6) continue;                 // 128x128 / 4 waves: never competitive (conv_bench)
     // wide tiles (one block per CU, never split): only where their grid still covers the chip

@@ -148,12 +148,12 @@ def test_conv2d_multisource_concat_and_residual():
     ((128, 128, 128), 128, 3, 1, (24, 32), 1, 3),  # three sources + forced split-K
     ((64,), 128, 7, 1, (12, 12), 1, 1),         # 49 taps
 ])
-@pytest.mark.parametrize("cfg", [4, 10, 11, 12, 13])
+@pytest.mark.parametrize("cfg", [4, 10, 11, 12, 13, 14, 15, 16, 17])
 def test_conv2d_glds3_vs_torch(srcs, cout, k, stride, hw, n, splitk, cfg):
     """8-wave global->LDS DMA kernels: 256x128 (cfg 4: 3-deep LDS ring, counted vmcnt, XCD-ordered
-    tiles) and the wide tiles 256x256 / 512x128 (cfg 10 / 11: BK 32 4-deep ring, 32x32x16 MFMA,
-    two-band epilogue; never split)."""
-    if cfg >= 10 and splitk != 1:
+    tiles), the wide tiles 256x256 / 512x128 (cfg 10 / 11: BK 32 4-deep ring, 32x32x16 MFMA,
+    two-band epilogue; never split) and the deep rings (cfg 14-17: 4-8 stages, up to 7 in flight)."""
+    if 10 <= cfg <= 13 and splitk != 1:
         pytest.skip("wide tiles are never split")
     O = ops()
     torch.manual_seed(11)
