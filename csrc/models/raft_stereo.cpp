@@ -101,15 +101,23 @@ class RaftStereo : public StereoEngine {
   float* proj_p_ = nullptr;
   // fused lookup + convc1 + convf1 (sa_raft_motion_head): fp32 [k][64] weights and biases
   float *mh_wc_ = nullptr, *mh_bc_ = nullptr, *mh_wf_ = nullptr, *mh_bf_ = nullptr;
+  void* me_w1_ = nullptr;  // fused motion encoder stage-1 weights (fp16 [128][96]) and bias [128]
+  float* me_b1_ = nullptr;
   bool fuse_motion_ = !(std::getenv("SA_RAFT_FUSE_MOTION") && std::getenv("SA_RAFT_FUSE_MOTION")[0] == '0');
+  // the whole motion encoder (head + convc2/convf2 + conv) as one kernel (sa_raft_motion_encoder): bitwise the
+  // same output as the head kernel + three convs (same fp16 operands, same k order), 4 launches -> 1 per
+  // iteration.  Measured in-process (tools/ab_engine.py): b1 10.38 vs 10.66 ms, b8 55.19 vs 54.95 ms/step, so
+  // auto = on below batch 4; SA_RAFT_FUSE_MENC=0/1 forces it.
+  int fuse_menc_mode_ = std::getenv("SA_RAFT_FUSE_MENC") ? std::atoi(std::getenv("SA_RAFT_FUSE_MENC")) : -1;
+  bool fuse_menc_ = true;
   // SA_RAFT_PARALLEL=0: run the motion encoder and the coarse GRU levels on one stream
   bool par_ = !(std::getenv("SA_RAFT_PARALLEL") && std::getenv("SA_RAFT_PARALLEL")[0] == '0');
   // Cross-iteration pipeline on a third stream: worth ~1.3 ms at batch 1 (small grids leave CUs idle), nothing
   // at batch 8 (56.19 vs 56.17 ms/step in-process, tools/ab_engine.py), where the big GEMMs fill the chip —
   // and there a third engine stream pushes the data-parallel step (copy stream + RCCL stream + torch
   // stream) past the 4 hardware queues per process: the H2D prefetch stopped overlapping the frame graph
-  // (0 % vs 95.5 % concurrent, profiles/dp_overlap_r02.txt).  Auto = on below batch 4;
-  // SA_RAFT_PIPELINE=0/1 forces it.
+  // (0 % vs 95.5 % concurrent, profiles/dp_overlap_r02.txt).  Auto = mode 2 below batch 4, off above;
+  // SA_RAFT_PIPELINE=0/1/2 forces a mode (1: G32 one iteration ahead; 2: G32 and G16 ahead, see forward()).
   int pipeline_mode_ = std::getenv("SA_RAFT_PIPELINE") ? std::atoi(std::getenv("SA_RAFT_PIPELINE")) : -1;
   // SA_RAFT_FUSE_FH: 0 = off, 1 = on, unset = auto.  With conv2 as a separate tap projection
   // (sa_tap_proj, below) the unfused head wins at every batch, measured in-process on MI355X
@@ -246,6 +254,21 @@ void RaftStereo::build(WeightSource& src) {
     mh_wf_ = up(hf);
     mh_bc_ = up(ws.get(u + "encoder.convc1.bias").data);
     mh_bf_ = up(ws.get(u + "encoder.convf1.bias").data);
+    // the fused encoder's stage-1 operand: block-diagonal fp16 [128][96] (convc1 | convf1 x-taps), bias [128]
+    std::vector<_Float16> w1((size_t)128 * 96, (_Float16)0.f);
+    for (int o = 0; o < 64; ++o) {
+      for (int k = 0; k < cor_planes; ++k) w1[(size_t)o * 96 + k] = (_Float16)hc[(size_t)k * 64 + o];
+      for (int t = 0; t < 49; ++t) w1[(size_t)(64 + o) * 96 + cor_planes + t] = (_Float16)hf[(size_t)t * 64 + o];
+    }
+    me_w1_ = a.alloc(w1.size() * 2);
+    HIP_CHECK(hipMemcpy(me_w1_, w1.data(), w1.size() * 2, hipMemcpyHostToDevice));
+    std::vector<float> b1(128);
+    for (int o = 0; o < 64; ++o) {
+      b1[o] = ws.get(u + "encoder.convc1.bias").data[o];
+      b1[64 + o] = ws.get(u + "encoder.convf1.bias").data[o];
+    }
+    me_b1_ = up(b1);
+    if (rc_.radius > 4) fuse_menc_ = false;
   } else {
     fuse_motion_ = false;
   }
@@ -424,7 +447,19 @@ void RaftStereo::forward(hipStream_t s) {
     }
   };
   // motion encoder: lookup -> convc1/convf1 -> convc2/convf2 -> conv (+ [flow, 0] tail)
+  const bool menc = fuse_motion_ && fuse_menc_ && (fuse_menc_mode_ >= 0 ? fuse_menc_mode_ != 0 : Bn < 4);
   auto motion = [&](hipStream_t ms) {
+    if (menc) {
+      const SaConvArgs c2 = convc2_.args({cor1_}, corflo_.slice_c(0, 64));
+      const SaConvArgs f2 = convf2_.args({flo1_}, corflo_.slice_c(64, 64));
+      const SaConvArgs m3 = mconv_.args({corflo_}, motion_.slice_c(0, 126));
+      SA_REQUIRE(c2.Kpad == 576 && f2.Kpad == 576 && m3.Kpad == 1152 && motion_.stride >= 128,
+                 "fused motion encoder layout (Kpad %d/%d/%d)", c2.Kpad, f2.Kpad, m3.Kpad);
+      check(sa_raft_motion_encoder(pyr_, flow_, Bn, h0, w0, w0, rc_.levels, rc_.radius, me_w1_, me_b1_, c2.weight,
+                                   c2.bias, f2.weight, f2.bias, m3.weight, m3.bias, motion_.ptr, motion_.stride, ms),
+            "motion encoder");
+      return;
+    }
     if (fuse_motion_) {
       check(sa_raft_motion_head(pyr_, flow_, Bn, h0, w0, w0, rc_.levels, rc_.radius, mh_wc_, mh_bc_, mh_wf_,
                                 mh_bf_, cor1_.ptr, cor1_.stride, flo1_.ptr, flo1_.stride,
@@ -443,8 +478,10 @@ void RaftStereo::forward(hipStream_t s) {
     mconv_.run(ms, {corflo_}, motion_.slice_c(0, 126), SA_ACT_RELU);
   };
   // finest GRU + flow head (+ mask head on the last iteration), coords1 += delta (x only)
-  auto fine_and_head = [&](bool last) {
-    if (rc_.n_gru > 1) {
+  auto fine_and_head = [&](bool last, bool head_only = false) {
+    if (head_only) {
+      // (the finest GRU was enqueued by the caller)
+    } else if (rc_.n_gru > 1) {
       interp(s, 0);
       gru(s, 0, {motion_, interp_[0]});
     } else {
@@ -485,9 +522,48 @@ void RaftStereo::forward(hipStream_t s) {
   };
 
   const int f = 1 << rc_.n_downsample;
-  const bool pipeline = pipeline_mode_ >= 0 ? pipeline_mode_ != 0 : Bn < 4;
-  const bool pipe = par && pipeline && rc_.n_gru == 3 && !rc_.slow_fast;
-  if (pipe) {
+  // 0 = off, 1 = G32 ahead, 2 = G32 + G16 ahead (default below batch 4)
+  const int pmode = pipeline_mode_ >= 0 ? pipeline_mode_ : (Bn < 4 ? 2 : 0);
+  const bool pipe = par && pmode > 0 && rc_.n_gru == 3 && !rc_.slow_fast;
+  // finest GRU (interp + z/r + q) and flow head as two halves, for the deeper pipeline
+  auto fine = [&]() {
+    interp(s, 0);
+    gru(s, 0, {motion_, interp_[0]});
+  };
+  if (pipe && pmode == 2) {
+    // Deeper cross-iteration pipeline (sceneflow at batch < 4).  Per iteration t:
+    //   side2: G32(t); then G16(t) once the finest q conv of t-1 is done (needs net0(t-1); the finest
+    //          interp of t-1, the last reader of net1(t-1), ran before it)
+    //   side : M(t) after FH(t-1) (needs flow(t-1); overwrites motion read by G08(t-1))
+    //   main : G08(t) after G16(t) and M(t); FH(t)
+    // so G16(t + 1) overlaps FH(t) + M(t + 1) instead of following them.  G32 and G16 share the side2
+    // split-K workspace (same stream).  Events: 0 = G16 done, 1 = FH done, 3 = M done, 4 = G08 q done.
+    rec(s, 1);
+    rec(s, 4);
+    rec(s, 0);
+    wait(side2_, 0);  // the first G32 reads the encoders' hidden states / context
+    for (int it = 0; it < rc_.iters; ++it) {
+      {
+        ScopedSplitK k2(&splitk_side2_);
+        gru32(side2_);
+        wait(side2_, 4);
+        gru16(side2_);
+        rec(side2_, 0);
+      }
+      {
+        ScopedSplitK k1(&splitk_side_);
+        wait(side_, 1);
+        motion(side_);
+        rec(side_, 3);
+      }
+      wait(s, 0);
+      wait(s, 3);
+      fine();
+      rec(s, 4);
+      fine_and_head(it == rc_.iters - 1, true);
+      rec(s, 1);
+    }
+  } else if (pipe) {
     // Cross-iteration pipeline on three streams (sceneflow: 3 levels, no slow-fast).  Per iteration t:
     //   side2: G32(t)  after G16(t-1)   (needs net1(t-1), net2(t-1); overwrites net2 read by G16(t-1))
     //   side : M(t)    after FH(t-1)    (needs flow(t-1); overwrites motion read by G08(t-1))

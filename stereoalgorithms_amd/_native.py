@@ -141,6 +141,7 @@ def _declare_dev(lib):
         "sa_corr1d_pyramid": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
         "sa_corr1d_lookup": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _p, _i, _i, _p, _i, _p]),
         "sa_raft_motion_head": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _i, _p, _i, _p, _i, _p]),
+        "sa_raft_motion_encoder": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p]),
         "sa_convex_upsample": (_i, [_p, _i, _p, _i, _i, _i, _i, _f, _p, _p]),
         "sa_preprocess": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, _p]),
         "sa_remap_bgr": (_i, [_p, _i, _i, _i, _p, _i, _i, _i, _p, _p]),

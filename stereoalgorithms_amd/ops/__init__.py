@@ -89,6 +89,31 @@ def raft_motion_head(pyr_buf, flow, b, h, w1, w2, convc1_w, convc1_b, convf1_w, 
     return cor, flo, fc[..., :2]
 
 
+def raft_motion_encoder(pyr_buf, flow, b, h, w1, w2, convc1_w, convc1_b, convf1_w, convf1_b, convc2_w, convc2_b,
+                        convf2_w, convf2_b, conv_w, conv_b, levels=4, radius=4):
+    """The fused RAFT motion encoder (sa_raft_motion_encoder): fp16 NHWC [b, h, w1, 128] =
+    [relu(conv([relu(convc2(cor1)), relu(convf2(flo1))])) (126) | flow_x | 0].  Torch-layout weights."""
+    nc = levels * (2 * radius + 1)
+    dev = flow.device
+    wb = torch.zeros(128, 96, dtype=torch.float32, device=dev)  # block-diagonal stage-1 B
+    wb[:64, :nc] = convc1_w.reshape(64, nc).float()
+    wb[64:, nc:nc + 49] = convf1_w[:, 0].reshape(64, 49).float()
+    wb = wb.half().contiguous()
+    b1 = torch.cat([convc1_b.float(), convf1_b.float()]).contiguous()
+    w2c, kc, _ = pack_conv_weight(convc2_w)
+    w2f, kf, _ = pack_conv_weight(convf2_w)
+    w3, k3, _ = pack_conv_weight(conv_w)
+    assert kc == 576 and kf == 576 and k3 == 1152
+    out = torch.empty(b, h, w1, 128, dtype=torch.float16, device=dev)
+    f = lambda t: t.float().contiguous()
+    bias = [f(convc2_b), f(convf2_b), f(conv_b)]
+    N.check(N.dev().sa_raft_motion_encoder(pyr_buf.data_ptr(), flow.contiguous().data_ptr(), b, h, w1, w2, levels,
+                                           radius, wb.data_ptr(), b1.data_ptr(), w2c.data_ptr(), bias[0].data_ptr(),
+                                           w2f.data_ptr(), bias[1].data_ptr(), w3.data_ptr(), bias[2].data_ptr(),
+                                           out.data_ptr(), 128, _stream()), "sa_raft_motion_encoder")
+    return out
+
+
 def splitk_workspace(floats: int = 1 << 22, counters: int = 4096, device="cuda"):
     return (torch.empty(floats, dtype=torch.float32, device=device),
             torch.zeros(counters, dtype=torch.int32, device=device))

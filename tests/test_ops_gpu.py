@@ -492,6 +492,45 @@ def test_raft_motion_head_vs_torch():
     assert torch.allclose(fc[..., 0].float(), flow, atol=1e-2) and fc[..., 1].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("b,h,w", [(2, 7, 44), (1, 24, 32), (1, 13, 37)])
+def test_raft_motion_encoder_vs_torch(b, h, w):
+    """The whole motion encoder in one kernel == lookup -> convc1/convf1 -> convc2/convf2 -> conv (fp32 torch on
+    the same fp16-rounded operands), including tiles that overhang the image (zero padding of every conv)."""
+    from stereoalgorithms_amd.models.raft_stereo import CorrBlock1D, coords_grid
+    O = ops()
+    torch.manual_seed(10)
+    c = 256
+    f1 = torch.randn(b, c, h, w, device=DEV)
+    f2 = torch.randn(b, c, h, w, device=DEV)
+    buf, _ = O.corr1d_pyramid(nhwc(f1).half(), nhwc(f2).half(), levels=4)
+    flow = torch.randn(b, h, w, device=DEV) * 5 - 2
+    wc = torch.randn(64, 36, 1, 1, device=DEV) / 6
+    bc = torch.randn(64, device=DEV) * 0.1
+    wf = torch.randn(64, 2, 7, 7, device=DEV) / 10
+    bf = torch.randn(64, device=DEV) * 0.1
+    w2c = torch.randn(64, 64, 3, 3, device=DEV) / 24
+    b2c = torch.randn(64, device=DEV) * 0.1
+    w2f = torch.randn(64, 64, 3, 3, device=DEV) / 24
+    b2f = torch.randn(64, device=DEV) * 0.1
+    w3 = torch.randn(126, 128, 3, 3, device=DEV) / 34
+    b3 = torch.randn(126, device=DEV) * 0.1
+    out = O.raft_motion_encoder(buf, flow, b, h, w, w, wc, bc, wf, bf, w2c, b2c, w2f, b2f, w3, b3)
+    cb = CorrBlock1D(f1.half().float(), f2.half().float(), 4, 4)
+    coords = coords_grid(b, h, w, DEV)
+    coords[:, 0] += flow
+    corr = cb(coords).half().float()
+    fl2 = torch.stack([flow, torch.zeros_like(flow)], 1)
+    hf = lambda t: t.half().float()
+    cor1 = hf(F.relu(F.conv2d(corr, hf(wc), bc)))
+    flo1 = hf(F.relu(F.conv2d(hf(fl2), hf(wf), bf, padding=3)))
+    cor2 = hf(F.relu(F.conv2d(cor1, hf(w2c), b2c, padding=1)))
+    flo2 = hf(F.relu(F.conv2d(flo1, hf(w2f), b2f, padding=1)))
+    ref = F.relu(F.conv2d(torch.cat([cor2, flo2], 1), hf(w3), b3, padding=1))
+    torch.cuda.synchronize()
+    assert rel_err(nchw(out[..., :126]), ref) < 5e-3
+    assert torch.allclose(out[..., 126].float(), flow, atol=1e-2) and out[..., 127].abs().max().item() == 0
+
+
 def test_convex_upsample_vs_oracle():
     from stereoalgorithms_amd.models.raft_stereo import RAFTStereo
     O = ops()

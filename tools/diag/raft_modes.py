@@ -19,13 +19,15 @@ def main():
     H, W = 480, 640
     l, r = batch_pairs(batch, H, W, seed=0)
     left, right = torch.from_numpy(l).cuda(), torch.from_numpy(r).cuda()
-    modes = [("par+pipe(auto)", {}), ("par,nopipe", {"SA_RAFT_PIPELINE": "0"}),
-             ("par,pipe", {"SA_RAFT_PIPELINE": "1"}), ("serial", {"SA_RAFT_PARALLEL": "0"}),
+    modes = [("serial", {"SA_RAFT_PARALLEL": "0"}), ("par+pipe(auto)", {}), ("par,nopipe", {"SA_RAFT_PIPELINE": "0"}),
+             ("par,pipe1", {"SA_RAFT_PIPELINE": "1"}), ("par,pipe2", {"SA_RAFT_PIPELINE": "2"}),
+             ("serial,unfused-menc", {"SA_RAFT_PARALLEL": "0", "SA_RAFT_FUSE_MENC": "0"}),
              ("serial,nograph", {"SA_RAFT_PARALLEL": "0", "SA_NO_GRAPH": "1"}),
              ("par,nograph", {"SA_NO_GRAPH": "1"})]
     ref = None
     for name, env in modes:
-        saved = {k: os.environ.get(k) for k in ("SA_RAFT_PIPELINE", "SA_RAFT_PARALLEL", "SA_NO_GRAPH")}
+        saved = {k: os.environ.get(k) for k in ("SA_RAFT_PIPELINE", "SA_RAFT_PARALLEL", "SA_NO_GRAPH",
+                                                 "SA_RAFT_FUSE_MENC")}
         for k in saved:
             os.environ.pop(k, None)
         os.environ.update(env)
