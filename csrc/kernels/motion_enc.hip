@@ -28,6 +28,7 @@
 #include <hip/hip_fp16.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "sa/kernels.h"
 
@@ -68,7 +69,11 @@ struct MotionEncArgs {
 // byte offset of (pixel, 16-B chunk) in a 256-B-per-pixel LDS image
 __device__ __forceinline__ int sw(int pix, int chunk) { return pix * 256 + ((chunk ^ (pix & 15)) << 4); }
 
-__global__ __launch_bounds__(256) void raft_motion_encoder_kernel(const MotionEncArgs p) {
+// NW waves per workgroup (4: one per SIMD, 2 x 16 output channels per wave in stages 2 / 3; 8: two per SIMD,
+// one 16-channel column tile per wave)
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void raft_motion_encoder_kernel(const MotionEncArgs p) {
+  constexpr int NT = 64 * NW, JN = 8 / NW;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   char* s1 = smem + S1_OFF;
   char* s2 = smem + S2_OFF;
@@ -85,7 +90,7 @@ __global__ __launch_bounds__(256) void raft_motion_encoder_kernel(const MotionEn
   const int ntap = 2 * p.radius + 1, nc = p.levels * ntap;
 
   // ---------------- stage 0: flow patch (image rows ty0-5 .., cols tx0-5 ..), zero outside ----------------
-  for (int i = tid; i < FH * FW; i += 256) {
+  for (int i = tid; i < FH * FW; i += NT) {
     const int y = ty0 - 5 + i / FW, x = tx0 - 5 + i % FW;
     fl[i] = ((unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W) ? p.flow[img_base + (long)y * p.W + x] : 0.f;
   }
@@ -93,16 +98,16 @@ __global__ __launch_bounds__(256) void raft_motion_encoder_kernel(const MotionEn
 
   // ---------------- stage 1a: the [240 x 96] operand ----------------
   // correlation taps: one (pixel, level) per work item (bilinear, align_corners, zero padding; the same
-  // arithmetic as sa_corr1d_lookup / sa_raft_motion_head).  Four items per thread per pass with all their
-  // ntap + 1 <= 10 row values loaded before any is used, so a pass costs one global latency, not 40.
-  constexpr int MAXT = 10;
+  // arithmetic as sa_corr1d_lookup / sa_raft_motion_head).  U items per thread per pass with all their
+  // ntap + 1 <= 10 row values loaded before any is used, so a pass costs one global latency, not 10 U.
+  constexpr int MAXT = 10, U = NW == 4 ? 4 : 2;  // items per thread per pass (960 items of 4 levels)
   const int nitems = P1 * p.levels;
-  for (int base = 0; base < nitems; base += 4 * 256) {
-    float v[4][MAXT];
-    float wa[4];
+  for (int base = 0; base < nitems; base += U * NT) {
+    float v[U][MAXT];
+    float wa[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int it = base + u * 256 + tid;
+    for (int u = 0; u < U; ++u) {
+      const int it = base + u * NT + tid;
       wa[u] = 0.f;
 #pragma unroll
       for (int k = 0; k < MAXT; ++k) v[u][k] = 0.f;
@@ -128,8 +133,8 @@ __global__ __launch_bounds__(256) void raft_motion_encoder_kernel(const MotionEn
       }
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int it = base + u * 256 + tid;
+    for (int u = 0; u < U; ++u) {
+      const int it = base + u * NT + tid;
       if (it < nitems) {
         const int q = it / P1, pix = it - q * P1;
         f16* ar = a1 + pix * AS + q * ntap;
@@ -141,7 +146,7 @@ __global__ __launch_bounds__(256) void raft_motion_encoder_kernel(const MotionEn
     }
   }
   // flow taps (k = nc + ky*7 + kx) and the zero tail up to KP
-  for (int it = tid; it < P1 * (KP - nc); it += 256) {
+  for (int it = tid; it < P1 * (KP - nc); it += NT) {
     const int pix = it / (KP - nc), k = nc + (it - pix * (KP - nc));
     const int r = pix / R1W, c = pix - r * R1W;
     float v = 0.f;
@@ -154,39 +159,45 @@ __global__ __launch_bounds__(256) void raft_motion_encoder_kernel(const MotionEn
   __syncthreads();
 
   // ---------------- stage 1b: S1 = relu([lookup | flow taps] x blockdiag(convc1, convf1)) ----------------
+  // wave w: column tiles w * JN .. w * JN + JN - 1 of all 15 row tiles
   {
-    half8 bfr[8][3];
-    float bias[8];
+    constexpr int NT1 = P1 / 16;  // 15
+    half8 bfr[JN][3];
+    float bias[JN];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int n = 16 * j + r16;
+    for (int j = 0; j < JN; ++j) {
+      const int n = 16 * (wave * JN + j) + r16;
       bias[j] = p.b1[n];
 #pragma unroll
       for (int ks = 0; ks < 3; ++ks) bfr[j][ks] = *reinterpret_cast<const half8*>(p.w1 + n * KP + ks * 32 + kofs);
     }
-    for (int tile = wave; tile < P1 / 16; tile += 4) {
-      floatx4 acc[8];
+    floatx4 acc[NT1][JN];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < NT1; ++i)
 #pragma unroll
-      for (int ks = 0; ks < 3; ++ks) {
-        const half8 a = *reinterpret_cast<const half8*>(a1 + (16 * tile + r16) * AS + ks * 32 + kofs);
+      for (int j = 0; j < JN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bfr[j][ks], acc[j], 0, 0, 0);
+    for (int ks = 0; ks < 3; ++ks)
+#pragma unroll
+      for (int i = 0; i < NT1; ++i) {
+        const half8 a = *reinterpret_cast<const half8*>(a1 + (16 * i + r16) * AS + ks * 32 + kofs);
+#pragma unroll
+        for (int j = 0; j < JN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bfr[j][ks], acc[i][j], 0, 0, 0);
       }
 #pragma unroll
+    for (int i = 0; i < NT1; ++i)
+#pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
-        const int pix = 16 * tile + (lane >> 4) * 4 + rr;
+        const int pix = 16 * i + (lane >> 4) * 4 + rr;
         const int r = pix / R1W, c = pix - r * R1W;
         const bool in = (unsigned)(ty0 - 2 + r) < (unsigned)p.H && (unsigned)(tx0 - 2 + c) < (unsigned)p.W;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int col = 16 * j + r16;
-          const float v = in ? fmaxf(acc[j][rr] + bias[j], 0.f) : 0.f;
+        for (int j = 0; j < JN; ++j) {
+          const int col = 16 * (wave * JN + j) + r16;
+          const float v = in ? fmaxf(acc[i][j][rr] + bias[j], 0.f) : 0.f;
           *reinterpret_cast<f16*>(s1 + sw(pix, col >> 3) + (col & 7) * 2) = (f16)v;
         }
       }
-    }
   }
   __syncthreads();
 
@@ -194,46 +205,56 @@ __global__ __launch_bounds__(256) void raft_motion_encoder_kernel(const MotionEn
   {
     constexpr int NT2 = (P2 + 15) / 16;  // 12 row tiles (192 rows, 180 valid)
     constexpr int NS2 = 18;              // 9 taps x 2 k32 halves of 64 channels
-    const int cb = wave < 2 ? 0 : 64;    // source / destination channel base (cor | flo)
-    const f16* wsrc = wave < 2 ? p.w2c : p.w2f;
-    const float* bsrc = wave < 2 ? p.b2c : p.b2f;
-    const int nb = (wave & 1) * 32;      // this wave's 32 output channels within the conv
-    int base[NT2];                       // S1 pixel of tap (0, 0) for this lane's row of each tile
+    const int ct0 = wave * JN;            // first of this wave's JN 16-channel column tiles (0-3 cor2, 4-7 flo2)
+    const int cb = ct0 < 4 ? 0 : 64;      // source / destination channel base (cor | flo)
+    const f16* wsrc = ct0 < 4 ? p.w2c : p.w2f;
+    const float* bsrc = ct0 < 4 ? p.b2c : p.b2f;
+    const int nb = (16 * ct0) & 63;       // first output channel within the conv
+    int base[NT2];                        // S1 pixel of tap (0, 0) for this lane's row of each tile
 #pragma unroll
     for (int i = 0; i < NT2; ++i) {
       int q = 16 * i + r16;
       q = q < P2 ? q : P2 - 1;
       base[i] = (q / R2W) * R1W + (q % R2W);
     }
-    const f16* wrow0 = wsrc + (size_t)(nb + r16) * 576 + kofs;
-    const f16* wrow1 = wsrc + (size_t)(nb + 16 + r16) * 576 + kofs;
-    floatx4 acc[NT2][2];
+    const f16* wrow[JN];
 #pragma unroll
-    for (int i = 0; i < NT2; ++i) acc[i][0] = acc[i][1] = floatx4{0.f, 0.f, 0.f, 0.f};
-    half8 bq[D][2];
+    for (int j = 0; j < JN; ++j) wrow[j] = wsrc + (size_t)(nb + 16 * j + r16) * 576 + kofs;
+    floatx4 acc[NT2][JN];
 #pragma unroll
-    for (int s = 0; s < D; ++s) {
-      bq[s][0] = *reinterpret_cast<const half8*>(wrow0 + s * 32);
-      bq[s][1] = *reinterpret_cast<const half8*>(wrow1 + s * 32);
-    }
+    for (int i = 0; i < NT2; ++i)
 #pragma unroll
-    for (int s = 0; s < NS2; ++s) {
-      const half8 b0 = bq[s % D][0], b1 = bq[s % D][1];
-      if (s + D < NS2) {
-        bq[s % D][0] = *reinterpret_cast<const half8*>(wrow0 + (s + D) * 32);
-        bq[s % D][1] = *reinterpret_cast<const half8*>(wrow1 + (s + D) * 32);
+      for (int j = 0; j < JN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // B fragments D k-steps ahead in a register shift queue (a partially unrolled loop keeps every index
+    // compile-time)
+    half8 bq[D][JN];
+#pragma unroll
+    for (int st = 0; st < D; ++st)
+#pragma unroll
+      for (int j = 0; j < JN; ++j) bq[st][j] = *reinterpret_cast<const half8*>(wrow[j] + st * 32);
+#pragma unroll 2
+    for (int st = 0; st < NS2; ++st) {
+      half8 b[JN];
+#pragma unroll
+      for (int j = 0; j < JN; ++j) {
+        b[j] = bq[0][j];
+#pragma unroll
+        for (int d = 0; d + 1 < D; ++d) bq[d][j] = bq[d + 1][j];
+        if (st + D < NS2) bq[D - 1][j] = *reinterpret_cast<const half8*>(wrow[j] + (st + D) * 32);
       }
-      const int tap = s >> 1, ky = tap / 3, kx = tap - ky * 3;
+      const int tap = st >> 1, ky = tap / 3, kx = tap - ky * 3;
       const int toff = ky * R1W + kx;
-      const int chunk = (cb + 32 * (s & 1) + kofs) >> 3;
+      const int chunk = (cb + 32 * (st & 1) + kofs) >> 3;
 #pragma unroll
       for (int i = 0; i < NT2; ++i) {
         const half8 a = *reinterpret_cast<const half8*>(s1 + sw(base[i] + toff, chunk));
-        acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b0, acc[i][0], 0, 0, 0);
-        acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b1, acc[i][1], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < JN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[j], acc[i][j], 0, 0, 0);
       }
     }
-    const float bias0 = bsrc[nb + r16], bias1 = bsrc[nb + 16 + r16];
+    float bias[JN];
+#pragma unroll
+    for (int j = 0; j < JN; ++j) bias[j] = bsrc[nb + 16 * j + r16];
 #pragma unroll
     for (int i = 0; i < NT2; ++i)
 #pragma unroll
@@ -242,11 +263,12 @@ __global__ __launch_bounds__(256) void raft_motion_encoder_kernel(const MotionEn
         if (q >= P2) continue;
         const int r = q / R2W, c = q - r * R2W;
         const bool in = (unsigned)(ty0 - 1 + r) < (unsigned)p.H && (unsigned)(tx0 - 1 + c) < (unsigned)p.W;
-        const int col0 = cb + nb + r16, col1 = col0 + 16;
-        const float v0 = in ? fmaxf(acc[i][0][rr] + bias0, 0.f) : 0.f;
-        const float v1 = in ? fmaxf(acc[i][1][rr] + bias1, 0.f) : 0.f;
-        *reinterpret_cast<f16*>(s2 + sw(q, col0 >> 3) + (col0 & 7) * 2) = (f16)v0;
-        *reinterpret_cast<f16*>(s2 + sw(q, col1 >> 3) + (col1 & 7) * 2) = (f16)v1;
+#pragma unroll
+        for (int j = 0; j < JN; ++j) {
+          const int col = cb + nb + 16 * j + r16;
+          const float v = in ? fmaxf(acc[i][j][rr] + bias[j], 0.f) : 0.f;
+          *reinterpret_cast<f16*>(s2 + sw(q, col >> 3) + (col & 7) * 2) = (f16)v;
+        }
       }
   }
   __syncthreads();
@@ -255,58 +277,66 @@ __global__ __launch_bounds__(256) void raft_motion_encoder_kernel(const MotionEn
   {
     constexpr int NT3 = TH * TW / 16;  // 8 row tiles
     constexpr int NS3 = 36;            // 9 taps x 4 k32 quarters of 128 channels
-    const int nb = wave * 32;          // this wave's 32 output channels
+    const int nb = wave * JN * 16;     // this wave's first output channel
     int base[NT3];
 #pragma unroll
     for (int i = 0; i < NT3; ++i) {
       const int q = 16 * i + r16;
       base[i] = (q / TW) * R2W + (q % TW);
     }
-    const f16* wrow0 = p.w3 + (size_t)(nb + r16) * 1152 + kofs;
-    const f16* wrow1 = p.w3 + (size_t)(nb + 16 + r16) * 1152 + kofs;
-    floatx4 acc[NT3][2];
+    const f16* wrow[JN];
 #pragma unroll
-    for (int i = 0; i < NT3; ++i) acc[i][0] = acc[i][1] = floatx4{0.f, 0.f, 0.f, 0.f};
-    half8 bq[D][2];
-#pragma unroll
-    for (int s = 0; s < D; ++s) {
-      bq[s][0] = *reinterpret_cast<const half8*>(wrow0 + s * 32);
-      bq[s][1] = *reinterpret_cast<const half8*>(wrow1 + s * 32);
-    }
-#pragma unroll
-    for (int s = 0; s < NS3; ++s) {
-      const half8 b0 = bq[s % D][0], b1 = bq[s % D][1];
-      if (s + D < NS3) {
-        bq[s % D][0] = *reinterpret_cast<const half8*>(wrow0 + (s + D) * 32);
-        bq[s % D][1] = *reinterpret_cast<const half8*>(wrow1 + (s + D) * 32);
-      }
-      const int tap = s >> 2, ky = tap / 3, kx = tap - ky * 3;
-      const int toff = ky * R2W + kx;
-      const int chunk = (32 * (s & 3) + kofs) >> 3;
-#pragma unroll
-      for (int i = 0; i < NT3; ++i) {
-        const half8 a = *reinterpret_cast<const half8*>(s2 + sw(base[i] + toff, chunk));
-        acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b0, acc[i][0], 0, 0, 0);
-        acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b1, acc[i][1], 0, 0, 0);
-      }
-    }
-    // bias + relu (channels < 126), [fx, 0] tail, staged in the (finished) S1 area
-    const int col0 = nb + r16, col1 = col0 + 16;
-    const float bias0 = col0 < 126 ? p.b3[col0] : 0.f, bias1 = col1 < 126 ? p.b3[col1] : 0.f;
-    char* so = s1;
+    for (int j = 0; j < JN; ++j) wrow[j] = p.w3 + (size_t)(nb + 16 * j + r16) * 1152 + kofs;
+    floatx4 acc[NT3][JN];
 #pragma unroll
     for (int i = 0; i < NT3; ++i)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int q = 16 * i + (lane >> 4) * 4 + rr;
-        const float fx = fl[((q / TW) + 5) * FW + (q % TW) + 5];
-        const float v0 = col0 < 126 ? fmaxf(acc[i][0][rr] + bias0, 0.f) : (col0 == 126 ? fx : 0.f);
-        const float v1 = col1 < 126 ? fmaxf(acc[i][1][rr] + bias1, 0.f) : (col1 == 126 ? fx : 0.f);
-        *reinterpret_cast<f16*>(so + sw(q, col0 >> 3) + (col0 & 7) * 2) = (f16)v0;
-        *reinterpret_cast<f16*>(so + sw(q, col1 >> 3) + (col1 & 7) * 2) = (f16)v1;
+      for (int j = 0; j < JN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // B fragments D k-steps ahead in a register shift queue (a partially unrolled loop keeps every index
+    // compile-time)
+    half8 bq[D][JN];
+#pragma unroll
+    for (int st = 0; st < D; ++st)
+#pragma unroll
+      for (int j = 0; j < JN; ++j) bq[st][j] = *reinterpret_cast<const half8*>(wrow[j] + st * 32);
+#pragma unroll 2
+    for (int st = 0; st < NS3; ++st) {
+      half8 b[JN];
+#pragma unroll
+      for (int j = 0; j < JN; ++j) {
+        b[j] = bq[0][j];
+#pragma unroll
+        for (int d = 0; d + 1 < D; ++d) bq[d][j] = bq[d + 1][j];
+        if (st + D < NS3) bq[D - 1][j] = *reinterpret_cast<const half8*>(wrow[j] + (st + D) * 32);
       }
+      const int tap = st >> 2, ky = tap / 3, kx = tap - ky * 3;
+      const int toff = ky * R2W + kx;
+      const int chunk = (32 * (st & 3) + kofs) >> 3;
+#pragma unroll
+      for (int i = 0; i < NT3; ++i) {
+        const half8 a = *reinterpret_cast<const half8*>(s2 + sw(base[i] + toff, chunk));
+#pragma unroll
+        for (int j = 0; j < JN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    // bias + relu (channels < 126), [fx, 0] tail, staged in the (finished) S1 area
+    char* so = s1;
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+      const int col = nb + 16 * j + r16;
+      const float bj = col < 126 ? p.b3[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < NT3; ++i)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int q = 16 * i + (lane >> 4) * 4 + rr;
+          const float fx = fl[((q / TW) + 5) * FW + (q % TW) + 5];
+          const float v = col < 126 ? fmaxf(acc[i][j][rr] + bj, 0.f) : (col == 126 ? fx : 0.f);
+          *reinterpret_cast<f16*>(so + sw(q, col >> 3) + (col & 7) * 2) = (f16)v;
+        }
+    }
     __syncthreads();
-    for (int i = tid; i < TH * TW * 16; i += 256) {
+    for (int i = tid; i < TH * TW * 16; i += NT) {
       const int q = i >> 4, ch = i & 15;
       const int y = ty0 + q / TW, x = tx0 + q % TW;
       if (y < p.H && x < p.W)
@@ -358,6 +388,11 @@ extern "C" int sa_raft_motion_encoder(const float* pyr, const float* flow, int B
   a.b3 = b3;
   a.out = (f16*)out;
   a.os = os;
-  hipLaunchKernelGGL(raft_motion_encoder_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+  // SA_MENC_WAVES=4|8 (default 4: 8 waves measured no faster at batch 1 and 1 % slower at batch 8), read per
+  // launch (a frame graph captures it once)
+  const char* e = std::getenv("SA_MENC_WAVES");
+  const int nw = e && e[0] == '8' ? 8 : 4;
+  if (nw == 4) hipLaunchKernelGGL(raft_motion_encoder_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL(raft_motion_encoder_kernel<8>, dim3((unsigned)blocks), dim3(512), 0, stream, a);
   return (int)hipGetLastError();
 }

@@ -492,11 +492,13 @@ def test_raft_motion_head_vs_torch():
     assert torch.allclose(fc[..., 0].float(), flow, atol=1e-2) and fc[..., 1].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("waves", ["4", "8"])
 @pytest.mark.parametrize("b,h,w", [(2, 7, 44), (1, 24, 32), (1, 13, 37)])
-def test_raft_motion_encoder_vs_torch(b, h, w):
+def test_raft_motion_encoder_vs_torch(b, h, w, waves, monkeypatch):
     """The whole motion encoder in one kernel == lookup -> convc1/convf1 -> convc2/convf2 -> conv (fp32 torch on
     the same fp16-rounded operands), including tiles that overhang the image (zero padding of every conv)."""
     from stereoalgorithms_amd.models.raft_stereo import CorrBlock1D, coords_grid
+    monkeypatch.setenv("SA_MENC_WAVES", waves)
     O = ops()
     torch.manual_seed(10)
     c = 256
