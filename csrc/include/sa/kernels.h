@@ -184,10 +184,13 @@ int sa_raft_motion_head(const float* pyr, const float* flow, int B, int H, int W
 // relu(convc2) / relu(convf2) -> relu(conv) + [fx, 0] tail, every intermediate kept in LDS per 8x16 output tile.
 // w1: fp16 [128][96] block-diagonal [convc1 (rows 0-63, k < L(2r+1)) | convf1 x-taps (rows 64-127, 49 k from
 // L(2r+1))], b1 [128]; w2c / w2f: convc2 / convf2 packed fp16 [>=64][576]; w3: conv packed [>=128][1152] (K order
-// (kh, kw, ci), ci over [cor2 | flo2]); b3 [126].  radius <= 4.  out: fp16 [B][H][W][os >= 128].
+// (kh, kw, ci), ci over [cor2 | flo2]); b3 [126].  levels = radius = 4.  out: fp16 [B][H][W][os >= 128].
 int sa_raft_motion_encoder(const float* pyr, const float* flow, int B, int H, int W, int W2, int levels, int radius,
                            const void* w1, const float* b1, const void* w2c, const float* b2c, const void* w2f,
                            const float* b2f, const void* w3, const float* b3, void* out, int os, hipStream_t stream);
+// diagnostics: s_memrealtime (100 MHz) stage marks of every workgroup of later sa_raft_motion_encoder launches into `buf`
+// ([blocks][8 marks][64] u64; NULL turns it off)
+void sa_raft_motion_encoder_stamps(void* buf);
 
 // ---- upsampling -----------------------------------------------------------------------------
 // RAFT convex upsampling: mask [B*H*W][9*f*f] fp16 (softmax over the 9), flow fp32 [B*H*W]

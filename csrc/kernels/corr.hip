@@ -25,6 +25,10 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int CORR_ROWS = 32;  // w1 rows per LDS slab
 
+// one bilinear tap of the lookup, in one fixed rounding order (every lookup kernel -- standalone, fused head,
+// fused encoder -- uses this, so they agree bit for bit whatever the compiler contracts elsewhere)
+__device__ __forceinline__ float lerp_tap(float v0, float v1, float a) { return __fmaf_rn(a, v1, __fmul_rn(1.f - a, v0)); }
+
 __global__ __launch_bounds__(256) void corr_pyramid_kernel(const f16* __restrict__ f1,
                                                            const f16* __restrict__ f2, int stride,
                                                            int H, int W1, int W2, int C,
@@ -112,7 +116,7 @@ __global__ void corr_lookup_kernel(const float* __restrict__ pyr, const float* _
     for (int k = 0; k < ntap; ++k) {
       int xi = x0 + k + 1;
       float nxt = (xi >= 0 && xi < Wl) ? row[xi] : 0.f;
-      vals[l * ntap + k] = (1.f - a) * prev + a * nxt;
+      vals[l * ntap + k] = lerp_tap(prev, nxt, a);
       prev = nxt;
     }
     Wl >>= 1;
@@ -175,7 +179,7 @@ __global__ __launch_bounds__(256) void raft_motion_head_kernel(
     for (int k = 0; k < ntap; ++k) {
       const int xi = x0 + k + 1;
       const float nxt = (xi >= 0 && xi < Wl) ? row[xi] : 0.f;
-      corr_s[lane][q * ntap + k] = (1.f - a) * prev + a * nxt;
+      corr_s[lane][q * ntap + k] = lerp_tap(prev, nxt, a);
       prev = nxt;
     }
   }
@@ -275,7 +279,7 @@ __global__ __launch_bounds__(256) void raft_motion_head_mfma_kernel(
     for (int k = 0; k < ntap; ++k) {
       const int xi = x0 + k + 1;
       const float nxt = (ok && xi >= 0 && xi < Wl) ? row[xi] : 0.f;
-      arow[q * ntap + k] = (f16)((1.f - a) * prev + a * nxt);
+      arow[q * ntap + k] = (f16)lerp_tap(prev, nxt, a);
       prev = nxt;
     }
   }

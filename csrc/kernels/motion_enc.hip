@@ -21,7 +21,8 @@
 //   stage 3  conv over the 8 x 16 tile from S2, K = 9 x 128; bias + relu, [fx, 0] tail, staged through LDS
 //            for 16-B coalesced stores of all 128 channels
 // All GEMMs are v_mfma_f32_16x16x32_f16; the stage 2 / 3 weights (packed [n][K] fp16 like every conv, L2
-// resident, shared by all workgroups) are loaded as B fragments straight into registers six k-steps ahead.
+// resident, shared by all workgroups) stream through per-wave global->LDS DMA rings in whichever LDS area
+// the stage has finished with (5 / 11 k-steps ahead, counted vmcnt, no barriers).
 // LDS rows are 256 B (128 channels) with the 16-B chunk XOR'd by the pixel index, so the 16 lanes of a
 // fragment read (16 consecutive pixels, same chunk) hit 16 different bank groups.
 #include <hip/hip_runtime.h>
@@ -46,7 +47,6 @@ constexpr int KP = 96, AS = 104;               // stage-1 K (padded) and operand
 constexpr int S1_OFF = 0, S2_OFF = S1_OFF + P1 * 256, A1_OFF = S2_OFF + P2 * 256, FL_OFF = A1_OFF + P1 * AS * 2;
 constexpr int SMEM = FL_OFF + FH * FW * 4;     // 159312 B
 static_assert(SMEM <= 163840, "LDS budget");
-constexpr int D = 6;                           // B-fragment prefetch depth (k-steps)
 
 struct MotionEncArgs {
   const float* pyr;
@@ -64,6 +64,59 @@ struct MotionEncArgs {
   const float* b3;  // [126]
   f16* out;  // [B][H][W][os], channels 0..127
   int os;
+  unsigned long long* stamps;  // diagnostics (sa_raft_motion_encoder_stamps): [block][8 marks][64 lanes] or null
+};
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// s_waitcnt vmcnt(N) through the intrinsic (gfx9 encoding: vmcnt bits [3:0] + [15:14], expcnt [6:4] and lgkmcnt
+// [11:8] left at their maxima): unlike an inline-asm wait, the compiler's own waitcnt pass sees it and does not
+// drain every counter in front of it, so LDS prefetch reads stay in flight
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+// vmcnt <= s * PER for a wave-uniform s in [0, K]
+template <int PER, int K>
+__device__ __forceinline__ void wait_vm_le(int s) {
+  if constexpr (K <= 0) {
+    wait_vm<0>();
+  } else {
+    if (s >= K) wait_vm<K * PER>();
+    else wait_vm_le<PER, K - 1>(s);
+  }
+}
+
+// Per-wave B ring for a conv stage: the wave's 16 * JN weight rows (KROW halfs each) stream through RING LDS
+// slots of [16 JN rows][64 B] (one 32-deep k-step) via global->LDS DMA, RING - 1 steps ahead; the 16-B chunk
+// of row r sits at slot chunk c ^ ((r >> 2) & 3) so a fragment read (16 rows, one chunk) is conflict-free.
+// Only the issuing wave reads its ring, so its own vmcnt is the only ordering needed.
+template <int JN, int RING, int KROW>
+struct BRing {
+  static constexpr int SLOT = JN * 1024;
+  char* base;        // this wave's ring (LDS)
+  const f16* src[JN];  // per DMA instruction: this lane's row / chunk source at k = 0
+  __device__ __forceinline__ void init(char* ring, const f16* w, int row0, int lane) {
+    base = ring;
+#pragma unroll
+    for (int i = 0; i < JN; ++i) {
+      const int r = 16 * i + (lane >> 2), c = lane & 3;
+      src[i] = w + (size_t)(row0 + r) * KROW + ((c ^ ((r >> 2) & 3)) << 3);
+    }
+  }
+  __device__ __forceinline__ void issue(int step) {
+    char* dst = base + (step % RING) * SLOT;
+#pragma unroll
+    for (int i = 0; i < JN; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(src[i] + step * 32), (lds_void_t*)(dst + i * 1024), 16, 0, 0);
+  }
+  // B fragment of column tile j for k-step `step` (lane: row 16 j + (lane & 15), k chunk lane >> 4)
+  __device__ __forceinline__ half8 frag(int step, int j, int lane) const {
+    const int r = 16 * j + (lane & 15);
+    return *reinterpret_cast<const half8*>(base + (step % RING) * SLOT + r * 64 +
+                                           ((((lane >> 4) ^ ((r >> 2) & 3))) << 4));
+  }
 };
 
 // byte offset of (pixel, 16-B chunk) in a 256-B-per-pixel LDS image
@@ -87,7 +140,11 @@ __global__ __launch_bounds__(64 * NW) void raft_motion_encoder_kernel(const Moti
   const int trem = blockIdx.x - bimg * tiles_x * tiles_y;
   const int ty0 = (trem / tiles_x) * TH, tx0 = (trem % tiles_x) * TW;
   const long img_base = (long)bimg * p.H * p.W;
-  const int ntap = 2 * p.radius + 1, nc = p.levels * ntap;
+  // stage timestamps of wave 0 (diagnostics only; every lane stores its own slot: plain vector stores)
+  auto stamp = [&](int mark) {
+    if (p.stamps && wave == 0) p.stamps[((size_t)blockIdx.x * 8 + mark) * 64 + lane] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
 
   // ---------------- stage 0: flow patch (image rows ty0-5 .., cols tx0-5 ..), zero outside ----------------
   for (int i = tid; i < FH * FW; i += NT) {
@@ -96,68 +153,55 @@ __global__ __launch_bounds__(64 * NW) void raft_motion_encoder_kernel(const Moti
   }
   __syncthreads();
 
+  stamp(1);
   // ---------------- stage 1a: the [240 x 96] operand ----------------
-  // correlation taps: one (pixel, level) per work item (bilinear, align_corners, zero padding; the same
-  // arithmetic as sa_corr1d_lookup / sa_raft_motion_head).  U items per thread per pass with all their
-  // ntap + 1 <= 10 row values loaded before any is used, so a pass costs one global latency, not 10 U.
-  constexpr int MAXT = 10, U = NW == 4 ? 4 : 2;  // items per thread per pass (960 items of 4 levels)
-  const int nitems = P1 * p.levels;
-  for (int base = 0; base < nitems; base += U * NT) {
-    float v[U][MAXT];
-    float wa[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int it = base + u * NT + tid;
-      wa[u] = 0.f;
-#pragma unroll
-      for (int k = 0; k < MAXT; ++k) v[u][k] = 0.f;
-      if (it < nitems) {
-        const int q = it / P1, pix = it - q * P1;
-        const int r = pix / R1W, c = pix - r * R1W;
-        const int y = ty0 - 2 + r, x = tx0 - 2 + c;
-        if ((unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W) {
-          const float fx = fl[(r + 3) * FW + (c + 3)];
-          const long off = q == 0 ? 0 : (q == 1 ? p.lvl_off1 : (q == 2 ? p.lvl_off2 : p.lvl_off3));
-          const int Wl = p.W2 >> q;
-          const float* row = p.pyr + off + (img_base + (long)y * p.W + x) * Wl;
-          const float xl = ((float)x + fx) / (float)(1 << q) - (float)p.radius;
-          const float x0f = floorf(xl);
-          wa[u] = xl - x0f;
-          const int x0 = (int)x0f;
-#pragma unroll
-          for (int k = 0; k < MAXT; ++k) {
-            const int xi = x0 + k;
-            if (k <= ntap && xi >= 0 && xi < Wl) v[u][k] = row[xi];
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int it = base + u * NT + tid;
-      if (it < nitems) {
-        const int q = it / P1, pix = it - q * P1;
-        f16* ar = a1 + pix * AS + q * ntap;
-        const float a = wa[u];
-#pragma unroll
-        for (int k = 0; k < MAXT - 1; ++k)
-          if (k < ntap) ar[k] = (f16)((1.f - a) * v[u][k] + a * v[u][k + 1]);
-      }
-    }
-  }
-  // flow taps (k = nc + ky*7 + kx) and the zero tail up to KP
-  for (int it = tid; it < P1 * (KP - nc); it += NT) {
-    const int pix = it / (KP - nc), k = nc + (it - pix * (KP - nc));
+  // one S1 pixel per thread: its 4 levels x 10 pyramid values are loaded before any is used (one global
+  // latency), the 9 bilinear taps per level (the arithmetic of sa_corr1d_lookup), its 49 flow taps from the
+  // patch and the zero tail are assembled in registers and stored as 12 16-B LDS writes.
+  // K layout: [0, 36) lookup (level-major), [36, 85) flow taps ky * 7 + kx, [85, 96) zero.
+  if (tid < P1) {
+    const int pix = tid;
     const int r = pix / R1W, c = pix - r * R1W;
-    float v = 0.f;
-    if (k < nc + 49) {
-      const int t = k - nc, ky = t / 7, kx = t - ky * 7;
-      v = fl[(r + ky) * FW + (c + kx)];
+    const int y = ty0 - 2 + r, x = tx0 - 2 + c;
+    const bool in = (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
+    const float fx = fl[(r + 3) * FW + (c + 3)];
+    float v[4][10], wa[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const long off = q == 0 ? 0 : (q == 1 ? p.lvl_off1 : (q == 2 ? p.lvl_off2 : p.lvl_off3));
+      const int Wl = p.W2 >> q;
+      const float* row = p.pyr + off + (img_base + (long)(in ? y : 0) * p.W + (in ? x : 0)) * Wl;
+      const float xl = ((float)x + fx) / (float)(1 << q) - 4.f;
+      const float x0f = floorf(xl);
+      wa[q] = xl - x0f;
+      const int x0 = (int)x0f;
+#pragma unroll
+      for (int k = 0; k < 10; ++k) {
+        const int xi = x0 + k;
+        v[q][k] = (in && xi >= 0 && xi < Wl) ? row[xi] : 0.f;
+      }
     }
-    a1[pix * AS + k] = (f16)v;
+    half8 hv[12];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int kk = 9 * q + k;
+        hv[kk >> 3][kk & 7] = (f16)__fmaf_rn(wa[q], v[q][k + 1], __fmul_rn(1.f - wa[q], v[q][k]));  // = lerp_tap (corr.hip)
+      }
+#pragma unroll
+    for (int t = 0; t < 49; ++t) {
+      const int kk = 36 + t, ky = t / 7, kx = t % 7;
+      hv[kk >> 3][kk & 7] = (f16)fl[(r + ky) * FW + (c + kx)];
+    }
+#pragma unroll
+    for (int kk = 85; kk < 96; ++kk) hv[kk >> 3][kk & 7] = (f16)0.f;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) *reinterpret_cast<half8*>(a1 + pix * AS + 8 * i) = hv[i];
   }
   __syncthreads();
 
+  stamp(2);
   // ---------------- stage 1b: S1 = relu([lookup | flow taps] x blockdiag(convc1, convf1)) ----------------
   // wave w: column tiles w * JN .. w * JN + JN - 1 of all 15 row tiles
   {
@@ -201,6 +245,7 @@ __global__ __launch_bounds__(64 * NW) void raft_motion_encoder_kernel(const Moti
   }
   __syncthreads();
 
+  stamp(3);
   // ---------------- stage 2: S2 = [relu(convc2(cor1)) | relu(convf2(flo1))] over the 10 x 18 region -------------
   {
     constexpr int NT2 = (P2 + 15) / 16;  // 12 row tiles (192 rows, 180 valid)
@@ -217,40 +262,65 @@ __global__ __launch_bounds__(64 * NW) void raft_motion_encoder_kernel(const Moti
       q = q < P2 ? q : P2 - 1;
       base[i] = (q / R2W) * R1W + (q % R2W);
     }
-    const f16* wrow[JN];
-#pragma unroll
-    for (int j = 0; j < JN; ++j) wrow[j] = wsrc + (size_t)(nb + 16 * j + r16) * 576 + kofs;
     floatx4 acc[NT2][JN];
 #pragma unroll
     for (int i = 0; i < NT2; ++i)
 #pragma unroll
       for (int j = 0; j < JN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    // B fragments D k-steps ahead in a register shift queue (a partially unrolled loop keeps every index
-    // compile-time)
-    half8 bq[D][JN];
-#pragma unroll
-    for (int st = 0; st < D; ++st)
-#pragma unroll
-      for (int j = 0; j < JN; ++j) bq[st][j] = *reinterpret_cast<const half8*>(wrow[j] + st * 32);
-#pragma unroll 2
-    for (int st = 0; st < NS2; ++st) {
-      half8 b[JN];
-#pragma unroll
-      for (int j = 0; j < JN; ++j) {
-        b[j] = bq[0][j];
-#pragma unroll
-        for (int d = 0; d + 1 < D; ++d) bq[d][j] = bq[d + 1][j];
-        if (st + D < NS2) bq[D - 1][j] = *reinterpret_cast<const half8*>(wrow[j] + (st + D) * 32);
-      }
+    // weights through a per-wave DMA ring in the (finished) stage-1 operand area
+    constexpr int RING = 6;
+    static_assert(NW * RING * JN * 1024 <= P1 * AS * 2, "stage-2 B rings fit the A1 area");
+    BRing<JN, RING, 576> br;
+    br.init(smem + A1_OFF + wave * RING * JN * 1024, wsrc, nb, lane);
+    // software pipeline: the A / B fragments of step st + 1 are read while step st's MFMAs run
+    auto readA = [&](int st, half8* a) {
       const int tap = st >> 1, ky = tap / 3, kx = tap - ky * 3;
       const int toff = ky * R1W + kx;
       const int chunk = (cb + 32 * (st & 1) + kofs) >> 3;
 #pragma unroll
-      for (int i = 0; i < NT2; ++i) {
-        const half8 a = *reinterpret_cast<const half8*>(s1 + sw(base[i] + toff, chunk));
+      for (int i = 0; i < NT2; ++i) a[i] = *reinterpret_cast<const half8*>(s1 + sw(base[i] + toff, chunk));
+    };
+    auto readB = [&](int st, half8* b) {
 #pragma unroll
-        for (int j = 0; j < JN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < JN; ++j) b[j] = br.frag(st, j, lane);
+    };
+    // One k-step: refill the ring slot freed by step st - 1 (the DMA goes first: the compiler drains lgkmcnt
+    // around it, which must not catch the prefetch reads), wait for step st + 1's weights, read step st + 1's
+    // A / B fragments, then step st's MFMAs.  Fully unrolled straight-line code (constant vmcnt), so the
+    // compiler's lgkmcnt tracking keeps the prefetch reads in flight under the MFMAs (a loop back-edge made it
+    // drain them before every step).
+    auto step = [&](int st, bool issue, bool prefetch, int ahead, const half8* ac, const half8* bc, half8* an,
+                    half8* bn) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (issue) br.issue(st + RING - 1);
+      if (prefetch) {
+        wait_vm_le<JN, RING - 2>(ahead);
+        readB(st + 1, bn);
+        readA(st + 1, an);
       }
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
+#pragma unroll
+      for (int i = 0; i < NT2; ++i)
+#pragma unroll
+        for (int j = 0; j < JN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ac[i], bc[j], acc[i][j], 0, 0, 0);
+    };
+#pragma unroll
+    for (int st = 0; st < RING - 1; ++st) br.issue(st);
+    half8 a0[NT2], a1v[NT2], b0[JN], b1v[JN];
+    wait_vm_le<JN, RING - 2>(RING - 2);
+    readB(0, b0);
+    readA(0, a0);
+    constexpr int MAIN = ((NS2 - RING + 1) / 2) * 2;  // steps with both a refill and a prefetch, in pairs
+#pragma unroll
+    for (int st = 0; st < MAIN; st += 2) {
+      step(st, true, true, RING - 2, a0, b0, a1v, b1v);
+      step(st + 1, true, true, RING - 2, a1v, b1v, a0, b0);
+    }
+#pragma unroll
+    for (int st = MAIN; st < NS2; ++st) {
+      const int ahead = NS2 - 2 - st < RING - 2 ? NS2 - 2 - st : RING - 2;
+      if ((st - MAIN) % 2 == 0) step(st, st + RING - 1 < NS2, st + 1 < NS2, ahead, a0, b0, a1v, b1v);
+      else step(st, st + RING - 1 < NS2, st + 1 < NS2, ahead, a1v, b1v, a0, b0);
     }
     float bias[JN];
 #pragma unroll
@@ -273,6 +343,7 @@ __global__ __launch_bounds__(64 * NW) void raft_motion_encoder_kernel(const Moti
   }
   __syncthreads();
 
+  stamp(4);
   // ---------------- stage 3: out = relu(conv([cor2 | flo2])) over the 8 x 16 tile, K = 9 x 128 ----------------
   {
     constexpr int NT3 = TH * TW / 16;  // 8 row tiles
@@ -284,41 +355,68 @@ __global__ __launch_bounds__(64 * NW) void raft_motion_encoder_kernel(const Moti
       const int q = 16 * i + r16;
       base[i] = (q / TW) * R2W + (q % TW);
     }
-    const f16* wrow[JN];
-#pragma unroll
-    for (int j = 0; j < JN; ++j) wrow[j] = p.w3 + (size_t)(nb + 16 * j + r16) * 1152 + kofs;
     floatx4 acc[NT3][JN];
 #pragma unroll
     for (int i = 0; i < NT3; ++i)
 #pragma unroll
       for (int j = 0; j < JN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    // B fragments D k-steps ahead in a register shift queue (a partially unrolled loop keeps every index
-    // compile-time)
-    half8 bq[D][JN];
-#pragma unroll
-    for (int st = 0; st < D; ++st)
-#pragma unroll
-      for (int j = 0; j < JN; ++j) bq[st][j] = *reinterpret_cast<const half8*>(wrow[j] + st * 32);
-#pragma unroll 2
-    for (int st = 0; st < NS3; ++st) {
-      half8 b[JN];
-#pragma unroll
-      for (int j = 0; j < JN; ++j) {
-        b[j] = bq[0][j];
-#pragma unroll
-        for (int d = 0; d + 1 < D; ++d) bq[d][j] = bq[d + 1][j];
-        if (st + D < NS3) bq[D - 1][j] = *reinterpret_cast<const half8*>(wrow[j] + (st + D) * 32);
-      }
+    // weights through per-wave DMA rings in the S1 and A1 areas (both finished): half the waves each
+    constexpr int RING = 12;
+    static_assert((NW / 2) * RING * JN * 1024 <= P1 * AS * 2 && (NW / 2) * RING * JN * 1024 <= P1 * 256,
+                  "stage-3 B rings fit the S1 / A1 areas");
+    BRing<JN, RING, 1152> br;
+    br.init(smem + (wave < NW / 2 ? S1_OFF : A1_OFF) + (wave % (NW / 2)) * RING * JN * 1024, p.w3, nb, lane);
+    auto readA = [&](int st, half8* a) {
       const int tap = st >> 2, ky = tap / 3, kx = tap - ky * 3;
       const int toff = ky * R2W + kx;
       const int chunk = (32 * (st & 3) + kofs) >> 3;
 #pragma unroll
-      for (int i = 0; i < NT3; ++i) {
-        const half8 a = *reinterpret_cast<const half8*>(s2 + sw(base[i] + toff, chunk));
+      for (int i = 0; i < NT3; ++i) a[i] = *reinterpret_cast<const half8*>(s2 + sw(base[i] + toff, chunk));
+    };
+    auto readB = [&](int st, half8* b) {
 #pragma unroll
-        for (int j = 0; j < JN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < JN; ++j) b[j] = br.frag(st, j, lane);
+    };
+    // One k-step: refill the ring slot freed by step st - 1 (the DMA goes first: the compiler drains lgkmcnt
+    // around it, which must not catch the prefetch reads), wait for step st + 1's weights, read step st + 1's
+    // A / B fragments, then step st's MFMAs.  Fully unrolled straight-line code (constant vmcnt), so the
+    // compiler's lgkmcnt tracking keeps the prefetch reads in flight under the MFMAs (a loop back-edge made it
+    // drain them before every step).
+    auto step = [&](int st, bool issue, bool prefetch, int ahead, const half8* ac, const half8* bc, half8* an,
+                    half8* bn) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (issue) br.issue(st + RING - 1);
+      if (prefetch) {
+        wait_vm_le<JN, RING - 2>(ahead);
+        readB(st + 1, bn);
+        readA(st + 1, an);
       }
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
+#pragma unroll
+      for (int i = 0; i < NT3; ++i)
+#pragma unroll
+        for (int j = 0; j < JN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ac[i], bc[j], acc[i][j], 0, 0, 0);
+    };
+#pragma unroll
+    for (int st = 0; st < RING - 1; ++st) br.issue(st);
+    half8 a0[NT3], a1v[NT3], b0[JN], b1v[JN];
+    wait_vm_le<JN, RING - 2>(RING - 2);
+    readB(0, b0);
+    readA(0, a0);
+    constexpr int MAIN = ((NS3 - RING + 1) / 2) * 2;  // steps with both a refill and a prefetch, in pairs
+#pragma unroll
+    for (int st = 0; st < MAIN; st += 2) {
+      step(st, true, true, RING - 2, a0, b0, a1v, b1v);
+      step(st + 1, true, true, RING - 2, a1v, b1v, a0, b0);
     }
+#pragma unroll
+    for (int st = MAIN; st < NS3; ++st) {
+      const int ahead = NS3 - 2 - st < RING - 2 ? NS3 - 2 - st : RING - 2;
+      if ((st - MAIN) % 2 == 0) step(st, st + RING - 1 < NS3, st + 1 < NS3, ahead, a0, b0, a1v, b1v);
+      else step(st, st + RING - 1 < NS3, st + 1 < NS3, ahead, a1v, b1v, a0, b0);
+    }
+    stamp(5);
+    __syncthreads();  // every wave is done with its ring before the S1 area takes the output tile
     // bias + relu (channels < 126), [fx, 0] tail, staged in the (finished) S1 area
     char* so = s1;
 #pragma unroll
@@ -344,17 +442,21 @@ __global__ __launch_bounds__(64 * NW) void raft_motion_encoder_kernel(const Moti
             *reinterpret_cast<const half8*>(so + sw(q, ch));
     }
   }
+  stamp(6);
 }
 
+unsigned long long* g_stamps = nullptr;
+
 }  // namespace
+
+// diagnostics: record s_memrealtime (100 MHz) stage marks of every workgroup into `buf` ([blocks][8][64] u64) on later launches
+extern "C" void sa_raft_motion_encoder_stamps(void* buf) { g_stamps = (unsigned long long*)buf; }
 
 extern "C" int sa_raft_motion_encoder(const float* pyr, const float* flow, int B, int H, int W, int W2, int levels,
                                       int radius, const void* w1, const float* b1, const void* w2c, const float* b2c,
                                       const void* w2f, const float* b2f, const void* w3, const float* b3, void* out,
                                       int os, hipStream_t stream) {
-  if (levels < 1 || levels > 4 || radius < 0 || radius > 4 || levels * (2 * radius + 1) > 36 || os < 128 || os % 8 ||
-      B < 1 || H < 1 || W < 1)
-    return -2;
+  if (levels != 4 || radius != 4 || os < 128 || os % 8 || B < 1 || H < 1 || W < 1) return -2;
   if (((uintptr_t)out | (uintptr_t)w1 | (uintptr_t)w2c | (uintptr_t)w2f | (uintptr_t)w3) & 15) return -2;
   long off[4] = {0, 0, 0, 0};
   long acc = 0;
@@ -388,6 +490,7 @@ extern "C" int sa_raft_motion_encoder(const float* pyr, const float* flow, int B
   a.b3 = b3;
   a.out = (f16*)out;
   a.os = os;
+  a.stamps = g_stamps;
   // SA_MENC_WAVES=4|8 (default 4: 8 waves measured no faster at batch 1 and 1 % slower at batch 8), read per
   // launch (a frame graph captures it once)
   const char* e = std::getenv("SA_MENC_WAVES");

@@ -106,8 +106,8 @@ class RaftStereo : public StereoEngine {
   bool fuse_motion_ = !(std::getenv("SA_RAFT_FUSE_MOTION") && std::getenv("SA_RAFT_FUSE_MOTION")[0] == '0');
   // the whole motion encoder (head + convc2/convf2 + conv) as one kernel (sa_raft_motion_encoder): bitwise the
   // same output as the head kernel + three convs (same fp16 operands, same k order), 4 launches -> 1 per
-  // iteration.  Measured in-process (tools/ab_engine.py): b1 10.38 vs 10.66 ms, b8 55.19 vs 54.95 ms/step, so
-  // auto = on below batch 4; SA_RAFT_FUSE_MENC=0/1 forces it.
+  // iteration.  Measured in-process (tools/ab_engine.py): b1 9.94 vs 10.57 ms, b8 53.61 vs 55.75 ms/step.
+  // SA_RAFT_FUSE_MENC=0/1 forces the unfused / fused path (default: by tile count, forward()).
   int fuse_menc_mode_ = std::getenv("SA_RAFT_FUSE_MENC") ? std::atoi(std::getenv("SA_RAFT_FUSE_MENC")) : -1;
   bool fuse_menc_ = true;
   // SA_RAFT_PARALLEL=0: run the motion encoder and the coarse GRU levels on one stream
@@ -268,7 +268,7 @@ void RaftStereo::build(WeightSource& src) {
       b1[64 + o] = ws.get(u + "encoder.convf1.bias").data[o];
     }
     me_b1_ = up(b1);
-    if (rc_.radius > 4) fuse_menc_ = false;
+    if (rc_.levels != 4 || rc_.radius != 4) fuse_menc_ = false;  // the fused kernel's K layout
   } else {
     fuse_motion_ = false;
   }
@@ -447,7 +447,10 @@ void RaftStereo::forward(hipStream_t s) {
     }
   };
   // motion encoder: lookup -> convc1/convf1 -> convc2/convf2 -> conv (+ [flow, 0] tail)
-  const bool menc = fuse_motion_ && fuse_menc_ && (fuse_menc_mode_ >= 0 ? fuse_menc_mode_ != 0 : Bn < 4);
+  // auto: fused once the frame has >= 128 of its 8x16 tiles (one workgroup each); the realtime preset's 1/8
+  // grid at batch 1 (40 tiles) runs the wider unfused kernels slightly faster (2.39 vs 2.41 ms)
+  const long menc_tiles = (long)Bn * ((h0 + 7) / 8) * ((w0 + 15) / 16);
+  const bool menc = fuse_motion_ && fuse_menc_ && (fuse_menc_mode_ >= 0 ? fuse_menc_mode_ != 0 : menc_tiles >= 128);
   auto motion = [&](hipStream_t ms) {
     if (menc) {
       const SaConvArgs c2 = convc2_.args({cor1_}, corflo_.slice_c(0, 64));
