@@ -236,8 +236,10 @@ typedef struct {
 } SaAgclArgs;
 int sa_agcl_corr(const SaAgclArgs* a, hipStream_t stream);
 
+// ws: fp32 workspace of sa_linear_attention_ws_floats(N, S, heads, dim) floats (per-chunk partial KV / Ksum)
+long sa_linear_attention_ws_floats(int N, int S, int heads, int dim);
 int sa_linear_attention(const void* q, int qs, const void* k, int ks, const void* v, int vs, void* out, int os,
-                        int N, int L, int S, int heads, int dim, float eps, hipStream_t stream);
+                        int N, int L, int S, int heads, int dim, float eps, float* ws, hipStream_t stream);
 int sa_layernorm(const void* x, int xs, const float* gamma, const float* beta, const void* res, int rs, void* out,
                  int os, long rows, int C, float eps, hipStream_t stream);
 

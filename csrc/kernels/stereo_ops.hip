@@ -5,8 +5,8 @@
 //                           3x3 window; "iter" mode warps the right features by the flow and takes
 //                           the window with replicate padding, "offset" mode samples the right
 //                           features at flow + window + learned offset with zero padding)
-//   * sa_linear_attention — LoFTR linear attention (ELU+1 kernel, KV/Ksum reduction per head staged
-//                           through LDS, fp32 math)
+//   * sa_linear_attention — LoFTR linear attention (ELU+1 kernel, fp32 math): per-64-token-chunk partial
+//                           KV / Ksum, then per-64-token-tile outputs summing the partials in order
 //   * sa_layernorm        — row LayerNorm with optional residual add
 //   * sa_ew               — elementwise activation / scale / add of channel slices (+ broadcast
 //                           addend, e.g. a positional encoding)
@@ -104,70 +104,93 @@ __global__ void zero_tail_kernel(f16* out, int stride, long P, int c0, int c1) {
 }
 
 // ------------------------------------------------------------------ linear attention
-// grid (N, heads); 256 threads.  Phase 1: KV[d][v] = sum_s phi(K)[s][d] V[s][v], Ksum[d] = sum_s
-// phi(K)[s][d] with 64-token tiles staged in LDS.  Phase 2: out[l][v] = sum_d phi(Q)[l][d] KV[d][v] /
-// (sum_d phi(Q)[l][d] Ksum[d] + eps).
+// out[l][v] = sum_d phi(Q)[l][d] KV[d][v] / (sum_d phi(Q)[l][d] Ksum[d] + eps), KV[d][v] = sum_s phi(K)[s][d] V[s][v],
+// Ksum[d] = sum_s phi(K)[s][d], phi = elu + 1, per (image, head) with head dim D.
+// Two kernels over many workgroups (round 1 ran one workgroup per (image, head): 8-16 workgroups on 256 CUs,
+// 0.6 ms per call): (1) one 64-token chunk of K / V per workgroup -> partial [KV | Ksum] into the workspace;
+// (2) one 64-token tile of Q per workgroup sums the partials in chunk order (deterministic) and writes its
+// outputs, phi(Q) computed once per element and staged in LDS.
+constexpr int LA_CHUNK = 64;
+
 template <int D>
-__global__ void linear_attn_kernel(const f16* __restrict__ q, int qs, const f16* __restrict__ k, int ks,
-                                   const f16* __restrict__ v, int vs, f16* __restrict__ out, int os, int L, int S,
-                                   float eps) {
-  __shared__ float kt[64][D + 1];
-  __shared__ float vt[64][D + 1];
+__global__ __launch_bounds__(256) void linear_attn_kv_kernel(const f16* __restrict__ k, int ks, const f16* __restrict__ v,
+                                                             int vs, int S, int heads, float* __restrict__ ws) {
+  __shared__ float kt[LA_CHUNK][D + 1];
+  __shared__ float vt[LA_CHUNK][D + 1];
+  const int c = blockIdx.x, h = blockIdx.y, n = blockIdx.z, tid = threadIdx.x;
+  const int nch = gridDim.x;
+  const int s0 = c * LA_CHUNK, hoff = h * D;
+  for (int e = tid; e < LA_CHUNK * D; e += 256) {
+    const int s = e / D, d = e % D;
+    float kk = 0.f, vv = 0.f;
+    if (s0 + s < S) {
+      const long row = (long)n * S + s0 + s;
+      kk = (float)k[row * ks + hoff + d];
+      kk = kk > 0.f ? kk + 1.f : __expf(kk);  // elu(x) + 1
+      vv = (float)v[row * vs + hoff + d];
+    }
+    kt[s][d] = kk;
+    vt[s][d] = vv;
+  }
+  __syncthreads();
+  float* dst = ws + (((size_t)n * heads + h) * nch + c) * (D * D + D);
+  for (int pidx = tid; pidx < D * D; pidx += 256) {
+    const int d = pidx / D, vv = pidx % D;
+    float a = 0.f;
+#pragma unroll 8
+    for (int s = 0; s < LA_CHUNK; ++s) a += kt[s][d] * vt[s][vv];
+    dst[pidx] = a;
+  }
+  if (tid < D) {
+    float a = 0.f;
+    for (int s = 0; s < LA_CHUNK; ++s) a += kt[s][tid];
+    dst[D * D + tid] = a;
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void linear_attn_out_kernel(const f16* __restrict__ q, int qs, const float* __restrict__ ws,
+                                                              int nch, int heads, f16* __restrict__ out, int os, int L,
+                                                              float eps) {
   __shared__ float kv[D][D + 1];
   __shared__ float ksum[D];
-  const int n = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
-  const int hoff = h * D;
-  constexpr int PAIRS = D * D / 256;  // (d, v) pairs per thread
-  float acc[PAIRS];
-  float ks_acc = 0.f;
-#pragma unroll
-  for (int j = 0; j < PAIRS; ++j) acc[j] = 0.f;
-  for (int s0 = 0; s0 < S; s0 += 64) {
-    for (int e = tid; e < 64 * D; e += 256) {
-      const int s = e / D, d = e % D;
-      float kk = 0.f, vv = 0.f;
-      if (s0 + s < S) {
-        const long row = (long)n * S + s0 + s;
-        kk = (float)k[row * ks + hoff + d];
-        kk = kk > 0.f ? kk + 1.f : __expf(kk);  // elu(x) + 1
-        vv = (float)v[row * vs + hoff + d];
-      }
-      kt[s][d] = kk;
-      vt[s][d] = vv;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < PAIRS; ++j) {
-      const int pidx = tid + 256 * j;
-      const int d = pidx / D, vv = pidx % D;
-      float a = acc[j];
-      for (int s = 0; s < 64; ++s) a += kt[s][d] * vt[s][vv];
-      acc[j] = a;
-    }
-    if (tid < D)
-      for (int s = 0; s < 64; ++s) ks_acc += kt[s][tid];
-    __syncthreads();
+  __shared__ float qt[LA_CHUNK][D + 1];
+  const int t = blockIdx.x, h = blockIdx.y, n = blockIdx.z, tid = threadIdx.x;
+  const int l0 = t * LA_CHUNK, hoff = h * D;
+  const float* src = ws + ((size_t)n * heads + h) * nch * (D * D + D);
+  for (int e = tid; e < D * D + D; e += 256) {
+    float a = 0.f;
+    for (int c = 0; c < nch; ++c) a += src[(size_t)c * (D * D + D) + e];
+    if (e < D * D) kv[e / D][e % D] = a;
+    else ksum[e - D * D] = a;
   }
-#pragma unroll
-  for (int j = 0; j < PAIRS; ++j) {
-    const int pidx = tid + 256 * j;
-    kv[pidx / D][pidx % D] = acc[j];
-  }
-  if (tid < D) ksum[tid] = ks_acc;
-  __syncthreads();
-  // phase 2: each thread handles (token, v) outputs
-  for (long e = tid; e < (long)L * D; e += 256) {
-    const int l = (int)(e / D), vv = (int)(e % D);
-    const long row = (long)n * L + l;
-    float num = 0.f, den = 0.f;
-    for (int d = 0; d < D; ++d) {
-      float qq = (float)q[row * qs + hoff + d];
+  for (int e = tid; e < LA_CHUNK * D; e += 256) {
+    const int l = e / D, d = e % D;
+    float qq = 0.f;
+    if (l0 + l < L) {
+      qq = (float)q[((long)n * L + l0 + l) * qs + hoff + d];
       qq = qq > 0.f ? qq + 1.f : __expf(qq);
-      num += qq * kv[d][vv];
-      den += qq * ksum[d];
     }
-    out[row * os + hoff + vv] = (f16)(num / (den + eps));
+    qt[l][d] = qq;
   }
+  __syncthreads();
+  // thread -> token tid / 4, 8 consecutive output channels (tid % 4) * 8 (D = 32)
+  constexpr int VPT = D / 4;
+  const int l = tid >> 2, vb = (tid & 3) * VPT;
+  if (l0 + l >= L) return;
+  float num[VPT], den = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) num[j] = 0.f;
+  for (int d = 0; d < D; ++d) {
+    const float qq = qt[l][d];
+    den += qq * ksum[d];
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) num[j] += qq * kv[d][vb + j];
+  }
+  const float inv = 1.f / (den + eps);
+  f16* op = out + ((long)n * L + l0 + l) * os + hoff + vb;
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) op[j] = (f16)(num[j] * inv);
 }
 
 // ------------------------------------------------------------------ layer norm (+ residual)
@@ -268,11 +291,19 @@ extern "C" int sa_agcl_corr(const SaAgclArgs* a, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+extern "C" long sa_linear_attention_ws_floats(int N, int S, int heads, int dim) {
+  return (long)N * heads * ((S + LA_CHUNK - 1) / LA_CHUNK) * (dim * dim + dim);
+}
+
 extern "C" int sa_linear_attention(const void* q, int qs, const void* k, int ks, const void* v, int vs, void* out,
-                                   int os, int N, int L, int S, int heads, int dim, float eps, hipStream_t stream) {
-  if (dim != 32) return -2;
-  hipLaunchKernelGGL(linear_attn_kernel<32>, dim3(N, heads), dim3(256), 0, stream, (const f16*)q, qs, (const f16*)k,
-                     ks, (const f16*)v, vs, (f16*)out, os, L, S, eps);
+                                   int os, int N, int L, int S, int heads, int dim, float eps, float* ws,
+                                   hipStream_t stream) {
+  if (dim != 32 || !ws || N < 1 || L < 1 || S < 1 || heads < 1 || N > 65535 || heads > 65535) return -2;
+  const int nch = (S + LA_CHUNK - 1) / LA_CHUNK;
+  hipLaunchKernelGGL(linear_attn_kv_kernel<32>, dim3(nch, heads, N), dim3(256), 0, stream, (const f16*)k, ks,
+                     (const f16*)v, vs, S, heads, ws);
+  hipLaunchKernelGGL(linear_attn_out_kernel<32>, dim3((L + LA_CHUNK - 1) / LA_CHUNK, heads, N), dim3(256), 0, stream,
+                     (const f16*)q, qs, ws, nch, heads, (f16*)out, os, L, eps);
   return (int)hipGetLastError();
 }
 

@@ -43,6 +43,7 @@ struct AttnLayer {
   ConvLayer q, kv, merge, mlp0, mlp2;
   float *n1g = nullptr, *n1b = nullptr, *n2g = nullptr, *n2b = nullptr;
   Tensor qb, kvb, att, m2, cat, h1, h2;
+  float* la_ws = nullptr;  // linear-attention partial KV / Ksum per 64-token chunk
   int N = 0, L = 0;
   void build(DeviceArena& a, WeightSource& src, const std::string& p, int N_, int L_) {
     N = N_;
@@ -77,13 +78,14 @@ struct AttnLayer {
     cat = make_tensor(a, N, 1, L, 256);  // normalised message (concat partner of x)
     h1 = make_tensor(a, N, 1, L, 512);
     h2 = make_tensor(a, N, 1, L, 256);
+    la_ws = (float*)a.alloc((size_t)sa_linear_attention_ws_floats(N, L, 8, 32) * 4);
   }
   // out = x + norm2(mlp([x, norm1(merge(attn(q(x), k(src), v(src))))])); x/src/out: [N][1][L][256]
   void run(hipStream_t s, const Tensor& x, const Tensor& source, const Tensor& out) const {
     q.run(s, {x}, qb);
     kv.run(s, {source}, kvb);
     int rc = sa_linear_attention(qb.ptr, qb.stride, kvb.ptr, kvb.stride, kvb.slice_c(256, 256).ptr, kvb.stride,
-                                 att.ptr, att.stride, N, L, L, 8, 32, 1e-6f, s);
+                                 att.ptr, att.stride, N, L, L, 8, 32, 1e-6f, la_ws, s);
     SA_REQUIRE(rc == 0, "linear attention failed");
     merge.run(s, {att}, m2);
     rc = sa_layernorm(m2.ptr, m2.stride, n1g, n1b, nullptr, 0, cat.ptr, cat.stride, (long)N * L, 256, 1e-5f, s);

@@ -142,12 +142,14 @@ def _declare_dev(lib):
         "sa_corr1d_lookup": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _i, _i, _p, _i, _i, _p, _i, _p]),
         "sa_raft_motion_head": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _i, _p, _i, _p, _i, _p]),
         "sa_raft_motion_encoder": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p]),
+        "sa_raft_motion_encoder_stamps": (None, [_p]),
         "sa_convex_upsample": (_i, [_p, _i, _p, _i, _i, _i, _i, _f, _p, _p]),
         "sa_preprocess": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, _p]),
         "sa_remap_bgr": (_i, [_p, _i, _i, _i, _p, _i, _i, _i, _p, _p]),
         "sa_reproject": (_i, [_p, _i, _f, _p, _i, _i, _i, _p, _p, _p, _p]),
         "sa_agcl_corr": (_i, [C.POINTER(SaAgclArgs), _p]),
-        "sa_linear_attention": (_i, [_p, _i, _p, _i, _p, _i, _p, _i, _i, _i, _i, _i, _i, _f, _p]),
+        "sa_linear_attention": (_i, [_p, _i, _p, _i, _p, _i, _p, _i, _i, _i, _i, _i, _i, _f, _p, _p]),
+        "sa_linear_attention_ws_floats": (C.c_long, [_i, _i, _i, _i]),
         "sa_layernorm": (_i, [_p, _i, _p, _p, _p, _i, _p, _i, C.c_long, _i, _f, _p]),
         "sa_ew": (_i, [C.POINTER(SaEwArgs), _p]),
         "sa_flow_features": (_i, [_p, _i, C.c_long, _p, _i, _i, _p, _i, _p]),

@@ -366,8 +366,11 @@ def linear_attention(q, k, v, heads=8, eps=1e-6):
     n, l, d = q.shape
     s = k.shape[1]
     out = torch.empty(n, l, d, dtype=torch.float16, device=q.device)
+    ws = torch.empty(N.dev().sa_linear_attention_ws_floats(n, s, heads, d // heads), dtype=torch.float32,
+                     device=q.device)
     N.check(N.dev().sa_linear_attention(_ptr(q), q.stride(1), _ptr(k), k.stride(1), _ptr(v), v.stride(1), _ptr(out),
-                                        out.stride(1), n, l, s, heads, d // heads, eps, _stream()), "sa_linear_attention")
+                                        out.stride(1), n, l, s, heads, d // heads, eps, _ptr(ws), _stream()),
+            "sa_linear_attention")
     return out
 
 
