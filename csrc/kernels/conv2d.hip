@@ -76,6 +76,13 @@ enum : int {
   kGldsDeep = 6,  // kGlds3 with the LDS ring as deep as 160 KB allows (up to 8 stages, NSTAGE - 1 in
                   // flight): for the small-M / deep-K convs of the coarse GRU levels and the motion
                   // encoder, whose k-steps wait on DMA latency rather than on the MFMAs
+  kPing = 7,  // 8-wave ping-pong: the kWide uniform-k DMA gather (BK = 32, channel-major K order) into a 4- or
+              // 6-deep LDS ring, waves 0-3 (one per SIMD) and 4-7 offset by one barrier so that on every SIMD
+              // one wave runs a 16x16x32 MFMA cluster while the other reads its next fragments and issues DMA
+              // (cdna_hip_programming.md §5 "256^2 8-phase template", T3-T5)
+  kPingM = 8,  // kPing with the DMA pieces issued between the MFMAs of the compute slot (an LDS-DMA issue costs
+               // ~60 cycles among bare MFMAs, 100-185 beside a slot's ds_reads: MI355X_MICROARCH.md), leaving only
+               // the fragment reads in the read slot
 };
 __host__ __device__ constexpr bool is_glds(int mode) { return mode == kGlds3 || mode == kGldsDeep; }
 
@@ -83,7 +90,9 @@ template <int BM, int BN, int WM, int WN, int MODE = kRegK32>
 struct ConvCfg {
   static constexpr bool GL = MODE == kDmaK64;
   static constexpr bool WIDE = MODE == kWide;
-  static constexpr int BK = (MODE == kRegK32 || WIDE) ? 32 : 64;
+  static constexpr bool PING = MODE == kPing || MODE == kPingM;
+  static constexpr bool BANDED = WIDE || PING;  // C tile staged through LDS in row bands
+  static constexpr int BK = (MODE == kRegK32 || WIDE || PING) ? 32 : 64;
   static constexpr int KCH = BK / 8;  // 16-byte chunks per row per stage
   static constexpr int TM = BM / WM, TN = BN / WN;
   // 16x16 fragment repeats (kWide keeps its own 32x32 accumulators: a 1x1 placeholder here)
@@ -95,16 +104,20 @@ struct ConvCfg {
   // kGlds3: three-deep LDS ring; kGldsDeep: as deep as 160 KB allows (<= 8); kWide: four-deep; everything
   // else double-buffered
   static constexpr int DEEP_NS = 163840 / (A_BYTES + B_BYTES) < 8 ? 163840 / (A_BYTES + B_BYTES) : 8;
-  static constexpr int NSTAGE = MODE == kGlds3 ? 3 : MODE == kGldsDeep ? DEEP_NS : (WIDE ? 4 : 2);
+  // kPing: as deep as 144 KB allows, at most 6 (256x256: 4 stages, 256x128: 6; a 5-deep 256x256 ring measured
+  // the same)
+  static constexpr int PING_NS = 147456 / (A_BYTES + B_BYTES) < 6 ? 147456 / (A_BYTES + B_BYTES) : 6;
+  static constexpr int NSTAGE = MODE == kGlds3 ? 3 : MODE == kGldsDeep ? DEEP_NS : PING ? PING_NS : (WIDE ? 4 : 2);
   static constexpr int STAGE_BYTES = NSTAGE * (A_BYTES + B_BYTES);
   // fp32 C tile, unpadded rows; columns XOR-swizzled in 16-float blocks (cswz) so the MFMA
   // write-out (4 row groups x 16 lanes) hits 64 distinct banks; aliases the stage buffers.
   // kWide stages it in bands of CROWS rows (128 KB of fp32 per band)
   static constexpr int CST = BN;
-  static constexpr int CROWS = WIDE ? (32768 / BN < BM ? 32768 / BN : BM) : BM;
+  static constexpr int CROWS = BANDED ? (32768 / BN < BM ? 32768 / BN : BM) : BM;
   static constexpr int C_BYTES = CROWS * CST * 4;
   static constexpr int SMEM = STAGE_BYTES > C_BYTES ? STAGE_BYTES : C_BYTES;
-  static_assert(WM * WN == 4 || (WM * WN == 8 && (is_glds(MODE) || WIDE)), "4 waves (8 for kGlds3; 4 or 8 for kWide) per workgroup");
+  static_assert(WM * WN == 4 || (WM * WN == 8 && (is_glds(MODE) || WIDE || PING)), "4 waves (8 for kGlds3; 4 or 8 for kWide) per workgroup");
+  static_assert(!PING || (WM == 2 && WN == 4 && BM == 256), "kPing: 2 x 4 waves, one 128-row half of the tile per wave group");
   static_assert(!is_glds(MODE) || NSTAGE >= 3, "DMA rings keep at least one stage in flight across the barrier");
   static_assert(TM % 16 == 0 && TN % 16 == 0, "wave tile must be 16-aligned");
   static_assert(!WIDE || (TM == 128 && (TN == 64 || TN == 128)), "kWide: 128x64 or 128x128 wave tiles");
@@ -530,8 +543,9 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
       cur = nxt;
     }
     __syncthreads();  // all fragment reads done before the epilogue reuses LDS
-  } else if constexpr (MODE == kWide) {
+  } else if constexpr (MODE == kWide || C::PING) {
     // ---------------- wide tile: uniform-k DMA gather, BK = 32, 4-deep LDS ring, 32x32x16 MFMA ----------
+    // (kPing shares the gather and the stage image, and runs its own ping-pong schedule below)
     // Stage image per operand: [rows][32 halfs] (64-B rows), lane-linear per wave instruction (16 rows x 4
     // chunks per 1 KB DMA piece) with the chunk XOR ((row >> 2) & 3) applied on the SOURCE side and on
     // the fragment reads (same involution; cdna_hip_programming.md §5.4 rule 21): the 16 lanes of each
@@ -547,7 +561,7 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
     static_assert(NA * NT == BM * 4 && NB * NT == BN * 4 && NA >= 1 && NB >= 1, "whole-wave DMA pieces");
     constexpr int NAB = NA + NB;
     constexpr int STG = (BM + BN) * 64;
-    static_assert(4 * STG <= C::SMEM, "ring fits");
+    static_assert(C::NSTAGE * STG <= C::SMEM && (C::PING || C::NSTAGE == 4), "ring fits");
     const int KH = p.KH, KW = p.KW;
     int pixb[NA];
     unsigned long long vmask[NA];
@@ -580,8 +594,10 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
     // tap-major order streams a whole tile's A panel between two uses and thrashes the XCD's L2 once 32
     // CUs each hold a different 256-row panel.  (kWide is never split: kt0 = 0.)
     const int taps_all = KD * KH * KW;
-    int tap = 0, ci0 = 0, kh_ = 0, kw_ = 0;
-    int toff = 0;
+    // (kWide is never split; a kPing split-K slice starts at stage kt0 = chunk * taps_all + tap)
+    int ci0 = (kt0 / taps_all) * 32, tap = kt0 - (kt0 / taps_all) * taps_all;
+    int kh_ = (tap % (KH * KW)) / KW, kw_ = tap % KW;
+    int toff = ((tap / (KH * KW)) * p.H + kh_ * p.dh) * p.W + kw_ * p.dw;
     const int sb1 = p.src[0].channels;
     const int sb2 = sb1 + (p.nsrc > 1 ? p.src[1].channels : 0);
     const int sb3 = sb2 + (p.nsrc > 2 ? p.src[2].channels : 0);
@@ -642,6 +658,224 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
         ci0 += 32;
       }
     };
+    if constexpr (C::PING) {
+      // ---- ping-pong schedule.  Wave group g = wave >> 2 (waves 0-3 and 4-7: one wave of each group per
+      // SIMD) owns the tile rows [128 g, 128 g + 128).  Between consecutive raw barriers ("slots") one group
+      // runs the MFMA cluster of a whole stage (8 x FN 16x16x32 MFMAs) while the other reads its fragments of
+      // a stage from LDS and issues its share of a later stage's DMA; group 1 starts one barrier late, so
+      //   slot 2s:   G0 MFMA(s)               G1 read(s) + DMA(s + NS - 1)
+      //   slot 2s+1: G0 read(s+1) + DMA(s+NS) G1 MFMA(s)
+      // RAW: every wave retires its DMA of stage s+1 (counted vmcnt, NS-2 later stages left in flight) before
+      // the barrier that opens slot 2s+1, the first slot reading s+1.  WAR: the buffer refilled in slot 2s
+      // (2s+1) was last read in slot 2s-2 (2s) and those reads were retired (lgkmcnt(0)) before the barrier.
+      // Each wave issues the stages strictly in order (issue() walks the k position).
+      constexpr int NS = C::NSTAGE;
+      static_assert(NS >= 3 && (NS - 2) * NAB <= 32, "ring depth / vmcnt literal range");
+      const int g = wave >> 2;
+      const int frow = lane & 15, lc = lane >> 4;
+      half8 fa[C::FM], fb[C::FN];
+      // 16x16x32 operands: lane (frow, lc) holds row frow, k = 8 lc .. 8 lc + 7 (64-B rows, chunk XOR (row>>2)&3)
+      auto read_stage = [&](int buf) {
+#ifdef SA_EXP_NOLDSREAD
+        if (buf < 0)  // never: the reads are skipped, the registers stay live (timing experiments only)
+#endif
+        {
+        const char* sa = smem + buf * STG;
+        const char* sb = sa + BM * 64;
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+          const int row = wm * C::TM + i * 16 + frow;
+          fa[i] = *reinterpret_cast<const half8*>(sa + row * 64 + ((lc ^ ((row >> 2) & 3)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) {
+          const int row = wn * C::TN + j * 16 + frow;
+          fb[j] = *reinterpret_cast<const half8*>(sb + row * 64 + ((lc ^ ((row >> 2) & 3)) << 4));
+        }
+        }
+      };
+      auto mfma_stage = [&]() {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int j = 0; j < C::FN; ++j) {
+#ifdef SA_EXP_NOMFMA
+            asm volatile("" ::"v"(fa[i]), "v"(fb[j]));
+#else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+#endif
+          }
+        __builtin_amdgcn_s_setprio(0);
+      };
+      // raw barrier pinned in the instruction stream (no MFMA / ds_read moves across it)
+      auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+#ifndef SA_EXP_NOBAR
+        __builtin_amdgcn_s_barrier();
+#endif
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      auto lgkm0 = [&]() {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      // stage s+1 landed (own DMA), later stages up to min(s + NS - 1, nk - 1) may stay in flight
+      auto wait_next = [&](int s) {
+        const int last = s + NS - 1 < nk - 1 ? s + NS - 1 : nk - 1;
+        wait_stages<NAB, NS - 2>(last - (s + 1));
+      };
+      // prologue: stages 0 .. NS-2 in flight, stage 0 landed
+#pragma unroll
+      for (int t = 0; t < NS - 1; ++t)
+        if (t < nk) issue(t);
+      if (nk > 0) wait_stages<NAB, NS - 2>((nk - 1 < NS - 2 ? nk - 1 : NS - 2));
+      bar();
+      if constexpr (MODE == kPingM) {
+        // The compute slot of stage s also issues this wave's pieces of stage s + NS - 1 (into the buffer of
+        // stage s - 1, whose last reads (G1, slot 2s - 2) were retired before the barrier opening slot 2s),
+        // one piece after every few MFMAs:
+        //   slot 2s:   G0 MFMA(s) + DMA(s+NS-1)   G1 read(s)
+        //   slot 2s+1: G0 read(s+1)               G1 MFMA(s) + DMA(s+NS-1)
+        // Before the barrier opening slot 2s+1 stage s+1 must have landed: G0 has issued through s+NS-1 at
+        // that point, G1 through s+NS-2.
+        constexpr int GAP = C::FM * C::FN / NAB;  // MFMAs between two pieces
+        static_assert(GAP >= 2, "MFMA slots per DMA piece");
+        auto mfma_dma = [&](int buf) {
+          char* sa = smem + buf * STG;
+          char* sb = sa + BM * 64;
+          const f16* sp;
+          int sst;
+          if (ci0 < sb1) { sp = sp0 + ci0; sst = ss0; }
+          else if (ci0 < sb2) { sp = sp1 + (ci0 - sb1); sst = ss1; }
+          else if (ci0 < sb3) { sp = sp2 + (ci0 - sb2); sst = ss2; }
+          else { sp = sp3 + (ci0 - sb3); sst = ss3; }
+          const int koff = tap * p.Cin + ci0;
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int t = 0; t < C::FM * C::FN; ++t) {
+            const int i = t / C::FN, j = t % C::FN;
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            if (t % GAP == 0 && t / GAP < NAB) {
+              const int q = t / GAP;
+              if (q < NA) {
+                const bool v = (vmask[q] >> tap) & 1ull;
+                const f16* ga = sp + ((pixb[q] + toff) * sst + lcho[q]);
+                __builtin_amdgcn_global_load_lds(v ? (const void*)ga : zero_src,
+                                                 (lds_void_t*)(sa + (wave * NA + q) * 1024), 16, 0, 0);
+              } else {
+                __builtin_amdgcn_global_load_lds((const void*)(wrow[q - NA] + koff),
+                                                 (lds_void_t*)(sb + (wave * NB + q - NA) * 1024), 16, 0, 0);
+              }
+            }
+          }
+          __builtin_amdgcn_s_setprio(0);
+          ++tap;
+          ++kw_;
+          toff += p.dw;
+          if (kw_ == KW) {
+            kw_ = 0;
+            toff += p.dh * p.W - KW * p.dw;
+            ++kh_;
+            if (kh_ == KH) {
+              kh_ = 0;
+              toff += p.H * p.W - KH * p.dh * p.W;
+            }
+          }
+          if (tap == taps_all) {
+            tap = 0;
+            toff = 0;
+            ci0 += 32;
+          }
+        };
+        int rbuf = 0, ibuf = NS - 1;
+        if (g == 0) {
+          if (nk > 0) read_stage(0);
+          rbuf = 1;
+          lgkm0();
+          bar();
+          for (int s = 0; s < nk; ++s) {
+            if (s + NS - 1 < nk) {
+              mfma_dma(ibuf);
+              ibuf = ibuf == NS - 1 ? 0 : ibuf + 1;
+            } else {
+              mfma_stage();
+            }
+            if (s + 1 < nk) {
+              const int last = s + NS - 1 < nk - 1 ? s + NS - 1 : nk - 1;
+              wait_stages<NAB, NS - 2>(last - (s + 1));
+            }
+            bar();
+            if (s + 1 < nk) {
+              read_stage(rbuf);
+              rbuf = rbuf == NS - 1 ? 0 : rbuf + 1;
+            }
+            lgkm0();
+            bar();
+          }
+        } else {
+          bar();
+          for (int s = 0; s < nk; ++s) {
+            read_stage(rbuf);
+            rbuf = rbuf == NS - 1 ? 0 : rbuf + 1;
+            lgkm0();
+            if (s + 1 < nk) {
+              const int last = s + NS - 2 < nk - 1 ? s + NS - 2 : nk - 1;
+              wait_stages<NAB, NS - 3>(last - (s + 1));
+            }
+            bar();
+            if (s + NS - 1 < nk) {
+              mfma_dma(ibuf);
+              ibuf = ibuf == NS - 1 ? 0 : ibuf + 1;
+            } else {
+              mfma_stage();
+            }
+            bar();
+          }
+        }
+      } else if (g == 0) {
+        int rbuf = 0;       // buffer of the next stage to read (s + 1 after the first read)
+        int ibuf = NS - 1;  // buffer of the next stage to issue
+        if (nk > 0) read_stage(0);
+        if (NS - 1 < nk) issue(ibuf);
+        ibuf = 0;
+        rbuf = 1;
+        lgkm0();
+        bar();
+        for (int s = 0; s < nk; ++s) {
+          mfma_stage();
+          if (s + 1 < nk) wait_next(s);
+          bar();
+          if (s + 1 < nk) {
+            read_stage(rbuf);
+#ifndef SA_EXP_NODMA
+            if (s + NS < nk) issue(ibuf);
+#endif
+            rbuf = rbuf == NS - 1 ? 0 : rbuf + 1;
+            ibuf = ibuf == NS - 1 ? 0 : ibuf + 1;
+          }
+          lgkm0();
+          bar();
+        }
+      } else {
+        int rbuf = 0, ibuf = NS - 1;
+        bar();
+        for (int s = 0; s < nk; ++s) {
+          read_stage(rbuf);
+#ifndef SA_EXP_NODMA
+          if (s + NS - 1 < nk) issue(ibuf);
+#endif
+          rbuf = rbuf == NS - 1 ? 0 : rbuf + 1;
+          ibuf = ibuf == NS - 1 ? 0 : ibuf + 1;
+          lgkm0();
+          if (s + 1 < nk) wait_next(s);
+          bar();
+          mfma_stage();
+          bar();
+        }
+      }
+      __syncthreads();  // all fragment reads done before the epilogue reuses LDS
+    } else {
     // 32x32x16 fragments of k16 half h of the stage in `buf`: lane = (r, hl) holds row r, k = 16h + 8hl..+7
     const int fr = lane & 31, fh = lane >> 5;
     auto frag = [&](const char* base, int row, int h) {
@@ -727,6 +961,7 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
       mfma_only(ya, yb);
     }
     __syncthreads();  // all fragment reads done before the epilogue reuses LDS
+    }  // kWide schedule
   } else if constexpr (C::GL) {
     // ---------------- DMA staging: [rows][64 halfs] (128 B) per stage, chunk XOR-swizzled ----------
     // LDS image is lane-linear per wave instruction (q*16 = row*128 + pch*16); the swizzle lives on
@@ -1081,7 +1316,7 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
 #pragma unroll
   for (int j = 0; j < 8; ++j) bias8[j] = (p.bias && j < nvalid) ? p.bias[co + j] : 0.f;
 
-  if constexpr (!C::WIDE) {
+  if constexpr (!C::BANDED) {
 #pragma unroll
     for (int i = 0; i < C::FM; ++i)
 #pragma unroll
@@ -1272,22 +1507,35 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
       }
     }
   };
-  if constexpr (C::WIDE) {
-    // two row bands: the waves owning a band's rows stage their 32x32 accumulators, everyone stores
+  if constexpr (C::BANDED) {
+    // row bands: the waves owning a band's rows stage their accumulators, everyone stores
 #pragma unroll
     for (int band = 0; band < BM / C::CROWS; ++band) {
       const int b0 = band * C::CROWS;
       if (wm * 128 >= b0 && wm * 128 < b0 + C::CROWS) {
+        if constexpr (C::WIDE) {
 #pragma unroll
-        for (int i = 0; i < WFM; ++i)
+          for (int i = 0; i < WFM; ++i)
 #pragma unroll
-          for (int j = 0; j < WFN; ++j)
+            for (int j = 0; j < WFN; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int row = wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) - b0;
-              const int col = wn * C::TN + j * 32 + (lane & 31);
-              ct[row * C::CST + cswz(row, col)] = acc32[i][j][r];
-            }
+              for (int r = 0; r < 16; ++r) {
+                const int row = wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) - b0;
+                const int col = wn * C::TN + j * 32 + (lane & 31);
+                ct[row * C::CST + cswz(row, col)] = acc32[i][j][r];
+              }
+        } else {
+#pragma unroll
+          for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+            for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int row = wm * C::TM + i * 16 + (lane >> 4) * 4 + r - b0;
+                const int col = wn * C::TN + j * 16 + (lane & 15);
+                ct[row * C::CST + cswz(row, col)] = acc[i][j][r];
+              }
+        }
       }
       __syncthreads();
       if (nvalid > 0) epi_rows(b0, b0 + C::CROWS, b0);
@@ -1393,6 +1641,33 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
   // round-robin over the 8 XCDs, so give each XCD a contiguous run of m-major tiles (neighbour tiles share
   // input rows through the 3x3 halo, the n tiles of one m share the whole A panel)
   int bx = blockIdx.x, by = blockIdx.y;
+  if constexpr (C::PING) {
+    // 1-D grid: the first `full` dispatch ids are whole tiles (XCD-aware order), the remaining ones split each
+    // of the last T - full tiles into S = p.splitk K slices, so a tile count that is not a multiple of the CU
+    // count does not leave most CUs idle in the last round (launch_ping)
+    const int M = p.N * (p.Do > 0 ? p.Do : 1) * p.Ho * p.Wo;
+    const int gy = (p.Cout + BN - 1) / BN;
+    const int T = ((M + BM - 1) / BM) * gy;
+    const int S = p.splitk > 1 ? p.splitk : 1;
+    const int nb = gridDim.x;
+    const int full = S > 1 ? (S * T - nb) / (S - 1) : T;
+    const int bid = blockIdx.x;
+    if (bid < full) {
+      const int q = full >> 3, r = full & 7, xcd = bid & 7;
+      const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+      bx = lin / gy;
+      by = lin - bx * gy;
+      conv_tile<BM, BN, WM, WN, MODE, PROJ>(p, smem, bx, by, 0, nk_all, 1, 0, 0, 0, 0, 0);
+    } else {
+      const int b2 = bid - full, t = b2 / S, z = b2 - t * S;
+      bx = (full + t) / gy;
+      by = full + t - bx * gy;
+      const int kt0 = (int)((long)z * nk_all / S);
+      const int nk = (int)((long)(z + 1) * nk_all / S) - kt0;
+      conv_tile<BM, BN, WM, WN, MODE, PROJ>(p, smem, bx, by, kt0, nk, S, z, t * S, t, 0, 0);
+    }
+    return;
+  }
   if constexpr (is_glds(MODE) || MODE == kWide) {
     const int nwg = gridDim.x * gridDim.y;
     const int bid = blockIdx.y * gridDim.x + blockIdx.x;
@@ -1558,6 +1833,44 @@ int launch_wide(const SaConvArgs* a, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+// kPing launcher (8 waves, 1 block per CU, never split): uniform-k gather.  Returns 1 when the shape does not
+// qualify.
+int device_cus();
+
+template <int BM, int BN, int MODE = kPing>
+int launch_ping(const SaConvArgs* a, hipStream_t stream) {
+  // (the projection epilogue's row reduce-scatter covers at most 16 channel chunks: BN <= 128)
+  if (!glds3_eligible(a) || a->splitk > 1 || a->splitk < 0 || (BN > 128 && a->epi == SA_EPI_PROJ)) return 1;
+  const int M = a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
+  const int gx = (M + BM - 1) / BM, gy = (a->Cout + BN - 1) / BN;
+  const long T = (long)gx * gy;
+  // splitk 0 (auto): split the tiles of the last, partial round over the CUs (all tiles when T < CUs);
+  // splitk 1: whole tiles only
+  using C = ConvCfg<BM, BN, 2, 4, MODE>;
+  const int nk = a->Kpad / C::BK;
+  const int cus = device_cus();
+  const long rem = T % cus;
+  int S = 1;
+  if (a->splitk == 0 && a->ws && a->counters && !a->stats && rem > 0 && 2 * rem <= cus) {
+    S = (int)(cus / rem);
+    if (S > 4) S = 4;
+    while (S > 1 && ((long)S * rem * BM * BN > a->ws_floats || rem > a->n_counters || nk / S < 2 * C::NSTAGE)) --S;
+  }
+  SaConvArgs b = *a;
+  b.splitk = S;
+  const long nb = S > 1 ? T - rem + S * rem : T;
+  note_split(S, S > 1 ? rem : 0, BM * BN);
+  if constexpr (BN <= 128) {
+    if (a->epi == SA_EPI_PROJ)
+      hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 2, 4, MODE, true>), dim3((unsigned)nb), dim3(512), 0, stream, b);
+    else
+      hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 2, 4, MODE, false>), dim3((unsigned)nb), dim3(512), 0, stream, b);
+  } else {
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 2, 4, MODE, false>), dim3((unsigned)nb), dim3(512), 0, stream, b);
+  }
+  return (int)hipGetLastError();
+}
+
 // the uniform-k DMA kernels need every source a multiple of 64 channels, K unpadded, <= 64 taps
 bool glds3_eligible(const SaConvArgs* a) {
   const int taps = (a->KD > 0 ? a->KD : 1) * a->KH * a->KW;
@@ -1591,8 +1904,8 @@ int pick_cfg(const SaConvArgs* a) {
 
 int cfg_bn(int cfg) {
   switch (cfg) {
-    case 10: case 12: return 256;
-    case 0: case 4: case 6: case 7: case 11: case 13: case 15: return 128;
+    case 10: case 12: case 18: case 20: return 256;
+    case 0: case 4: case 6: case 7: case 11: case 13: case 15: case 19: case 21: return 128;
     case 1: case 3: case 5: case 8: case 9: case 14: case 16: case 17: return 64;
     case 2: return 16;
     default: return 0;
@@ -1660,6 +1973,15 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
                   : cfg == 11 ? launch_wide<512, 128, 4, 2>(a, stream)
                   : cfg == 12 ? launch_wide<256, 256, 2, 2>(a, stream)
                               : launch_wide<512, 128, 4, 1>(a, stream);
+      return r == 1 ? -5 : r;
+    }
+    case 18: case 19: case 20: case 21: {
+      // 8-wave ping-pong: 256x256 (4-deep ring) / 256x128 (6-deep ring); 18 / 19 issue the DMA in the read
+      // slot (kPing), 20 / 21 between the MFMAs of the compute slot (kPingM)
+      const int r = cfg == 18   ? launch_ping<256, 256>(a, stream)
+                    : cfg == 19 ? launch_ping<256, 128>(a, stream)
+                    : cfg == 20 ? launch_ping<256, 256, kPingM>(a, stream)
+                                : launch_ping<256, 128, kPingM>(a, stream);
       return r == 1 ? -5 : r;
     }
     default: return -3;

@@ -688,16 +688,20 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
   PlanEntry best{-1, 1, 1e30f};
   const bool can_split = a.ws && a.counters && !a.stats;
   // (cfgs 12 / 13, the 4-wave wide tiles, lose everywhere on MI355X (tools/conv_bench.py): not timed;
-  // 14-17 are the deep DMA rings)
-  for (int cfg = 0; cfg <= 17; ++cfg) {
+  // 14-17 are the deep DMA rings, 18 / 19 the 8-wave ping-pong tiles)
+  for (int cfg = 0; cfg <= 21; ++cfg) {
     if (cfg == 12 || cfg == 13) continue;
     if (cfg == 2 && a.Cout > 32) continue;  // 256x16 tile: narrow outputs only
     if (cfg == 6) continue;                 // 128x128 / 4 waves: never competitive (conv_bench)
     // wide tiles (one block per CU, never split): only where their grid still covers the chip
     if ((cfg == 10 || cfg == 12) && (a.Cout <= 128 || ((M + 255) / 256) * ((a.Cout + 255) / 256) < 256)) continue;
     if ((cfg == 11 || cfg == 13) && ((M + 511) / 512) * ((a.Cout + 127) / 128) < 256) continue;
+    // ping-pong tiles: 20 / 21 (DMA inside the MFMA slot) measured no better than 18 / 19 and 20 spills: A/B only
+    if (cfg == 20 || cfg == 21) continue;
+    if (cfg == 18 && a.Cout <= 128) continue;
     for (int sk : {1, 0, -1}) {
-      if (sk == 0 && (!can_split || cfg >= 9)) continue;
+      // (ping-pong tiles: splitk 0 = K-split only the tiles of the last, partial round)
+      if (sk == 0 && (!can_split || (cfg >= 9 && cfg < 18))) continue;
       if (sk == -1 && (!can_split || cfg < 4 || cfg > 8)) continue;  // stream-K: DMA-ring family only
       t.tile_cfg = cfg;
       t.splitk = sk;

@@ -148,13 +148,17 @@ def test_conv2d_multisource_concat_and_residual():
     ((128, 128, 128), 128, 3, 1, (24, 32), 1, 3),  # three sources + forced split-K
     ((64,), 128, 7, 1, (12, 12), 1, 1),         # 49 taps
 ])
-@pytest.mark.parametrize("cfg", [4, 10, 11, 12, 13, 14, 15, 16, 17])
+@pytest.mark.parametrize("cfg", [4, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21])
 def test_conv2d_glds3_vs_torch(srcs, cout, k, stride, hw, n, splitk, cfg):
     """8-wave global->LDS DMA kernels: 256x128 (cfg 4: 3-deep LDS ring, counted vmcnt, XCD-ordered
     tiles), the wide tiles 256x256 / 512x128 (cfg 10 / 11: BK 32 4-deep ring, 32x32x16 MFMA,
-    two-band epilogue; never split) and the deep rings (cfg 14-17: 4-8 stages, up to 7 in flight)."""
+    two-band epilogue; never split), the deep rings (cfg 14-17: 4-8 stages, up to 7 in flight) and the 8-wave
+    ping-pong tiles (cfg 18 / 19: 256x256 / 256x128, wave groups offset by one barrier; 20 / 21 with the DMA
+    issued inside the MFMA slot; never split)."""
     if 10 <= cfg <= 13 and splitk != 1:
         pytest.skip("wide tiles are never split")
+    if cfg >= 18 and splitk > 1:
+        splitk = 0  # ping-pong tiles: automatic K split of the last round's tiles (here: every tile)
     O = ops()
     torch.manual_seed(11)
     xs = [torch.randn(n, c, *hw, device=DEV) for c in srcs]
@@ -205,6 +209,29 @@ def test_conv2d_streamk_vs_torch(srcs, cout, k, hw, n, cfg):
     assert int(ws[1].abs().sum()) == 0, "tile counters not reset"
 
 
+@pytest.mark.parametrize("cfg,splitk", [(18, 1), (19, 1), (20, 1), (21, 1), (18, 0), (19, 0)])
+def test_conv2d_ping_pong_full_size_race_screen(cfg, splitk):
+    """Ping-pong tiles at the RAFT-SF batch-8 GRU z/r shape (600 / 1200 tiles, 108 ring stages per tile):
+    matches torch and repeated launches are bitwise identical (a misplaced vmcnt / barrier shows up as rare
+    wrong tiles that differ between launches).  splitk 0: the 88 tiles of cfg 18's partial last round are
+    K-split in two (fixed-order slab reduction)."""
+    O = ops()
+    torch.manual_seed(17)
+    n, h, w = 8, 120, 160
+    xs = [torch.randn(n, 128, h, w, device=DEV) for _ in range(3)]
+    w3 = torch.randn(256, 384, 3, 3, device=DEV) / math.sqrt(384 * 9)
+    ref = F.conv2d(torch.cat([x.half().float() for x in xs], 1), w3.half().float(), padding=1)
+    wp, kpad, _ = O.pack_conv_weight(w3)
+    xh = [nhwc(x).half() for x in xs]
+    ws = O.splitk_workspace(1 << 25, 8192) if splitk == 0 else None
+    outs = []
+    for _ in range(4):
+        outs.append(O.conv2d(xh, wp, kpad, 256, 3, 3, tile_cfg=cfg, splitk=splitk, workspace=ws).clone())
+    torch.cuda.synchronize()
+    assert rel_err(nchw(outs[0]), ref) < 2e-3
+    assert all(torch.equal(o, outs[0]) for o in outs[1:])
+
+
 def test_conv2d_streamk_gru_zr_epilogue():
     """Stream-K with the fused ConvGRU z / r*h epilogue (the RAFT b1 hot conv)."""
     O = ops()
@@ -230,7 +257,7 @@ def test_conv2d_streamk_gru_zr_epilogue():
     assert rel_err(nchw(rhb), r * net.half().float()) < 3e-3
 
 
-@pytest.mark.parametrize("cfg", [4, 10, 11, 12, 13])
+@pytest.mark.parametrize("cfg", [4, 10, 11, 12, 13, 18, 19, 20, 21])
 def test_conv2d_glds3_gru_and_stats_epilogues(cfg):
     O = ops()
     torch.manual_seed(12)
@@ -264,7 +291,7 @@ def test_conv2d_glds3_gru_and_stats_epilogues(cfg):
 
 
 @pytest.mark.parametrize("n,hw,cfg,oc", [(1, (24, 40), -1, 1), (2, (13, 21), 4, 1), (1, (30, 17), 5, 1),
-                                            (1, (9, 11), 0, 1)])
+                                            (1, (9, 11), 0, 1), (2, (13, 21), 19, 1), (1, (30, 17), 21, 1)])
 def test_conv2d_projection_epilogue_flow_head(n, hw, cfg, oc):
     """RAFT flow head fused: conv1 (3x3 128->256, ReLU) with the 3x3 256->oc conv2 projected in its
     epilogue and summed by the stencil == conv2(relu(conv1(x))) (+ the running flow)."""

@@ -32,6 +32,10 @@ SHAPES = {
     "zr32": (1, 30, 40, 256, 256, 3, 0),     # GRU 1/16 z,r at batch 1
     "zr8l": (1, 60, 80, 384, 256, 3, 0),     # GRU 1/8 z,r at batch 1
     "fr8": (16, 480, 640, 64, 64, 3, 1),     # RAFT-SF fnet layer1 at batch 8 (full resolution, both images)
+    # same GEMM as zr8 / q8 but 1x1 over K = 3456 channels: no im2col re-reads (isolates the gather's
+    # cache traffic from the main loop)
+    "zr8g": (8, 120, 160, 3456, 256, 1, 1),
+    "q8g": (8, 120, 160, 3456, 128, 1, 1),
 }
 
 
@@ -42,6 +46,8 @@ def main():
     ap.add_argument("--cfgs", default="-1", help="comma list of tile configs (-1 = launcher's choice, 4 = glds3)")
     ap.add_argument("--splits", default="", help="comma list of split-K modes (0 = auto, 1 = off, >1 forced, -1 = stream-K); "
                     "default: the shape's own setting")
+    ap.add_argument("--gemm-ref", type=int, default=0,
+                    help="also time torch.matmul (hipBLASLt) on the conv's GEMM view [M,K] x [K,N], fp16")
     ap.add_argument("--stats", type=int, default=0, help="fuse instance-norm statistics over N slots (engine: 16)")
     a = ap.parse_args()
     import torch
@@ -55,6 +61,23 @@ def main():
         wp, kpad, _ = O.pack_conv_weight(wt)
         b = torch.zeros(cout, device="cuda")
         out = torch.empty(n, h, w, cout, device="cuda", dtype=torch.float16)
+        if a.gemm_ref:
+            M, K = n * h * w, cin * k * k
+            ga = torch.randn(M, K, device="cuda").half()
+            gb = (torch.randn(K, cout, device="cuda") / K ** 0.5).half()
+            for _ in range(3):
+                torch.matmul(ga, gb)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                torch.matmul(ga, gb)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) / a.iters * 1e3
+            print(f"{name:6s} hipBLASLt matmul M={M:7d} K={K:5d} N={cout:4d}: {us:8.2f} us  "
+                  f"{2.0 * M * K * cout / us / 1e6:7.1f} TFLOP/s", flush=True)
+            del ga, gb
         combos = [(cfg, sp) for cfg in map(int, a.cfgs.split(","))
                   for sp in (map(int, a.splits.split(",")) if a.splits else [sk])]
         for cfg, sk in combos:
