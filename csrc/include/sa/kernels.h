@@ -97,6 +97,9 @@ typedef struct {
   // copy b % slots): atomics of the thousands of blocks of one image no longer pile onto one row of
   // addresses.  sa_stats_reduce() folds the copies into copy 0 before the statistics are read.
   int32_t stats_slots;
+  // real input channels when the single source is zero-padded beyond them (0 = all channels real); lets
+  // the 7x7 stem kernel (tile_cfg 22) stage only the real channels
+  int32_t cin_real;
 } SaConvArgs;
 
 int sa_conv2d(const SaConvArgs* a, hipStream_t stream);
@@ -106,6 +109,17 @@ int sa_conv2d(const SaConvArgs* a, hipStream_t stream);
 int sa_conv3x3_c64_direct(const void* x, int xs, const void* w, int kpad, const float* bias, void* out, int os,
                           int N, int H, int W, int act, float alpha, sa_stat_t* stats, int slots, int max_blocks,
                           hipStream_t stream);
+// 7x7 / pad 3 / stride 1 or 2 stem conv, <= 4 real input channels (pixel stride xs, 8-B aligned) -> 64
+// channels, weights packed [>=64][kpad] with K ordered (kh, kw, ci < cpad); act none / relu / leaky; optional
+// slotted IN statistics.  Also reachable through sa_conv2d with tile_cfg = 22.
+int sa_conv7x7_stem(const void* x, int xs, int creal, const void* w, int kpad, int cpad, const float* bias, void* out,
+                    int os, int N, int H, int W, int stride, int act, float alpha, sa_stat_t* stats, int slots,
+                    hipStream_t stream);
+// Same conv, two waves per SIMD (8-wave workgroups, channel-split stationary weights, register epilogue with
+// buffer stores, optional residual y = act2(act(acc + bias) + res) without statistics); tile_cfg = 23.  -5 when the output span exceeds 32-bit buffer offsets.
+int sa_conv3x3_c64_direct2(const void* x, int xs, const void* w, int kpad, const float* bias, void* out, int os,
+                           int N, int H, int W, int act, float alpha, sa_stat_t* stats, int slots, const void* res,
+                           int rs, int act2, int max_blocks, hipStream_t stream);
 // Number of n-tiles (projection slices) sa_conv2d() will use for these args.
 int sa_conv2d_nslices(const SaConvArgs* a);
 // split-K footprint of the calling thread's last successful sa_conv2d launch: slab floats and tile

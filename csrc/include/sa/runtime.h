@@ -244,7 +244,7 @@ class ConvLayer {
   void upload(DeviceArena& arena, const std::vector<float>& w, const std::vector<float>& b, int cout,
               int cin, const std::vector<ChanSeg>& segs, int kd = 1);
   ConvSpec spec_;
-  int cout_ = 0, cin_pad_ = 0, kpad_ = 0;
+  int cout_ = 0, cin_pad_ = 0, cin_real_ = 0, kpad_ = 0;
   int up_ = 0, cout_real_ = 0;  // transposed-conv parity scatter (2: 2-D, 3: 3-D)
   void* wdev_ = nullptr;
   float* bdev_ = nullptr;

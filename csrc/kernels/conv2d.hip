@@ -1936,18 +1936,40 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
     case 1: return launch_cfg<128, 64, 2, 2>(a, stream);
     case 2: return launch_cfg<256, 16, 4, 1>(a, stream);
     case 3: return launch_cfg<64, 64, 2, 2>(a, stream);
-    case 9: {
+    case 9: case 23: {
       // direct conv: one 64-channel source, 64 outputs, 3x3 / stride 1 / pad 1, plain store epilogue
       const bool ok = a->nsrc == 1 && a->src[0].channels == 64 && a->Cin == 64 && a->Cout == 64 && a->KH == 3 &&
                       a->KW == 3 && a->sh == 1 && a->sw == 1 && a->ph == 1 && a->pw == 1 && a->dh == 1 &&
-                      a->dw == 1 && a->KD <= 0 && a->up == 0 && !a->gate && !a->res && a->epi == SA_EPI_STORE &&
+                      a->dw == 1 && a->KD <= 0 && a->up == 0 && !a->gate && (!a->res || cfg == 23) &&
+                      a->epi == SA_EPI_STORE &&
                       a->Kpad >= 576 && a->out_stride % 8 == 0 && a->src[0].stride % 8 == 0 && a->Ho == a->H &&
                       a->Wo == a->W;
       if (!ok) return -5;
       note_split(1, 0, 0);
+      if (cfg == 23)
+        return a->scale != 1.f ? -5
+                               : sa_conv3x3_c64_direct2(a->src[0].ptr, a->src[0].stride, a->weight, a->Kpad, a->bias,
+                                                        a->out, a->out_stride, a->N, a->H, a->W, a->act, a->alpha,
+                                                        a->stats, a->stats_slots, a->res, a->res_stride, a->act2, 0,
+                                                        stream);
       return sa_conv3x3_c64_direct(a->src[0].ptr, a->src[0].stride, a->weight, a->Kpad, a->bias, a->out,
                                    a->out_stride, a->N, a->H, a->W, a->act, a->alpha, a->stats, a->stats_slots, 0,
                                    stream);
+    }
+    case 22: {
+      // 7x7 stem conv (conv_stem.hip): one <= 4-real-channel source, 64 outputs, pad 3, stride 1 / 2
+      const int cr = a->cin_real > 0 ? a->cin_real : a->Cin;
+      const bool ok = a->nsrc == 1 && a->src[0].channels == a->Cin && cr <= 4 && a->KH == 7 && a->KW == 7 &&
+                      a->sh == a->sw && (a->sh == 1 || a->sh == 2) && a->ph == 3 && a->pw == 3 && a->dh == 1 &&
+                      a->dw == 1 && a->KD <= 0 && a->up == 0 && !a->gate && !a->res && a->epi == SA_EPI_STORE &&
+                      a->scale == 1.f && a->Cout == 64 && a->Kpad >= 49 * a->Cin && a->out_stride % 8 == 0 &&
+                      a->src[0].stride % 4 == 0 &&
+                      (a->act == SA_ACT_NONE || a->act == SA_ACT_RELU || a->act == SA_ACT_LEAKY);
+      if (!ok) return -5;
+      note_split(1, 0, 0);
+      return sa_conv7x7_stem(a->src[0].ptr, a->src[0].stride, cr, a->weight, a->Kpad, a->Cin, a->bias, a->out,
+                             a->out_stride, a->N, a->H, a->W, a->sh, a->act, a->alpha, a->stats, a->stats_slots,
+                             stream);
     }
     case 4: case 5: case 6: case 7: case 8: {
       const int r = cfg == 4 ? launch_glds3<256, 128, 4, 2>(a, stream, true)

@@ -285,6 +285,316 @@ __global__ __launch_bounds__(256) void conv3x3_c64_direct_kernel(const DirectArg
   if (p.stats && stat_img >= 0) flush_stats();
 }
 
+
+// ---------------------------------------------------------------------------------------------------
+// Version 2 (tile_cfg 23): two waves per SIMD.  The ablations of the kernel above on the RAFT-SF b8
+// full-resolution layer (tools/conv_bench.py fr8, SA_DIRECT_ABL; profiles/direct_conv_r02.txt) put its
+// MFMA + LDS-read loop alone at 0.83 PFLOP/s and the whole kernel at 0.40: one wave per SIMD exposes
+// every DMA wait, barrier and the LDS-staged epilogue.  Here
+//   * 8 waves per workgroup, one workgroup per CU: wave w owns 32 pixels (pixel group w & 3 of the
+//     2 x 64 tile) x 32 output channels (half w >> 2), so the stationary weights are 144 VGPRs and two
+//     waves share each SIMD (one computes while the other waits or stores);
+//   * roles swapped (C^T = W * X^T): weights are the MFMA A operand, the staged input pixels the B
+//     operand; the weight rows are permuted so that each lane ends up with 8 consecutive output
+//     channels of one pixel -> one 16-B store per pixel fragment straight from the accumulators;
+//   * stores are buffer stores (out-of-range pixels dropped by the descriptor's range check), so every
+//     wave issues exactly the same vector-memory ops per tile and the counted vmcnt of the DMA ring is
+//     exact (the wait above also counted the epilogue stores as ring pieces);
+//   * LDS chunk swizzle by (pixel >> 1) & 7: the 16 lanes of one ds_read_b128 phase (16 consecutive
+//     pixels, one 16-B chunk each) cover all 64 banks;
+//   * one barrier per tile: DMA of tile t + 3 is issued right after the barrier that also retires the
+//     reads of tile t - 1's buffer.
+constexpr int V2_WAVES = 8;
+constexpr int V2_PIECES = IN_INSTR;                                    // 33 DMA wave-instructions per tile
+constexpr int V2_PER_WAVE = (V2_PIECES + V2_WAVES - 1) / V2_WAVES;     // 5 (waves 1..7: one dummy)
+// LDS layout: NB ring buffers | 1 KB sink for the dummy pieces | 64 fp32 biases | (STATS) per-lane running
+// IN sums [512 lanes][sum 8 | sumsq 8] -- in LDS, not VGPRs: 16 more live registers next to the 144 of the
+// stationary weights made the compiler drop the fragment prefetch (a lgkmcnt(0) after every ds_read)
+template <bool STATS>
+struct V2Lds {
+  static constexpr int NB = STATS ? 3 : 4;  // ring depth (3 leaves room for the statistics)
+  static constexpr int DUMMY = NB * IN_BYTES;
+  static constexpr int BIAS = DUMMY + 1024;
+  static constexpr int ST = BIAS + 256;
+  static constexpr int SMEM = ST + (STATS ? 512 * 64 : 0);
+};
+
+// sum over the 16 lanes of a DPP row (every lane gets the row total)
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
+  return v;
+}
+
+__device__ __forceinline__ int v2_swz(int pp) { return (pp >> 1) & 7; }
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (0..31)
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+#define SA_VM(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    SA_VM(0) SA_VM(1) SA_VM(2) SA_VM(3) SA_VM(4) SA_VM(5) SA_VM(6) SA_VM(7) SA_VM(8) SA_VM(9) SA_VM(10)
+    SA_VM(11) SA_VM(12) SA_VM(13) SA_VM(14) SA_VM(15) SA_VM(16) SA_VM(17) SA_VM(18) SA_VM(19) SA_VM(20)
+#undef SA_VM
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+struct DirectArgs2 {
+  const f16* x;
+  int xs;
+  const f16* w;
+  int kpad;
+  const float* bias;
+  f16* out;
+  int os;
+  unsigned out_bytes;  // buffer-store range of `out`
+  unsigned res_bytes;  // buffer-load range of `res`
+  int N, H, W;
+  float alpha;
+  sa_stat_t* stats;
+  int slots;
+  const f16* res;  // optional residual (RES): y = act2(act(acc + bias) + res)
+  int rs;
+  int act2;
+  int abl;  // profiling only (SA_DIRECT2_ABL): 1 = no per-tile statistics, 2 = no flush, 4 = non-stats kernel with
+            // the statistics variant's 3-deep ring
+};
+
+template <int ACT, bool STATS, bool RES, int NBO = 0>
+__global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const DirectArgs2 p) {
+  using L = V2Lds<STATS>;
+  constexpr int NB = NBO ? NBO : L::NB;
+  __shared__ __attribute__((aligned(16))) char smem[L::SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int frow = lane & 15, kq = lane >> 4;
+  const int tiles_x = (p.W + TC - 1) / TC, tiles_y = (p.H + TR - 1) / TR;
+  const int tiles_img = tiles_x * tiles_y;
+  const int ntiles = p.N * tiles_img;
+  const void* zero = g_zero16d;
+
+  auto issue_tile = [&](int t, int buf) {
+    const int n = t / tiles_img, r = t - n * tiles_img;
+    const int ty = r / tiles_x, tx = r - ty * tiles_x;
+    const int y0 = ty * TR - 1, x0 = tx * TC - 1;
+    char* ib = smem + buf * IN_BYTES;
+    // laundered lane index: keeps the compiler from hoisting the tile-invariant piece decomposition out of
+    // the tile loop into ~20 long-lived VGPRs (which spilled, and a spill reload waits on the whole ring)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int i = 0; i < V2_PER_WAVE; ++i) {
+      const int ins = i * V2_WAVES + wave;
+      const void* src = zero;
+      char* dst = smem + L::DUMMY;
+      if (ins < V2_PIECES) {
+        const int g = ins * 64 + ln;
+        const int pp = g >> 3, s = g & 7;
+        const int q = s ^ v2_swz(pp);
+        const int iy = y0 + pp / IC, ix = x0 + pp % IC;
+        if (g < IN_PIECES && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W)
+          src = p.x + ((size_t)((size_t)n * p.H + iy) * p.W + ix) * p.xs + q * 8;
+        dst = ib + ins * 1024;
+      }
+      __builtin_amdgcn_global_load_lds(src, (lds_void_t*)dst, 16, 0, 0);
+    }
+  };
+
+  // wave roles: pixel group pg (row pg >> 1 of the tile, columns (pg & 1) * 32 .. +32), channel half hc
+  const int pg = wave & 3, hc = wave >> 2;
+  const int prow = pg >> 1, pcol = (pg & 1) * 32;
+  // A fragments: row rr of fragment j = output channel hc*32 + (rr >> 2) * 8 + j * 4 + (rr & 3)
+  half8 wa[KTOT / 32][2];
+#pragma unroll
+  for (int ks = 0; ks < KTOT / 32; ++ks)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int co = hc * 32 + (frow >> 2) * 8 + j * 4 + (frow & 3);
+      wa[ks][j] = *reinterpret_cast<const half8*>(p.w + (size_t)co * p.kpad + ks * 32 + kq * 8);
+    }
+  // this lane's 8 output channels: hc*32 + kq*8 + e, e = 4 j + r
+  const int c0 = hc * 32 + kq * 8;
+  // instance-norm statistics: per-lane running sums of the lane's 8 channels over its pixels, across tiles
+  // of one image; row-reduced with DPP and flushed to the slotted fixed-point atomics when the image changes
+  floatx4* st_lane = reinterpret_cast<floatx4*>(smem + L::ST) + tid * 4;  // [sum 0-3, sum 4-7, sq 0-3, sq 4-7]
+  if constexpr (STATS) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) st_lane[v] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+  int stat_img = -1;
+  auto flush_stats = [&]() {
+    if constexpr (STATS) {
+      float f[16];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const floatx4 x4 = st_lane[v];
+        st_lane[v] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) f[v * 4 + u] = row16_sum(x4[u]);
+      }
+      if (frow == 0 && stat_img >= 0) {
+        sa_stat_t* st = p.stats + (size_t)(blockIdx.x % (p.slots > 1 ? p.slots : 1)) * p.N * 64 * 2;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          unsigned long long* sp = reinterpret_cast<unsigned long long*>(st) + ((size_t)stat_img * 64 + c0 + e) * 2;
+          atomicAdd(sp, (unsigned long long)__double2ll_rn((double)f[e] * SA_STAT_SCALE));
+          atomicAdd(sp + 1, (unsigned long long)__double2ll_rn((double)f[8 + e] * SA_STAT_SCALE));
+        }
+      }
+    }
+  };
+  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(p.out, 0, p.out_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rrsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(p.res), 0, RES ? p.res_bytes : 0, 0x00020000);
+  // biases staged in LDS: an epilogue global load would make the compiler wait for the whole DMA ring
+  // (vmcnt counts in issue order); the first loop barrier publishes them
+  float* bias_lds = reinterpret_cast<float*>(smem + L::BIAS);
+  if (tid < 64) bias_lds[tid] = p.bias ? p.bias[tid] : 0.f;
+
+  const int G = gridDim.x;
+  const int t0 = blockIdx.x;
+  const int kb = t0 < ntiles ? (ntiles - 1 - t0) / G + 1 : 0;  // tiles of this workgroup
+#pragma unroll
+  for (int k = 0; k < NB - 1; ++k)
+    if (k < kb) issue_tile(t0 + k * G, k);
+
+  for (int k = 0; k < kb; ++k) {
+    const int t = t0 + k * G;
+    const int cur = k % NB;
+    // ops this wave issued after tile t's DMA: the ring pieces of tiles k+1, k+2 and the stores of the
+    // (at most 3) tiles computed since
+    const int ahead = (kb - 1 - k) < NB - 2 ? (kb - 1 - k) : NB - 2;
+    constexpr int kOpsPerTile = RES ? 4 : 2;  // buffer stores (+ residual buffer loads), range-checked, never skipped
+    wait_vmcnt(ahead * V2_PER_WAVE + (k < NB - 1 ? k : NB - 1) * kOpsPerTile);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int n = t / tiles_img, rr = t - n * tiles_img;
+    const int ty = rr / tiles_x, tx = rr - ty * tiles_x;
+    const int oy = ty * TR + prow;
+    // residual of this tile's pixels, issued before the next DMA so the epilogue's wait for it leaves the
+    // ring pieces of tile k+3 in flight
+    half8 rv[2];
+    if constexpr (RES) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int ox = tx * TC + pcol + i * 16 + frow;
+        const bool ok = oy < p.H && ox < p.W;
+        const size_t pix = ((size_t)n * p.H + oy) * p.W + ox;
+        const unsigned roff = ok ? (unsigned)(pix * p.rs + c0) * 2u : 0xFFFFFFF0u;
+        typedef unsigned uint4v __attribute__((ext_vector_type(4)));
+        rv[i] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rrsrc, roff, 0, 0));
+      }
+    }
+    // every wave is past tile k-1: its buffer takes tile k+NB-1
+    if (k + NB - 1 < kb) issue_tile(t + (NB - 1) * G, (k + NB - 1) % NB);
+    const char* ib = smem + cur * IN_BYTES;
+
+    floatx4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    auto load = [&](int ks, half8* bf) {
+      const int tap = ks >> 1, kh = tap / 3, kw = tap - kh * 3;
+      const int q = (ks & 1) * 4 + kq;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int pp = (prow + kh) * IC + pcol + i * 16 + frow + kw;
+        bf[i] = *reinterpret_cast<const half8*>(ib + pp * 128 + ((q ^ v2_swz(pp)) << 4));
+      }
+    };
+    half8 b0[2], b1[2];
+    load(0, b0);
+#pragma unroll
+    for (int ks = 0; ks < KTOT / 32; ks += 2) {
+      load(ks + 1, b1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[ks][j], b0[i], acc[i][j], 0, 0, 0);
+      if (ks + 2 < KTOT / 32) load(ks + 2, b0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[ks + 1][j], b1[i], acc[i][j], 0, 0, 0);
+    }
+
+    if constexpr (STATS) {
+      if (n != stat_img) {
+        if (stat_img >= 0 && !(p.abl & 2)) flush_stats();
+        stat_img = n;
+      }
+    }
+    // bias re-read per tile from LDS: 8 VGPRs fewer across the main loop
+    float tsum[8], tsq[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) tsum[e] = tsq[e] = 0.f;
+    float bias8[8];
+    {
+      const floatx4 b0v = *reinterpret_cast<const floatx4*>(bias_lds + c0);
+      const floatx4 b1v = *reinterpret_cast<const floatx4*>(bias_lds + c0 + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bias8[e] = b0v[e], bias8[e + 4] = b1v[e];
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ox = tx * TC + pcol + i * 16 + frow;
+      const bool ok = oy < p.H && ox < p.W;
+      const size_t pix = ((size_t)n * p.H + oy) * p.W + ox;
+      half8 h;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int e = 4 * j + r;
+          float v = act_apply(acc[i][j][r] + bias8[e], ACT, p.alpha);
+          if constexpr (RES) v = p.act2 == SA_ACT_RELU ? fmaxf(v + (float)rv[i][e], 0.f) : v + (float)rv[i][e];
+          h[e] = (f16)v;
+          if constexpr (STATS) {
+            const float vm = ok ? v : 0.f;
+            tsum[e] += vm;
+            tsq[e] = fmaf(vm, vm, tsq[e]);
+          }
+        }
+      const unsigned off = ok ? (unsigned)(pix * p.os + c0) * 2u : 0xFFFFFFF0u;
+      typedef unsigned uint4v __attribute__((ext_vector_type(4)));
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, h), orsrc, off, 0, 0);
+    }
+    if (STATS && !(p.abl & 1)) {
+      st_lane[0] += floatx4{tsum[0], tsum[1], tsum[2], tsum[3]};
+      st_lane[1] += floatx4{tsum[4], tsum[5], tsum[6], tsum[7]};
+      st_lane[2] += floatx4{tsq[0], tsq[1], tsq[2], tsq[3]};
+      st_lane[3] += floatx4{tsq[4], tsq[5], tsq[6], tsq[7]};
+    }
+  }
+  if constexpr (STATS) {
+    if (stat_img >= 0) flush_stats();
+  }
+}
+
+template <bool STATS, bool RES>
+void launch_direct2(const DirectArgs2& a, int act, unsigned g, hipStream_t s) {
+  if (!STATS && !RES && (a.abl & 4)) {
+    hipLaunchKernelGGL((conv3x3_c64_direct2_kernel<SA_ACT_NONE, false, false, 3>), dim3(g), dim3(512), 0, s, a);
+    return;
+  }
+  switch (act) {
+    case SA_ACT_RELU:
+      hipLaunchKernelGGL((conv3x3_c64_direct2_kernel<SA_ACT_RELU, STATS, RES>), dim3(g), dim3(512), 0, s, a);
+      break;
+    case SA_ACT_LEAKY:
+      hipLaunchKernelGGL((conv3x3_c64_direct2_kernel<SA_ACT_LEAKY, STATS, RES>), dim3(g), dim3(512), 0, s, a);
+      break;
+    default:
+      hipLaunchKernelGGL((conv3x3_c64_direct2_kernel<SA_ACT_NONE, STATS, RES>), dim3(g), dim3(512), 0, s, a);
+      break;
+  }
+}
+
 }  // namespace
 
 extern "C" int sa_conv3x3_c64_direct(const void* x, int xs, const void* w, int kpad, const float* bias, void* out,
@@ -298,5 +608,29 @@ extern "C" int sa_conv3x3_c64_direct(const void* x, int xs, const void* w, int k
   if (g > ntiles) g = ntiles;
   if (g < 1) return 0;
   hipLaunchKernelGGL(conv3x3_c64_direct_kernel, dim3((unsigned)g), dim3(256), 0, stream, a);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_conv3x3_c64_direct2(const void* x, int xs, const void* w, int kpad, const float* bias, void* out,
+                                      int os, int N, int H, int W, int act, float alpha, sa_stat_t* stats, int slots,
+                                      const void* res, int rs, int act2, int max_blocks, hipStream_t stream) {
+  if (kpad < KTOT || xs < 64 || os < 64 || xs % 8 || os % 8 ||
+      (act != SA_ACT_NONE && act != SA_ACT_RELU && act != SA_ACT_LEAKY))
+    return -2;
+  if (res && (stats || rs < 64 || rs % 8 || (act2 != SA_ACT_NONE && act2 != SA_ACT_RELU))) return -5;
+  const size_t span = (((size_t)N * H - 1) * W + (W - 1)) * (size_t)os * 2 + 128;  // last pixel's 64 channels
+  const size_t rspan = res ? (((size_t)N * H - 1) * W + (W - 1)) * (size_t)rs * 2 + 128 : 0;
+  if (span >= 0xFFFFFF00ull || rspan >= 0xFFFFFF00ull) return -5;  // 32-bit buffer offsets
+  DirectArgs2 a{(const f16*)x, xs, (const f16*)w, kpad, bias, (f16*)out, os, (unsigned)span, (unsigned)rspan, N, H, W,
+                alpha, stats, slots, (const f16*)res, rs, act2, 0};
+  static const int abl = std::getenv("SA_DIRECT2_ABL") ? std::atoi(std::getenv("SA_DIRECT2_ABL")) : 0;
+  a.abl = abl;
+  const long ntiles = (long)N * ((H + TR - 1) / TR) * ((W + TC - 1) / TC);
+  long g = max_blocks > 0 ? max_blocks : 256;
+  if (g > ntiles) g = ntiles;
+  if (g < 1) return 0;
+  if (stats) launch_direct2<true, false>(a, act, (unsigned)g, stream);
+  else if (res) launch_direct2<false, true>(a, act, (unsigned)g, stream);
+  else launch_direct2<false, false>(a, act, (unsigned)g, stream);
   return (int)hipGetLastError();
 }

@@ -81,23 +81,40 @@ __global__ __launch_bounds__(256) void instnorm_apply_kernel(const SaNormArgs a,
   if (rs) norm8(a.res_stats, n, a.C, c, a.HW, a.eps, rmean, rrstd);
   const long p0 = (long)blockIdx.x * pix_per_block;
   const long p1 = p0 + pix_per_block < a.HW ? p0 + pix_per_block : a.HW;
-  for (long p = p0 + tid / C8; p < p1; p += lanes_per_c) {
-    const long pix = (long)n * a.HW + p;
-    float v[8];
-    ld8(reinterpret_cast<const f16*>(a.x) + pix * a.x_stride + c, v);
+  // 4 pixels per step, every load issued before the first store (out may alias x: the compiler would
+  // otherwise keep one 16-B load in flight per thread)
+  constexpr int U = 4;
+  const f16* xb = reinterpret_cast<const f16*>(a.x);
+  const f16* rb = reinterpret_cast<const f16*>(a.res);
+  f16* ob = reinterpret_cast<f16*>(a.out);
+  for (long pb = p0 + tid / C8; pb < p1; pb += (long)U * lanes_per_c) {
+    half8 hx[U], hr[U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = act_apply((v[j] - mean[j]) * rstd[j], a.act, a.alpha);
-    if (a.res) {
-      float r[8];
-      ld8(reinterpret_cast<const f16*>(a.res) + pix * a.res_stride + c, r);
-      if (rs) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) r[j] = (r[j] - rmean[j]) * rrstd[j];
+    for (int u = 0; u < U; ++u) {
+      const long p = pb + (long)u * lanes_per_c;
+      if (p < p1) {
+        const long pix = (long)n * a.HW + p;
+        hx[u] = *reinterpret_cast<const half8*>(xb + pix * a.x_stride + c);
+        if (rb) hr[u] = *reinterpret_cast<const half8*>(rb + pix * a.res_stride + c);
       }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j] + r[j], a.act2, a.alpha);
     }
-    st8(reinterpret_cast<f16*>(a.out) + pix * a.out_stride + c, v);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long p = pb + (long)u * lanes_per_c;
+      if (p >= p1) break;
+      const long pix = (long)n * a.HW + p;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = act_apply(((float)hx[u][j] - mean[j]) * rstd[j], a.act, a.alpha);
+      if (rb) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float r = rs ? ((float)hr[u][j] - rmean[j]) * rrstd[j] : (float)hr[u][j];
+          v[j] = act_apply(v[j] + r, a.act2, a.alpha);
+        }
+      }
+      st8(ob + pix * a.out_stride + c, v);
+    }
   }
 }
 

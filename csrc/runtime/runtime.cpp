@@ -237,6 +237,7 @@ void ConvLayer::upload(DeviceArena& arena, const std::vector<float>& w, const st
   SA_REQUIRE(real_sum == cin, "conv input segments (%d) != checkpoint Cin (%d)", real_sum, cin);
   cout_ = cout;
   cin_pad_ = pad_sum;
+  cin_real_ = real_sum;
   const int KH = spec_.kh, KW = spec_.kw;
   const int K = KD * KH * KW * cin_pad_;  // ordered (kd, kh, kw, ci)
   kpad_ = round_up(K, 64);  // 64-aligned K enables the DMA-staged BK=64 conv path
@@ -454,6 +455,7 @@ SaConvArgs ConvLayer::args(const std::vector<Tensor>& srcs, const Tensor& out) c
   }
   SA_REQUIRE(cin == cin_pad_, "conv input channels %d != packed %d", cin, cin_pad_);
   a.nsrc = (int)srcs.size();
+  a.cin_real = srcs.size() == 1 && cin_real_ < cin_pad_ ? cin_real_ : 0;
   a.N = srcs[0].n;
   a.H = srcs[0].h;
   a.W = srcs[0].w;
@@ -689,7 +691,7 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
   const bool can_split = a.ws && a.counters && !a.stats;
   // (cfgs 12 / 13, the 4-wave wide tiles, lose everywhere on MI355X (tools/conv_bench.py): not timed;
   // 14-17 are the deep DMA rings, 18 / 19 the 8-wave ping-pong tiles)
-  for (int cfg = 0; cfg <= 21; ++cfg) {
+  for (int cfg = 0; cfg <= 23; ++cfg) {
     if (cfg == 12 || cfg == 13) continue;
     if (cfg == 2 && a.Cout > 32) continue;  // 256x16 tile: narrow outputs only
     if (cfg == 6) continue;                 // 128x128 / 4 waves: never competitive (conv_bench)
@@ -701,7 +703,7 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
     if (cfg == 18 && a.Cout <= 128) continue;
     for (int sk : {1, 0, -1}) {
       // (ping-pong tiles: splitk 0 = K-split only the tiles of the last, partial round)
-      if (sk == 0 && (!can_split || (cfg >= 9 && cfg < 18))) continue;
+      if (sk == 0 && (!can_split || (cfg >= 9 && cfg < 18) || cfg >= 22)) continue;
       if (sk == -1 && (!can_split || cfg < 4 || cfg > 8)) continue;  // stream-K: DMA-ring family only
       t.tile_cfg = cfg;
       t.splitk = sk;

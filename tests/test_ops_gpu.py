@@ -337,11 +337,12 @@ def test_tap_proj_skinny_conv(n, hw, c, xs, oc):
     assert rel_err(out - flow0, ref) < 2e-3
 
 
+@pytest.mark.parametrize("cfg", [9, 23])
 @pytest.mark.parametrize("n,hw,act,stats", [(2, (17, 70), "relu", False), (1, (48, 128), "none", True),
-                                             (3, (5, 9), "leaky", True)])
-def test_conv3x3_c64_direct(n, hw, act, stats):
-    """LDS-resident-weight direct conv (tile_cfg 9): tails in both dims, several images per block,
-    slotted statistics folded to the unsplit sums."""
+                                             (3, (5, 9), "leaky", True), (2, (33, 190), "none", True)])
+def test_conv3x3_c64_direct(n, hw, act, stats, cfg):
+    """Direct 3x3 64 -> 64 conv (tile_cfg 9: one wave per SIMD; 23: two waves per SIMD, buffer-store
+    epilogue): tails in both dims, several images per block, slotted statistics folded to the unsplit sums."""
     O = ops()
     torch.manual_seed(31)
     x = torch.randn(n, 64, *hw, device=DEV)
@@ -354,7 +355,7 @@ def test_conv3x3_c64_direct(n, hw, act, stats):
     if stats:
         st = torch.zeros(16, n, 64, 2, dtype=torch.int64, device=DEV)
         kw = dict(stats=st, stats_slots=16)
-    out = O.conv2d(nhwc(x).half(), wp, kpad, 64, 3, 3, bias=b.contiguous(), act=act, alpha=0.1, tile_cfg=9, **kw)
+    out = O.conv2d(nhwc(x).half(), wp, kpad, 64, 3, 3, bias=b.contiguous(), act=act, alpha=0.1, tile_cfg=cfg, **kw)
     torch.cuda.synchronize()
     assert rel_err(nchw(out), ref) < 2e-3
     if stats:
@@ -363,6 +364,68 @@ def test_conv3x3_c64_direct(n, hw, act, stats):
         y = nchw(out)
         assert rel_err(st[0, ..., 0].double() / 2 ** 24, y.sum((2, 3))) < 1e-3
         assert rel_err(st[0, ..., 1].double() / 2 ** 24, (y * y).sum((2, 3))) < 1e-3
+
+
+@pytest.mark.parametrize("n,hw,stride,act,stats", [(2, (37, 70), 1, "relu", False), (1, (48, 128), 1, "none", True),
+                                                    (3, (9, 5), 1, "leaky", True), (2, (33, 47), 2, "relu", False),
+                                                    (1, (64, 130), 2, "none", True)])
+def test_conv7x7_stem(n, hw, stride, act, stats):
+    """7x7 stem conv (tile_cfg 22) on the encoders' 3-real-of-8-channel input: tails in both dims, several
+    images per block, junk in the padding channels ignored, slotted statistics folded to the unsplit sums."""
+    O = ops()
+    torch.manual_seed(37)
+    x = torch.rand(n, 3, *hw, device=DEV) * 2 - 1
+    xp = torch.zeros(n, *hw, 8, device=DEV, dtype=torch.float16)
+    xp[..., :3] = nhwc(x).half()
+    xp[..., 3:] = 7.0  # never read: only the real channels are staged
+    w = torch.randn(64, 3, 7, 7, device=DEV) / 12
+    b = torch.randn(64, device=DEV) * 0.1
+    ref = F.conv2d(x.half().float(), w.half().float(), b, stride=stride, padding=3)
+    ref = {"relu": F.relu, "none": lambda t: t, "leaky": lambda t: F.leaky_relu(t, 0.1)}[act](ref)
+    wp, kpad, cin_pad = O.pack_conv_weight(w, [(3, 8)])
+    assert cin_pad == 8
+    kw = {}
+    if stats:
+        st = torch.zeros(16, n, 64, 2, dtype=torch.int64, device=DEV)
+        kw = dict(stats=st, stats_slots=16)
+    out = O.conv2d(xp, wp, kpad, 64, 7, 7, bias=b.contiguous(), stride=stride, act=act, alpha=0.1, tile_cfg=22,
+                   cin_real=3, **kw)
+    torch.cuda.synchronize()
+    assert out.shape[1:3] == ref.shape[2:]
+    assert rel_err(nchw(out), ref) < 2e-3
+    # the generic implicit GEMM on the same args agrees (the tuner's first candidate)
+    gen = O.conv2d(xp, wp, kpad, 64, 7, 7, bias=b.contiguous(), stride=stride, act=act, alpha=0.1, tile_cfg=1,
+                   cin_real=3)
+    xp[..., 3:] = 0
+    gen0 = O.conv2d(xp, wp, kpad, 64, 7, 7, bias=b.contiguous(), stride=stride, act=act, alpha=0.1, tile_cfg=1)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(gen0), ref) < 2e-3 and torch.isfinite(gen).all()
+    if stats:
+        O.stats_reduce(st, 16)
+        torch.cuda.synchronize()
+        y = nchw(out)
+        assert rel_err(st[0, ..., 0].double() / 2 ** 24, y.sum((2, 3))) < 1e-3
+        assert rel_err(st[0, ..., 1].double() / 2 ** 24, (y * y).sum((2, 3))) < 1e-3
+
+
+@pytest.mark.parametrize("n,hw,act2", [(2, (17, 70), "relu"), (1, (33, 190), "none")])
+def test_conv3x3_c64_direct2_residual(n, hw, act2):
+    """Direct conv v2 (tile_cfg 23) residual epilogue y = act2(relu(conv + b) + res) (the batch-norm
+    ResidualBlock's second conv), residual read from a channel slice of a wider tensor."""
+    O = ops()
+    torch.manual_seed(33)
+    x = torch.randn(n, 64, *hw, device=DEV)
+    w = torch.randn(64, 64, 3, 3, device=DEV) / 24
+    b = torch.randn(64, device=DEV) * 0.1
+    big = torch.randn(n, *hw, 128, device=DEV).half()
+    res = big[..., 64:]
+    ref = F.relu(F.conv2d(x.half().float(), w.half().float(), b, padding=1)) + nchw(res)
+    ref = F.relu(ref) if act2 == "relu" else ref
+    wp, kpad, _ = O.pack_conv_weight(w)
+    out = O.conv2d(nhwc(x).half(), wp, kpad, 64, 3, 3, bias=b.contiguous(), act="relu", res=res, act2=act2,
+                   tile_cfg=23)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(out), ref) < 2e-3
 
 
 def test_conv2d_padded_channels_and_output_slice():

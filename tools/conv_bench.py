@@ -32,6 +32,10 @@ SHAPES = {
     "zr32": (1, 30, 40, 256, 256, 3, 0),     # GRU 1/16 z,r at batch 1
     "zr8l": (1, 60, 80, 384, 256, 3, 0),     # GRU 1/8 z,r at batch 1
     "fr8": (16, 480, 640, 64, 64, 3, 1),     # RAFT-SF fnet layer1 at batch 8 (full resolution, both images)
+    # 7x7 stems (3 real of 8 padded channels): RAFT-SF fnet conv1 at batch 1 / 8, RAFT-RT stride 2
+    "stem1": (2, 480, 640, 8, 64, 7, 1),
+    "stem8": (16, 480, 640, 8, 64, 7, 1),
+    "stemrt": (2, 480, 640, 8, 64, -7, 1),
     # same GEMM as zr8 / q8 but 1x1 over K = 3456 channels: no im2col re-reads (isolates the gather's
     # cache traffic from the main loop)
     "zr8g": (8, 120, 160, 3456, 256, 1, 1),
@@ -56,11 +60,20 @@ def main():
     ws = O.splitk_workspace(1 << 25, 8192)
     for name in a.shapes.split(","):
         n, h, w, cin, cout, k, sk = SHAPES[name]
+        stride, k = (2, -k) if k < 0 else (1, k)
         x = torch.randn(n, h, w, cin, device="cuda").half()
-        wt = torch.randn(cout, cin, k, k, device="cuda") / (cin * k * k) ** 0.5
-        wp, kpad, _ = O.pack_conv_weight(wt)
+        extra = dict(stride=stride)
+        if k == 7:  # stem: 3 real channels in an 8-channel pixel
+            x[..., 3:] = 0
+            wt = torch.randn(cout, 3, k, k, device="cuda") / (3 * k * k) ** 0.5
+            wp, kpad, _ = O.pack_conv_weight(wt, [(3, 8)])
+            extra["cin_real"] = 3
+        else:
+            wt = torch.randn(cout, cin, k, k, device="cuda") / (cin * k * k) ** 0.5
+            wp, kpad, _ = O.pack_conv_weight(wt)
+        h, w = (h + 2 * (k // 2) - k) // stride + 1, (w + 2 * (k // 2) - k) // stride + 1
         b = torch.zeros(cout, device="cuda")
-        out = torch.empty(n, h, w, cout, device="cuda", dtype=torch.float16)
+        out = torch.empty(n, h, w, cout, device="cuda", dtype=torch.float16)  # output grid
         if a.gemm_ref:
             M, K = n * h * w, cin * k * k
             ga = torch.randn(M, K, device="cuda").half()
@@ -81,7 +94,7 @@ def main():
         combos = [(cfg, sp) for cfg in map(int, a.cfgs.split(","))
                   for sp in (map(int, a.splits.split(",")) if a.splits else [sk])]
         for cfg, sk in combos:
-            kw = dict(bias=b, out=out, splitk=sk, workspace=ws if sk != 1 else None, tile_cfg=cfg)
+            kw = dict(bias=b, out=out, splitk=sk, workspace=ws if sk != 1 else None, tile_cfg=cfg, **extra)
             if a.stats:
                 kw["stats"] = torch.zeros(16, n, cout, 2, dtype=torch.int64, device="cuda")
                 kw["stats_slots"] = a.stats
@@ -100,7 +113,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) / a.iters * 1e3
-            flop = 2.0 * n * h * w * cout * cin * k * k
+            flop = 2.0 * n * h * w * cout * (3 if k == 7 else cin) * k * k
             print(f"{name:6s} cfg {cfg:2d} split {sk} M={n * h * w:7d} K={cin * k * k:5d} N={cout:4d}: {us:8.2f} us  "
                   f"{flop / us / 1e6:7.1f} TFLOP/s", flush=True)
 

@@ -1,0 +1,9 @@
+# encoder kernels (stem / direct v2 / IN apply): op tests, conv bench, then engine timings with fresh plans
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 200 python -u -m pytest tests/test_ops_gpu.py -x -q --timeout 120 --timeout-method thread -k "direct or stem or instnorm or norm" > gpurun_out/enc_tests.log 2>&1; rc=$?; tail -n 3 gpurun_out/enc_tests.log; [ $rc -eq 0 ] || exit 1
+timeout -k 10 200 python -u tools/conv_bench.py --iters 20 --shapes fr8,fnet --cfgs=9,23 --stats 16 > gpurun_out/enc_bench.log 2>&1 && cat gpurun_out/enc_bench.log || exit 1
+for cfg in "raftstereo-sceneflow 8 10" "raftstereo-sceneflow 1 20" "raftstereo-realtime 1 20"; do set -- $cfg
+  SA_PLAN_CACHE=gpurun_out/plan_${1}_b$2.txt timeout -k 10 200 python -u tools/run_engine.py --model $1 --batch $2 --frames $3 2>&1 | grep -v amdgpu.ids | tail -n 2 || exit 1
+done
