@@ -316,7 +316,8 @@ struct V2Lds {
   static constexpr int DUMMY = NB * IN_BYTES;
   static constexpr int BIAS = DUMMY + 1024;
   static constexpr int ST = BIAS + 256;
-  static constexpr int SMEM = ST + (STATS ? 512 * 64 : 0);
+  static constexpr int RED = ST + (STATS ? 512 * 64 : 0);  // flush: [8 waves][4 kq][16] wave totals
+  static constexpr int SMEM = RED + (STATS ? 8 * 4 * 16 * 4 : 0);
 };
 
 // sum over the 16 lanes of a DPP row (every lane gets the row total)
@@ -434,7 +435,18 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const Direc
 #pragma unroll
         for (int u = 0; u < 4; ++u) f[v * 4 + u] = row16_sum(x4[u]);
       }
-      if (frow == 0 && stat_img >= 0) {
+      // the four waves of a channel half (pixel groups 0..3) are summed in LDS in a fixed order: a quarter of
+      // the atomics (block-uniform: every wave flushes at the same tile)
+      float* red = reinterpret_cast<float*>(smem + L::RED);
+      if (frow == 0)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) red[(wave * 4 + kq) * 16 + e] = f[e];
+      lds_barrier();
+      if (pg == 0 && frow == 0 && stat_img >= 0) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+          f[e] = red[((wave + 0) * 4 + kq) * 16 + e] + red[((wave + 1) * 4 + kq) * 16 + e] +
+                 red[((wave + 2) * 4 + kq) * 16 + e] + red[((wave + 3) * 4 + kq) * 16 + e];
         sa_stat_t* st = p.stats + (size_t)(blockIdx.x % (p.slots > 1 ? p.slots : 1)) * p.N * 64 * 2;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -453,15 +465,20 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const Direc
   float* bias_lds = reinterpret_cast<float*>(smem + L::BIAS);
   if (tid < 64) bias_lds[tid] = p.bias ? p.bias[tid] : 0.f;
 
+  // each workgroup walks a contiguous run of tiles (row-major within an image): an image boundary is crossed
+  // at most once or twice per workgroup, so the statistics flushes (whose atomics, when every workgroup
+  // crossed images in lockstep under a grid stride, cost 150 us of 800 at RAFT-SF b8) are rare and spread out,
+  // and vertically adjacent tiles (10 apart) reuse their halo rows from the same XCD's L2
   const int G = gridDim.x;
-  const int t0 = blockIdx.x;
-  const int kb = t0 < ntiles ? (ntiles - 1 - t0) / G + 1 : 0;  // tiles of this workgroup
+  const int per = (ntiles + G - 1) / G;
+  const int t0 = blockIdx.x * per;
+  const int kb = t0 < ntiles ? (ntiles - t0 < per ? ntiles - t0 : per) : 0;  // tiles of this workgroup
 #pragma unroll
   for (int k = 0; k < NB - 1; ++k)
-    if (k < kb) issue_tile(t0 + k * G, k);
+    if (k < kb) issue_tile(t0 + k, k);
 
   for (int k = 0; k < kb; ++k) {
-    const int t = t0 + k * G;
+    const int t = t0 + k;
     const int cur = k % NB;
     // ops this wave issued after tile t's DMA: the ring pieces of tiles k+1, k+2 and the stores of the
     // (at most 3) tiles computed since
@@ -488,7 +505,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const Direc
       }
     }
     // every wave is past tile k-1: its buffer takes tile k+NB-1
-    if (k + NB - 1 < kb) issue_tile(t + (NB - 1) * G, (k + NB - 1) % NB);
+    if (k + NB - 1 < kb) issue_tile(t + NB - 1, (k + NB - 1) % NB);
     const char* ib = smem + cur * IN_BYTES;
 
     floatx4 acc[2][2];

@@ -80,6 +80,7 @@ template <int S, int ACT, bool STATS>
 __global__ __launch_bounds__(256, 2) void conv7x7_stem_kernel(const StemArgs p) {
   using G = StemGeom<S>;
   __shared__ __attribute__((aligned(16))) half4 tile[G::PIX];
+  __shared__ float red[STATS ? 4 * 64 * 2 : 1];  // flush: per-wave channel totals [wave][64][sum, sumsq]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int frow = lane & 15, kq = lane >> 4;
@@ -124,16 +125,26 @@ __global__ __launch_bounds__(256, 2) void conv7x7_stem_kernel(const StemArgs p) 
           ssum[e] += __shfl_xor(ssum[e], off);
           ssq[e] += __shfl_xor(ssq[e], off);
         }
-      if (frow == 0 && stat_img >= 0) {
-        sa_stat_t* st = p.stats + (size_t)(blockIdx.x % (p.slots > 1 ? p.slots : 1)) * p.N * 64 * 2;
+      // the 4 waves' totals summed in LDS in a fixed order, then one wave issues the atomics (a quarter of
+      // them; the flush is block-uniform)
+      if (frow == 0)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          unsigned long long* sp =
-              reinterpret_cast<unsigned long long*>(st) + ((size_t)stat_img * 64 + kq * 16 + e) * 2;
-          atomicAdd(sp, (unsigned long long)__double2ll_rn((double)ssum[e] * SA_STAT_SCALE));
-          atomicAdd(sp + 1, (unsigned long long)__double2ll_rn((double)ssq[e] * SA_STAT_SCALE));
+          red[(wave * 64 + kq * 16 + e) * 2] = ssum[e];
+          red[(wave * 64 + kq * 16 + e) * 2 + 1] = ssq[e];
         }
+      __syncthreads();
+      if (wave == 0 && stat_img >= 0) {
+        sa_stat_t* st = p.stats + (size_t)(blockIdx.x % (p.slots > 1 ? p.slots : 1)) * p.N * 64 * 2;
+        const int c = lane;  // one channel per lane
+        float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) a0 += red[(w * 64 + c) * 2], a1 += red[(w * 64 + c) * 2 + 1];
+        unsigned long long* sp = reinterpret_cast<unsigned long long*>(st) + ((size_t)stat_img * 64 + c) * 2;
+        atomicAdd(sp, (unsigned long long)__double2ll_rn((double)a0 * SA_STAT_SCALE));
+        atomicAdd(sp + 1, (unsigned long long)__double2ll_rn((double)a1 * SA_STAT_SCALE));
       }
+      __syncthreads();
 #pragma unroll
       for (int e = 0; e < 16; ++e) ssum[e] = ssq[e] = 0.f;
     }
@@ -160,17 +171,21 @@ __global__ __launch_bounds__(256, 2) void conv7x7_stem_kernel(const StemArgs p) 
     }
   };
 
-  const int Gd = gridDim.x;
-  int t = blockIdx.x;
-  if (t < ntiles) fetch(t);
-  for (; t < ntiles; t += Gd) {
+  // contiguous run of tiles per workgroup: image boundaries (statistics flushes) are crossed once or twice
+  // per workgroup instead of in lockstep by all of them
+  const int per = (ntiles + gridDim.x - 1) / gridDim.x;
+  const int tb = blockIdx.x * per;
+  const int te = tb + per < ntiles ? tb + per : ntiles;
+  int t = tb;
+  if (t < te) fetch(t);
+  for (; t < te; ++t) {
 #pragma unroll
     for (int i = 0; i < G::PER_THREAD; ++i) {
       const int q = tid + 256 * i;
       if (q < G::PIX) tile[q] = pre[i];
     }
     __syncthreads();
-    if (t + Gd < ntiles) fetch(t + Gd);  // next tile's pixels in flight under the MFMAs
+    if (t + 1 < te) fetch(t + 1);  // next tile's pixels in flight under the MFMAs
 
     floatx4 acc[PF][4];
 #pragma unroll
