@@ -10,6 +10,7 @@
 #include <string>
 #include <vector>
 
+#include "sa/hostcopy.h"
 #include "sa/runtime.h"
 
 namespace sa {
@@ -153,6 +154,10 @@ class StereoEngine {
   const char* stage_name_[kMaxStages] = {};  // set during the eager conv-tuning forward (branches serialised)
   uint8_t* pin_in_ = nullptr;
   float* pin_out_ = nullptr;
+  // run_host: chunked D2H (one event per chunk) copied out by a small thread pool as the chunks land
+  static constexpr int kCopyEvents = 8;
+  hipEvent_t ev_copy_[kCopyEvents] = {};
+  std::unique_ptr<HostCopyPool> copy_pool_;
   long launches_per_frame_ = 0;
 };
 

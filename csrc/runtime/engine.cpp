@@ -2,6 +2,7 @@
 // graph capture, host-side timed path.
 #include "sa/engine.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -79,6 +80,9 @@ StereoEngine::StereoEngine(const EngineConfig& cfg) : cfg_(cfg) {
 StereoEngine::~StereoEngine() {
   graph_[0].reset();
   graph_[1].reset();
+  copy_pool_.reset();
+  for (auto& e : ev_copy_)
+    if (e) (void)hipEventDestroy(e);
   if (pin_in_) (void)hipHostFree(pin_in_);
   if (pin_out_) (void)hipHostFree(pin_out_);
   if (ev_in_) (void)hipEventDestroy(ev_in_);
@@ -150,6 +154,8 @@ void StereoEngine::init() {
   cloud_ = (float*)arena_.alloc((size_t)B() * H() * W() * 6 * 4);
   HIP_CHECK(hipHostMalloc((void**)&pin_in_, 2 * img, hipHostMallocDefault));
   HIP_CHECK(hipHostMalloc((void**)&pin_out_, (size_t)B() * H() * W() * 7 * 4 + 2 * img, hipHostMallocDefault));
+  for (auto& e : ev_copy_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  copy_pool_ = std::make_unique<HostCopyPool>(3);
   // generous split-K / stream-K workspaces for the tuning pass (128 MiB of fp32 slabs, 8192 tile counters);
   // right-sized to the tuned plan's high-water mark afterwards
   splitk_.alloc(arena_, 32l << 20, 8192);
@@ -403,8 +409,7 @@ void StereoEngine::run_host(uint8_t* left, uint8_t* right, float* disp, float* c
   hipStream_t s = stream_;
   const size_t img = (size_t)B() * H() * W() * 3;
   const size_t n = (size_t)B() * H() * W();
-  std::memcpy(pin_in_, left, img);
-  std::memcpy(pin_in_ + img, right, img);
+  copy_pool_->run({{pin_in_, left, img, nullptr}, {pin_in_ + img, right, img, nullptr}});
   uint8_t* dl = rectify ? raw_left_ : in_left_;
   uint8_t* dr = rectify ? raw_right_ : in_right_;
   HIP_CHECK(hipMemcpyAsync(dl, pin_in_, img, hipMemcpyHostToDevice, s));
@@ -413,19 +418,33 @@ void StereoEngine::run_host(uint8_t* left, uint8_t* right, float* disp, float* c
   float* pd = pin_out_;
   float* pc = pin_out_ + n;
   uint8_t* pr = reinterpret_cast<uint8_t*>(pin_out_ + 7 * n);
-  if (disp) HIP_CHECK(hipMemcpyAsync(pd, disp_, n * 4, hipMemcpyDeviceToHost, s));
-  if (cloud && have_Q_) HIP_CHECK(hipMemcpyAsync(pc, cloud_, n * 24, hipMemcpyDeviceToHost, s));
-  if (rectify) {
-    HIP_CHECK(hipMemcpyAsync(pr, in_left_, img, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipMemcpyAsync(pr + img, in_right_, img, hipMemcpyDeviceToHost, s));
+  // outputs: each D2H piece gets an event; the pool copies a piece into the caller's array once it landed,
+  // overlapping the rest of the transfer
+  std::vector<HostCopyPool::Task> out;
+  int ev = 0;
+  auto d2h = [&](void* dst, void* pinned, const void* dev, size_t bytes) {
+    HIP_CHECK(hipMemcpyAsync(pinned, dev, bytes, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipEventRecord(ev_copy_[ev], s));
+    out.push_back({dst, pinned, bytes, ev_copy_[ev]});
+    ++ev;
+  };
+  if (disp) d2h(disp, pd, disp_, n * 4);
+  if (cloud && have_Q_) {
+    constexpr int kChunks = kCopyEvents - 3;
+    const size_t total = n * 24, step = (total / kChunks + 4095) & ~(size_t)4095;
+    for (size_t o = 0; o < total; o += step) {
+      const size_t b = std::min(step, total - o);
+      d2h(reinterpret_cast<char*>(cloud) + o, reinterpret_cast<char*>(pc) + o, reinterpret_cast<const char*>(cloud_) + o,
+          b);
+    }
   }
-  HIP_CHECK(hipStreamSynchronize(s));
-  if (disp) std::memcpy(disp, pd, n * 4);
-  if (cloud && have_Q_) std::memcpy(cloud, pc, n * 24);
   if (rectify) {  // reference semantics: inputs are overwritten with their rectified versions
-    std::memcpy(left, pr, img);
-    std::memcpy(right, pr + img, img);
+    d2h(left, pr, in_left_, img);
+    d2h(right, pr + img, in_right_, img);
   }
+  SA_REQUIRE(ev <= kCopyEvents, "run_host: %d copy events", ev);
+  copy_pool_->run(out);
+  HIP_CHECK(hipStreamSynchronize(s));
 }
 
 }  // namespace sa
