@@ -1956,6 +1956,20 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
                                    a->out_stride, a->N, a->H, a->W, a->act, a->alpha, a->stats, a->stats_slots, 0,
                                    stream);
     }
+    case 24: {
+      // direct 3x3 96 -> 96 (conv_direct96.hip): one 96-channel source, stride 1 / pad 1, store epilogue with
+      // optional IN statistics or residual
+      const bool ok = a->nsrc == 1 && a->src[0].channels == 96 && a->Cin == 96 && a->Cout == 96 && a->KH == 3 &&
+                      a->KW == 3 && a->sh == 1 && a->sw == 1 && a->ph == 1 && a->pw == 1 && a->dh == 1 &&
+                      a->dw == 1 && a->KD <= 0 && a->up == 0 && !a->gate && a->epi == SA_EPI_STORE &&
+                      a->scale == 1.f && a->Kpad >= 864 && a->out_stride % 4 == 0 && a->src[0].stride % 8 == 0 &&
+                      a->Ho == a->H && a->Wo == a->W;
+      if (!ok) return -5;
+      note_split(1, 0, 0);
+      return sa_conv3x3_c96_direct(a->src[0].ptr, a->src[0].stride, a->weight, a->Kpad, a->bias, a->out,
+                                   a->out_stride, a->N, a->H, a->W, a->act, a->alpha, a->stats, a->stats_slots,
+                                   a->res, a->res_stride, a->act2, stream);
+    }
     case 22: {
       // 7x7 stem conv (conv_stem.hip): one <= 4-real-channel source, 64 outputs, pad 3, stride 1 / 2
       const int cr = a->cin_real > 0 ? a->cin_real : a->Cin;

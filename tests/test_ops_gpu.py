@@ -408,6 +408,41 @@ def test_conv7x7_stem(n, hw, stride, act, stats):
         assert rel_err(st[0, ..., 1].double() / 2 ** 24, (y * y).sum((2, 3))) < 1e-3
 
 
+@pytest.mark.parametrize("n,hw,act,mode", [(2, (17, 70), "relu", "plain"), (1, (48, 128), "none", "stats"),
+                                           (3, (5, 9), "leaky", "stats"), (2, (33, 97), "relu", "res"),
+                                           (1, (30, 66), "none", "res_none")])
+def test_conv3x3_c96_direct(n, hw, act, mode):
+    """Direct 3x3 96 -> 96 conv (tile_cfg 24): tails in both dims, several images per workgroup, slotted
+    statistics folded to the unsplit sums, residual epilogue from a channel slice of a wider tensor."""
+    O = ops()
+    torch.manual_seed(41)
+    x = torch.randn(n, 96, *hw, device=DEV)
+    w = torch.randn(96, 96, 3, 3, device=DEV) / 29
+    b = torch.randn(96, device=DEV) * 0.1
+    ref = F.conv2d(x.half().float(), w.half().float(), b, padding=1)
+    ref = {"relu": F.relu, "none": lambda t: t, "leaky": lambda t: F.leaky_relu(t, 0.1)}[act](ref)
+    wp, kpad, _ = O.pack_conv_weight(w)
+    kw = {}
+    if mode == "stats":
+        st = torch.zeros(16, n, 96, 2, dtype=torch.int64, device=DEV)
+        kw = dict(stats=st, stats_slots=16)
+    if mode.startswith("res"):
+        big = torch.randn(n, *hw, 192, device=DEV).half()
+        res = big[..., 96:]
+        kw = dict(res=res, act2="relu" if mode == "res" else "none")
+        ref = ref + nchw(res)
+        ref = F.relu(ref) if mode == "res" else ref
+    out = O.conv2d(nhwc(x).half(), wp, kpad, 96, 3, 3, bias=b.contiguous(), act=act, alpha=0.1, tile_cfg=24, **kw)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(out), ref) < 2e-3
+    if mode == "stats":
+        O.stats_reduce(st, 16)
+        torch.cuda.synchronize()
+        y = nchw(out)
+        assert rel_err(st[0, ..., 0].double() / 2 ** 24, y.sum((2, 3))) < 1e-3
+        assert rel_err(st[0, ..., 1].double() / 2 ** 24, (y * y).sum((2, 3))) < 1e-3
+
+
 @pytest.mark.parametrize("n,hw,act2", [(2, (17, 70), "relu"), (1, (33, 190), "none")])
 def test_conv3x3_c64_direct2_residual(n, hw, act2):
     """Direct conv v2 (tile_cfg 23) residual epilogue y = act2(relu(conv + b) + res) (the batch-norm

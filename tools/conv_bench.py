@@ -33,6 +33,8 @@ SHAPES = {
     "zr8l": (1, 60, 80, 384, 256, 3, 0),     # GRU 1/8 z,r at batch 1
     "fr8": (16, 480, 640, 64, 64, 3, 1),     # RAFT-SF fnet layer1 at batch 8 (full resolution, both images)
     # 7x7 stems (3 real of 8 padded channels): RAFT-SF fnet conv1 at batch 1 / 8, RAFT-RT stride 2
+    "l2b8": (16, 240, 320, 96, 96, 3, 1),    # RAFT-SF fnet layer2 96 -> 96 at batch 8 (1/2 resolution, both images)
+    "l2b1": (2, 240, 320, 96, 96, 3, 1),
     "stem1": (2, 480, 640, 8, 64, 7, 1),
     "stem8": (16, 480, 640, 8, 64, 7, 1),
     "stemrt": (2, 480, 640, 8, 64, -7, 1),
