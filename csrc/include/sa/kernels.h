@@ -120,12 +120,12 @@ int sa_conv7x7_stem(const void* x, int xs, int creal, const void* w, int kpad, i
 int sa_conv3x3_c64_direct2(const void* x, int xs, const void* w, int kpad, const float* bias, void* out, int os,
                            int N, int H, int W, int act, float alpha, sa_stat_t* stats, int slots, const void* res,
                            int rs, int act2, int max_blocks, hipStream_t stream);
-// Direct 3x3 / stride 1 / pad 1 conv, 96 -> 96 channels (12-wave persistent tiles, weights stationary in
-// registers, DMA ring); act none / relu / leaky, optional slotted IN statistics or residual (not both);
-// tile_cfg = 24.  -5 when the output span exceeds 32-bit buffer offsets.
-int sa_conv3x3_c96_direct(const void* x, int xs, const void* w, int kpad, const float* bias, void* out, int os,
-                          int N, int H, int W, int act, float alpha, sa_stat_t* stats, int slots, const void* res,
-                          int rs, int act2, hipStream_t stream);
+// Direct 3x3 / pad 1 conv to 96 channels: 96 -> 96 at stride 1 or 64 -> 96 at stride 2 (12-wave persistent
+// tiles, weights stationary in registers, DMA ring); act none / relu / leaky, optional slotted IN statistics or
+// residual (not both); tile_cfg = 24.  -5 for other shapes or an output span past 32-bit buffer offsets.
+int sa_conv3x3_c96_direct(const void* x, int xs, int cin, int stride, const void* w, int kpad, const float* bias,
+                          void* out, int os, int N, int H, int W, int act, float alpha, sa_stat_t* stats, int slots,
+                          const void* res, int rs, int act2, hipStream_t stream);
 // Number of n-tiles (projection slices) sa_conv2d() will use for these args.
 int sa_conv2d_nslices(const SaConvArgs* a);
 // split-K footprint of the calling thread's last successful sa_conv2d launch: slab floats and tile

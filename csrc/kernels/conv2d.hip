@@ -1957,16 +1957,17 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
                                    stream);
     }
     case 24: {
-      // direct 3x3 96 -> 96 (conv_direct96.hip): one 96-channel source, stride 1 / pad 1, store epilogue with
-      // optional IN statistics or residual
-      const bool ok = a->nsrc == 1 && a->src[0].channels == 96 && a->Cin == 96 && a->Cout == 96 && a->KH == 3 &&
-                      a->KW == 3 && a->sh == 1 && a->sw == 1 && a->ph == 1 && a->pw == 1 && a->dh == 1 &&
-                      a->dw == 1 && a->KD <= 0 && a->up == 0 && !a->gate && a->epi == SA_EPI_STORE &&
-                      a->scale == 1.f && a->Kpad >= 864 && a->out_stride % 4 == 0 && a->src[0].stride % 8 == 0 &&
-                      a->Ho == a->H && a->Wo == a->W;
+      // direct 3x3 -> 96 (conv_direct96.hip): one 96-channel source at stride 1 or a 64-channel one at stride 2,
+      // pad 1, store epilogue with optional IN statistics or residual
+      const bool shape = (a->Cin == 96 && a->sh == 1 && a->Ho == a->H && a->Wo == a->W) ||
+                         (a->Cin == 64 && a->sh == 2 && a->Ho == (a->H - 1) / 2 + 1 && a->Wo == (a->W - 1) / 2 + 1);
+      const bool ok = shape && a->nsrc == 1 && a->src[0].channels == a->Cin && a->Cout == 96 && a->KH == 3 &&
+                      a->KW == 3 && a->sw == a->sh && a->ph == 1 && a->pw == 1 && a->dh == 1 && a->dw == 1 &&
+                      a->KD <= 0 && a->up == 0 && !a->gate && a->epi == SA_EPI_STORE && a->scale == 1.f &&
+                      a->Kpad >= 9 * a->Cin && a->out_stride % 4 == 0 && a->src[0].stride % 8 == 0;
       if (!ok) return -5;
       note_split(1, 0, 0);
-      return sa_conv3x3_c96_direct(a->src[0].ptr, a->src[0].stride, a->weight, a->Kpad, a->bias, a->out,
+      return sa_conv3x3_c96_direct(a->src[0].ptr, a->src[0].stride, a->Cin, a->sh, a->weight, a->Kpad, a->bias, a->out,
                                    a->out_stride, a->N, a->H, a->W, a->act, a->alpha, a->stats, a->stats_slots,
                                    a->res, a->res_stride, a->act2, stream);
     }

@@ -1,5 +1,5 @@
-// Direct 3x3 convolution, 96 -> 96 channels, stride 1, pad 1 (tile_cfg 24): the 1/2-resolution layer2 convs of
-// the RAFT-Stereo / CREStereo encoders (three per trunk).  The implicit GEMM runs them at ~0.3 PFLOP/s at
+// Direct 3x3 convolution to 96 channels, pad 1 (tile_cfg 24): 96 -> 96 at stride 1, the 1/2-resolution layer2
+// convs of the RAFT-Stereo / CREStereo encoders (three per trunk), and 64 -> 96 at stride 2 (layer2.0.conv1).  The implicit GEMM runs them at ~0.3 PFLOP/s at
 // RAFT-SF b8 (682 us per call, profiles/r02_sf_b8_serial_kernels.txt): K = 864 is only 14 64-deep k-steps per
 // tile epilogue and N = 96 leaves a quarter of every 128-wide tile idle.  Same scheme as the 64-channel direct
 // conv v2 (conv_direct.hip):
@@ -31,29 +31,37 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef unsigned uint2v __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-constexpr int C = 96;                          // channels in and out
+constexpr int C = 96;                          // output channels
 constexpr int TR = 2, TC = 32;                 // output tile
-constexpr int IR = TR + 2, IC = TC + 2;        // input tile with halo (4 x 34)
-constexpr int PB = C * 2;                      // bytes per staged pixel
-constexpr int CH = C / 8;                      // 16-B chunks per pixel (12)
-constexpr int PIECES = IR * IC * CH;           // 1632
-constexpr int INSTR = (PIECES + 63) / 64;      // 26 DMA wave-instructions per tile
-constexpr int BUF = INSTR * 1024;              // 26624 B (the last instruction's spare lanes land in the pad)
 constexpr int NW = 12;
-constexpr int PER_WAVE = (INSTR + NW - 1) / NW;  // 3 (36 slots: 10 dummies)
-constexpr int KS = 9 * C / 32;                 // 27 k-steps
 constexpr int PF = TC / 16;                    // 2 pixel fragments per wave
-constexpr int NB = 4;
-constexpr int DUMMY = NB * BUF;
-constexpr int BIAS = DUMMY + 1024;
-constexpr int ST = BIAS + C * 4;               // per-lane IN sums [768][sum 4 | sumsq 4]
-constexpr int RED = ST + NW * 64 * 32;         // flush: [12 waves][4 kq][8]
-constexpr int SMEM = RED + NW * 4 * 8 * 4;
-static_assert(SMEM <= 163840, "LDS budget");
+
+// staged-input geometry for CIN input channels at stride S (96 / 1: the layer2 convs; 64 / 2: layer2.0.conv1)
+template <int CIN, int S>
+struct Geo {
+  static constexpr int IR = (TR - 1) * S + 3, IC = (TC - 1) * S + 3;  // input tile with halo (4 x 34 / 5 x 65)
+  static constexpr int PB = CIN * 2;                                  // bytes per staged pixel
+  static constexpr int CH = CIN / 8;                                  // 16-B chunks per pixel
+  static constexpr int PIECES = IR * IC * CH;                         // 1632 / 2600
+  static constexpr int INSTR = (PIECES + 63) / 64;                    // DMA wave-instructions per tile (26 / 41)
+  static constexpr int BUF = INSTR * 1024;                            // the last instruction's spare lanes: pad
+  static constexpr int PER_WAVE = (INSTR + NW - 1) / NW;              // 3 / 4
+  static constexpr int KS = 9 * CIN / 32;                             // k-steps (27 / 18)
+  static constexpr int NB = S == 1 ? 4 : 3;                           // ring depth
+  static constexpr int DUMMY = NB * BUF;
+  static constexpr int BIAS = DUMMY + 1024;
+  static constexpr int ST = BIAS + C * 4;                             // per-lane IN sums [768][sum 4 | sumsq 4]
+  static constexpr int RED = ST + NW * 64 * 32;                       // flush: [12 waves][4 kq][8]
+  static constexpr int SMEM = RED + NW * 4 * 8 * 4;
+  static_assert(SMEM <= 163840, "LDS budget");
+  // 16-B chunk swizzle.  96 channels (12 chunks, 192-B rows), stride 1: c ^ ((pixel >> 2) & 3) keeps a chunk in
+  // its aligned group of 4 and spreads 16 consecutive pixels over all 64 banks.  64 channels (128-B rows),
+  // stride 2: the 16 lanes read every other pixel, c ^ ((pixel >> 1) & 7) leaves a 2-way conflict (8 chunk
+  // slots per half of the banks, 16 lanes)
+  static __device__ __forceinline__ int swz(int pp) { return CIN == 96 ? (pp >> 2) & 3 : (pp >> 1) & 7; }
+};
 
 __device__ __attribute__((aligned(16))) const unsigned char g_zero16c[64] = {0};
-
-__device__ __forceinline__ int swz(int pp) { return (pp >> 2) & 3; }
 
 __device__ __forceinline__ float act_apply(float v, int act, float alpha) {
   switch (act) {
@@ -91,7 +99,7 @@ struct D96Args {
   f16* out;
   int os;
   unsigned out_bytes, res_bytes;
-  int N, H, W;
+  int N, H, W, Ho, Wo;
   int act;
   float alpha;
   sa_stat_t* stats;
@@ -101,13 +109,17 @@ struct D96Args {
   int act2;
 };
 
-template <bool STATS, bool RES>
+template <int CIN, int S, bool STATS, bool RES>
 __global__ __launch_bounds__(768, 1) void conv3x3_c96_direct_kernel(const D96Args p) {
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  using Gm = Geo<CIN, S>;
+  constexpr int IC = Gm::IC, CH = Gm::CH, PIECES = Gm::PIECES, INSTR = Gm::INSTR, BUF = Gm::BUF;
+  constexpr int PER_WAVE = Gm::PER_WAVE, KS = Gm::KS, NB = Gm::NB, PB = Gm::PB;
+  constexpr int DUMMY = Gm::DUMMY, BIAS = Gm::BIAS, ST = Gm::ST, RED = Gm::RED;
+  __shared__ __attribute__((aligned(16))) char smem[Gm::SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int frow = lane & 15, kq = lane >> 4;
-  const int tiles_x = (p.W + TC - 1) / TC, tiles_y = (p.H + TR - 1) / TR;
+  const int tiles_x = (p.Wo + TC - 1) / TC, tiles_y = (p.Ho + TR - 1) / TR;
   const int tiles_img = tiles_x * tiles_y;
   const int ntiles = p.N * tiles_img;
   const void* zero = g_zero16c;
@@ -115,7 +127,7 @@ __global__ __launch_bounds__(768, 1) void conv3x3_c96_direct_kernel(const D96Arg
   auto issue_tile = [&](int t, int buf) {
     const int n = t / tiles_img, r = t - n * tiles_img;
     const int ty = r / tiles_x, tx = r - ty * tiles_x;
-    const int y0 = ty * TR - 1, x0 = tx * TC - 1;
+    const int y0 = ty * TR * S - 1, x0 = tx * TC * S - 1;
     char* ib = smem + buf * BUF;
     int ln = lane;
     asm volatile("" : "+v"(ln));  // no hoisting of the tile-invariant piece decomposition (see conv_direct.hip)
@@ -126,8 +138,8 @@ __global__ __launch_bounds__(768, 1) void conv3x3_c96_direct_kernel(const D96Arg
       char* dst = smem + DUMMY;
       if (ins < INSTR) {
         const int g = ins * 64 + ln;
-        const int pp = g / CH, s = g - pp * CH;
-        const int q = s ^ swz(pp);
+        const int pp = g / CH, sl = g - pp * CH;
+        const int q = sl ^ Gm::swz(pp);
         const int iy = y0 + pp / IC, ix = x0 + pp % IC;
         if (g < PIECES && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W)
           src = p.x + ((size_t)((size_t)n * p.H + iy) * p.W + ix) * p.xs + q * 8;
@@ -202,13 +214,13 @@ __global__ __launch_bounds__(768, 1) void conv3x3_c96_direct_kernel(const D96Arg
     const int n = t / tiles_img, rr = t - n * tiles_img;
     const int ty = rr / tiles_x, tx = rr - ty * tiles_x;
     const int oy = ty * TR + prow;
-    half4 rv[PF];
+    half4 rv[PF];  // (residual pixels are output pixels)
     if constexpr (RES) {
 #pragma unroll
       for (int i = 0; i < PF; ++i) {
         const int ox = tx * TC + i * 16 + frow;
-        const bool ok = oy < p.H && ox < p.W;
-        const size_t pix = ((size_t)n * p.H + oy) * p.W + ox;
+        const bool ok = oy < p.Ho && ox < p.Wo;
+        const size_t pix = ((size_t)n * p.Ho + oy) * p.Wo + ox;
         const unsigned roff = ok ? (unsigned)(pix * p.rs + c0) * 2u : 0xFFFFFFF0u;
         rv[i] = __builtin_bit_cast(half4, __builtin_amdgcn_raw_buffer_load_b64(rrsrc, roff, 0, 0));
       }
@@ -224,12 +236,13 @@ __global__ __launch_bounds__(768, 1) void conv3x3_c96_direct_kernel(const D96Arg
     int fr = frow, kql = kq;
     asm volatile("" : "+v"(fr), "+v"(kql));
     auto load = [&](int ks, half8* bf) {
-      const int tap = ks / 3, kh = tap / 3, kw = tap - kh * 3;
-      const int q = (ks - tap * 3) * 4 + kql;
+      constexpr int KPT = CIN / 32;  // k-steps per tap
+      const int tap = ks / KPT, kh = tap / 3, kw = tap - kh * 3;
+      const int q = (ks - tap * KPT) * 4 + kql;
 #pragma unroll
       for (int i = 0; i < PF; ++i) {
-        const int pp = (prow + kh) * IC + i * 16 + fr + kw;
-        bf[i] = *reinterpret_cast<const half8*>(ib + pp * PB + ((q ^ swz(pp)) << 4));
+        const int pp = (prow * S + kh) * IC + (i * 16 + fr) * S + kw;
+        bf[i] = *reinterpret_cast<const half8*>(ib + pp * PB + ((q ^ Gm::swz(pp)) << 4));
       }
     };
     // one k-step of fragments in flight under the MFMAs of the previous one; the memory clobber per k-step keeps
@@ -263,8 +276,8 @@ __global__ __launch_bounds__(768, 1) void conv3x3_c96_direct_kernel(const D96Arg
 #pragma unroll
     for (int i = 0; i < PF; ++i) {
       const int ox = tx * TC + i * 16 + frow;
-      const bool ok = oy < p.H && ox < p.W;
-      const size_t pix = ((size_t)n * p.H + oy) * p.W + ox;
+      const bool ok = oy < p.Ho && ox < p.Wo;
+      const size_t pix = ((size_t)n * p.Ho + oy) * p.Wo + ox;
       half4 h;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -292,24 +305,34 @@ __global__ __launch_bounds__(768, 1) void conv3x3_c96_direct_kernel(const D96Arg
 
 }  // namespace
 
-extern "C" int sa_conv3x3_c96_direct(const void* x, int xs, const void* w, int kpad, const float* bias, void* out,
-                                     int os, int N, int H, int W, int act, float alpha, sa_stat_t* stats, int slots,
-                                     const void* res, int rs, int act2, hipStream_t stream) {
-  if (kpad < 9 * C || xs < C || os < C || xs % 8 || os % 4 ||
+extern "C" int sa_conv3x3_c96_direct(const void* x, int xs, int cin, int stride, const void* w, int kpad,
+                                     const float* bias, void* out, int os, int N, int H, int W, int act, float alpha,
+                                     sa_stat_t* stats, int slots, const void* res, int rs, int act2,
+                                     hipStream_t stream) {
+  if (!((cin == 96 && stride == 1) || (cin == 64 && stride == 2))) return -5;
+  if (kpad < 9 * cin || xs < cin || os < C || xs % 8 || os % 4 ||
       (act != SA_ACT_NONE && act != SA_ACT_RELU && act != SA_ACT_LEAKY))
     return -2;
   if (res && (stats || rs < C || rs % 4 || (act2 != SA_ACT_NONE && act2 != SA_ACT_RELU))) return -5;
-  const size_t last = ((size_t)N * H - 1) * W + (W - 1);
+  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  const size_t last = ((size_t)N * Ho - 1) * Wo + (Wo - 1);
   const size_t span = last * (size_t)os * 2 + 2 * C, rspan = res ? last * (size_t)rs * 2 + 2 * C : 0;
   if (span >= 0xFFFFFF00ull || rspan >= 0xFFFFFF00ull) return -5;
-  D96Args a{(const f16*)x, xs, (const f16*)w, kpad, bias, (f16*)out, os, (unsigned)span, (unsigned)rspan, N, H, W, act,
-            alpha, stats, slots, (const f16*)res, rs, act2};
-  const long ntiles = (long)N * ((H + TR - 1) / TR) * ((W + TC - 1) / TC);
+  D96Args a{(const f16*)x, xs, (const f16*)w, kpad, bias, (f16*)out, os, (unsigned)span, (unsigned)rspan, N, H, W, Ho,
+            Wo, act, alpha, stats, slots, (const f16*)res, rs, act2};
+  const long ntiles = (long)N * ((Ho + TR - 1) / TR) * ((Wo + TC - 1) / TC);
   long g = 256;
   if (g > ntiles) g = ntiles;
   if (g < 1) return 0;
-  if (stats) hipLaunchKernelGGL((conv3x3_c96_direct_kernel<true, false>), dim3((unsigned)g), dim3(768), 0, stream, a);
-  else if (res) hipLaunchKernelGGL((conv3x3_c96_direct_kernel<false, true>), dim3((unsigned)g), dim3(768), 0, stream, a);
-  else hipLaunchKernelGGL((conv3x3_c96_direct_kernel<false, false>), dim3((unsigned)g), dim3(768), 0, stream, a);
+  const dim3 grid((unsigned)g), block(768);
+  if (cin == 96) {
+    if (stats) hipLaunchKernelGGL((conv3x3_c96_direct_kernel<96, 1, true, false>), grid, block, 0, stream, a);
+    else if (res) hipLaunchKernelGGL((conv3x3_c96_direct_kernel<96, 1, false, true>), grid, block, 0, stream, a);
+    else hipLaunchKernelGGL((conv3x3_c96_direct_kernel<96, 1, false, false>), grid, block, 0, stream, a);
+  } else {
+    if (stats) hipLaunchKernelGGL((conv3x3_c96_direct_kernel<64, 2, true, false>), grid, block, 0, stream, a);
+    else if (res) hipLaunchKernelGGL((conv3x3_c96_direct_kernel<64, 2, false, true>), grid, block, 0, stream, a);
+    else hipLaunchKernelGGL((conv3x3_c96_direct_kernel<64, 2, false, false>), grid, block, 0, stream, a);
+  }
   return (int)hipGetLastError();
 }

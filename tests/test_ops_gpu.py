@@ -411,15 +411,18 @@ def test_conv7x7_stem(n, hw, stride, act, stats):
 @pytest.mark.parametrize("n,hw,act,mode", [(2, (17, 70), "relu", "plain"), (1, (48, 128), "none", "stats"),
                                            (3, (5, 9), "leaky", "stats"), (2, (33, 97), "relu", "res"),
                                            (1, (30, 66), "none", "res_none")])
-def test_conv3x3_c96_direct(n, hw, act, mode):
-    """Direct 3x3 96 -> 96 conv (tile_cfg 24): tails in both dims, several images per workgroup, slotted
-    statistics folded to the unsplit sums, residual epilogue from a channel slice of a wider tensor."""
+@pytest.mark.parametrize("cin,stride", [(96, 1), (64, 2)])
+def test_conv3x3_c96_direct(n, hw, act, mode, cin, stride):
+    """Direct 3x3 -> 96 conv (tile_cfg 24; 96 -> 96 stride 1, 64 -> 96 stride 2): tails in both dims, several
+    images per workgroup, slotted statistics folded to the unsplit sums, residual epilogue from a channel slice
+    of a wider tensor."""
     O = ops()
     torch.manual_seed(41)
-    x = torch.randn(n, 96, *hw, device=DEV)
-    w = torch.randn(96, 96, 3, 3, device=DEV) / 29
+    x = torch.randn(n, cin, *hw, device=DEV)
+    w = torch.randn(96, cin, 3, 3, device=DEV) / math.sqrt(cin * 9)
     b = torch.randn(96, device=DEV) * 0.1
-    ref = F.conv2d(x.half().float(), w.half().float(), b, padding=1)
+    ref = F.conv2d(x.half().float(), w.half().float(), b, stride=stride, padding=1)
+    hw = tuple(ref.shape[2:])
     ref = {"relu": F.relu, "none": lambda t: t, "leaky": lambda t: F.leaky_relu(t, 0.1)}[act](ref)
     wp, kpad, _ = O.pack_conv_weight(w)
     kw = {}
@@ -432,7 +435,8 @@ def test_conv3x3_c96_direct(n, hw, act, mode):
         kw = dict(res=res, act2="relu" if mode == "res" else "none")
         ref = ref + nchw(res)
         ref = F.relu(ref) if mode == "res" else ref
-    out = O.conv2d(nhwc(x).half(), wp, kpad, 96, 3, 3, bias=b.contiguous(), act=act, alpha=0.1, tile_cfg=24, **kw)
+    out = O.conv2d(nhwc(x).half(), wp, kpad, 96, 3, 3, bias=b.contiguous(), stride=stride, act=act, alpha=0.1,
+                   tile_cfg=24, **kw)
     torch.cuda.synchronize()
     assert rel_err(nchw(out), ref) < 2e-3
     if mode == "stats":

@@ -35,6 +35,8 @@ SHAPES = {
     # 7x7 stems (3 real of 8 padded channels): RAFT-SF fnet conv1 at batch 1 / 8, RAFT-RT stride 2
     "l2b8": (16, 240, 320, 96, 96, 3, 1),    # RAFT-SF fnet layer2 96 -> 96 at batch 8 (1/2 resolution, both images)
     "l2b1": (2, 240, 320, 96, 96, 3, 1),
+    "l2s8": (16, 480, 640, 64, 96, -3, 1),   # layer2.0.conv1 64 -> 96 stride 2 at batch 8
+    "l2s1": (2, 480, 640, 64, 96, -3, 1),
     "stem1": (2, 480, 640, 8, 64, 7, 1),
     "stem8": (16, 480, 640, 8, 64, 7, 1),
     "stemrt": (2, 480, 640, 8, 64, -7, 1),
