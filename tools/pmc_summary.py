@@ -42,6 +42,11 @@ def main():
             # SQ_BUSY_CYCLES counts per SE (32 on MI355X); MFMA busy is per SIMD (1024 SIMDs)
             print(f"  -> MFMA busy / (SQ_BUSY_CYCLES x 1024 / 32): "
                   f"{med['SQ_VALU_MFMA_BUSY_CYCLES'] / (med['SQ_BUSY_CYCLES'] * 1024 / 32):.3f}")
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in med and med.get("GRBM_GUI_ACTIVE", 0) > 0:
+            # GRBM_GUI_ACTIVE is summed over the 8 XCDs: /8 = the dispatch's cycles at the clock it actually held
+            # (MI355X_MICROARCH.md 'DVFS give-back'); MFMA busy cycles are summed over the 1024 SIMDs
+            print(f"  -> MFMA busy fraction at the held clock, busy / (GRBM_GUI_ACTIVE / 8 x 1024): "
+                  f"{med['SQ_VALU_MFMA_BUSY_CYCLES'] / (med['GRBM_GUI_ACTIVE'] / 8 * 1024):.3f}")
     return 0
 
 
