@@ -126,6 +126,12 @@ int sa_conv3x3_c64_direct2(const void* x, int xs, const void* w, int kpad, const
 int sa_conv3x3_c96_direct(const void* x, int xs, int cin, int stride, const void* w, int kpad, const float* bias,
                           void* out, int os, int N, int H, int W, int act, float alpha, sa_stat_t* stats, int slots,
                           const void* res, int rs, int act2, hipStream_t stream);
+// Strided 1x1 conv, 64 -> 96 or 96 -> 128 channels (the encoders' residual downsample), weights in registers,
+// B fragments loaded straight from global memory; act none / relu / leaky, optional slotted IN statistics
+// (needs Ho * Wo % 16 == 0); tile_cfg = 25.  -5 for other shapes.
+int sa_conv1x1_point(const void* x, int xs, int cin, const void* w, int kpad, const float* bias, void* out, int os,
+                     int cout, int N, int H, int W, int stride, int act, float alpha, sa_stat_t* stats, int slots,
+                     hipStream_t stream);
 // Number of n-tiles (projection slices) sa_conv2d() will use for these args.
 int sa_conv2d_nslices(const SaConvArgs* a);
 // split-K footprint of the calling thread's last successful sa_conv2d launch: slab floats and tile

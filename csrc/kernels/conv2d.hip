@@ -1971,6 +1971,19 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
                                    a->out_stride, a->N, a->H, a->W, a->act, a->alpha, a->stats, a->stats_slots,
                                    a->res, a->res_stride, a->act2, stream);
     }
+    case 25: {
+      // strided 1x1 conv (conv_point.hip): 64 -> 96 / 96 -> 128, weights in registers, no LDS
+      const bool ok = a->nsrc == 1 && a->src[0].channels == a->Cin && a->KH == 1 && a->KW == 1 && a->ph == 0 &&
+                      a->pw == 0 && a->sh == a->sw && a->sh >= 1 && a->dh == 1 && a->dw == 1 && a->KD <= 0 &&
+                      a->up == 0 && !a->gate && !a->res && a->epi == SA_EPI_STORE && a->scale == 1.f &&
+                      a->Ho == (a->H - 1) / a->sh + 1 && a->Wo == (a->W - 1) / a->sw + 1 &&
+                      a->out_stride % 8 == 0 && a->src[0].stride % 8 == 0;
+      if (!ok) return -5;
+      note_split(1, 0, 0);
+      return sa_conv1x1_point(a->src[0].ptr, a->src[0].stride, a->Cin, a->weight, a->Kpad, a->bias, a->out,
+                              a->out_stride, a->Cout, a->N, a->H, a->W, a->sh, a->act, a->alpha, a->stats,
+                              a->stats_slots, stream);
+    }
     case 22: {
       // 7x7 stem conv (conv_stem.hip): one <= 4-real-channel source, 64 outputs, pad 3, stride 1 / 2
       const int cr = a->cin_real > 0 ? a->cin_real : a->Cin;

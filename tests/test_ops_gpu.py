@@ -447,6 +447,37 @@ def test_conv3x3_c96_direct(n, hw, act, mode, cin, stride):
         assert rel_err(st[0, ..., 1].double() / 2 ** 24, (y * y).sum((2, 3))) < 1e-3
 
 
+@pytest.mark.parametrize("cin,cout,n,hw,act,stats", [(64, 96, 2, (31, 63), "relu", False),
+                                                     (64, 96, 3, (32, 64), "none", True),
+                                                     (96, 128, 2, (17, 9), "leaky", False),
+                                                     (96, 128, 1, (64, 32), "none", True)])
+def test_conv1x1_point(cin, cout, n, hw, act, stats):
+    """Strided 1x1 conv (tile_cfg 25, the encoders' downsample): odd sizes, images spanning waves, slotted
+    statistics folded to the unsplit sums."""
+    O = ops()
+    torch.manual_seed(43)
+    x = torch.randn(n, cin, *hw, device=DEV)
+    w = torch.randn(cout, cin, 1, 1, device=DEV) / math.sqrt(cin)
+    b = torch.randn(cout, device=DEV) * 0.1
+    ref = F.conv2d(x.half().float(), w.half().float(), b, stride=2)
+    ref = {"relu": F.relu, "none": lambda t: t, "leaky": lambda t: F.leaky_relu(t, 0.1)}[act](ref)
+    wp, kpad, _ = O.pack_conv_weight(w)
+    kw = {}
+    if stats:
+        st = torch.zeros(16, n, cout, 2, dtype=torch.int64, device=DEV)
+        kw = dict(stats=st, stats_slots=16)
+    out = O.conv2d(nhwc(x).half(), wp, kpad, cout, 1, 1, bias=b.contiguous(), stride=2, pad=0, act=act, alpha=0.1,
+                   tile_cfg=25, **kw)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(out), ref) < 2e-3
+    if stats:
+        O.stats_reduce(st, 16)
+        torch.cuda.synchronize()
+        y = nchw(out)
+        assert rel_err(st[0, ..., 0].double() / 2 ** 24, y.sum((2, 3))) < 1e-3
+        assert rel_err(st[0, ..., 1].double() / 2 ** 24, (y * y).sum((2, 3))) < 1e-3
+
+
 @pytest.mark.parametrize("n,hw,act2", [(2, (17, 70), "relu"), (1, (33, 190), "none")])
 def test_conv3x3_c64_direct2_residual(n, hw, act2):
     """Direct conv v2 (tile_cfg 23) residual epilogue y = act2(relu(conv + b) + res) (the batch-norm

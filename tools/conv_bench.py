@@ -37,6 +37,9 @@ SHAPES = {
     "l2b1": (2, 240, 320, 96, 96, 3, 1),
     "l2s8": (16, 480, 640, 64, 96, -3, 1),   # layer2.0.conv1 64 -> 96 stride 2 at batch 8
     "l2s1": (2, 480, 640, 64, 96, -3, 1),
+    "ds8": (16, 480, 640, 64, 96, -1, 1),    # layer2.0.downsample 1x1 stride 2 at batch 8
+    "ds1": (2, 480, 640, 64, 96, -1, 1),
+    "ds38": (16, 240, 320, 96, 128, -1, 1),  # layer3.0.downsample
     "stem1": (2, 480, 640, 8, 64, 7, 1),
     "stem8": (16, 480, 640, 8, 64, 7, 1),
     "stemrt": (2, 480, 640, 8, 64, -7, 1),
