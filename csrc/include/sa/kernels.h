@@ -148,6 +148,11 @@ int sa_proj_stencil(const float* P, int nslices, long plane, int N, int H, int W
 // the fp16 input exactly once (the implicit-GEMM conv re-reads it per tap).  x: fp16, pixel stride xs,
 // C % 32 == 0, C <= 256; w: fp16 [16][C] (ntaps <= 16) or [32][C], taps >= ntaps zero.
 // sa_proj_stencil() then forms the conv (tap index (ky*kw+kx)*oc + o).
+// tap_proj + proj_stencil of a 3x3 C -> 1 conv in one launch (halo-tiled, planes in LDS):
+// flow[n][y][x] += bias[0] + sum_{ky,kx} sum_c y[n][y+ky-1][x+kx-1][c] * w16[ky*3+kx][c] (zero padding);
+// w16 fp16 [16][C] (taps >= 9 zero), C % 32 == 0, C <= 256, flow fp32 [N][H][W].
+int sa_flow_head_tail(const void* y, int ys, int C, const void* w16, const float* bias, float* flow, int N, int H,
+                      int W, hipStream_t stream);
 int sa_tap_proj(const void* x, int xs, long M, int C, const void* w, int ntaps, float* P, long plane,
                 hipStream_t stream);
 

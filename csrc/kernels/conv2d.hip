@@ -2117,6 +2117,81 @@ __global__ __launch_bounds__(256) void tap_proj_kernel(const f16* __restrict__ x
 }
 }  // namespace
 
+namespace {
+// Flow-head tail in one launch: the per-pixel 3x3-tap projections of a C -> 1 conv over a (TH+2) x (TW+2) halo
+// region (MFMA, fp32 planes in LDS; halo pixels outside the image project zero activations, which is exactly the
+// following conv's zero padding), then the 9-tap stencil + bias accumulated into the fp32 flow.  Replaces
+// tap_proj + proj_stencil (two launches and an HBM round trip of the 9 planes) on every GRU iteration's critical
+// path; the halo recompute (2.1x at 2 x 32 tiles, 1.5x at 4 x 64) only re-reads activations.
+template <int TH, int TW>
+__global__ __launch_bounds__(256) void flow_head_tail_kernel(const f16* __restrict__ y, int ys, int C,
+                                                             const f16* __restrict__ w16, const float* __restrict__ bias,
+                                                             float* __restrict__ flow, int N, int H, int W) {
+  constexpr int RH = TH + 2, RW = TW + 2, R = RH * RW, NF = (R + 15) / 16, PS = 9;
+  __shared__ float P[NF * 16 * PS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int frow = lane & 15, kq = lane >> 4;
+  const int tiles_x = (W + TW - 1) / TW, tiles_y = (H + TH - 1) / TH;
+  const int t = blockIdx.x, n = t / (tiles_x * tiles_y), rr = t - n * tiles_x * tiles_y;
+  const int ty = rr / tiles_x, tx = rr - ty * tiles_x;
+  const int y0 = ty * TH - 1, x0 = tx * TW - 1;
+  const int ks = C >> 5;
+  const half8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
+  half8 b[8];  // B = the 16 (9 used) tap rows of the projection, column frow, k = kq*8 .. of each 32-deep step
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    b[k] = k < ks ? *reinterpret_cast<const half8*>(w16 + (size_t)frow * C + k * 32 + kq * 8) : zero8;
+  for (int f = wave; f < NF; f += 4) {
+    const int q = f * 16 + frow;  // halo pixel of this lane's A row
+    const int hy = q / RW, hx = q - hy * RW;
+    const int gy = y0 + hy, gx = x0 + hx;
+    const bool ok = q < R && gy >= 0 && gy < H && gx >= 0 && gx < W;
+    const f16* src = y + ((size_t)((size_t)n * H + (ok ? gy : 0)) * W + (ok ? gx : 0)) * ys + kq * 8;
+    half8 a[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = (ok && k < ks) ? *reinterpret_cast<const half8*>(src + k * 32) : zero8;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (k < ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[k], b[k], acc, 0, 0, 0);
+    // acc[r]: halo pixel f*16 + kq*4 + r, tap frow
+    if (frow < PS)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) P[(f * 16 + kq * 4 + r) * PS + frow] = acc[r];
+  }
+  __syncthreads();
+  const float b0 = bias ? bias[0] : 0.f;
+  for (int o = threadIdx.x; o < TH * TW; o += 256) {
+    const int oy = o / TW, ox = o - oy * TW;
+    const int gy = ty * TH + oy, gx = tx * TW + ox;
+    if (gy >= H || gx >= W) continue;
+    float s = b0;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) s += P[((oy + ky) * RW + ox + kx) * PS + ky * 3 + kx];
+    flow[((size_t)n * H + gy) * W + gx] += s;
+  }
+}
+}  // namespace
+
+extern "C" int sa_flow_head_tail(const void* y, int ys, int C, const void* w16, const float* bias, float* flow, int N,
+                                 int H, int W, hipStream_t stream) {
+  if (C % 32 || C > 256 || C < 32 || ys < C || ys % 8 || N < 1 || H < 1 || W < 1) return -2;
+  const long M = (long)N * H * W;
+  // small frames (batch 1 at 1/4 resolution): 2 x 32 tiles, enough blocks to cover the CUs; else 4 x 64 (less halo)
+  if (M <= 40000) {
+    const long tiles = (long)N * ((H + 1) / 2) * ((W + 31) / 32);
+    hipLaunchKernelGGL((flow_head_tail_kernel<2, 32>), dim3((unsigned)tiles), dim3(256), 0, stream, (const f16*)y, ys,
+                       C, (const f16*)w16, bias, flow, N, H, W);
+  } else {
+    const long tiles = (long)N * ((H + 3) / 4) * ((W + 63) / 64);
+    hipLaunchKernelGGL((flow_head_tail_kernel<4, 64>), dim3((unsigned)tiles), dim3(256), 0, stream, (const f16*)y, ys,
+                       C, (const f16*)w16, bias, flow, N, H, W);
+  }
+  return (int)hipGetLastError();
+}
+
 extern "C" int sa_tap_proj(const void* x, int xs, long M, int C, const void* w, int ntaps, float* P, long plane,
                            hipStream_t stream) {
   if (C % 32 || C > 256 || C < 32 || ntaps < 1 || ntaps > 32 || xs < C || xs % 8 || plane < M || M < 1)

@@ -130,6 +130,8 @@ class RaftStereo : public StereoEngine {
   // activation once per tap.  SA_RAFT_FH2_PROJ=0 restores the implicit GEMM.
   bool fh2_proj_ = !std::getenv("SA_RAFT_FH2_PROJ") || std::atoi(std::getenv("SA_RAFT_FH2_PROJ")) != 0;
   void* fh2_w16_ = nullptr;  // fp16 [16][256], taps 9..15 zero
+  // tap projection + stencil as one halo-tiled launch (sa_flow_head_tail); SA_RAFT_FH_TAIL=0 restores the two
+  bool fh_tail_ = !std::getenv("SA_RAFT_FH_TAIL") || std::atoi(std::getenv("SA_RAFT_FH_TAIL")) != 0;
   float* tap_p_ = nullptr;   // [9][B*h0*w0]
   float* pyr_ = nullptr;
   float* flow_ = nullptr;
@@ -495,8 +497,12 @@ void RaftStereo::forward(hipStream_t s) {
       else fh1_.run(s, {net_[0]}, fh_.slice_c(0, 256), SA_ACT_RELU);
       if (fh2_proj_) {
         const long M = (long)Bn * h0 * w0;
-        check(sa_tap_proj(fh_.ptr, fh_.stride, M, 256, fh2_w16_, 9, tap_p_, M, s), "flow-head taps");
-        check(sa_proj_stencil(tap_p_, 1, M, Bn, h0, w0, 3, 3, 1, proj_b_, flow_, 1, 1, s), "flow-head stencil");
+        if (fh_tail_) {
+          check(sa_flow_head_tail(fh_.ptr, fh_.stride, 256, fh2_w16_, proj_b_, flow_, Bn, h0, w0, s), "flow-head tail");
+        } else {
+          check(sa_tap_proj(fh_.ptr, fh_.stride, M, 256, fh2_w16_, 9, tap_p_, M, s), "flow-head taps");
+          check(sa_proj_stencil(tap_p_, 1, M, Bn, h0, w0, 3, 3, 1, proj_b_, flow_, 1, 1, s), "flow-head stencil");
+        }
       } else {
         SaConvArgs fa = fh2_.args({fh_.slice_c(0, 256)}, Tensor{flow_, Bn, h0, w0, 1, 1, DT::F32});
         fa.epi = SA_EPI_FLOW_ACC;

@@ -72,6 +72,18 @@ def tap_proj(x, w):
     return P
 
 
+def flow_head_tail(y, w, bias, flow):
+    """Fused tap projection + 3x3 stencil of a C -> 1 conv: fp16 NHWC ``y`` [n,h,w,C] (pixel stride may exceed C),
+    ``w`` [9, C] (tap ky*3+kx), fp32 ``flow`` [n,h,w] += bias + conv(y) in place."""
+    n, h, wd, c = y.shape
+    w16 = torch.zeros(16, c, dtype=torch.float16, device=y.device)
+    w16[:9] = w.to(torch.float16)
+    assert flow.dtype == torch.float32 and flow.is_contiguous() and flow.shape == (n, h, wd)
+    N.check(N.dev().sa_flow_head_tail(y.data_ptr(), _pix_stride(y), c, w16.data_ptr(), bias.data_ptr(),
+                                      flow.data_ptr(), n, h, wd, _stream()), "sa_flow_head_tail")
+    return flow
+
+
 def raft_motion_head(pyr_buf, flow, b, h, w1, w2, convc1_w, convc1_b, convf1_w, convf1_b, levels=4, radius=4):
     """Fused lookup + relu(convc1) + relu(convf1 on [flow_x, 0]): returns (cor1, flo1, flowcopy) fp16
     NHWC.  ``convc1_w`` [64, L*(2r+1), 1, 1], ``convf1_w`` [64, 2, 7, 7] (torch layouts)."""

@@ -315,6 +315,24 @@ def test_conv2d_projection_epilogue_flow_head(n, hw, cfg, oc):
     assert rel_err(out - flow0, ref - flow0) < 3e-3
 
 
+@pytest.mark.parametrize("n,hw", [(1, (120, 160)), (8, (120, 160)), (2, (37, 70)), (1, (5, 3))])
+def test_flow_head_tail(n, hw):
+    """Fused tap projection + stencil (one launch, halo-tiled; both tile shapes) == F.conv2d 256 -> 1 in fp32
+    on the same fp16 operands, accumulated into the flow."""
+    O = ops()
+    torch.manual_seed(47)
+    base = torch.randn(n, *hw, 320, device=DEV).half()
+    y = base[..., :256]
+    w2 = torch.randn(1, 256, 3, 3, device=DEV) / 48
+    b2 = torch.randn(1, device=DEV) * 0.1
+    flow0 = torch.randn(n, *hw, device=DEV)
+    flow = flow0.clone()
+    O.flow_head_tail(y, w2[0].permute(1, 2, 0).reshape(9, 256), b2.contiguous(), flow)
+    torch.cuda.synchronize()
+    ref = F.conv2d(y.float().permute(0, 3, 1, 2), w2.half().float(), b2, padding=1)[:, 0]
+    assert rel_err(flow - flow0, ref) < 2e-3
+
+
 @pytest.mark.parametrize("n,hw,c,xs,oc", [(2, (24, 40), 256, 512, 1), (1, (13, 21), 256, 256, 1),
                                             (1, (7, 9), 96, 104, 1), (2, (11, 30), 256, 512, 2)])
 def test_tap_proj_skinny_conv(n, hw, c, xs, oc):
