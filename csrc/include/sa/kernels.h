@@ -100,6 +100,11 @@ typedef struct {
   // real input channels when the single source is zero-padded beyond them (0 = all channels real); lets
   // the 7x7 stem kernel (tile_cfg 22) stage only the real channels
   int32_t cin_real;
+  // input instance norm fused into the conv's input staging (tile_cfg 23 only): the source is the raw previous
+  // conv output and every in-image pixel is replaced by in_act((x - mean) * rstd) before the GEMM, mean / rstd from
+  // in_stats [N][Cin][2] (fixed point, slots already folded), eps 1e-5; padding stays zero
+  const sa_stat_t* in_stats;
+  int32_t in_act;
 } SaConvArgs;
 
 int sa_conv2d(const SaConvArgs* a, hipStream_t stream);
@@ -119,7 +124,8 @@ int sa_conv7x7_stem(const void* x, int xs, int creal, const void* w, int kpad, i
 // buffer stores, optional residual y = act2(act(acc + bias) + res) without statistics); tile_cfg = 23.  -5 when the output span exceeds 32-bit buffer offsets.
 int sa_conv3x3_c64_direct2(const void* x, int xs, const void* w, int kpad, const float* bias, void* out, int os,
                            int N, int H, int W, int act, float alpha, sa_stat_t* stats, int slots, const void* res,
-                           int rs, int act2, int max_blocks, hipStream_t stream);
+                           int rs, int act2, const sa_stat_t* in_stats, int in_act, int max_blocks,
+                           hipStream_t stream);
 // Direct 3x3 / pad 1 conv to 96 channels: 96 -> 96 at stride 1 or 64 -> 96 at stride 2 (12-wave persistent
 // tiles, weights stationary in registers, DMA ring); act none / relu / leaky, optional slotted IN statistics or
 // residual (not both); tile_cfg = 24.  -5 for other shapes or an output span past 32-bit buffer offsets.

@@ -1881,6 +1881,7 @@ bool glds3_eligible(const SaConvArgs* a) {
 
 int pick_cfg(const SaConvArgs* a) {
   if (a->tile_cfg >= 0) return a->tile_cfg;
+  if (a->in_stats) return 23;  // the fused input norm exists in the direct 64-channel conv only
   static const int glds3_mode = [] {  // SA_CONV_GLDS3: 0 = never, 1 = auto (default)
     const char* e = std::getenv("SA_CONV_GLDS3");
     return e ? std::atoi(e) : 1;
@@ -1927,6 +1928,7 @@ extern "C" int sa_conv2d_nslices(const SaConvArgs* a) {
 extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
   if (a->Kpad % 32 != 0 || a->Cin % 8 != 0 || a->nsrc < 1 || a->nsrc > 4) return -2;
   const int cfg = pick_cfg(a);
+  if (a->in_stats && cfg != 23) return -5;
   // the projection epilogue reduces whole rows of an n-tile: every tile must be full
   if (a->epi == SA_EPI_PROJ && (cfg_bn(cfg) == 0 || a->Cout % cfg_bn(cfg) != 0 || !a->proj_w || !a->proj_out ||
                                 a->proj_taps * a->proj_oc > 9 || a->proj_taps * a->proj_oc < 1))
@@ -1950,8 +1952,8 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
         return a->scale != 1.f ? -5
                                : sa_conv3x3_c64_direct2(a->src[0].ptr, a->src[0].stride, a->weight, a->Kpad, a->bias,
                                                         a->out, a->out_stride, a->N, a->H, a->W, a->act, a->alpha,
-                                                        a->stats, a->stats_slots, a->res, a->res_stride, a->act2, 0,
-                                                        stream);
+                                                        a->stats, a->stats_slots, a->res, a->res_stride, a->act2,
+                                                        a->in_stats, a->in_act, 0, stream);
       return sa_conv3x3_c64_direct(a->src[0].ptr, a->src[0].stride, a->weight, a->Kpad, a->bias, a->out,
                                    a->out_stride, a->N, a->H, a->W, a->act, a->alpha, a->stats, a->stats_slots, 0,
                                    stream);

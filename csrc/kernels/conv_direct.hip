@@ -317,7 +317,8 @@ struct V2Lds {
   static constexpr int BIAS = DUMMY + 1024;
   static constexpr int ST = BIAS + 256;
   static constexpr int RED = ST + (STATS ? 512 * 64 : 0);  // flush: [8 waves][4 kq][16] wave totals
-  static constexpr int SMEM = RED + (STATS ? 8 * 4 * 16 * 4 : 0);
+  static constexpr int NRM = RED + (STATS ? 8 * 4 * 16 * 4 : 0);  // fused input norm: fp16 scale[64] | shift[64]
+  static constexpr int SMEM = NRM + 256;
 };
 
 // sum over the 16 lanes of a DPP row (every lane gets the row total)
@@ -361,9 +362,11 @@ struct DirectArgs2 {
   int act2;
   int abl;  // profiling only (SA_DIRECT2_ABL): 1 = no per-tile statistics, 2 = no flush, 4 = non-stats kernel with
             // the statistics variant's 3-deep ring
+  const sa_stat_t* in_stats;  // fused input instance norm (INN): folded fixed-point sums [N][64][2]
+  int in_act;
 };
 
-template <int ACT, bool STATS, bool RES, int NBO = 0>
+template <int ACT, bool STATS, bool RES, int NBO = 0, bool INN = false>
 __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const DirectArgs2 p) {
   using L = V2Lds<STATS>;
   constexpr int NB = NBO ? NBO : L::NB;
@@ -507,18 +510,55 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const Direc
     // every wave is past tile k-1: its buffer takes tile k+NB-1
     if (k + NB - 1 < kb) issue_tile(t + NB - 1, (k + NB - 1) % NB);
     const char* ib = smem + cur * IN_BYTES;
+    if constexpr (INN) {
+      // fused input instance norm: this image's per-channel fp16 scale / shift (same mean / rstd as
+      // instnorm_apply), then every in-image staged pixel x -> act(x * scale + shift) in place (packed fp16
+      // FMA); halo pixels outside the image stay zero, which is the normalised tensor's zero padding
+      _Float16* nrm = reinterpret_cast<_Float16*>(smem + L::NRM);
+      if (tid < 64) {
+        const sa_stat_t* sp = p.in_stats + ((size_t)n * 64 + tid) * 2;
+        const double inv = 1.0 / ((double)p.H * p.W * SA_STAT_SCALE);
+        const double m = (double)sp[0] * inv, var = (double)sp[1] * inv - m * m;
+        const float rstd = rsqrtf((float)(var > 0.0 ? var : 0.0) + 1e-5f);
+        nrm[tid] = (_Float16)rstd;
+        nrm[64 + tid] = (_Float16)(-(float)m * rstd);
+      }
+      lds_barrier();
+      const int y0 = ty * TR - 1, x0 = tx * TC - 1;
+      char* ibw = smem + cur * IN_BYTES;
+      int tl = tid;
+      asm volatile("" : "+v"(tl));  // tile-invariant piece decomposition: recomputed, not held across the loop
+      for (int g = tl; g < IN_PIECES; g += 512) {
+        const int pp = g >> 3, q = (g & 7) ^ v2_swz(pp);
+        const int iy = y0 + pp / IC, ix = x0 + pp % IC;
+        if (iy < 0 || iy >= p.H || ix < 0 || ix >= p.W) continue;
+        half8 v = *reinterpret_cast<const half8*>(ibw + g * 16);
+        const half8 sc = *reinterpret_cast<const half8*>(nrm + q * 8);
+        const half8 sh = *reinterpret_cast<const half8*>(nrm + 64 + q * 8);
+        v = v * sc + sh;
+        if (p.in_act == SA_ACT_RELU) {
+          const half8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+          v = __builtin_elementwise_max(v, z);
+        }
+        *reinterpret_cast<half8*>(ibw + g * 16) = v;
+      }
+      lds_barrier();
+    }
 
     floatx4 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // (fused input norm: its piece loop leaves no room for the 36 hoisted fragment addresses -> recompute per tile)
+    int fr = frow, kql = kq;
+    if constexpr (INN) asm volatile("" : "+v"(fr), "+v"(kql));
     auto load = [&](int ks, half8* bf) {
       const int tap = ks >> 1, kh = tap / 3, kw = tap - kh * 3;
-      const int q = (ks & 1) * 4 + kq;
+      const int q = (ks & 1) * 4 + kql;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const int pp = (prow + kh) * IC + pcol + i * 16 + frow + kw;
+        const int pp = (prow + kh) * IC + pcol + i * 16 + fr + kw;
         bf[i] = *reinterpret_cast<const half8*>(ib + pp * 128 + ((q ^ v2_swz(pp)) << 4));
       }
     };
@@ -595,6 +635,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const Direc
 
 template <bool STATS, bool RES>
 void launch_direct2(const DirectArgs2& a, int act, unsigned g, hipStream_t s) {
+  if (STATS && !RES && a.in_stats) {  // fused input norm: the instance-norm trunk's second block conv only
+    hipLaunchKernelGGL((conv3x3_c64_direct2_kernel<SA_ACT_NONE, true, false, 0, true>), dim3(g), dim3(512), 0, s, a);
+    return;
+  }
   if (!STATS && !RES && (a.abl & 4)) {
     hipLaunchKernelGGL((conv3x3_c64_direct2_kernel<SA_ACT_NONE, false, false, 3>), dim3(g), dim3(512), 0, s, a);
     return;
@@ -630,16 +674,19 @@ extern "C" int sa_conv3x3_c64_direct(const void* x, int xs, const void* w, int k
 
 extern "C" int sa_conv3x3_c64_direct2(const void* x, int xs, const void* w, int kpad, const float* bias, void* out,
                                       int os, int N, int H, int W, int act, float alpha, sa_stat_t* stats, int slots,
-                                      const void* res, int rs, int act2, int max_blocks, hipStream_t stream) {
+                                      const void* res, int rs, int act2, const sa_stat_t* in_stats, int in_act,
+                                      int max_blocks, hipStream_t stream) {
   if (kpad < KTOT || xs < 64 || os < 64 || xs % 8 || os % 8 ||
       (act != SA_ACT_NONE && act != SA_ACT_RELU && act != SA_ACT_LEAKY))
     return -2;
   if (res && (stats || rs < 64 || rs % 8 || (act2 != SA_ACT_NONE && act2 != SA_ACT_RELU))) return -5;
+  // fused input norm: statistics variant with a plain (pre-norm) output only
+  if (in_stats && (!stats || res || act != SA_ACT_NONE || (in_act != SA_ACT_NONE && in_act != SA_ACT_RELU))) return -5;
   const size_t span = (((size_t)N * H - 1) * W + (W - 1)) * (size_t)os * 2 + 128;  // last pixel's 64 channels
   const size_t rspan = res ? (((size_t)N * H - 1) * W + (W - 1)) * (size_t)rs * 2 + 128 : 0;
   if (span >= 0xFFFFFF00ull || rspan >= 0xFFFFFF00ull) return -5;  // 32-bit buffer offsets
   DirectArgs2 a{(const f16*)x, xs, (const f16*)w, kpad, bias, (f16*)out, os, (unsigned)span, (unsigned)rspan, N, H, W,
-                alpha, stats, slots, (const f16*)res, rs, act2, 0};
+                alpha, stats, slots, (const f16*)res, rs, act2, 0, in_stats, in_act};
   static const int abl = std::getenv("SA_DIRECT2_ABL") ? std::atoi(std::getenv("SA_DIRECT2_ABL")) : 0;
   a.abl = abl;
   const long ntiles = (long)N * ((H + TR - 1) / TR) * ((W + TC - 1) / TC);

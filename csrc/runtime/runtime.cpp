@@ -632,6 +632,7 @@ std::string plan_key(const SaConvArgs& a) {
   char buf[512];
   int n = std::snprintf(buf, sizeof(buf), "%s|%d,%d,%d,%d|", g_arch.c_str(), a.N, a.H, a.W, a.Cin);
   for (int i = 0; i < a.nsrc; ++i) n += std::snprintf(buf + n, sizeof(buf) - n, "%d.", a.src[i].channels);
+  if (a.in_stats) n += std::snprintf(buf + n, sizeof(buf) - n, "|i%d", a.in_act);
   std::snprintf(buf + n, sizeof(buf) - n, "|k%dx%dx%d|s%d,%d,%d|p%d,%d,%d|d%d,%d|o%dx%d|D%d,%d|c%d,%d|e%d,%d,%d,%d,%d|w%d",
                 a.KD, a.KH, a.KW, a.sd, a.sh, a.sw, a.pd, a.ph, a.pw, a.dh, a.dw, a.Ho, a.Wo, a.Do, a.Di, a.Cout,
                 a.Kpad, a.epi, (int)(a.stats != nullptr), a.up, (int)(a.gate != nullptr), (int)(a.res != nullptr),

@@ -496,6 +496,36 @@ def test_conv1x1_point(cin, cout, n, hw, act, stats):
         assert rel_err(st[0, ..., 1].double() / 2 ** 24, (y * y).sum((2, 3))) < 1e-3
 
 
+@pytest.mark.parametrize("n,hw", [(2, (17, 70)), (1, (48, 128)), (3, (5, 9))])
+def test_conv3x3_c64_direct2_input_norm(n, hw):
+    """Direct conv v2 with the input instance norm fused into its staging (tile_cfg 23, in_stats): conv2 of the
+    instance-norm ResidualBlock reads conv1's raw output y and its folded statistics; == F.conv2d on
+    relu(instance_norm(y)) with zero padding applied after the norm, and its own output statistics."""
+    O = ops()
+    torch.manual_seed(53)
+    y = (torch.randn(n, 64, *hw, device=DEV) * 2 + 0.7).half()
+    w = torch.randn(64, 64, 3, 3, device=DEV) / 24
+    b = torch.randn(64, device=DEV) * 0.1
+    yf = y.float()
+    mean = yf.mean((2, 3), keepdim=True)
+    var = yf.var((2, 3), unbiased=False, keepdim=True)
+    a = F.relu((yf - mean) / torch.sqrt(var + 1e-5))
+    ref = F.conv2d(a, w.half().float(), b, padding=1)
+    # fixed-point input statistics [n][64][2], folded (slot 0)
+    ist = torch.stack([yf.sum((2, 3)), (yf * yf).sum((2, 3))], -1).double() * 2 ** 24
+    ist = ist.round().to(torch.int64).contiguous()
+    wp, kpad, _ = O.pack_conv_weight(w)
+    st = torch.zeros(16, n, 64, 2, dtype=torch.int64, device=DEV)
+    out = O.conv2d(nhwc(y), wp, kpad, 64, 3, 3, bias=b.contiguous(), act="none", tile_cfg=23, stats=st,
+                   stats_slots=16, in_stats=ist, in_act="relu")
+    torch.cuda.synchronize()
+    assert rel_err(nchw(out), ref) < 5e-3  # the staged input is normalised in packed fp16
+    O.stats_reduce(st, 16)
+    torch.cuda.synchronize()
+    yo = nchw(out)
+    assert rel_err(st[0, ..., 0].double() / 2 ** 24, yo.sum((2, 3))) < 1e-3
+
+
 @pytest.mark.parametrize("n,hw,act2", [(2, (17, 70), "relu"), (1, (33, 190), "none")])
 def test_conv3x3_c64_direct2_residual(n, hw, act2):
     """Direct conv v2 (tile_cfg 23) residual epilogue y = act2(relu(conv + b) + res) (the batch-norm
