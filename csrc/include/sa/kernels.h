@@ -196,6 +196,10 @@ int sa_avgpool_k(const void* x, int x_stride, void* out, int out_stride, int N, 
 int sa_interp_bilinear(const void* x, int x_stride, void* out, int out_stride, int N, int H,
                        int W, int C, int Ho, int Wo, int align_corners, float mul,
                        hipStream_t stream);
+// sa_avgpool3s2 (p*) and sa_interp_bilinear (i*) in one launch (disjoint block ranges; bitwise the same results)
+int sa_pool_interp(const void* px, int pxs, void* pout, int pos, int pN, int pH, int pW, int pC, const void* ix,
+                   int ixs, void* iout, int ios, int iN, int iH, int iW, int iC, int iHo, int iWo, int align_corners,
+                   float mul, hipStream_t stream);
 
 // ---- RAFT-Stereo correlation ----------------------------------------------------------------
 // corr[b,h,w1,w2] = <f1[b,h,w1,:], f2[b,h,w2,:]>/sqrt(C), plus avg-pool pyramid along w2.

@@ -129,12 +129,26 @@ __global__ void stats_reduce_kernel(sa_stat_t* stats, int slots, long count) {
   }
 }
 
-__global__ void avgpool3s2_kernel(const f16* __restrict__ x, int xs, f16* __restrict__ out, int os,
-                                  int N, int H, int W, int C, int Ho, int Wo) {
-  const int C8 = C >> 3;
-  const long total = (long)N * Ho * Wo * C8;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
-       i += (long)gridDim.x * blockDim.x) {
+struct PoolJob {
+  const f16* x;
+  int xs;
+  f16* out;
+  int os, N, H, W, C, Ho, Wo;
+};
+struct InterpJob {
+  const f16* x;
+  int xs;
+  f16* out;
+  int os, N, H, W, C, Ho, Wo, ac;
+  float mul;
+};
+
+// 3x3 / stride 2 / pad 1 average (count_include_pad), elements i0, i0 + step, ...
+__device__ __forceinline__ void avgpool3s2_body(const PoolJob& j, long i0, long step) {
+  const f16* __restrict__ x = j.x;
+  const int C8 = j.C >> 3, H = j.H, W = j.W, Ho = j.Ho, Wo = j.Wo;
+  const long total = (long)j.N * Ho * Wo * C8;
+  for (long i = i0; i < total; i += step) {
     // 32-bit index decomposition (total < 2^31, host-checked): 64-bit div/mod is a long emulated
     // sequence per element that outweighed the 8-channel arithmetic
     const unsigned ii = (unsigned)i;
@@ -152,15 +166,19 @@ __global__ void avgpool3s2_kernel(const f16* __restrict__ x, int xs, f16* __rest
         int iw = ow * 2 + dx;
         if (iw < 0 || iw >= W) continue;
         float v[8];
-        ld8(x + ((long)(n * H + ih) * W + iw) * xs + c, v);
+        ld8(x + ((long)(n * H + ih) * W + iw) * j.xs + c, v);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += v[j];
+        for (int q = 0; q < 8; ++q) acc[q] += v[q];
       }
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] *= (1.f / 9.f);
-    st8(out + ((long)(n * Ho + oh) * Wo + ow) * os + c, acc);
+    for (int q = 0; q < 8; ++q) acc[q] *= (1.f / 9.f);
+    st8(j.out + ((long)(n * Ho + oh) * Wo + ow) * j.os + c, acc);
   }
+}
+
+__global__ void avgpool3s2_kernel(const PoolJob j) {
+  avgpool3s2_body(j, blockIdx.x * (long)blockDim.x + threadIdx.x, (long)gridDim.x * blockDim.x);
 }
 
 __global__ void avgpoolk_kernel(const f16* __restrict__ x, int xs, f16* __restrict__ out, int os,
@@ -199,14 +217,13 @@ __device__ __forceinline__ float src_index(int dst, int in_size, int out_size, i
   return s < 0.f ? 0.f : s;
 }
 
-__global__ void interp_kernel(const f16* __restrict__ x, int xs, f16* __restrict__ out, int os,
-                              int N, int H, int W, int C, int Ho, int Wo, int ac, float mul) {
-  const int C8 = C >> 3;
-  const long total = (long)N * Ho * Wo * C8;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
-       i += (long)gridDim.x * blockDim.x) {
-    // 32-bit index decomposition (total < 2^31, host-checked): 64-bit div/mod is a long emulated
-    // sequence per element that outweighed the 8-channel arithmetic
+// bilinear resize (align_corners = ac) times mul, elements i0, i0 + step, ...
+__device__ __forceinline__ void interp_body(const InterpJob& j, long i0, long step) {
+  const f16* __restrict__ x = j.x;
+  const int C8 = j.C >> 3, H = j.H, W = j.W, Ho = j.Ho, Wo = j.Wo;
+  const long total = (long)j.N * Ho * Wo * C8;
+  for (long i = i0; i < total; i += step) {
+    // 32-bit index decomposition (total < 2^31, host-checked)
     const unsigned ii = (unsigned)i;
     const int c = (int)(ii % (unsigned)C8) * 8;
     unsigned p = ii / (unsigned)C8;
@@ -214,7 +231,7 @@ __global__ void interp_kernel(const f16* __restrict__ x, int xs, f16* __restrict
     p /= (unsigned)Wo;
     const int oh = (int)(p % (unsigned)Ho);
     const int n = (int)(p / (unsigned)Ho);
-    float sy = src_index(oh, H, Ho, ac), sx = src_index(ow, W, Wo, ac);
+    float sy = src_index(oh, H, Ho, j.ac), sx = src_index(ow, W, Wo, j.ac);
     int y0 = (int)floorf(sy), x0 = (int)floorf(sx);
     y0 = y0 > H - 1 ? H - 1 : y0;
     x0 = x0 > W - 1 ? W - 1 : x0;
@@ -222,17 +239,27 @@ __global__ void interp_kernel(const f16* __restrict__ x, int xs, f16* __restrict
     int x1 = x0 + 1 < W ? x0 + 1 : W - 1;
     float ly = sy - y0, lx = sx - x0;
     float v00[8], v01[8], v10[8], v11[8];
-    ld8(x + ((long)(n * H + y0) * W + x0) * xs + c, v00);
-    ld8(x + ((long)(n * H + y0) * W + x1) * xs + c, v01);
-    ld8(x + ((long)(n * H + y1) * W + x0) * xs + c, v10);
-    ld8(x + ((long)(n * H + y1) * W + x1) * xs + c, v11);
+    ld8(x + ((long)(n * H + y0) * W + x0) * j.xs + c, v00);
+    ld8(x + ((long)(n * H + y0) * W + x1) * j.xs + c, v01);
+    ld8(x + ((long)(n * H + y1) * W + x0) * j.xs + c, v10);
+    ld8(x + ((long)(n * H + y1) * W + x1) * j.xs + c, v11);
     float r[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      r[j] = mul * ((1.f - ly) * ((1.f - lx) * v00[j] + lx * v01[j]) +
-                    ly * ((1.f - lx) * v10[j] + lx * v11[j]));
-    st8(out + ((long)(n * Ho + oh) * Wo + ow) * os + c, r);
+    for (int q = 0; q < 8; ++q)
+      r[q] = j.mul * ((1.f - ly) * ((1.f - lx) * v00[q] + lx * v01[q]) + ly * ((1.f - lx) * v10[q] + lx * v11[q]));
+    st8(j.out + ((long)(n * Ho + oh) * Wo + ow) * j.os + c, r);
   }
+}
+
+__global__ void interp_kernel(const InterpJob j) {
+  interp_body(j, blockIdx.x * (long)blockDim.x + threadIdx.x, (long)gridDim.x * blockDim.x);
+}
+
+// a pool job and an interp job of one GRU level's inputs in one launch: blocks [0, gp) pool, the rest interp
+// (same per-element arithmetic as the two kernels, so the results are bitwise those of two launches)
+__global__ void pool_interp_kernel(const PoolJob pj, const InterpJob ij, int gp) {
+  if ((int)blockIdx.x < gp) avgpool3s2_body(pj, blockIdx.x * (long)blockDim.x + threadIdx.x, (long)gp * blockDim.x);
+  else interp_body(ij, (blockIdx.x - gp) * (long)blockDim.x + threadIdx.x, (long)(gridDim.x - gp) * blockDim.x);
 }
 
 // max |a - b| and max |b| over n elements (fp16 or fp32), as float bits in res[0] / res[1] (non-negative
@@ -307,7 +334,7 @@ extern "C" int sa_avgpool3s2(const void* x, int xs, void* out, int os, int N, in
   long work = (long)N * Ho * Wo * (C / 8);
   if (work >= (1L << 31)) return -2;  // 32-bit index math in the kernel
   hipLaunchKernelGGL(avgpool3s2_kernel, dim3(grid_for(work)), dim3(256), 0, stream,
-                     (const f16*)x, xs, (f16*)out, os, N, H, W, C, Ho, Wo);
+                     PoolJob{(const f16*)x, xs, (f16*)out, os, N, H, W, C, Ho, Wo});
   return (int)hipGetLastError();
 }
 
@@ -327,8 +354,22 @@ extern "C" int sa_interp_bilinear(const void* x, int xs, void* out, int os, int 
   if (C % 8) return -2;
   long work = (long)N * Ho * Wo * (C / 8);
   if (work >= (1L << 31)) return -2;  // 32-bit index math in the kernel
-  hipLaunchKernelGGL(interp_kernel, dim3(grid_for(work)), dim3(256), 0, stream, (const f16*)x, xs,
-                     (f16*)out, os, N, H, W, C, Ho, Wo, ac, mul);
+  hipLaunchKernelGGL(interp_kernel, dim3(grid_for(work)), dim3(256), 0, stream,
+                     InterpJob{(const f16*)x, xs, (f16*)out, os, N, H, W, C, Ho, Wo, ac, mul});
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_pool_interp(const void* px, int pxs, void* pout, int pos, int pN, int pH, int pW, int pC,
+                              const void* ix, int ixs, void* iout, int ios, int iN, int iH, int iW, int iC, int iHo,
+                              int iWo, int ac, float mul, hipStream_t stream) {
+  if (pC % 8 || iC % 8) return -2;
+  const int pHo = (pH - 1) / 2 + 1, pWo = (pW - 1) / 2 + 1;
+  const long pwork = (long)pN * pHo * pWo * (pC / 8), iwork = (long)iN * iHo * iWo * (iC / 8);
+  if (pwork >= (1L << 31) || iwork >= (1L << 31)) return -2;
+  const int gp = grid_for(pwork), gi = grid_for(iwork);
+  hipLaunchKernelGGL(pool_interp_kernel, dim3(gp + gi), dim3(256), 0, stream,
+                     PoolJob{(const f16*)px, pxs, (f16*)pout, pos, pN, pH, pW, pC, pHo, pWo},
+                     InterpJob{(const f16*)ix, ixs, (f16*)iout, ios, iN, iH, iW, iC, iHo, iWo, ac, mul}, gp);
   return (int)hipGetLastError();
 }
 

@@ -132,6 +132,7 @@ class RaftStereo : public StereoEngine {
   void* fh2_w16_ = nullptr;  // fp16 [16][256], taps 9..15 zero
   // tap projection + stencil as one halo-tiled launch (sa_flow_head_tail); SA_RAFT_FH_TAIL=0 restores the two
   bool fh_tail_ = !std::getenv("SA_RAFT_FH_TAIL") || std::atoi(std::getenv("SA_RAFT_FH_TAIL")) != 0;
+  bool pool_interp_ = !std::getenv("SA_RAFT_POOL_INTERP") || std::atoi(std::getenv("SA_RAFT_POOL_INTERP")) != 0;
   float* tap_p_ = nullptr;   // [9][B*h0*w0]
   float* pyr_ = nullptr;
   float* flow_ = nullptr;
@@ -440,11 +441,20 @@ void RaftStereo::forward(hipStream_t s) {
     gru(st, 2, {pool_[1]});
   };
   auto gru16 = [&](hipStream_t st) {
-    pool(st, 0);
     if (rc_.n_gru == 3) {
-      interp(st, 1);
+      // pool2x(net[0]) and interp(net[2]) as one launch (SA_RAFT_POOL_INTERP=0: two)
+      if (pool_interp_) {
+        check(sa_pool_interp(net_[0].ptr, net_[0].stride, pool_[0].ptr, pool_[0].stride, Bn, lh_[0], lw_[0], hd,
+                             net_[2].ptr, net_[2].stride, interp_[1].ptr, interp_[1].stride, Bn, lh_[2], lw_[2], hd,
+                             lh_[1], lw_[1], 1, 1.f, st),
+              "pool2x + interp");
+      } else {
+        pool(st, 0);
+        interp(st, 1);
+      }
       gru(st, 1, {pool_[0], interp_[1]});
     } else {
+      pool(st, 0);
       gru(st, 1, {pool_[0]});
     }
   };
