@@ -112,11 +112,12 @@ class RaftStereo : public StereoEngine {
   bool fuse_menc_ = true;
   // SA_RAFT_PARALLEL=0: run the motion encoder and the coarse GRU levels on one stream
   bool par_ = !(std::getenv("SA_RAFT_PARALLEL") && std::getenv("SA_RAFT_PARALLEL")[0] == '0');
-  // Cross-iteration pipeline on a third stream: worth ~1.3 ms at batch 1 (small grids leave CUs idle), nothing
-  // at batch 8 (56.19 vs 56.17 ms/step in-process, tools/ab_engine.py), where the big GEMMs fill the chip —
-  // and there a third engine stream pushes the data-parallel step (copy stream + RCCL stream + torch
-  // stream) past the 4 hardware queues per process: the H2D prefetch stopped overlapping the frame graph
-  // (0 % vs 95.5 % concurrent, profiles/dp_overlap_r02.txt).  Auto = mode 2 below batch 4, off above;
+  // Cross-iteration pipeline on a third stream (the 1/16 and 1/8 GRU levels of iteration t+1 under the finest
+  // level + flow head of t).  Round 2 first measured it neutral at batch 8 (56.19 vs 56.17 ms/step) and turned it
+  // off there, to keep the data-parallel step's copy / RCCL / torch streams within the 4 hardware queues per
+  // process; once the encoders and flow head got faster the same A/B in bench.py gives mode 2 at batch 8 172.0 ->
+  // 176.2 FPS, and with the RCCL all-gather forced at world size 1 (SA_DP_GATHER_WORLD1=1) 174.2 -> 177.2 FPS
+  // (profiles/pipeline_b8_r02.txt), so mode 2 is now the default at every batch.
   // SA_RAFT_PIPELINE=0/1/2 forces a mode (1: G32 one iteration ahead; 2: G32 and G16 ahead, see forward()).
   int pipeline_mode_ = std::getenv("SA_RAFT_PIPELINE") ? std::atoi(std::getenv("SA_RAFT_PIPELINE")) : -1;
   // SA_RAFT_FUSE_FH: 0 = off, 1 = on, unset = auto.  With conv2 as a separate tap projection
@@ -542,7 +543,7 @@ void RaftStereo::forward(hipStream_t s) {
 
   const int f = 1 << rc_.n_downsample;
   // 0 = off, 1 = G32 ahead, 2 = G32 + G16 ahead (default below batch 4)
-  const int pmode = pipeline_mode_ >= 0 ? pipeline_mode_ : (Bn < 4 ? 2 : 0);
+  const int pmode = pipeline_mode_ >= 0 ? pipeline_mode_ : 2;
   const bool pipe = par && pmode > 0 && rc_.n_gru == 3 && !rc_.slow_fast;
   // finest GRU (interp + z/r + q) and flow head as two halves, for the deeper pipeline
   auto fine = [&]() {

@@ -1,0 +1,4 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 400 python -u tools/ab_engine.py --knob SA_RAFT_PIPELINE --values 0,1,2 --batch 8 --rounds 5 2>&1 | grep -v "amdgpu.ids\|^\[I\]" | tee gpurun_out/pipe_b8.log
