@@ -682,7 +682,7 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
     HIP_CHECK(hipMalloc((void**)&res, 2 * sizeof(unsigned)));
   }
   bool have_ref = false;
-  int ref_cfg = -1, ref_sk = 0;
+  int ref_cfg = -1, ref_sk = 0, ref_slices = 0;
   if (t.stats) t.stats = reinterpret_cast<sa_stat_t*>(scratch + out_bytes);
   if (t.proj_out) t.proj_out = reinterpret_cast<float*>(scratch + out_bytes + stats_bytes);
   hipEvent_t e0, e1;
@@ -720,11 +720,14 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
           have_ref = true;
           ref_cfg = cfg;
           ref_sk = sk;
+          ref_slices = proj_bytes ? sa_conv2d_nslices(&t) : 0;
         } else {
           HIP_CHECK(hipMemsetAsync(res, 0, 2 * sizeof(unsigned), s));
           HIP_CHECK((hipError_t)sa_absdiff_max(scratch, ref, (long)(out_bytes / (out_f32 ? 4 : 2)), out_f32 ? 1 : 0,
                                                res, s));
-          if (proj_bytes)
+          // projection planes are laid out per n-tile slice: only comparable between tactics of the same
+          // n-tile width (a 64-wide tile writes 4 slices where a 128-wide one writes 2 -- the stencil sums them)
+          if (proj_bytes && sa_conv2d_nslices(&t) == ref_slices)
             HIP_CHECK((hipError_t)sa_absdiff_max(scratch + out_bytes + stats_bytes, ref + out_bytes + stats_bytes,
                                                  (long)(proj_bytes / 4), 1, res, s));
           unsigned h[2];
