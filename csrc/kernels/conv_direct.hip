@@ -525,13 +525,17 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const Direc
       }
       lds_barrier();
       const int y0 = ty * TR - 1, x0 = tx * TC - 1;
+      // interior tiles (every staged pixel inside the image) skip the per-piece coordinate test
+      const bool interior = y0 >= 0 && y0 + IR <= p.H && x0 >= 0 && x0 + IC <= p.W;
       char* ibw = smem + cur * IN_BYTES;
       int tl = tid;
       asm volatile("" : "+v"(tl));  // tile-invariant piece decomposition: recomputed, not held across the loop
       for (int g = tl; g < IN_PIECES; g += 512) {
         const int pp = g >> 3, q = (g & 7) ^ v2_swz(pp);
-        const int iy = y0 + pp / IC, ix = x0 + pp % IC;
-        if (iy < 0 || iy >= p.H || ix < 0 || ix >= p.W) continue;
+        if (!interior) {
+          const int iy = y0 + pp / IC, ix = x0 + pp % IC;
+          if (iy < 0 || iy >= p.H || ix < 0 || ix >= p.W) continue;
+        }
         half8 v = *reinterpret_cast<const half8*>(ibw + g * 16);
         const half8 sc = *reinterpret_cast<const half8*>(nrm + q * 8);
         const half8 sh = *reinterpret_cast<const half8*>(nrm + 64 + q * 8);

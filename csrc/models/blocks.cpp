@@ -39,11 +39,14 @@ void instnorm(hipStream_t s, const Tensor& x, const sa_stat_t* stats, const Tens
   SA_LAUNCH_CHECK(s);
 }
 
-// SA_FUSE_IN=0: materialise relu(IN(conv1)) before conv2 even where conv2 could normalise its staged input
-// (64 -> 64 blocks: the direct conv v2 stages y1 and normalises it in LDS, tactic 23)
+// SA_FUSE_IN=1: conv2 of the 64 -> 64 instance-norm blocks stages conv1's raw output and normalises it in LDS
+// (direct conv v2, tactic 23) instead of reading a materialised relu(IN(conv1)).  Off by default: the in-LDS
+// transform is a serial phase between two barriers (~250 us of the 520 us conv at b8), which eats the saved
+// HBM pass -- measured neutral (b8 44.66 vs 44.58 ms/step, b1 9.09 vs 9.12 ms, profiles/fused_input_norm_r02.txt)
+// while normalising in fp16 instead of fp32.
 static bool fused_input_norm(int in_planes, int planes) {
   // read at every call (engine build and graph capture): tools/ab_engine.py sets it per engine
-  const bool on = !(std::getenv("SA_FUSE_IN") && std::getenv("SA_FUSE_IN")[0] == '0');
+  const bool on = std::getenv("SA_FUSE_IN") && std::getenv("SA_FUSE_IN")[0] == '1';
   return on && in_planes == 64 && planes == 64;
 }
 
