@@ -18,6 +18,7 @@ def _pairs(b, h, w):
     ("raftstereo-sceneflow", 6, (96, 128), "0"),
     ("raftstereo-sceneflow", 6, (96, 128), "1"),  # flow head conv2 fused into conv1's epilogue
     ("raftstereo-sceneflow", 6, (96, 128), "nomotion"),  # unfused lookup / convc1 / convf1
+    ("raftstereo-sceneflow", 6, (96, 128), "fusein"),  # conv2 of the 64-channel IN blocks normalises its input
 ])
 def test_engine_matches_oracle(tmp_path, monkeypatch, preset, iters, hw, fuse):
     from stereoalgorithms_amd.models import raft_stereo as R
@@ -26,6 +27,8 @@ def test_engine_matches_oracle(tmp_path, monkeypatch, preset, iters, hw, fuse):
     h, w = hw
     if fuse == "nomotion":
         monkeypatch.setenv("SA_RAFT_FUSE_MOTION", "0")
+    elif fuse == "fusein":
+        monkeypatch.setenv("SA_FUSE_IN", "1")
     elif fuse:
         monkeypatch.setenv("SA_RAFT_FUSE_FH", fuse)
     m = R.build(preset, seed=0)
