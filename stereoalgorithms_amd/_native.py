@@ -84,6 +84,7 @@ class SaConvArgs(C.Structure):
         ("up", C.c_int32), ("cout_real", C.c_int32), ("gate", C.c_void_p), ("gate_stride", C.c_int32),
         ("proj_w", C.c_void_p), ("proj_out", C.c_void_p), ("proj_taps", C.c_int32), ("proj_oc", C.c_int32),
         ("proj_plane", C.c_int64), ("stats_slots", C.c_int32), ("cin_real", C.c_int32),
+        ("in_stats", C.c_void_p), ("in_act", C.c_int32),
     ]
 
 

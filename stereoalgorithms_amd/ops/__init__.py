@@ -155,7 +155,7 @@ def pack_conv_weight(w: torch.Tensor, segs: Sequence[tuple[int, int]] | None = N
 def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1, act="none",
            act2="none", res=None, out=None, epi="store", scale=1.0, alpha=0.01, stats=None,
            ctx=None, aux=None, hbuf=None, rh=None, tile_cfg=-1, splitk=1, workspace=None, up=0, cout_real=0,
-           gate=None, proj=None, stats_slots=1, cin_real=0):
+           gate=None, proj=None, stats_slots=1, cin_real=0, in_stats=None, in_act="none"):
     """NHWC fp16 implicit-GEMM conv.  ``proj = (w2 fp32 [taps*oc, cout], taps, oc)`` with
     ``epi="proj"``: the epilogue projects the activated output onto the taps of a following conv
     and the call returns ``(out_or_None, P, nslices)`` for :func:`proj_stencil`.  ``splitk``: 1 = off, 0 = auto, >1 = forced; needs
@@ -186,6 +186,9 @@ def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1
         cin += x.shape[3]
     a.nsrc = len(xs)
     a.cin_real = cin_real  # single zero-padded source: real channels (the 7x7 stem kernel stages only those)
+    if in_stats is not None:  # fused input instance norm (tile_cfg 23): folded fixed-point sums [n][cin][2]
+        assert in_stats.dtype == torch.int64
+        a.in_stats, a.in_act = in_stats.data_ptr(), N.ACT[in_act]
     a.N, a.H, a.W, a.Cin = n, h, w, cin
     a.KH, a.KW, a.sh, a.sw, a.ph, a.pw, a.dh, a.dw = kh, kw, sh, sw, ph, pw, dil, dil
     a.Ho, a.Wo = ho, wo
