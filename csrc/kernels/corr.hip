@@ -46,7 +46,8 @@ __global__ __launch_bounds__(256) void corr_pyramid_kernel(const f16* __restrict
   const half8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
   long lvl_off[4] = {0, lvl_off1, lvl_off2, lvl_off3};
 
-  for (int w1b = 0; w1b < W1; w1b += CORR_ROWS) {
+  // slabs of this row: blockIdx.y, +gridDim.y, ... (small frames split a row's slabs over workgroups)
+  for (int w1b = blockIdx.y * CORR_ROWS; w1b < W1; w1b += gridDim.y * CORR_ROWS) {
     const int ntiles = (CORR_ROWS / 16) * nct;
     for (int t = wave; t < ntiles; t += 4) {
       const int tr = t / nct, tc = t % nct;
@@ -371,7 +372,12 @@ extern "C" int sa_corr1d_pyramid(const void* f1, const void* f2, int stride, int
   }
   size_t smem = (size_t)CORR_ROWS * (W2 + 1) * sizeof(float);
   if (smem > 160 * 1024) return -3;
-  hipLaunchKernelGGL(corr_pyramid_kernel, dim3(B * H), dim3(256), smem, stream, (const f16*)f1,
+  // one workgroup per image row fills the chip at batch 8 (960 rows); at batch 1 (120 rows) the row's 32-row
+  // slabs go to separate workgroups (each re-reads the row's right features from L2)
+  const int nslab = (W1 + CORR_ROWS - 1) / CORR_ROWS;
+  const char* e = std::getenv("SA_CORR_SPLIT");  // 0 = one workgroup per row always (A/B; read at capture)
+  const int split = (B * H >= 512 || (e && e[0] == '0')) ? 1 : nslab;
+  hipLaunchKernelGGL(corr_pyramid_kernel, dim3(B * H, split), dim3(256), smem, stream, (const f16*)f1,
                      (const f16*)f2, stride, H, W1, W2, C, levels, off[1], off[2], off[3], pyr);
   return (int)hipGetLastError();
 }
