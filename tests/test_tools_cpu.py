@@ -95,3 +95,23 @@ def test_host_sanitizers(tmp_path):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "host_check ok" in r.stdout
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr
+
+
+def test_pmc_summary_busy_fraction(tmp_path):
+    """tools/pmc_summary.py: per-dispatch counters summed over rows, medians per (kernel, grid), and the MFMA busy
+    fraction at the held clock = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)."""
+    csv = tmp_path / "run_counter_collection.csv"
+    rows = ["Dispatch_Id,Kernel_Name,Grid_Size,Counter_Name,Counter_Value"]
+    for d in range(3):
+        # two rows per counter and dispatch (e.g. per XCD slices) are summed
+        rows += [f"{d},conv_igemm_kernel<256>,614400,SQ_VALU_MFMA_BUSY_CYCLES,{1.0e8}",
+                 f"{d},conv_igemm_kernel<256>,614400,SQ_VALU_MFMA_BUSY_CYCLES,{1.0e8}",
+                 f"{d},conv_igemm_kernel<256>,614400,GRBM_GUI_ACTIVE,{4.0e6}",
+                 f"{d},other_kernel,256,GRBM_GUI_ACTIVE,{1.0e3}"]
+    csv.write_text("\n".join(rows) + "\n")
+    out = subprocess.run([sys.executable, str(ROOT / "tools" / "pmc_summary.py"), str(csv), "--match", "conv_igemm"],
+                         capture_output=True, text=True, check=True).stdout
+    assert "other_kernel" not in out
+    assert "SQ_VALU_MFMA_BUSY_CYCLES         2e+08" in out
+    # 2e8 / (4e6 / 8 * 1024) = 0.390625
+    assert "held clock, busy / (GRBM_GUI_ACTIVE / 8 x 1024): 0.391" in out
