@@ -47,12 +47,18 @@ __global__ void agcl_kernel(const SaAgclArgs a) {
   const int Cg = a.C / G;
   const int px = a.small_patch ? 3 : 9, py = a.small_patch ? 3 : 1;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int k = (int)(i % ntap);
-    const int g = (int)((i / ntap) % G);
-    const long pix = i / (ntap * G);
-    const int w = (int)(pix % a.W);
-    const int h = (int)((pix / a.W) % a.H);
-    const int n = (int)(pix / ((long)a.W * a.H));
+    // 32-bit index decomposition (total < 2^31, host-checked): the 64-bit div / mod chain is an emulated
+    // sequence per element
+    const unsigned ii = (unsigned)i;
+    const int k = (int)(ii % (unsigned)ntap);
+    const unsigned q = ii / (unsigned)ntap;
+    const int g = (int)(q % (unsigned)G);
+    const unsigned pixu = q / (unsigned)G;
+    const long pix = (long)pixu;
+    const int w = (int)(pixu % (unsigned)a.W);
+    const unsigned hw = pixu / (unsigned)a.W;
+    const int h = (int)(hw % (unsigned)a.H);
+    const int n = (int)(hw / (unsigned)a.H);
     const int dx = k % px - px / 2, dy = k / px - py / 2;
     float sx, sy;
     if (a.iter_mode) {
@@ -88,8 +94,10 @@ __global__ void agcl_kernel(const SaAgclArgs a) {
       for (int c = 0; c < Cg; c += 8) {
         const half8 l8 = *reinterpret_cast<const half8*>(lp + c);
         const half8 r8 = *reinterpret_cast<const half8*>(rp + c);
+        typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s += (float)l8[j] * (float)r8[j];
+        for (int j = 0; j < 8; j += 2)  // fp16 pairs, fp32 accumulation (v_dot2_f32_f16)
+          s = __builtin_amdgcn_fdot2(half2v{l8[j], l8[j + 1]}, half2v{r8[j], r8[j + 1]}, s, false);
       }
       acc += wts[t] * s;
     }
@@ -282,6 +290,7 @@ __global__ void interp_flow_kernel(const float* __restrict__ x, float* __restric
 extern "C" int sa_agcl_corr(const SaAgclArgs* a, hipStream_t stream) {
   if (a->C % 32 || a->out_channels < 36) return -2;
   const long total = (long)a->N * a->H * a->W * 36;
+  if (total >= (1L << 31)) return -2;  // 32-bit index math in the kernel
   hipLaunchKernelGGL(agcl_kernel, dim3(grid_for(total)), dim3(256), 0, stream, *a);
   if (a->out_channels > 36) {
     const long P = (long)a->N * a->H * a->W;
