@@ -14,6 +14,8 @@
 //   * sa_interp_flow      — fp32 multi-channel bilinear resize (align_corners) with scale
 // Upstream ops: SURVEY.md §2.6 (grid_sample / local group correlation / linear attention rows).
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 #include <hip/hip_fp16.h>
 
 #include "sa/kernels.h"
@@ -102,6 +104,74 @@ __global__ void agcl_kernel(const SaAgclArgs a) {
       acc += wts[t] * s;
     }
     reinterpret_cast<f16*>(a.out)[pix * a.out_stride + g * ntap + k] = (f16)(acc / (float)Cg);
+  }
+}
+
+// Same op, 8 lanes per (pixel, group, tap): lane c8 owns channels 8*c8 .. +8 of the group's 64, so the left chunk
+// and each bilinear corner's right chunk are one contiguous 128-B line per 8 lanes (the one-thread-per-tap kernel
+// above issues 8 scattered 16-B loads per line and per thread); the 8 partial dot products are summed with DPP.
+// Needs C / 4 == 64 channels per group (CREStereo: C = 256 at every level).
+__global__ void agcl8_kernel(const SaAgclArgs a) {
+  constexpr int ntap = 9, G = 4, CG = 64;
+  const unsigned total = (unsigned)a.N * a.H * a.W * G * ntap;
+  const int px = a.small_patch ? 3 : 9, py = a.small_patch ? 3 : 1;
+  const int c8 = threadIdx.x & 7;
+  typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+  for (unsigned ii = (blockIdx.x * (unsigned)blockDim.x + threadIdx.x) >> 3; ii < total;
+       ii += (gridDim.x * (unsigned)blockDim.x) >> 3) {
+    const int k = (int)(ii % (unsigned)ntap);
+    const unsigned q = ii / (unsigned)ntap;
+    const int g = (int)(q % (unsigned)G);
+    const unsigned pixu = q / (unsigned)G;
+    const long pix = (long)pixu;
+    const int w = (int)(pixu % (unsigned)a.W);
+    const unsigned hw = pixu / (unsigned)a.W;
+    const int h = (int)(hw % (unsigned)a.H);
+    const int n = (int)(hw / (unsigned)a.H);
+    const int dx = k % px - px / 2, dy = k / px - py / 2;
+    float sx, sy;
+    if (a.iter_mode) {
+      int hh = h + dy, ww = w + dx;
+      hh = hh < 0 ? 0 : (hh >= a.H ? a.H - 1 : hh);
+      ww = ww < 0 ? 0 : (ww >= a.W ? a.W - 1 : ww);
+      const float* f = a.flow + (((long)n * a.H + hh) * a.W + ww) * 2;
+      sx = (float)ww + f[0];
+      sy = (float)hh + f[1];
+    } else {
+      const float* f = a.flow + pix * 2;
+      sx = (float)w + f[0] + (float)dx;
+      sy = (float)h + f[1] + (float)dy;
+      if (a.offset) {
+        const f16* o = reinterpret_cast<const f16*>(a.offset) + pix * a.offset_stride + k * 2;
+        sx += (float)o[0];
+        sy += (float)o[1];
+      }
+    }
+    const float x0f = floorf(sx), y0f = floorf(sy);
+    const int x0 = (int)x0f, y0 = (int)y0f;
+    const float ax = sx - x0f, ay = sy - y0f;
+    const half8 l8 = *reinterpret_cast<const half8*>(reinterpret_cast<const f16*>(a.f1) + pix * a.f1_stride + g * CG +
+                                                     c8 * 8);
+    float acc = 0.f;
+    const float wts[4] = {(1.f - ax) * (1.f - ay), ax * (1.f - ay), (1.f - ax) * ay, ax * ay};
+    const bool finite = isfinite(sx) && isfinite(sy);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int xx = x0 + (t & 1), yy = y0 + (t >> 1);
+      if (!finite || xx < 0 || xx >= a.W || yy < 0 || yy >= a.H || wts[t] == 0.f) continue;
+      const half8 r8 = *reinterpret_cast<const half8*>(reinterpret_cast<const f16*>(a.f2) +
+                                                       (((long)n * a.H + yy) * a.W + xx) * a.f2_stride + g * CG + c8 * 8);
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; j += 2)
+        s = __builtin_amdgcn_fdot2(half2v{l8[j], l8[j + 1]}, half2v{r8[j], r8[j + 1]}, s, false);
+      acc += wts[t] * s;
+    }
+    // sum over the 8 lanes of this tap (quad_perm xor 1, xor 2, then row_ror 4 within the 8-lane half-row)
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    acc += __shfl_xor(acc, 4);
+    if (c8 == 0) reinterpret_cast<f16*>(a.out)[pix * a.out_stride + g * ntap + k] = (f16)(acc / (float)CG);
   }
 }
 
@@ -291,7 +361,11 @@ extern "C" int sa_agcl_corr(const SaAgclArgs* a, hipStream_t stream) {
   if (a->C % 32 || a->out_channels < 36) return -2;
   const long total = (long)a->N * a->H * a->W * 36;
   if (total >= (1L << 31)) return -2;  // 32-bit index math in the kernel
-  hipLaunchKernelGGL(agcl_kernel, dim3(grid_for(total)), dim3(256), 0, stream, *a);
+  const char* e = std::getenv("SA_AGCL8");  // 0 = one thread per tap (A/B; read at launch / graph capture)
+  if (a->C == 256 && total * 8 < (1L << 31) && !(e && e[0] == '0'))
+    hipLaunchKernelGGL(agcl8_kernel, dim3(grid_for(total * 8)), dim3(256), 0, stream, *a);
+  else
+    hipLaunchKernelGGL(agcl_kernel, dim3(grid_for(total)), dim3(256), 0, stream, *a);
   if (a->out_channels > 36) {
     const long P = (long)a->N * a->H * a->W;
     hipLaunchKernelGGL(zero_tail_kernel, dim3(grid_for(P * (a->out_channels - 36))), dim3(256), 0, stream,
