@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
 
+#include <cstdlib>
+
 #include "sa/kernels.h"
 
 namespace {
@@ -59,6 +61,65 @@ __global__ void dwconv_kernel(const f16* __restrict__ x, int xs, const float* __
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = (f16)act_apply(acc[j], act, 0.01f);
     *reinterpret_cast<half8*>(out + ((long)(n * Ho + oh) * Wo + ow) * os + c) = o;
+  }
+}
+
+// Same op with the weights staged once per workgroup in LDS as [tap][C] fp32 (two 16-B LDS reads per tap instead
+// of 8 scalar global loads), bias in LDS, 32-bit index decomposition and all 9 taps' 16-B input loads issued before
+// the first FMA (out-of-image taps read as zero).  Used when 10 * C floats fit the LDS budget below.
+constexpr int kDwMaxC = 1024;
+__global__ __launch_bounds__(256) void dwconv_lds_kernel(const f16* __restrict__ x, int xs, const float* __restrict__ w,
+                                                         const float* __restrict__ b, f16* __restrict__ out, int os,
+                                                         int N, int H, int W, int C, int Ho, int Wo, int s, int act) {
+  extern __shared__ float dw_lds[];
+  float* wl = dw_lds;          // [9][C]
+  float* bl = dw_lds + 9 * C;  // [C]
+  for (int k = threadIdx.x; k < 9 * C; k += blockDim.x) {
+    const int c = k / 9, t = k - c * 9;
+    wl[t * C + c] = w[k];
+  }
+  for (int c = threadIdx.x; c < C; c += blockDim.x) bl[c] = b ? b[c] : 0.f;
+  __syncthreads();
+  const unsigned C8 = (unsigned)C >> 3, uWo = (unsigned)Wo, uHo = (unsigned)Ho;
+  const unsigned total = (unsigned)N * uHo * uWo * C8;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const unsigned p = i / C8;
+    const int c = (int)(i - p * C8) * 8;
+    const unsigned q = p / uWo;
+    const int ow = (int)(p - q * uWo);
+    const int n = (int)(q / uHo), oh = (int)(q - (unsigned)n * uHo);
+    half8 v[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ih = oh * s - 1 + t / 3, iw = ow * s - 1 + t % 3;
+      if (ih >= 0 && ih < H && iw >= 0 && iw < W)
+        v[t] = *reinterpret_cast<const half8*>(x + ((size_t)(n * H + ih) * W + iw) * xs + c);
+      else
+        v[t] = half8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    float acc[8];
+    {
+      const float4 b0 = *reinterpret_cast<const float4*>(bl + c), b1 = *reinterpret_cast<const float4*>(bl + c + 4);
+      acc[0] = b0.x, acc[1] = b0.y, acc[2] = b0.z, acc[3] = b0.w, acc[4] = b1.x, acc[5] = b1.y, acc[6] = b1.z,
+      acc[7] = b1.w;
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const float4 w0 = *reinterpret_cast<const float4*>(wl + t * C + c);
+      const float4 w1 = *reinterpret_cast<const float4*>(wl + t * C + c + 4);
+      acc[0] = fmaf((float)v[t][0], w0.x, acc[0]);
+      acc[1] = fmaf((float)v[t][1], w0.y, acc[1]);
+      acc[2] = fmaf((float)v[t][2], w0.z, acc[2]);
+      acc[3] = fmaf((float)v[t][3], w0.w, acc[3]);
+      acc[4] = fmaf((float)v[t][4], w1.x, acc[4]);
+      acc[5] = fmaf((float)v[t][5], w1.y, acc[5]);
+      acc[6] = fmaf((float)v[t][6], w1.z, acc[6]);
+      acc[7] = fmaf((float)v[t][7], w1.w, acc[7]);
+    }
+    half8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (f16)act_apply(acc[j], act, 0.01f);
+    *reinterpret_cast<half8*>(out + ((size_t)(n * Ho + oh) * Wo + ow) * os + c) = o;
   }
 }
 
@@ -242,7 +303,18 @@ extern "C" int sa_dwconv3x3(const void* x, int xs, const float* w, const float* 
                             int W, int C, int stride, int act, hipStream_t stream) {
   if (C % 8 || xs % 8 || os % 8) return -2;
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
-  hipLaunchKernelGGL(dwconv_kernel, dim3(grid_for((long)N * Ho * Wo * (C / 8))), dim3(256), 0, stream,
+  const long total = (long)N * Ho * Wo * (C / 8);
+  const char* knob = getenv("SA_DWCONV_LDS");  // "0": the one-thread-per-chunk kernel above (A/B)
+  const bool lds_path = !(knob && knob[0] == '0');
+  if (lds_path && C <= kDwMaxC && total < (1L << 31) && (long)N * H * W * xs < (1L << 31)) {
+    // <= 8 workgroups per CU so every workgroup's one-time weight staging is amortised over several tiles
+    long g = (total + 255) / 256;
+    if (g > 2048) g = 2048;
+    hipLaunchKernelGGL(dwconv_lds_kernel, dim3((unsigned)(g < 1 ? 1 : g)), dim3(256), (size_t)10 * C * sizeof(float),
+                       stream, (const f16*)x, xs, w, b, (f16*)out, os, N, H, W, C, Ho, Wo, stride, act);
+    return (int)hipGetLastError();
+  }
+  hipLaunchKernelGGL(dwconv_kernel, dim3(grid_for(total)), dim3(256), 0, stream,
                      (const f16*)x, xs, w, b, (f16*)out, os, N, H, W, C, Ho, Wo, stride, act);
   return (int)hipGetLastError();
 }
