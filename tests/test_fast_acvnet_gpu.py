@@ -94,11 +94,12 @@ def test_transposed_conv_parity_scatter(is3d):
     assert rel_err(got, ref) < 3e-3
 
 
-def test_norm_corr_volume():
+@pytest.mark.parametrize("D", [24, 21])
+def test_norm_corr_volume(D):
     from stereoalgorithms_amd.models.fast_acvnet import norm_correlation_volume
     O = ops()
     torch.manual_seed(3)
-    n, c, h, w, D = 2, 48, 9, 40, 24
+    n, c, h, w = 2, 48, 9, 40
     l = torch.randn(n, c, h, w, device=DEV).half().float()
     r = torch.randn(n, c, h, w, device=DEV).half().float()
     ref = norm_correlation_volume(l, r, D)[:, 0]  # [n, D, h, w]
