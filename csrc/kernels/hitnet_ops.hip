@@ -4,6 +4,8 @@
 // Hypotheses are fp32 [n][th][tw][16] = [d, dx, dy, p0..p12] (d in level pixels); the conv layers that
 // refine them consume an fp16 copy written next to the local cost features (one 64-channel source).
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 #include <hip/hip_fp16.h>
 
 #include "sa/kernels.h"
@@ -166,6 +168,66 @@ __global__ void __launch_bounds__(128) warp_cost_kernel(const f16* __restrict__ 
   }
 }
 
+// Same costs with one thread per (candidate, tile, tile pixel) instead of one per (candidate, tile): T*T times the
+// threads (the T = 4 levels launched 300 workgroups of 2 waves and walked 16 pixels x 3 shifts serially per
+// thread), u fastest so a wave's left / right feature reads are contiguous pixels.  Per pixel the arithmetic is
+// the per-tile kernel's in the same order, but the compiler's FMA contraction can differ, so costs may differ in
+// the last bits; with random-init weights the candidate selection downstream amplifies that at a few pixels
+// (profiles/hit_warp_px_r02.txt).  The stage-by-stage oracle tests (tests/test_hitnet_gpu.py) hold.
+template <int C, int T>
+__global__ void __launch_bounds__(256) warp_cost_px_kernel(const f16* __restrict__ el, int els,
+                                                           const f16* __restrict__ er, int ers, int B, int H, int W,
+                                                           const float* __restrict__ hyp, int ncand, int th, int tw,
+                                                           f16* __restrict__ out, int ostride, int ccand) {
+  const unsigned Q = (unsigned)B * th * tw;
+  const unsigned total = (unsigned)ncand * Q * (T * T);
+  constexpr float c0 = (T - 1) * 0.5f;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const unsigned pq = i / (T * T);
+    const int t = (int)(i - pq * (T * T));
+    const int u = t % T, v = t / T;
+    const unsigned k = pq / Q;
+    const unsigned q = pq - k * Q;
+    const unsigned qy = q / (unsigned)tw;
+    const int x = (int)(q - qy * (unsigned)tw);
+    const int img = (int)(qy / (unsigned)th), y = (int)(qy - (unsigned)img * th);
+    const float* h = hyp + (size_t)pq * 16;
+    const float d = h[0], sx = h[1], sy = h[2];
+    f16* orow = out + (size_t)q * ostride + (size_t)k * ccand;
+    const int py = T * y + v, px = T * x + u;
+    const f16* lrow = el + ((size_t)img * H + py) * W * els;
+    const f16* rrow = er + ((size_t)img * H + py) * W * ers;
+    float lv[C];
+#pragma unroll
+    for (int cc = 0; cc < C; cc += 8) {
+      const half8 a = *reinterpret_cast<const half8*>(lrow + (size_t)px * els + cc);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) lv[cc + j] = (float)a[j];
+    }
+    const float dp = d + sx * ((float)u - c0) + sy * ((float)v - c0);
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const float xr = (float)px - (dp + (float)(s - 1));
+      const float x0f = floorf(xr);
+      const float a = xr - x0f;
+      const int x0 = (int)x0f;
+      float cost = 0.f;
+      const bool ok0 = x0 >= 0 && x0 <= W - 1, ok1 = x0 + 1 >= 0 && x0 + 1 <= W - 1;
+#pragma unroll
+      for (int cc = 0; cc < C; cc += 8) {
+        half8 r0 = {0, 0, 0, 0, 0, 0, 0, 0}, r1 = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (ok0) r0 = *reinterpret_cast<const half8*>(rrow + (size_t)x0 * ers + cc);
+        if (ok1) r1 = *reinterpret_cast<const half8*>(rrow + (size_t)(x0 + 1) * ers + cc);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cost += fabsf(lv[cc + j] - ((1.f - a) * (float)r0[j] + a * (float)r1[j]));
+      }
+      orow[s * T * T + v * T + u] = (f16)cost;
+    }
+    f16* hc = orow + 3 * T * T;
+    for (int j = t; j < 16; j += T * T) hc[j] = (f16)h[j];
+  }
+}
+
 // h' = cand + delta[:16] (d clamped >= 0); with confidences (delta channel 16 of each candidate block)
 // keep the first candidate with the strictly highest one.  cand [ncand][P][16]; delta [P][dstr] with
 // candidate k's block at channel k * dcand.
@@ -271,6 +333,27 @@ extern "C" int sa_hitnet_hyp_init(const float* dinit, const void* desc, int ds, 
 template <int C>
 int launch_warp(int T, dim3 g, const f16* el, int els, const f16* er, int ers, int B, int H, int W, const float* hyp,
                 int ncand, int th, int tw, f16* out, int ostride, int ccand, hipStream_t stream) {
+  const char* knob = getenv("SA_HIT_WARP_PX");  // "0": one thread per (candidate, tile) (A/B)
+  const long px_total = (long)ncand * B * H * W;
+  if (!(knob && knob[0] == '0') && px_total < (1L << 31)) {
+    const dim3 gp(grid_for(px_total, 256));
+    switch (T) {
+      case 4:
+        hipLaunchKernelGGL((warp_cost_px_kernel<C, 4>), gp, dim3(256), 0, stream, el, els, er, ers, B, H, W, hyp, ncand,
+                           th, tw, out, ostride, ccand);
+        return (int)hipGetLastError();
+      case 2:
+        hipLaunchKernelGGL((warp_cost_px_kernel<C, 2>), gp, dim3(256), 0, stream, el, els, er, ers, B, H, W, hyp, ncand,
+                           th, tw, out, ostride, ccand);
+        return (int)hipGetLastError();
+      case 1:
+        hipLaunchKernelGGL((warp_cost_px_kernel<C, 1>), gp, dim3(256), 0, stream, el, els, er, ers, B, H, W, hyp, ncand,
+                           th, tw, out, ostride, ccand);
+        return (int)hipGetLastError();
+      default:
+        return -2;
+    }
+  }
   switch (T) {
     case 4:
       hipLaunchKernelGGL((warp_cost_kernel<C, 4>), g, dim3(128), 0, stream, el, els, er, ers, B, H, W, hyp, ncand, th, tw,
