@@ -242,6 +242,51 @@ __global__ __launch_bounds__(256) void topk_kernel(const f16* __restrict__ att, 
 }
 
 // out[n][k][h][w][c] = p_k * (c < Cl ? left[c] : right(w - d_k)[c - Cl]), linear interpolation along x
+// Same volume with one thread per (n, k, h, w, 8-channel chunk), chunk fastest: a wave's 16-B loads and stores
+// are contiguous instead of each thread walking its own 2 * Cl-channel row (os apart from its neighbours').
+__global__ __launch_bounds__(256) void concat_volume_chunk_kernel(const f16* __restrict__ l, int ls,
+                                                                  const f16* __restrict__ r, int rs,
+                                                                  const float* __restrict__ prob,
+                                                                  const float* __restrict__ disp, int N, int H, int W,
+                                                                  int Cl, int K, f16* __restrict__ out, int os) {
+  const unsigned CC = (unsigned)Cl >> 3;
+  const unsigned total = (unsigned)N * K * H * W * CC;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const unsigned item = i / CC;
+    const int c = (int)(i - item * CC) * 8;
+    const unsigned q = item / (unsigned)W;
+    const int w = (int)(item - q * (unsigned)W);
+    const unsigned q2 = q / (unsigned)H;
+    const int h = (int)(q - q2 * (unsigned)H);
+    const int n = (int)(q2 / (unsigned)K), k = (int)(q2 - (unsigned)n * K);
+    const size_t pix = ((size_t)n * H + h) * W + w;
+    const float pk = prob[pix * K + k];
+    const float x = (float)w - disp[pix * K + k];
+    const float x0f = floorf(x);
+    const int x0 = (int)x0f;
+    const float a = x - x0f;
+    f16* o = out + (size_t)item * os;
+    const half8 lv = *reinterpret_cast<const half8*>(l + pix * ls + c);
+    half8 ov;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ov[j] = (f16)((float)lv[j] * pk);
+    *reinterpret_cast<half8*>(o + c) = ov;
+    float rv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int xx = x0 + t;
+      const float wt = t ? a : 1.f - a;
+      if (xx < 0 || xx >= W || wt == 0.f) continue;
+      const half8 qv = *reinterpret_cast<const half8*>(r + (((size_t)n * H + h) * W + xx) * rs + c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) rv[j] += wt * (float)qv[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ov[j] = (f16)(rv[j] * pk);
+    *reinterpret_cast<half8*>(o + Cl + c) = ov;
+  }
+}
+
 __global__ void concat_volume_kernel(const f16* __restrict__ l, int ls, const f16* __restrict__ r, int rs,
                                      const float* __restrict__ prob, const float* __restrict__ disp, int N, int H,
                                      int W, int Cl, int K, f16* __restrict__ out, int os) {
@@ -398,6 +443,13 @@ extern "C" int sa_topk_disparity(const void* att, int as, int N, int D, int H, i
 extern "C" int sa_concat_volume(const void* l, int ls, const void* r, int rs, const float* prob, const float* disp,
                                 int N, int H, int W, int Cl, int K, void* out, int os, hipStream_t stream) {
   if (Cl % 8 || os < 2 * Cl) return -2;
+  // opt-in until measured on the GPU ("1": chunk-parallel kernel; default: one thread per volume row)
+  const char* knob = getenv("SA_CONCAT_CHUNK");
+  if (knob && knob[0] == '1' && Cl % 8 == 0 && (long)N * K * H * W * (Cl / 8) < (1L << 31)) {
+    hipLaunchKernelGGL(concat_volume_chunk_kernel, dim3(grid_for((long)N * K * H * W * (Cl / 8))), dim3(256), 0,
+                       stream, (const f16*)l, ls, (const f16*)r, rs, prob, disp, N, H, W, Cl, K, (f16*)out, os);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(concat_volume_kernel, dim3(grid_for((long)N * K * H * W)), dim3(256), 0, stream, (const f16*)l,
                      ls, (const f16*)r, rs, prob, disp, N, H, W, Cl, K, (f16*)out, os);
   return (int)hipGetLastError();
