@@ -443,9 +443,8 @@ extern "C" int sa_topk_disparity(const void* att, int as, int N, int D, int H, i
 extern "C" int sa_concat_volume(const void* l, int ls, const void* r, int rs, const float* prob, const float* disp,
                                 int N, int H, int W, int Cl, int K, void* out, int os, hipStream_t stream) {
   if (Cl % 8 || os < 2 * Cl) return -2;
-  // opt-in until measured on the GPU ("1": chunk-parallel kernel; default: one thread per volume row)
-  const char* knob = getenv("SA_CONCAT_CHUNK");
-  if (knob && knob[0] == '1' && Cl % 8 == 0 && (long)N * K * H * W * (Cl / 8) < (1L << 31)) {
+  const char* knob = getenv("SA_CONCAT_CHUNK");  // "0": one thread per volume row (A/B, profiles/concat_chunk_r02.txt)
+  if (!(knob && knob[0] == '0') && Cl % 8 == 0 && (long)N * K * H * W * (Cl / 8) < (1L << 31)) {
     hipLaunchKernelGGL(concat_volume_chunk_kernel, dim3(grid_for((long)N * K * H * W * (Cl / 8))), dim3(256), 0,
                        stream, (const f16*)l, ls, (const f16*)r, rs, prob, disp, N, H, W, Cl, K, (f16*)out, os);
     return (int)hipGetLastError();
