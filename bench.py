@@ -76,17 +76,42 @@ def _free_port() -> int:
     return port
 
 
+def visible_gpus() -> int | None:
+    """GPUs this process may use, counted without touching HIP: the KFD topology in sysfs (nodes with a GFX target),
+    narrowed by HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES.  None when sysfs is unreadable."""
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        n = 0
+        for d in os.listdir(root):
+            try:
+                props = open(os.path.join(root, d, "properties")).read().split()
+            except OSError:
+                continue
+            kv = dict(zip(props[0::2], props[1::2]))
+            if int(kv.get("gfx_target_version", "0")) != 0:
+                n += 1
+    except OSError:
+        return None
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
 def launch(args, argv) -> int:
     """Parent of a self-launched N-rank job: spawn, forward output, propagate failure.
 
-    Runs before anything initialises a GPU in this process (torch.cuda.device_count() does not on this
-    image), so the children are fresh processes, never an exec of a GPU-initialised one."""
+    The parent never initialises HIP (no torch.cuda call: on ROCm torch without amdsmi even device_count() would),
+    so the children are fresh processes, never a fork / exec of a GPU-initialised one.  GPUs are counted from sysfs;
+    each child re-checks LOCAL_RANK against its own device count."""
     n = args.gpus
     backend = os.environ.get("SA_DIST_BACKEND", "nccl")
+    torch_mod = sys.modules.get("torch")
+    assert torch_mod is None or not torch_mod.cuda.is_initialized(), "bench.py launcher: GPU initialised before spawn"
     if backend == "nccl" and args.device == "gpu":
-        import torch
-        ndev = torch.cuda.device_count()
-        if n > ndev:
+        ndev = visible_gpus()
+        if ndev is not None and n > ndev:
             print(f"bench.py: --gpus {n} but only {ndev} GPU(s) visible; RCCL needs one GPU per rank "
                   f"(SA_DIST_BACKEND=gloo to rehearse more ranks)", file=sys.stderr, flush=True)
             return 2
@@ -126,16 +151,22 @@ class OracleEngine:
         self.iters = iters if iters > 0 else R.PRESETS[preset].valid_iters
         self.device_bytes = 0
 
-    def run(self, left, right, out=None):
+    def set_Q(self, Q):
+        self.Q = Q
+
+    def run(self, left, right, out=None, cloud=False, cloud_out=None):
         import torch
         with torch.no_grad():
             l = left.flip(-1).permute(0, 3, 1, 2).float()
             r = right.flip(-1).permute(0, 3, 1, 2).float()
             _, up = self.model(l, r, iters=self.iters)
             d = -up[:, 0]
-        if out is not None:
-            return out.copy_(d)
-        return d.contiguous()
+        d = out.copy_(d) if out is not None else d.contiguous()
+        if not cloud:
+            return d
+        from stereoalgorithms_amd.utils.geometry import reproject_cloud_torch
+        c = reproject_cloud_torch(d, left, self.Q)
+        return d, (cloud_out.copy_(c) if cloud_out is not None else c)
 
 
 def main(argv=None) -> int:
@@ -194,11 +225,14 @@ def main(argv=None) -> int:
     Q = np.array([[1, 0, 0, -W / 2], [0, 1, 0, -H / 2], [0, 0, 0, 500.0], [0, 0, 1 / 60.0, 0]], np.float32)
     if cpu:
         eng = OracleEngine(args.model, H, W, B, args.iters, seed=0)
+        eng.set_Q(Q)
     else:
         from stereoalgorithms_amd.models.engine import NativeStereoEngine
         eng = NativeStereoEngine(args.model, None, H, W, batch=B, iters=args.iters, device=dev.index, seed=0)
         eng.set_Q(Q)
-    dp = DataParallelStereo(eng, world_size=world, rank=rank, force_gather=force_gather)
+    # every rank reprojects its frames' point clouds in the frame graph and keeps them (the reference produces a
+    # cloud per frame inside its timed region, RAFTStereo/src/TRTRAFTStereo.cpp:140-144)
+    dp = DataParallelStereo(eng, world_size=world, rank=rank, force_gather=force_gather, cloud=True)
     l_np, r_np = batch_pairs(B, H, W, seed=100 * rank)
     left_h, right_h = torch.from_numpy(l_np), torch.from_numpy(r_np)
     if cpu:
@@ -209,7 +243,9 @@ def main(argv=None) -> int:
             pass
     else:
         left_h, right_h = left_h.pin_memory(), right_h.pin_memory()
-        h2d = H2DPrefetcher([left_h, right_h], dev)
+        # the H2D prefetch rides the engine's side stream (idle between captures): engine + side + torch + RCCL
+        # streams = 4 = GPU_MAX_HW_QUEUES per rank
+        h2d = H2DPrefetcher([left_h, right_h], dev, stream=eng.copy_stream)
 
         def step():
             # every step copies its inputs H2D (copy stream, double-buffered: overlaps the previous step's
@@ -232,6 +268,7 @@ def main(argv=None) -> int:
     for _ in range(args.steps):
         pending = step()
     out = pending.wait()
+    cloud = pending.cloud
     dp.flush()  # every step's collective is complete inside the timed region
     sync()
     if world > 1:
@@ -264,12 +301,14 @@ def main(argv=None) -> int:
         dist.all_gather_object(gathered, ranks[0])
         ranks = gathered
     assert out.shape == (world * B, H, W) and torch.isfinite(out).all()
+    assert cloud is not None and cloud.shape == (B, H, W, 6)
 
     ms_step = dt / args.steps * 1e3
     fps = world * B * args.steps / dt
     extra = {}
     # batch-1 latency block: single-process GPU runs only (in a multi-rank job the other ranks would sit in
     # process-group teardown while rank 0 builds and tunes more engines)
+    plan_b8 = None if cpu else eng.plan_status
     if rank == 0 and world == 1 and not args.no_latency and not cpu:
         dev_bytes_b8 = eng.device_bytes
         del eng
@@ -304,6 +343,7 @@ def main(argv=None) -> int:
                              "baseline_ms_rtx3090": base,
                              "speedup_vs_baseline": round(base / float(ts.mean()), 3) if base else None,
                              "device_bytes": dev_b1,
+                             "plan_loaded": e1.plan_status["loaded"], "plan_saved": e1.plan_status["saved"],
                              "device_stages_ms": {k: round(v, 3) for k, v in e1.stage_times()}}
             e1.close()
     else:
@@ -339,6 +379,8 @@ def main(argv=None) -> int:
             "ms_per_frame_per_gpu": round(ms_step / B, 3),
             "allgather_ms": gather_ms,
             "allgather_bytes_per_rank": B * H * W * 4,
+            "point_clouds": f"per rank [{B},{H},{W},6] fp32 XYZRGB, reprojected in the frame graph, kept local",
+            "plan": None if cpu else plan_b8,
             "device_bytes": dev_bytes_b8,
             "latency_b1": extra,
         }

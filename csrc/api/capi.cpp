@@ -76,6 +76,7 @@ int sa_engine_run_host(void* e, void* left, void* right, float* disp, float* clo
   });
 }
 
+void* sa_engine_copy_stream(void* e) { return static_cast<sa::StereoEngine*>(e)->copy_stream(); }
 long long sa_engine_device_bytes(void* e) {
   return (long long)static_cast<sa::StereoEngine*>(e)->device_bytes();
 }
@@ -86,6 +87,13 @@ const float* sa_engine_aux_output(void* e, int* n) {
 
 const char* sa_engine_plan_path(void* e) { return static_cast<sa::StereoEngine*>(e)->plan_path().c_str(); }
 long sa_engine_tuned_shapes(void* e) { return static_cast<sa::StereoEngine*>(e)->tuned_shapes(); }
+// plan file at build: *loaded = entries loaded (-1 absent, -2 written by another library build, -3 not consulted),
+// *saved = 0 ok / errno of the failed write / -1 not attempted (nothing tuned)
+void sa_engine_plan_status(void* e, int* loaded, int* saved) {
+  *loaded = static_cast<sa::StereoEngine*>(e)->plan_loaded();
+  *saved = static_cast<sa::StereoEngine*>(e)->plan_saved();
+}
+const char* sa_plan_build_id() { return sa::conv_plan_build_id().c_str(); }
 long sa_engine_nonzero_splitk_counters(void* e) { return static_cast<sa::StereoEngine*>(e)->nonzero_splitk_counters(); }
 long sa_conv_tune_count(void) { return sa::conv_tune_count(); }
 long sa_conv_tune_rejects(void) { return sa::conv_tune_rejects(); }

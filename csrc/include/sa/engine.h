@@ -70,10 +70,19 @@ class StereoEngine {
   void run_host(uint8_t* left, uint8_t* right, float* disp, float* cloud, bool rectify);
 
   hipStream_t stream() const { return stream_; }
+  // The engine's side stream.  It only carries work while a frame is being captured (graph replays run every
+  // branch from the instantiated graph), so between frames it is free for the caller's input copies: the
+  // data-parallel step issues its H2D prefetch there instead of on a stream of its own, keeping a rank within
+  // GPU_MAX_HW_QUEUES = 4 (engine, copy/side, caller, RCCL).
+  hipStream_t copy_stream() const { return side_; }
   size_t device_bytes() const { return arena_.bytes(); }
   // tuned-plan file used by this engine ("" = none) and how many conv shapes it had to time
   const std::string& plan_path() const { return plan_path_; }
   long tuned_shapes() const { return tuned_shapes_; }
+  // plan file at build: entries loaded (-1 absent, -2 other library build, -3 not consulted); save result
+  // (0 ok, errno of the failing step, -1 not attempted because nothing was tuned)
+  int plan_loaded() const { return plan_loaded_; }
+  int plan_saved() const { return plan_saved_; }
   // diagnostic: split-K tile counters that are not zero (every split conv's last arriver resets its
   // tiles' counters, so a non-zero one after a completed frame means two launches raced on them)
   long nonzero_splitk_counters();
@@ -138,6 +147,7 @@ class StereoEngine {
   std::string default_plan_path() const;
   std::string plan_path_;
   long tuned_shapes_ = 0;
+  int plan_loaded_ = -3, plan_saved_ = -1;
   SplitKWorkspace splitk_;
   hipStream_t side_ = nullptr;
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;

@@ -9,6 +9,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstddef>
+#include <cstdint>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -32,15 +33,15 @@ class HostCopyPool {
 
  private:
   void worker();
-  void drain(const std::vector<Task>* tasks, int n);
+  void drain(const std::vector<Task>* tasks, int n, uint32_t gen);
   std::vector<std::thread> th_;
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   const std::vector<Task>* tasks_ = nullptr;
   int n_ = 0;
-  std::atomic<int> next_{0};
+  std::atomic<uint64_t> claim_{0};  // (generation << 32) | next task index
   int remaining_ = 0, active_ = 0;
-  unsigned long gen_ = 0;
+  uint32_t gen_ = 0;
   bool stop_ = false;
 };
 

@@ -174,8 +174,11 @@ long conv_tune_rejects();   // tactic candidates rejected by the tuner's output 
 void conv_plan_clear();     // drop the in-process plan (tests: prove a plan file is used)
 void conv_plan_set_arch(const std::string& gcn_arch_name);  // plan keys carry the device's arch
 const std::string& conv_plan_arch();
-int conv_plan_load(const std::string& file);  // merge a plan file; returns entries added, -1 if absent
+// merge a plan file; returns entries added, -1 if absent, -2 if it was written by another library build
+int conv_plan_load(const std::string& file);
+// write the plan entries of `keys` (atomic rename); 0 or the errno of the failing step
 int conv_plan_save(const std::string& file, const std::vector<std::string>& keys);
+const std::string& conv_plan_build_id();  // hash of the loaded kernel library (plan files carry it)
 // collects every plan key consulted by conv_apply_plan in this thread (the engine's own shapes)
 struct ScopedPlanCollect {
   std::vector<std::string>* prev;

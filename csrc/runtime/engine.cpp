@@ -175,8 +175,10 @@ void StereoEngine::init() {
     // arch skips tactic timing entirely
     plan_path_ = default_plan_path();
     if (!plan_path_.empty()) {
-      const int n = conv_plan_load(plan_path_);
-      if (n >= 0) SA_LOGI("tactic plan %s: %d entries loaded", plan_path_.c_str(), n);
+      plan_loaded_ = conv_plan_load(plan_path_);
+      if (plan_loaded_ >= 0) SA_LOGI("tactic plan %s: %d entries loaded", plan_path_.c_str(), plan_loaded_);
+      else if (plan_loaded_ == -2)
+        SA_LOGW("tactic plan %s was written by another library build: ignored (re-tuning)", plan_path_.c_str());
     }
     const long tuned0 = conv_tune_count();
     std::vector<std::string> keys;
@@ -194,8 +196,9 @@ void StereoEngine::init() {
     }
     tuned_shapes_ = conv_tune_count() - tuned0;
     if (!plan_path_.empty() && tuned_shapes_ > 0) {
-      if (conv_plan_save(plan_path_, keys) == 0) SA_LOGI("tactic plan saved to %s", plan_path_.c_str());
-      else SA_LOGW("could not write tactic plan %s", plan_path_.c_str());
+      plan_saved_ = conv_plan_save(plan_path_, keys);
+      if (plan_saved_ == 0) SA_LOGI("tactic plan saved to %s", plan_path_.c_str());
+      else SA_LOGE("could not write tactic plan %s: %s", plan_path_.c_str(), std::strerror(plan_saved_));
     }
     // right-size the split-K workspaces to what the tuned plan actually launches (every stream's
     // workspace serves a subset of the same convs, so the pass's high-water mark bounds each)

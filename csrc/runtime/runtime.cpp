@@ -6,7 +6,10 @@
 #include <mutex>
 #include <unordered_map>
 #include <cstring>
+#include <cerrno>
+#include <dlfcn.h>
 #include <fstream>
+#include <sstream>
 #include <unistd.h>
 
 #include "sa/json.h"
@@ -612,11 +615,56 @@ std::string plan_file() {
   return std::string(e);
 }
 
-void load_plan_file(std::unordered_map<std::string, PlanEntry>& m, const std::string& f) {
+// Identity of the kernel library that timed a plan: FNV-1a over the bytes of the loaded libstereo_amd.so.  Tactic
+// numbers, eligibility rules and kernels change between builds, so a plan file written by another build (or an A/B
+// library loaded with SA_NATIVE_LIB) is ignored rather than trusted.
+const std::string& build_id() {
+  static const std::string id = [] {
+    Dl_info info{};
+    uint64_t h = 1469598103934665603ull;
+    if (dladdr(reinterpret_cast<void*>(&conv_plan_load), &info) && info.dli_fname) {
+      std::ifstream f(info.dli_fname, std::ios::binary);
+      char buf[1 << 16];
+      while (f) {
+        f.read(buf, sizeof(buf));
+        for (std::streamsize i = 0; i < f.gcount(); ++i) {
+          h ^= (unsigned char)buf[i];
+          h *= 1099511628211ull;
+        }
+      }
+    }
+    char s[24];
+    std::snprintf(s, sizeof(s), "%016llx", (unsigned long long)h);
+    return std::string(s);
+  }();
+  return id;
+}
+
+// Plan files: an optional "# sa-plan build=<id>" header, then "key cfg splitk us" lines.  Returns the entries read,
+// or -2 when the header names another build (nothing is taken from such a file).
+int load_plan_file(std::unordered_map<std::string, PlanEntry>& m, const std::string& f) {
   std::ifstream in(f);
-  std::string key;
-  PlanEntry e;
-  while (in >> key >> e.cfg >> e.splitk >> e.us) m[key] = e;
+  std::string line;
+  int n = 0;
+  bool first = true;
+  while (std::getline(in, line)) {
+    if (line.empty()) continue;
+    if (line[0] == '#') {
+      const size_t b = line.find("build=");
+      if (first && b != std::string::npos && line.substr(b + 6, 16) != build_id()) return -2;
+      first = false;
+      continue;
+    }
+    first = false;
+    std::istringstream ls(line);
+    std::string key;
+    PlanEntry e;
+    if (ls >> key >> e.cfg >> e.splitk >> e.us) {
+      m[key] = e;
+      ++n;
+    }
+  }
+  return n;
 }
 
 std::unordered_map<std::string, PlanEntry>& plan_map() {  // caller holds g_plan_mu
@@ -812,9 +860,13 @@ int conv_plan_load(const std::string& file) {
   const size_t before = m.size();
   std::ifstream in(file);
   if (!in.good()) return -1;
-  load_plan_file(m, file);
+  std::unordered_map<std::string, PlanEntry> fresh;
+  if (load_plan_file(fresh, file) == -2) return -2;
+  for (auto& kv : fresh) m[kv.first] = kv.second;
   return (int)(m.size() - before);
 }
+
+const std::string& conv_plan_build_id() { return build_id(); }
 
 int conv_plan_save(const std::string& file, const std::vector<std::string>& keys) {
   std::lock_guard<std::mutex> lk(g_plan_mu);
@@ -823,7 +875,8 @@ int conv_plan_save(const std::string& file, const std::vector<std::string>& keys
   const std::string tmp = file + ".tmp." + std::to_string((long)::getpid());
   {
     std::ofstream out(tmp);
-    if (!out.good()) return -1;
+    if (!out.good()) return errno ? errno : EIO;
+    out << "# sa-plan build=" << build_id() << '\n';
     int n = 0;
     std::vector<std::string> seen;
     for (const std::string& k : keys) {
@@ -833,10 +886,19 @@ int conv_plan_save(const std::string& file, const std::vector<std::string>& keys
       out << k << ' ' << it->second.cfg << ' ' << it->second.splitk << ' ' << it->second.us << '\n';
       ++n;
     }
-    if (!out.good()) return -1;
+    out.flush();
+    if (!out.good()) {
+      const int err = errno ? errno : EIO;
+      std::remove(tmp.c_str());
+      return err;
+    }
   }
   // atomic replace: concurrent engines (one per rank) never see a half-written plan
-  if (std::rename(tmp.c_str(), file.c_str()) != 0) return -1;
+  if (std::rename(tmp.c_str(), file.c_str()) != 0) {
+    const int err = errno ? errno : EIO;
+    std::remove(tmp.c_str());
+    return err;
+  }
   return 0;
 }
 
@@ -867,7 +929,9 @@ void conv_apply_plan(SaConvArgs& a, hipStream_t s) {
     ++g_tuned;
     const std::string f = plan_file();
     if (!f.empty() && e.cfg >= 0) {
+      const bool fresh = !std::ifstream(f).good();
       std::ofstream out(f, std::ios::app);
+      if (fresh) out << "# sa-plan build=" << build_id() << '\n';
       out << key << ' ' << e.cfg << ' ' << e.splitk << ' ' << e.us << '\n';
     }
   }

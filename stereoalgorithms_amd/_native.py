@@ -172,10 +172,13 @@ def _declare_dev(lib):
         "sa_engine_run_device": (_i, [_p, _p, _p, _p, _p, _i, _p, _p, _p]),
         "sa_engine_run_host": (_i, [_p, _p, _p, _p, _p, _i]),
         "sa_engine_device_bytes": (C.c_longlong, [_p]),
+        "sa_engine_copy_stream": (C.c_void_p, [_p]),
         "sa_engine_aux_output": (_p, [_p, C.POINTER(_i)]),
         "sa_engine_stream": (_p, [_p]),
         "sa_engine_plan_path": (C.c_char_p, [_p]),
         "sa_engine_tuned_shapes": (C.c_long, [_p]),
+        "sa_engine_plan_status": (None, [_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+        "sa_plan_build_id": (C.c_char_p, []),
         "sa_engine_nonzero_splitk_counters": (C.c_long, [_p]),
         "sa_conv_tune_count": (C.c_long, []),
         "sa_conv_tune_rejects": (C.c_long, []),

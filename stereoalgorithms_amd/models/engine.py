@@ -61,6 +61,12 @@ class NativeStereoEngine:
         return int(self._lib.sa_engine_device_bytes(self._h))
 
     @property
+    def copy_stream(self) -> torch.cuda.ExternalStream:
+        """The engine's side stream as a torch stream: idle outside graph capture, so callers stage their input
+        copies there (parallel.dp.H2DPrefetcher) instead of creating a stream of their own."""
+        return torch.cuda.ExternalStream(self._lib.sa_engine_copy_stream(self._h), device=self.device)
+
+    @property
     def plan_path(self) -> str:
         """Tuned-plan cache file of this engine ('' when disabled: SA_PLAN_CACHE set, SA_PLAN_DIR='')."""
         return self._lib.sa_engine_plan_path(self._h).decode()
@@ -69,6 +75,15 @@ class NativeStereoEngine:
     def tuned_shapes(self) -> int:
         """Conv shapes this engine had to time at build (0 when its plan file covered everything)."""
         return int(self._lib.sa_engine_tuned_shapes(self._h))
+
+    @property
+    def plan_status(self) -> dict:
+        """Tuned-plan cache at build: path, entries loaded (-1 absent, -2 written by another library build, -3 not
+        consulted), save result (0 ok, errno of a failed write, -1 not attempted) and the library build id."""
+        ld, sv = C.c_int(0), C.c_int(0)
+        self._lib.sa_engine_plan_status(self._h, C.byref(ld), C.byref(sv))
+        return {"path": self.plan_path, "loaded": ld.value, "saved": sv.value, "tuned_shapes": self.tuned_shapes,
+                "build": self._lib.sa_plan_build_id().decode()}
 
     def nonzero_splitk_counters(self) -> int:
         """Diagnostic: split-K tile counters left non-zero (0 after every correctly ordered frame)."""
@@ -87,13 +102,19 @@ class NativeStereoEngine:
                                                      mr.ctypes.data_as(C.c_void_p)), "set_rectify_maps")
 
     def run(self, left: torch.Tensor, right: torch.Tensor, cloud: bool = False, rectify: bool = False,
-            out: torch.Tensor | None = None, rectified: bool = False):
-        """left/right: uint8 BGR [B,H,W,3] CUDA tensors -> disparity fp32 [B,H,W] (+cloud [B,H,W,6])."""
+            out: torch.Tensor | None = None, rectified: bool = False, cloud_out: torch.Tensor | None = None):
+        """left/right: uint8 BGR [B,H,W,3] CUDA tensors -> disparity fp32 [B,H,W] (+cloud [B,H,W,6], written into
+        ``cloud_out`` when given).  The cloud needs set_Q(); it is reprojected inside the frame graph."""
         b, h, w = self.batch, self.height, self.width
         assert left.shape == (b, h, w, 3) and left.dtype == torch.uint8 and left.is_cuda
+        if cloud and not self.has_q:
+            raise RuntimeError("point cloud requested but no Q matrix set (set_Q)")
         left, right = left.contiguous(), right.contiguous()
         disp = out if out is not None else torch.empty(b, h, w, dtype=torch.float32, device=left.device)
-        pc = torch.empty(b, h, w, 6, dtype=torch.float32, device=left.device) if cloud else None
+        pc = None
+        if cloud:
+            pc = cloud_out if cloud_out is not None else torch.empty(b, h, w, 6, dtype=torch.float32, device=left.device)
+            assert pc.shape == (b, h, w, 6) and pc.dtype == torch.float32 and pc.is_contiguous()
         rl = torch.empty_like(left) if (rectify and rectified) else None
         rr = torch.empty_like(right) if (rectify and rectified) else None
         stream = C.c_void_p(torch.cuda.current_stream(left.device).cuda_stream)

@@ -28,10 +28,14 @@ def shard_indices_round_robin(total: int, world: int, rank: int) -> list[int]:
 
 
 class PendingGather:
-    """Handle of an in-flight disparity all-gather (see DataParallelStereo.step_async)."""
+    """Handle of an in-flight disparity all-gather (see DataParallelStereo.step_async).
 
-    def __init__(self, out: torch.Tensor, work):
-        self.out, self._work = out, work
+    ``cloud`` is this rank's point-cloud shard [B,H,W,6] (XYZRGB, reprojected in the same frame graph) when the
+    step was run with ``cloud=True``; it stays on the rank and is valid until the step two calls
+    later reuses its slot."""
+
+    def __init__(self, out: torch.Tensor, work, cloud: torch.Tensor | None = None):
+        self.out, self._work, self.cloud = out, work, cloud
 
     def wait(self) -> torch.Tensor:
         """Make the current stream wait for the collective; returns the gathered [world*B,H,W] tensor."""
@@ -54,6 +58,12 @@ class DataParallelStereo:
 
     ``gather_dtype=torch.float16`` halves the gathered bytes (0.61 MB per 480x640 frame instead of 1.23,
     SURVEY.md §5.8); fp16 keeps disparities below 256 px to within 1/8 px.
+
+    ``cloud=True``: every rank also produces the point clouds of its own frames, as the reference does for each
+    frame (RAFTStereo/src/TRTRAFTStereo.cpp:140-144: reprojection + copy-out inside its timed region).  The
+    engine reprojects in the same frame graph; the cloud shard [B,H,W,6] stays on the rank (``last_cloud``,
+    ``PendingGather.cloud``) -- 7.4 MB per 480x640 frame is 6x the disparity, so it is not all-gathered.
+    ``gather_clouds_to_rank0`` collects them on rank 0 when a consumer needs them in one place.
     """
     engine: object  # anything with .run(left, right[, out=]) -> [B,H,W] and .batch
     world_size: int = 1
@@ -62,18 +72,38 @@ class DataParallelStereo:
     slots: int = 2
     gather_dtype: torch.dtype | None = None
     force_gather: bool = False  # run the collective even at world size 1 (overlap traces on one GPU)
+    cloud: bool = False  # also produce this rank's point clouds (engine needs its Q matrix)
 
     def __post_init__(self):
         self._out = None
+        self._clouds: list = [None] * self.slots
+        self.last_cloud = None
         self._cast: list = [None] * self.slots
         self._send: list = [None] * self.slots
         self._recv: list = [None] * self.slots
         self._work: list = [None] * self.slots
         self._i = 0
 
+    def _run(self, left, right, slot, send):
+        """engine.run into the slot's buffers -> (disparity [B,H,W], cloud [B,H,W,6] or None)."""
+        if self.cloud:
+            c = self._clouds[slot]
+            disp, cl = self.engine.run(left, right, cloud=True, out=send, cloud_out=c)
+            self._clouds[slot] = cl
+            self.last_cloud = cl
+            return disp, cl
+        try:
+            disp = self.engine.run(left, right, out=send) if send is not None else self.engine.run(left, right)
+        except TypeError:  # engines without an ``out=`` argument
+            disp = self.engine.run(left, right)
+            if send is not None:
+                disp = send.copy_(disp)
+        return disp, None
+
     def step(self, left: torch.Tensor, right: torch.Tensor) -> torch.Tensor:
-        """left/right: this rank's shard [B,H,W,3] u8 -> gathered disparity [world*B,H,W]."""
-        disp = self.engine.run(left, right)
+        """left/right: this rank's shard [B,H,W,3] u8 -> gathered disparity [world*B,H,W]
+        (the rank's point clouds in ``last_cloud`` when ``cloud=True``)."""
+        disp, _ = self._run(left, right, 0, None)
         if self.world_size == 1 or not self.gather:
             return disp
         if self.gather_dtype is not None:
@@ -88,15 +118,10 @@ class DataParallelStereo:
             self._work[slot].wait()
             self._work[slot] = None
         send = self._send[slot]
-        try:
-            disp = self.engine.run(left, right, out=send) if send is not None else self.engine.run(left, right)
-        except TypeError:  # engines without an ``out=`` argument
-            disp = self.engine.run(left, right)
-            if send is not None:
-                disp = send.copy_(disp)
+        disp, cl = self._run(left, right, slot, send)
         self._send[slot] = disp
         if not self.gather or (self.world_size == 1 and not self.force_gather):
-            return PendingGather(disp, None)
+            return PendingGather(disp, None, cl)
         if self.gather_dtype is not None and disp.dtype != self.gather_dtype:
             c = self._cast[slot]
             if c is None or c.shape != disp.shape or c.device != disp.device:
@@ -108,7 +133,7 @@ class DataParallelStereo:
             recv = self._recv[slot] = torch.empty(shape, dtype=disp.dtype, device=disp.device)
         work = _all_gather_async(disp, self.world_size, recv)
         self._work[slot] = work
-        return PendingGather(recv, work)
+        return PendingGather(recv, work, cl)
 
     def flush(self):
         """Order every outstanding collective before the current stream's next work."""
@@ -149,6 +174,19 @@ def gather_to_rank0(disp: torch.Tensor, world: int, rank: int):
     return torch.cat(parts, 0) if rank == 0 else None
 
 
+def gather_clouds_to_rank0(cloud: torch.Tensor, world: int, rank: int):
+    """Every rank's point-cloud shard [B,H,W,6] -> [world*B,H,W,6] on rank 0 (None elsewhere); one collective.
+    RCCL has no gather primitive over torch's all_gather_into_tensor path, so on GPU this is an all-gather whose
+    result only rank 0 keeps (xGMI is point-to-point: the other ranks' receive traffic rides idle links)."""
+    if world == 1:
+        return cloud
+    if cloud.is_cuda and dist.get_backend() == "nccl":
+        out = torch.empty((world * cloud.shape[0],) + tuple(cloud.shape[1:]), dtype=cloud.dtype, device=cloud.device)
+        dist.all_gather_into_tensor(out, cloud.contiguous())
+        return out if rank == 0 else None
+    return gather_to_rank0(cloud, world, rank)
+
+
 class H2DPrefetcher:
     """Double-buffered host->device input staging on a copy stream.
 
@@ -159,9 +197,12 @@ class H2DPrefetcher:
     own inputs; only the overlap changes.
     """
 
-    def __init__(self, host_tensors, device, slots: int = 2):
+    def __init__(self, host_tensors, device, slots: int = 2, stream=None):
+        """``stream``: the copy stream to use (e.g. ``NativeStereoEngine.copy_stream``, so the data-parallel step
+        adds no stream of its own: engine + its side stream + caller + RCCL stay within 4 hardware queues);
+        default a new stream."""
         self.device = torch.device(device)
-        self.stream = torch.cuda.Stream(self.device)
+        self.stream = stream if stream is not None else torch.cuda.Stream(self.device)
         self.slots = slots
         self.bufs = [[torch.empty_like(h, device=self.device) for h in host_tensors] for _ in range(slots)]
         # The caching allocator hands out blocks whose previous owner may still have work pending on

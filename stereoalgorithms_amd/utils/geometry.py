@@ -88,6 +88,21 @@ def reproject_image_to_3d(disp: np.ndarray, Q) -> np.ndarray:
         return (v[..., :3] / v[..., 3:4]).astype(np.float32)
 
 
+def reproject_cloud_torch(disp, left_bgr, Q):
+    """Batched XYZRGB point cloud [B,H,W,6] fp32 of disparity [B,H,W] with the full 4x4 Q, colours from the left
+    BGR u8 image as RGB -- the contract of the reprojection kernel (csrc/kernels/prepost.hip) and of the
+    reference's reprojectImageTo3D kernels (RAFTStereo/src/stereo_preprocess.cu:41-68).  torch, any device."""
+    import torch
+    q = torch.as_tensor(np.asarray(Q, np.float32).reshape(4, 4), device=disp.device)
+    b, h, w = disp.shape
+    c = torch.arange(w, device=disp.device, dtype=torch.float32).view(1, 1, w).expand(b, h, w)
+    r = torch.arange(h, device=disp.device, dtype=torch.float32).view(1, h, 1).expand(b, h, w)
+    d = disp.float()
+    comp = [q[i, 0] * c + q[i, 1] * r + q[i, 2] * d + q[i, 3] for i in range(4)]
+    xyz = torch.stack([comp[0] / comp[3], comp[1] / comp[3], comp[2] / comp[3]], -1)
+    return torch.cat([xyz, left_bgr.flip(-1).float()], -1).contiguous()
+
+
 def rectify_maps_from_calib(calib: dict, size=(640, 480)):
     """Left/right maps from a StereoCalibration.yml dict (keys of the reference)."""
     ml = init_undistort_rectify_map(calib["intrinsic_left"], calib["distCoeffs_left"], calib["R_L"], calib["P1"], size)

@@ -27,14 +27,27 @@ def test_round_robin_shards_partition():
     assert got == list(range(10))
 
 
+Q = [[1, 0, 0, -4.0], [0, 1, 0, -3.0], [0, 0, 0, 500.0], [0, 0, 1 / 60.0, 0]]
+
+
 class FakeEngine:
-    """Deterministic per-frame 'disparity' = mean of the left image + frame marker."""
+    """Deterministic per-frame 'disparity' = mean of the left image + frame marker; point clouds with the
+    native engine's reprojection contract."""
 
     def __init__(self, batch, h, w):
         self.batch, self.height, self.width = batch, h, w
 
-    def run(self, left, right):
-        return (left.float().mean(-1) - right.float().mean(-1)).contiguous()
+    def run(self, left, right, cloud=False, out=None, cloud_out=None):
+        from stereoalgorithms_amd.utils.geometry import reproject_cloud_torch
+        d = (left.float().mean(-1) - right.float().mean(-1)).contiguous()
+        if out is not None:
+            d = out.copy_(d)
+        if not cloud:
+            return d
+        c = reproject_cloud_torch(d, left, Q)
+        if cloud_out is not None:
+            c = cloud_out.copy_(c)
+        return d, c
 
 
 def _free_port():
@@ -115,6 +128,53 @@ def test_dp_pipelined_allgather_gloo(gdt):
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker_async, args=(r, world, port, 2, 6, 8, 5, q, gdt)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert all(res[r] for r in range(world)), res
+
+
+def _worker_cloud(rank, world, port, B, H, W, steps, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from stereoalgorithms_amd.utils.geometry import reproject_cloud_torch
+        eng = FakeEngine(B, H, W)
+        step = dp.DataParallelStereo(eng, world_size=world, rank=rank, cloud=True)
+        ok = True
+        for t in range(steps):
+            g = torch.Generator().manual_seed(200 + t)
+            all_l = torch.randint(0, 255, (world * B, H, W, 3), generator=g, dtype=torch.uint8)
+            all_r = torch.randint(0, 255, (world * B, H, W, 3), generator=g, dtype=torch.uint8)
+            s, e = dp.shard_range(world * B, world, rank)
+            h = step.step_async(all_l[s:e], all_r[s:e])
+            disp_all = h.wait()
+            ref_disp = eng.run(all_l, all_r)
+            # every rank keeps exactly its own frames' clouds [B,H,W,6] (XYZ from Q, RGB from the left image)
+            ref_cloud = reproject_cloud_torch(ref_disp[s:e], all_l[s:e], Q)
+            ok = ok and h.cloud.shape == (B, H, W, 6) and torch.allclose(h.cloud, ref_cloud, rtol=0, atol=0, equal_nan=True)
+            ok = ok and torch.equal(disp_all, ref_disp) and step.last_cloud is h.cloud
+            full = dp.gather_clouds_to_rank0(h.cloud, world, rank)
+            if rank == 0:
+                ok = ok and torch.allclose(full, reproject_cloud_torch(ref_disp, all_l, Q), rtol=0, atol=0, equal_nan=True)
+            else:
+                ok = ok and full is None
+        step.flush()
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_point_clouds_per_rank_gloo():
+    """SURVEY §5.8 / VERDICT r2: each rank reprojects its own shard ([B,H,W,6] kept local), disparity is
+    all-gathered, and gather_clouds_to_rank0 assembles the job's clouds on rank 0 on request."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_cloud, args=(r, world, port, 2, 6, 8, 3, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in procs)

@@ -25,7 +25,12 @@ def test_second_initialize_skips_tuning(tmp_path, monkeypatch):
     assert path.startswith(str(tmp_path)) and path.endswith(".plan"), path
     assert "rt_b2_96x160" in os.path.basename(path) and "gfx" in os.path.basename(path)
     assert os.path.exists(path) and e1.tuned_shapes > 0
-    entries = open(path).read().splitlines()
+    st = e1.plan_status
+    assert st["saved"] == 0, f"plan write failed: {os.strerror(st['saved']) if st['saved'] > 0 else st}"
+    assert st["loaded"] == -1  # no file before the first build
+    lines = open(path).read().splitlines()
+    assert lines[0] == f"# sa-plan build={st['build']}"
+    entries = lines[1:]
     assert len(entries) >= e1.tuned_shapes
     d1 = e1.run(*_pairs(2, 96, 160)).clone()
     e1.close()
@@ -33,12 +38,39 @@ def test_second_initialize_skips_tuning(tmp_path, monkeypatch):
     before = lib.sa_conv_tune_count()
     e2 = NativeStereoEngine("", str(w), 96, 160, batch=2, iters=3)
     assert e2.tuned_shapes == 0 and lib.sa_conv_tune_count() == before
+    assert e2.plan_status["loaded"] == len(entries) and e2.plan_status["saved"] == -1
     d2 = e2.run(*_pairs(2, 96, 160))
     torch.cuda.synchronize()
     assert torch.equal(d1, d2)  # same tactics => bitwise identical
     # a different shape gets its own file
     e3 = NativeStereoEngine("", str(w), 96, 192, batch=2, iters=3)
     assert e3.plan_path != path and e3.tuned_shapes > 0
+
+
+def test_plan_of_another_build_is_ignored(tmp_path, monkeypatch):
+    """A plan file whose header names another library build (renumbered tactics, A/B builds) is not trusted: the
+    engine re-tunes and overwrites it with its own build id."""
+    from stereoalgorithms_amd import _native as N
+    from stereoalgorithms_amd.models.engine import NativeStereoEngine
+    monkeypatch.delenv("SA_PLAN_CACHE", raising=False)
+    monkeypatch.setenv("SA_PLAN_DIR", str(tmp_path))
+    lib = N.require_native()
+    lib.sa_conv_plan_clear()
+    e1 = NativeStereoEngine("raftstereo-realtime", None, 64, 96, batch=1, iters=2, seed=11)
+    path = e1.plan_path
+    assert e1.plan_status["saved"] == 0
+    e1.close()
+    lines = open(path).read().splitlines()
+    # same keys, bogus build and an impossible tactic: taking it would fail the launch
+    open(path, "w").write("# sa-plan build=0000000000000000\n" +
+                          "\n".join(l.split()[0] + " 99 1 1.0" for l in lines[1:]) + "\n")
+    lib.sa_conv_plan_clear()
+    e2 = NativeStereoEngine("raftstereo-realtime", None, 64, 96, batch=1, iters=2, seed=11)
+    assert e2.plan_status["loaded"] == -2 and e2.tuned_shapes > 0 and e2.plan_status["saved"] == 0
+    assert open(path).readline().strip() == f"# sa-plan build={e2.plan_status['build']}"
+    d = e2.run(*_pairs(1, 64, 96))
+    torch.cuda.synchronize()
+    assert torch.isfinite(d).all()
 
 
 def test_plan_cache_disabled(tmp_path, monkeypatch):
@@ -60,6 +92,8 @@ def test_activation_plan_footprint():
     workspaces sized from the tuned plan (round 1 held 13.25 GB)."""
     from stereoalgorithms_amd.models.engine import NativeStereoEngine
     e = NativeStereoEngine("raftstereo-sceneflow", None, 480, 640, batch=8, iters=2)
+    st = e.plan_status
+    assert st["saved"] in (0, -1), f"plan write to {st['path']} failed: {os.strerror(st['saved'])}"
     gb = e.device_bytes / 1e9
     print(f"b8 sceneflow device bytes {gb:.2f} GB")
     assert gb < 6.0

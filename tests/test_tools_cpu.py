@@ -97,6 +97,20 @@ def test_host_sanitizers(tmp_path):
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr
 
 
+def test_hostcopy_pool_tsan(tmp_path):
+    """The timed-region copy pool (csrc/runtime/hostcopy.cpp) under ThreadSanitizer: 100k back-to-back run() calls
+    with 1-5 tiny tasks each.  The round-2 pool lost a task when a worker woke late for a finished run (a hang
+    under this stress); claims now carry the run's generation."""
+    import shutil
+    if not shutil.which("g++") or not os.path.exists("/opt/rocm/lib/libamdhip64.so"):
+        pytest.skip("g++ / HIP runtime not available")
+    r = subprocess.run(["bash", str(ROOT / "tools" / "sanitize" / "hostcopy_tsan.sh"), str(tmp_path), "100000"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "hostcopy_stress: 100000 runs x 3 workers ok" in r.stdout
+    assert "ThreadSanitizer" not in r.stderr
+
+
 def test_pmc_summary_busy_fraction(tmp_path):
     """tools/pmc_summary.py: per-dispatch counters summed over rows, medians per (kernel, grid), and the MFMA busy
     fraction at the held clock = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)."""

@@ -31,6 +31,9 @@ SHAPES = {
     "cf1": (1, 120, 160, 8, 64, 7, 0),       # motion encoder convf1 (7x7, 2 -> 8 padded channels)
     "zr32": (1, 30, 40, 256, 256, 3, 0),     # GRU 1/16 z,r at batch 1
     "zr8l": (1, 60, 80, 384, 256, 3, 0),     # GRU 1/8 z,r at batch 1
+    "q8l": (1, 60, 80, 384, 128, 3, 0),      # GRU 1/8 q at batch 1 (SF 1/8 level, RT finest level)
+    "q32": (1, 30, 40, 256, 128, 3, 0),      # GRU 1/16 q at batch 1
+    "fhrt": (1, 60, 80, 128, 256, 3, 0),     # RT flow head conv1 at batch 1
     "fr8": (16, 480, 640, 64, 64, 3, 1),     # RAFT-SF fnet layer1 at batch 8 (full resolution, both images)
     # 7x7 stems (3 real of 8 padded channels): RAFT-SF fnet conv1 at batch 1 / 8, RAFT-RT stride 2
     "l2b8": (16, 240, 320, 96, 96, 3, 1),    # RAFT-SF fnet layer2 96 -> 96 at batch 8 (1/2 resolution, both images)
@@ -59,6 +62,8 @@ def main():
                     "default: the shape's own setting")
     ap.add_argument("--gemm-ref", type=int, default=0,
                     help="also time torch.matmul (hipBLASLt) on the conv's GEMM view [M,K] x [K,N], fp16")
+    ap.add_argument("--graph", action="store_true",
+                    help="time the --iters launches as one captured graph (no host launch overhead between calls)")
     ap.add_argument("--stats", type=int, default=0, help="fuse instance-norm statistics over N slots (engine: 16)")
     a = ap.parse_args()
     import torch
@@ -66,7 +71,15 @@ def main():
     torch.manual_seed(0)
     ws = O.splitk_workspace(1 << 25, 8192)
     for name in a.shapes.split(","):
-        n, h, w, cin, cout, k, sk = SHAPES[name]
+        if name in SHAPES:
+            n, h, w, cin, cout, k, sk = SHAPES[name]
+        else:  # ad-hoc "NxHxWxCINxCOUTkK" (3x3 / 1x1 / 7x7 stride 1, split auto), e.g. 1x30x40x256x256k3
+            import re
+            m = re.fullmatch(r"(\d+)x(\d+)x(\d+)x(\d+)x(\d+)k(\d)", name)
+            if not m:
+                raise SystemExit(f"unknown shape {name}")
+            n, h, w, cin, cout, k = map(int, m.groups())
+            sk = 0
         stride, k = (2, -k) if k < 0 else (1, k)
         x = torch.randn(n, h, w, cin, device="cuda").half()
         extra = dict(stride=stride)
@@ -114,10 +127,21 @@ def main():
                 continue
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(a.iters):
-                O.conv2d(x, wp, kpad, cout, k, k, **kw)
-            e1.record()
+            if a.graph:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for _ in range(a.iters):
+                        O.conv2d(x, wp, kpad, cout, k, k, **kw)
+                g.replay()
+                torch.cuda.synchronize()
+                e0.record()
+                g.replay()
+                e1.record()
+            else:
+                e0.record()
+                for _ in range(a.iters):
+                    O.conv2d(x, wp, kpad, cout, k, k, **kw)
+                e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) / a.iters * 1e3
             flop = 2.0 * n * h * w * cout * (3 if k == 7 else cin) * k * k

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Kernel-trace timelines of batch-1 frames (run under gpurun):  bash tools/gpu/r3_timeline.sh [tag]
+# For each model: tune once into a plan file, then a csv kernel trace of a few graph replays, summarised by
+# tools/timeline.py (frame span / busy / idle, per-iteration spans, critical chain).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+TAG=${1:-r3}
+mkdir -p gpurun_out/tl
+run() {  # name model iter-marker
+  local name=$1 model=$2 marker=$3
+  export SA_PLAN_CACHE=/tmp/sa_plan_$name.txt
+  timeout -k 10 180 python3 tools/run_engine.py --model $model --batch 1 --frames 20 > gpurun_out/tl/${TAG}_${name}_time.log 2>&1 || return 1
+  rm -rf /tmp/tl_$name
+  timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d /tmp/tl_$name -o run -- \
+    python3 tools/run_engine.py --model $model --batch 1 --frames 4 > gpurun_out/tl/${TAG}_${name}_prof.log 2>&1 || return 1
+  python3 tools/timeline.py /tmp/tl_$name --iter-marker "$marker" --chain 40 > gpurun_out/tl/${TAG}_${name}.txt 2>&1 || return 1
+  cp $(find /tmp/tl_$name -name "*kernel_trace.csv" | head -1) gpurun_out/tl/${TAG}_${name}_kernels.csv
+}
+run sf raftstereo-sceneflow motion_encoder && \
+run rt raftstereo-realtime motion_head && \
+run cre10 crestereo-iter10 "" && \
+echo done
