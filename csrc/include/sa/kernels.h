@@ -29,8 +29,11 @@ enum SaEpi {
   SA_EPI_GRU_Q = 2,     // q = tanh(acc+b+cq) ; h = (1-z)h + zq  (in place on h)
   SA_EPI_FLOW_ACC = 3,  // fp32 out[m*out_stride + c] += acc*scale + bias for c < min(Cout, out_stride)
   SA_EPI_STORE_F32 = 4,  // y = act(acc*scale + bias) -> fp32
-  SA_EPI_PROJ = 5        // y = act(acc*scale + bias) projected onto the taps of a following conv
+  SA_EPI_PROJ = 5,       // y = act(acc*scale + bias) projected onto the taps of a following conv
                          // (proj_* fields; y itself is stored only when out != NULL)
+  SA_EPI_GRU_ZRQ = 6     // Cout = 3 Hd stacked [convz | convr | convq restricted to the x inputs]: z -> aux,
+                         // r*h -> rh as SA_EPI_GRU_ZR, and the x half of q's pre-activation (acc + bias + cq)
+                         // -> out (fp16); the following SA_EPI_GRU_Q conv over r*h alone adds it back (res)
 };
 
 typedef struct {
@@ -53,7 +56,7 @@ typedef struct {
   int32_t epi, act, act2;
   float alpha;  // leaky slope
   float scale;  // multiplies acc before bias
-  const void* res;  // residual fp16 (SA_EPI_STORE)
+  const void* res;  // residual fp16 (SA_EPI_STORE); SA_EPI_GRU_Q: pre-activation addend (the ZRQ conv's out)
   int32_t res_stride;
   const void* ctx;  // GRU context biases fp16: ZR reads [cz | cr], Q reads cq (NULL = none)
   int32_t ctx_stride;

@@ -1469,8 +1469,8 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
           const int t = PF * cc + j;
           if (t < np) pout[(size_t)t * p.proj_plane] = y[j];
         }
-      } else if (p.epi == SA_EPI_GRU_ZR) {
-        const int Hd = p.Cout >> 1;
+      } else if (p.epi == SA_EPI_GRU_ZR || p.epi == SA_EPI_GRU_ZRQ) {
+        const int Hd = p.epi == SA_EPI_GRU_ZR ? p.Cout >> 1 : p.Cout / 3;
         float c8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         if (p.ctx) load8(reinterpret_cast<const f16*>(p.ctx) + (size_t)m * p.ctx_stride + co, c8);
         if (co < Hd) {
@@ -1478,17 +1478,29 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
 #pragma unroll
           for (int j = 0; j < 8; ++j) z[j] = sigmoidf_(v[j] + c8[j]);
           store8(reinterpret_cast<f16*>(p.aux) + (size_t)m * p.aux_stride + co, z);
-        } else {
+        } else if (co < 2 * Hd) {
           const int ch = co - Hd;
           float h8[8], rh[8];
           load8(reinterpret_cast<const f16*>(p.hbuf) + (size_t)m * p.h_stride + ch, h8);
 #pragma unroll
           for (int j = 0; j < 8; ++j) rh[j] = sigmoidf_(v[j] + c8[j]) * h8[j];
           store8(reinterpret_cast<f16*>(p.rh) + (size_t)m * p.rh_stride + ch, rh);
+        } else {
+          // SA_EPI_GRU_ZRQ: the x-input half of convq's pre-activation (+ its bias and context) for the q conv
+          float q8[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) q8[j] = v[j] + c8[j];
+          store8(reinterpret_cast<f16*>(p.out) + (size_t)m * p.out_stride + (co - 2 * Hd), q8);
         }
       } else if (p.epi == SA_EPI_GRU_Q) {
         float c8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, z8[8], h8[8];
         if (p.ctx) load8(reinterpret_cast<const f16*>(p.ctx) + (size_t)m * p.ctx_stride + co, c8);
+        if (p.res) {  // the x half of the pre-activation, computed by the SA_EPI_GRU_ZRQ conv
+          float x8[8];
+          load8(reinterpret_cast<const f16*>(p.res) + (size_t)m * p.res_stride + co, x8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) c8[j] += x8[j];
+        }
         load8(reinterpret_cast<const f16*>(p.aux) + (size_t)m * p.aux_stride + co, z8);
         f16* hp = reinterpret_cast<f16*>(p.hbuf) + (size_t)m * p.h_stride + co;
         load8(hp, h8);

@@ -100,7 +100,7 @@ struct AttnLayer {
 // per-resolution state of the cascaded update
 struct Level {
   int h = 0, w = 0;
-  Tensor net, xin, corr, cor1, corflo, flo1, flowfeat, z, rh, fh, mask;
+  Tensor net, xin, corr, cor1, corflo, flo1, flowfeat, z, rh, fh, mask, qx;
   float* flow = nullptr;
   void build(DeviceArena& a, int B, int h_, int w_) {
     h = h_;
@@ -116,6 +116,7 @@ struct Level {
     rh = make_tensor(a, B, h, w, 128);
     fh = make_tensor(a, B, h, w, 512);
     mask = make_tensor(a, B, h, w, 144);
+    qx = make_tensor(a, B, h, w, 128);
     flow = (float*)a.alloc((size_t)B * h * w * 2 * 4);
   }
 };
@@ -142,6 +143,10 @@ class CreStereo : public StereoEngine {
   ConvLayer fconv2_, offc8_, offc16_;
   AttnLayer self_, cross_;
   ConvLayer convc1_, convc2_, convf1_, convf2_, mconv_, zr_[2], q_[2], fh1_, fh1mask_, fh2_, mask2_;
+  // SepConvGRU with q's x-input half hoisted into the z/r conv (SA_EPI_GRU_ZRQ; see raft_stereo.cpp gzrq_): the q
+  // conv on the recurrent chain reads r*h alone (K = 5 x 128 instead of 5 x 384).  SA_CRE_GRU_SPLIT=0: z/r + q.
+  ConvLayer zrq_[2], qh_[2];
+  bool gru_split_ = !std::getenv("SA_CRE_GRU_SPLIT") || std::atoi(std::getenv("SA_CRE_GRU_SPLIT")) != 0;
   Level lv_[3];  // 0: 1/4, 1: 1/8, 2: 1/16
   // SA_CRE_FH2_PROJ=0: flow-head conv2 as the N=2 implicit GEMM instead of tap projection + stencil
   bool fh2_proj_ = !std::getenv("SA_CRE_FH2_PROJ") || std::atoi(std::getenv("SA_CRE_FH2_PROJ")) != 0;
@@ -217,6 +222,26 @@ void CreStereo::build(WeightSource& src) {
     ConvSpec sp;  // (1,5) pad (0,2) / (5,1) pad (2,0)
     zr_[d].build(a, ws, {u + "gru.convz" + sfx, u + "gru.convr" + sfx}, {{128, 128}, {256, 256}}, sp);
     q_[d].build(a, ws, {u + "gru.convq" + sfx}, {{128, 128}, {256, 256}}, sp);
+    if (gru_split_) {
+      // convq [128][384][kh][kw] -> x half (h taps zeroed, bias kept) and h half [128][128][kh][kw] (no bias)
+      const std::string qn = u + "gru.convq" + sfx;
+      const HostTensor& wq = ws.get(qn + ".weight");
+      const int taps = 5;
+      HostTensor qxw = wq, qhw;
+      qhw.shape = {128, 128, wq.shape[2], wq.shape[3]};
+      qhw.data.resize((size_t)128 * 128 * taps);
+      for (int o = 0; o < 128; ++o)
+        for (int c = 0; c < 128; ++c)
+          for (int t = 0; t < taps; ++t) {
+            qhw.data[((size_t)o * 128 + c) * taps + t] = wq.data[((size_t)o * 384 + c) * taps + t];
+            qxw.data[((size_t)o * 384 + c) * taps + t] = 0.f;
+          }
+      src.ws->put(qn + "@x.weight", std::move(qxw));
+      src.ws->put(qn + "@x.bias", ws.get(qn + ".bias"));
+      src.ws->put(qn + "@h.weight", std::move(qhw));
+      zrq_[d].build(a, ws, {u + "gru.convz" + sfx, u + "gru.convr" + sfx, qn + "@x"}, {{128, 128}, {256, 256}}, sp);
+      qh_[d].build(a, ws, {qn + "@h"}, {{128, 128}}, sp);
+    }
   }
   src.conv(u + "flow_head.conv1", 256, 128, 3, 3);
   src.conv(u + "flow_head.conv2", 2, 256, 3, 3);
@@ -284,7 +309,27 @@ void CreStereo::update(hipStream_t s, Level& L, const Tensor& f1, const Tensor& 
   convf2_.run(s, {L.flo1}, L.corflo.slice_c(192, 64), SA_ACT_RELU);
   mconv_.run(s, {L.corflo}, L.xin.slice_c(128, 126), SA_ACT_RELU);
   // SepConvGRU: horizontal then vertical; z/r and q gates fused into the conv epilogues
-  for (int d = 0; d < 2; ++d) {
+  for (int d = 0; d < 2 && gru_split_; ++d) {
+    SaConvArgs za = zrq_[d].args({L.net, L.xin}, L.qx);
+    za.epi = SA_EPI_GRU_ZRQ;
+    za.aux = L.z.ptr;
+    za.aux_stride = L.z.stride;
+    za.hbuf = L.net.ptr;
+    za.h_stride = L.net.stride;
+    za.rh = L.rh.ptr;
+    za.rh_stride = L.rh.stride;
+    zrq_[d].launch(s, za);
+    SaConvArgs qa = qh_[d].args({L.rh}, L.net);
+    qa.epi = SA_EPI_GRU_Q;
+    qa.res = L.qx.ptr;
+    qa.res_stride = L.qx.stride;
+    qa.aux = L.z.ptr;
+    qa.aux_stride = L.z.stride;
+    qa.hbuf = L.net.ptr;
+    qa.h_stride = L.net.stride;
+    qh_[d].launch(s, qa);
+  }
+  for (int d = 0; d < 2 && !gru_split_; ++d) {
     SaConvArgs za = zr_[d].args({L.net, L.xin}, L.z);
     za.epi = SA_EPI_GRU_ZR;
     za.aux = L.z.ptr;

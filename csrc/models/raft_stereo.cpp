@@ -89,6 +89,14 @@ class RaftStereo : public StereoEngine {
   // update block
   ConvLayer convc1_, convc2_, convf1_, convf2_, mconv_;
   ConvLayer gzr_[3], gq_[3];
+  // ConvGRU with q's x-input half hoisted into the z/r conv (SA_EPI_GRU_ZRQ): gzrq_ = [convz | convr | convq with
+  // its h-input taps zeroed] over [h, x] (Cout 3 hd), gqh_ = convq's h-input taps over r*h alone (K = 9 hd instead
+  // of 9 (hd + x)), qx_ = the hoisted x half of q's pre-activation.  Same sums, regrouped: the q conv on the
+  // recurrent chain gets 3x shorter, the z/r conv gets a third more columns (more workgroups at batch 1).
+  // SA_RAFT_GRU_SPLIT=0 restores the z/r + q pair.
+  ConvLayer gzrq_[3], gqh_[3];
+  Tensor qx_[3];
+  bool gru_split_ = !std::getenv("SA_RAFT_GRU_SPLIT") || std::atoi(std::getenv("SA_RAFT_GRU_SPLIT")) != 0;
   ConvLayer fh1_, fh1mask_, fh2_, mask2_;
   Tensor corr_feat_, flow_feat_, cor1_, flo1_, corflo_, motion_;
   Tensor z_[3], rh_[3];
@@ -294,6 +302,26 @@ void RaftStereo::build(WeightSource& src) {
     gq_[i].build(a, ws, {p + ".convq"}, segs, s3);
     z_[i] = make_tensor(a, Bn, lh_[i], lw_[i], hd);
     rh_[i] = make_tensor(a, Bn, lh_[i], lw_[i], hd);
+    if (gru_split_) {
+      // convq [hd][hd + xin][3][3] -> x half (h taps zeroed, bias kept) and h half [hd][hd][3][3] (no bias)
+      const HostTensor& wq = ws.get(p + ".convq.weight");
+      const int ci = hd + xin;
+      HostTensor qxw = wq, qhw;
+      qhw.shape = {hd, hd, 3, 3};
+      qhw.data.resize((size_t)hd * hd * 9);
+      for (int o = 0; o < hd; ++o)
+        for (int c = 0; c < hd; ++c)
+          for (int t = 0; t < 9; ++t) {
+            qhw.data[((size_t)o * hd + c) * 9 + t] = wq.data[((size_t)o * ci + c) * 9 + t];
+            qxw.data[((size_t)o * ci + c) * 9 + t] = 0.f;
+          }
+      src.ws->put(p + ".convq@x.weight", std::move(qxw));
+      src.ws->put(p + ".convq@x.bias", ws.get(p + ".convq.bias"));
+      src.ws->put(p + ".convq@h.weight", std::move(qhw));
+      gzrq_[i].build(a, ws, {p + ".convz", p + ".convr", p + ".convq@x"}, segs, s3);
+      gqh_[i].build(a, ws, {p + ".convq@h"}, {{hd, hd}}, s3);
+      qx_[i] = make_tensor(a, Bn, lh_[i], lw_[i], hd);
+    }
   }
   const int f = 1 << rc_.n_downsample;
   src.conv(u + "flow_head.conv1", 256, hd, 3, 3);
@@ -346,6 +374,30 @@ void RaftStereo::build(WeightSource& src) {
 void RaftStereo::gru(hipStream_t s, int i, const std::vector<Tensor>& x) const {
   std::vector<Tensor> srcs = {net_[i]};
   srcs.insert(srcs.end(), x.begin(), x.end());
+  if (gru_split_) {
+    SaConvArgs za = gzrq_[i].args(srcs, qx_[i]);
+    za.epi = SA_EPI_GRU_ZRQ;
+    za.ctx = czrq_[i].ptr;  // [cz | cr | cq]
+    za.ctx_stride = czrq_[i].stride;
+    za.aux = z_[i].ptr;
+    za.aux_stride = z_[i].stride;
+    za.hbuf = net_[i].ptr;
+    za.h_stride = net_[i].stride;
+    za.rh = rh_[i].ptr;
+    za.rh_stride = rh_[i].stride;
+    gzrq_[i].launch(s, za);
+    SaConvArgs qa = gqh_[i].args({rh_[i]}, net_[i]);
+    qa.epi = SA_EPI_GRU_Q;
+    qa.ctx = nullptr;  // cq and convq's bias are in qx
+    qa.res = qx_[i].ptr;
+    qa.res_stride = qx_[i].stride;
+    qa.aux = z_[i].ptr;
+    qa.aux_stride = z_[i].stride;
+    qa.hbuf = net_[i].ptr;
+    qa.h_stride = net_[i].stride;
+    gqh_[i].launch(s, qa);
+    return;
+  }
   SaConvArgs za = gzr_[i].args(srcs, z_[i]);
   za.epi = SA_EPI_GRU_ZR;
   za.ctx = czrq_[i].ptr;
@@ -401,28 +453,47 @@ void RaftStereo::forward(hipStream_t s) {
   Tensor x = cnet_.out().slice_n(0, Bn);
   Tensor lvl_in[3];
   lvl_in[0] = x;
+  auto heads = [&](hipStream_t st, int i) {  // hidden state, context and its z/r/q biases of level i
+    Tensor hin[2] = {lvl_in[i], lvl_in[i]};
+    if (i < 2) {
+      head_rb_[i][0].run(st, sp_, lvl_in[i]);
+      head_rb_[i][1].run(st, sp_, lvl_in[i]);
+      hin[0] = head_rb_[i][0].out;
+      hin[1] = head_rb_[i][1].out;
+    }
+    head_conv_[i][0].run(st, {hin[0]}, net_[i], SA_ACT_TANH);
+    head_conv_[i][1].run(st, {hin[1]}, ctxh_[i], SA_ACT_RELU);
+    zqr_[i].run(st, {ctxh_[i]}, czrq_[i]);
+  };
+  // The context heads of the finer levels only need their level's input: at batch 1 their ~15 small convs
+  // (38-150 workgroups each) are latency-bound, so they run on side2 beside the coarser trunk layers
+  // (level 0 after the trunk, level 1 after layer4; main: layer4, layer5, level-2 heads).  Events 5-7.
+  const bool par_heads = par && rc_.n_gru >= 2;
+  if (par_heads) rec(s, 5);
+  if (par_heads) {
+    ScopedSplitK k2(&splitk_side2_);
+    wait(side2_, 5);
+    heads(side2_, 0);
+  }
   if (rc_.n_gru >= 2) {
     layer4_[0].run(s, sp_, x);
     layer4_[1].run(s, sp_, layer4_[0].out);
     lvl_in[1] = layer4_[1].out;
+  }
+  if (par_heads) {
+    rec(s, 6);
+    ScopedSplitK k2(&splitk_side2_);
+    wait(side2_, 6);
+    heads(side2_, 1);
+    rec(side2_, 7);
   }
   if (rc_.n_gru >= 3) {
     layer5_[0].run(s, sp_, lvl_in[1]);
     layer5_[1].run(s, sp_, layer5_[0].out);
     lvl_in[2] = layer5_[1].out;
   }
-  for (int i = 0; i < rc_.n_gru; ++i) {
-    Tensor hin[2] = {lvl_in[i], lvl_in[i]};
-    if (i < 2) {
-      head_rb_[i][0].run(s, sp_, lvl_in[i]);
-      head_rb_[i][1].run(s, sp_, lvl_in[i]);
-      hin[0] = head_rb_[i][0].out;
-      hin[1] = head_rb_[i][1].out;
-    }
-    head_conv_[i][0].run(s, {hin[0]}, net_[i], SA_ACT_TANH);
-    head_conv_[i][1].run(s, {hin[1]}, ctxh_[i], SA_ACT_RELU);
-    zqr_[i].run(s, {ctxh_[i]}, czrq_[i]);
-  }
+  for (int i = par_heads ? 2 : 0; i < rc_.n_gru; ++i) heads(s, i);
+  if (par_heads) wait(s, 7);
   if (par) join(s);
   device_zero(flow_, (size_t)Bn * h0 * w0 * 4, s);
   stage(s, "encoders+corr");
@@ -544,14 +615,110 @@ void RaftStereo::forward(hipStream_t s) {
   const int f = 1 << rc_.n_downsample;
   // 0 = off, 1 = G32 ahead, 2 = G32 + G16 ahead (default below batch 4)
   const int pmode = pipeline_mode_ >= 0 ? pipeline_mode_ : 2;
-  SA_REQUIRE(pmode >= 0 && pmode <= 3, "SA_RAFT_PIPELINE=%d (0..3)", pmode);
+  SA_REQUIRE(pmode >= 0 && pmode <= 4, "SA_RAFT_PIPELINE=%d (0..4)", pmode);
   const bool pipe = par && pmode > 0 && rc_.n_gru == 3 && !rc_.slow_fast;
+  // realtime preset (2 levels, slow-fast): the chain G08(t) -> pool -> G16 -> G16 -> interp -> G08(t + 1) on the
+  // main stream, flow head + motion encoder beside it (the same structure as pipeline mode 4)
+  const bool rt_pipe = par && pmode >= 3 && rc_.n_gru == 2 && rc_.slow_fast;
   // finest GRU (interp + z/r + q) and flow head as two halves, for the deeper pipeline
   auto fine = [&]() {
     interp(s, 0);
     gru(s, 0, {motion_, interp_[0]});
   };
-  if (pipe && pmode == 3) {
+  if (rt_pipe) {
+    // the slow-fast update runs the 1/16 GRU twice on the same pooled 1/8 state (net0 is unchanged between the
+    // two calls), so the pooling is done once per iteration
+    auto g16x2 = [&]() {
+      pool(s, 0);
+      gru(s, 1, {pool_[0]});
+      gru(s, 1, {pool_[0]});
+    };
+    auto head = [&](hipStream_t st, bool last) {
+      if (last) fh1mask_.run(st, {net_[0]}, fh_, SA_ACT_RELU);
+      else fh1_.run(st, {net_[0]}, fh_.slice_c(0, 256), SA_ACT_RELU);
+      check(sa_flow_head_tail(fh_.ptr, fh_.stride, 256, fh2_w16_, proj_b_, flow_, Bn, h0, w0, st), "flow-head tail");
+      if (last) mask2_.run(st, {fh_.slice_c(256, 256)}, mask_);
+    };
+    SA_REQUIRE(fh2_proj_ && fh_tail_, "realtime pipeline needs the flow-head tail kernel");
+    rec(s, 4);
+    {
+      ScopedSplitK k1(&splitk_side_);
+      wait(side_, 4);
+      motion(side_);
+      rec(side_, 3);
+    }
+    g16x2();
+    for (int it = 0; it < rc_.iters; ++it) {
+      const bool last = it == rc_.iters - 1;
+      interp(s, 0);
+      wait(s, 3);
+      gru(s, 0, {motion_, interp_[0]});
+      rec(s, 4);
+      if (!last) g16x2();
+      {
+        ScopedSplitK k1(&splitk_side_);
+        wait(side_, 4);
+        head(side_, last);
+        if (!last) motion(side_);
+        rec(side_, last ? 1 : 3);
+      }
+    }
+    wait(s, 1);
+  } else if (pipe && pmode == 4) {
+    // Mode 3's dependencies, captured so that at every fork of the chain the on-chain successor is captured
+    // before the off-chain one (in the b1 timeline the successor captured second started ~13 us after its
+    // producer, the first ~5 us): the interp of net1(t) forks G08(t) (main) and G32(t + 1) (side2); G08 q(t)
+    // forks G16(t + 1) (main) and FH(t) + M(t + 1) (side).
+    auto fh = [&](hipStream_t st, bool last) {
+      if (last) fh1mask_.run(st, {net_[0]}, fh_, SA_ACT_RELU);
+      else fh1_.run(st, {net_[0]}, fh_.slice_c(0, 256), SA_ACT_RELU);
+      check(sa_flow_head_tail(fh_.ptr, fh_.stride, 256, fh2_w16_, proj_b_, flow_, Bn, h0, w0, st), "flow-head tail");
+      if (last) mask2_.run(st, {fh_.slice_c(256, 256)}, mask_);
+    };
+    SA_REQUIRE(fh2_proj_ && fh_tail_, "pipeline mode 4 needs the flow-head tail kernel");
+    rec(s, 0);
+    rec(s, 4);
+    {
+      ScopedSplitK k2(&splitk_side2_);
+      wait(side2_, 0);
+      gru32(side2_);
+      rec(side2_, 2);
+    }
+    {
+      ScopedSplitK k1(&splitk_side_);
+      wait(side_, 4);
+      motion(side_);
+      rec(side_, 3);
+    }
+    wait(s, 2);
+    gru16(s);
+    for (int it = 0; it < rc_.iters; ++it) {
+      const bool last = it == rc_.iters - 1;
+      interp(s, 0);
+      rec(s, 0);
+      wait(s, 3);
+      gru(s, 0, {motion_, interp_[0]});
+      rec(s, 4);
+      if (!last) {
+        {
+          ScopedSplitK k2(&splitk_side2_);
+          wait(side2_, 0);
+          gru32(side2_);
+          rec(side2_, 2);
+        }
+        wait(s, 2);
+        gru16(s);
+      }
+      {
+        ScopedSplitK k1(&splitk_side_);
+        wait(side_, 4);
+        fh(side_, last);
+        if (!last) motion(side_);
+        rec(side_, last ? 1 : 3);
+      }
+    }
+    wait(s, 1);
+  } else if (pipe && pmode == 3) {
     // Critical-chain schedule (b1 timeline, profiles/timeline_r03.md).  The update's inherent recurrence is
     // G16(t) -> G08(t) -> G16(t + 1) (the 1/8 level pools net0(t), the 1/4 level interpolates net1(t)), so that
     // chain stays on ONE stream -- consecutive kernels of one queue start back to back, a cross-stream event edge

@@ -714,6 +714,13 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
     t.aux = scratch;
     t.rh = scratch + (((size_t)Mo * width * 2 + 255) & ~(size_t)255);
   }
+  if (t.epi == SA_EPI_GRU_ZRQ) {  // qx, z and r*h (fp16, <= 2/3 of the width each) in disjoint thirds
+    const size_t third = ((size_t)Mo * width * 4 / 3) & ~(size_t)255;
+    SA_REQUIRE((size_t)Mo * std::max({a.out_stride, a.aux_stride, a.rh_stride}) * 2 <= third, "ZRQ tuning scratch");
+    t.out = scratch;
+    t.aux = scratch + third;
+    t.rh = scratch + 2 * third;
+  }
   if (t.epi == SA_EPI_GRU_Q) t.hbuf = scratch;
   // Tactic verification: every candidate's output (from zeroed scratch, so in-place epilogues start from
   // the same state) is compared with the first candidate's; one that disagrees is logged and never chosen.

@@ -120,7 +120,7 @@ class SaEwArgs(C.Structure):
 
 
 ACT = {"none": 0, "relu": 1, "leaky": 2, "tanh": 3, "sigmoid": 4, "relu6": 5}
-EPI = {"store": 0, "gru_zr": 1, "gru_q": 2, "flow_acc": 3, "store_f32": 4, "proj": 5}
+EPI = {"store": 0, "gru_zr": 1, "gru_q": 2, "flow_acc": 3, "store_f32": 4, "proj": 5, "gru_zrq": 6}
 PRE = {"raw": 0, "unit": 1, "imagenet": 2, "signed": 3}
 
 _i = C.c_int

@@ -274,6 +274,76 @@ class FastACVNetPlus(nn.Module):
         return context_upsample(pred, spx_pred) * 4
 
 
+def near_tie_mask(m: FastACVNetPlus, left, right, rel: float = 2e-2):
+    """Forward pass plus a full-resolution mask of the pixels whose result hangs on a near-tie selection:
+    the attention top-k cut (the k-th and (k+1)-th probabilities within ``rel``) or the final top-2 cut (the
+    2nd and 3rd cost logits within ``rel`` of the logit spread) of any 1/4-resolution pixel in the 3x3
+    neighbourhood the superpixel upsampling reads.  An implementation with other rounding may pick the other
+    candidate there; elsewhere it must track the oracle.  Returns (disparity [B,H,W], mask [B,H,W])."""
+    fl, fr = m.feature_up(m.feature(left), m.feature(right))
+    stem_2x, stem_2y = m.stem_2(left), m.stem_2(right)
+    stem_4x, stem_4y = m.stem_4(stem_2x), m.stem_4(stem_2y)
+    fl[0] = torch.cat((fl[0], stem_4x), 1)
+    fr[0] = torch.cat((fr[0], stem_4y), 1)
+    match_l, match_r = m.desc(m.conv(fl[0])), m.desc(m.conv(fr[0]))
+    corr = m.corr_stem(norm_correlation_volume(match_l, match_r, m.maxdisp // 4))
+    att_weights = m.hourglass_att(m.corr_feature_att_4(corr, fl[0]), fl)
+    prob = F.softmax(att_weights, dim=2)
+    sp, ind = prob.sort(dim=2, descending=True, stable=True)
+    k = m.topk
+    tie = (sp[:, 0, k - 1] - sp[:, 0, k]) <= rel * sp[:, 0, k - 1]
+    ind_k = ind[:, :, :k].sort(2, False)[0]
+    att_topk = torch.gather(prob, 2, ind_k)
+    samples = ind_k.squeeze(1).float()
+    cl, cr = m.concat_feature(fl[0]), m.concat_feature(fr[0])
+    vol = torch.cat((cl.unsqueeze(2).expand(-1, -1, samples.shape[1], -1, -1), warp_right(cr, samples)), 1)
+    vol = m.concat_feature_att_4(m.concat_stem(att_topk * vol), fl[0])
+    cost = m.hourglass(vol, fl).squeeze(1)
+    sc, ci = cost.sort(dim=1, descending=True, stable=True)
+    spread = (sc[:, 0] - sc[:, -1]).clamp_min(1e-12)
+    tie = tie | ((sc[:, 1] - sc[:, 2]) <= rel * spread)
+    pi = ci[:, :2]
+    p2 = F.softmax(torch.gather(cost, 1, pi), 1)
+    pred = (torch.gather(samples, 1, pi) * p2).sum(1, keepdim=True)
+    xspx = m.spx_2(m.spx_4(fl[0]), stem_2x)
+    spx_pred = F.softmax(m.spx(xspx), 1)
+    disp = context_upsample(pred, spx_pred) * 4
+    tie = F.max_pool2d(tie.float().unsqueeze(1), 3, 1, 1)  # the upsampling reads each 1/4 pixel's 3x3 neighbours
+    tie = F.interpolate(tie, scale_factor=4, mode="nearest")[:, 0] > 0
+    return disp, tie
+
+
+def forward_forced(m: FastACVNetPlus, left, right, samples, top2=None):
+    """Teacher-forced forward pass: every continuous stage is computed here in fp32 from the images, the two
+    discrete selections are taken from the caller -- ``samples`` [B,k,h,w] (the top-k disparity indices,
+    ascending) and optionally ``top2`` [B,2,h,w] (the candidate slots of the final regression; default: this
+    pass's own top-2).  Returns (disparity [B,H,W], attention logits [B,D,h,w], cost logits [B,k,h,w]) so a test
+    can check that the forced selections are legitimate top-k / top-2 choices of the oracle's own logits (up to
+    a near-tie tolerance) and that everything else tracks the oracle end to end."""
+    fl, fr = m.feature_up(m.feature(left), m.feature(right))
+    stem_2x, stem_2y = m.stem_2(left), m.stem_2(right)
+    stem_4x, stem_4y = m.stem_4(stem_2x), m.stem_4(stem_2y)
+    fl[0] = torch.cat((fl[0], stem_4x), 1)
+    fr[0] = torch.cat((fr[0], stem_4y), 1)
+    match_l, match_r = m.desc(m.conv(fl[0])), m.desc(m.conv(fr[0]))
+    corr = m.corr_stem(norm_correlation_volume(match_l, match_r, m.maxdisp // 4))
+    att_weights = m.hourglass_att(m.corr_feature_att_4(corr, fl[0]), fl)
+    prob = F.softmax(att_weights, dim=2)
+    ind_k = samples.long().unsqueeze(1)
+    att_topk = torch.gather(prob, 2, ind_k)
+    samples = samples.float()
+    cl, cr = m.concat_feature(fl[0]), m.concat_feature(fr[0])
+    vol = torch.cat((cl.unsqueeze(2).expand(-1, -1, samples.shape[1], -1, -1), warp_right(cr, samples)), 1)
+    vol = m.concat_feature_att_4(m.concat_stem(att_topk * vol), fl[0])
+    cost = m.hourglass(vol, fl).squeeze(1)
+    pi = top2.long() if top2 is not None else cost.sort(dim=1, descending=True, stable=True)[1][:, :2]
+    p2 = F.softmax(torch.gather(cost, 1, pi), 1)
+    pred = (torch.gather(samples, 1, pi) * p2).sum(1, keepdim=True)
+    xspx = m.spx_2(m.spx_4(fl[0]), stem_2x)
+    spx_pred = F.softmax(m.spx(xspx), 1)
+    return context_upsample(pred, spx_pred) * 4, att_weights[:, 0], cost
+
+
 def build(preset: str = "fastacvnet-plus", seed: int = 0) -> FastACVNetPlus:
     torch.manual_seed(seed)
     m = FastACVNetPlus(**PRESETS[preset]).eval()

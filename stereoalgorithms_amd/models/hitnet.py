@@ -275,6 +275,67 @@ class HITNet(nn.Module):
         return expand_final(h, 1)
 
 
+def scale_init(m: HITNet, gain: float = (6.0 / (1 + SLOPE ** 2)) ** 0.5) -> HITNet:
+    """Variance-preserving init for the full-configuration tests: PyTorch's default conv init (uniform with
+    var 1 / (3 fan_in)) shrinks a leaky-ReLU signal ~2.4x per layer, so after the 14-layer feature U-Net the
+    coarse features of a random network are ~1e-7 -- below fp16's normal range -- and every tile-init argmin
+    compares noise.  Multiplying the feature and tile-embedding weights by sqrt(6 / (1 + slope^2)) (He init for
+    leaky ReLU) keeps the features O(1), so the fp16 engine and the fp32 oracle see the same matching problem.
+    The update networks keep the default init (their outputs are deltas on the hypotheses)."""
+    with torch.no_grad():
+        for mod in list(m.feature.modules()) + [t.tile for t in m.init]:
+            if isinstance(mod, (nn.Conv2d, nn.ConvTranspose2d)):
+                mod.weight.mul_(gain)
+    return m
+
+
+def near_tie_mask(m: HITNet, x6, rel: float = 1e-2, eps: float = 0.0):
+    """Full-resolution mask of the pixels whose result hangs on a near-tie decision of the network: the tile-init
+    argmin of any ancestor tile whose best two costs are within ``rel * cost + eps``, or the confidence argmax
+    of any ancestor tile whose two candidates' confidences are within ``rel * |conf| + eps``.  An implementation
+    that rounds differently (fp16 operands, another summation order) may legitimately decide those the other
+    way; everywhere else its disparity must track the oracle's.  Returns (disparity [B,H,W], mask [B,H,W])."""
+    b, _, H, W = x6.shape
+    e = m.feature(torch.cat((x6[:, :3], x6[:, 3:]), 0))
+    el = [t[:b] for t in e]
+    er = [t[b:] for t in e]
+    tie = torch.zeros(b, H, W, dtype=torch.bool, device=x6.device)
+
+    def mark(mask_tiles, l):  # level-l 4x4 tiles cover (4 << l)^2 input pixels
+        f = 4 << l
+        up = mask_tiles.repeat_interleave(f, 1).repeat_interleave(f, 2)[:, :H, :W]
+        tie[:, :up.shape[1], :up.shape[2]] |= up
+
+    h = None
+    for l in range(HYP_LEVELS - 1, -1, -1):
+        tl, tr = m.init[l].tiles(el[l], er[l])
+        nd = m.maxdisp >> l
+        wr = tr.shape[-1]
+        xs = torch.arange(tl.shape[-1], device=tl.device) * 4
+        costs = []
+        for d in range(nd):
+            j = xs - d
+            valid = (j >= 0) & (j < wr)
+            cst = (tl - tr[..., j.clamp(0, wr - 1)]).abs().sum(1)
+            costs.append(torch.where(valid.view(1, 1, -1), cst, torch.full_like(cst, float("inf"))))
+        two = torch.stack(costs, 1).topk(2, dim=1, largest=False).values
+        mark((two[:, 1] - two[:, 0]) <= rel * two[:, 0].abs() + eps, l)
+        hi = m.init[l](el[l], er[l], nd)
+        cands = [hi] if h is None else [upsample_hyp(h), hi]
+        outs, confs = m.prop[l]([warp_cost(el[l], er[l], c) for c in cands], cands)
+        best, conf = outs[0], confs[0]
+        for o, cf in zip(outs[1:], confs[1:]):
+            mark(((cf - conf).abs() <= rel * conf.abs() + eps)[:, 0], l)
+            take = cf > conf
+            best = torch.where(take, o, best)
+            conf = torch.where(take, cf, conf)
+        h = best
+    for t, net in zip((2, 1), m.refine):
+        h = split_hyp(h, 2 * t)
+        (h,), _ = net([warp_cost(el[0], er[0], h, t)], [h])
+    return expand_final(h, 1), tie
+
+
 def build(preset: str = "hitnet-d400", seed: int = 0) -> HITNet:
     torch.manual_seed(seed)
     return HITNet(**PRESETS[preset]).eval()

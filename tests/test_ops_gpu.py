@@ -596,6 +596,44 @@ def test_conv2d_gru_epilogues():
     assert rel_err(nchw(net_h), ref) < 3e-3
 
 
+@pytest.mark.parametrize("cfg,splitk", [(-1, 1), (5, 1), (4, 1), (16, 2), (7, 3)])
+def test_conv2d_gru_zrq_split(cfg, splitk):
+    """ConvGRU with q's x-input half hoisted into the z/r conv (SA_EPI_GRU_ZRQ, Cout = 3 hd, q's h-input weights
+    zeroed there) and the q conv over r*h alone adding it back (SA_EPI_GRU_Q + res), against the fp32 GRU."""
+    O = ops()
+    torch.manual_seed(5)
+    n, hd, h, w = 1, 128, 30, 40
+    net = torch.randn(n, hd, h, w, device=DEV).tanh()
+    x = torch.randn(n, 256, h, w, device=DEV)
+    cz, cr, cq = (torch.randn(n, hd, h, w, device=DEV) * 0.5 for _ in range(3))
+    wz, wr, wq = (torch.randn(hd, hd + 256, 3, 3, device=DEV) / math.sqrt((hd + 256) * 9) for _ in range(3))
+    bz, br, bq = (torch.randn(hd, device=DEV) * 0.1 for _ in range(3))
+    hx = torch.cat([net, x], 1).half().float()
+    z = torch.sigmoid(F.conv2d(hx, wz.half().float(), bz, padding=1) + cz.half().float())
+    r = torch.sigmoid(F.conv2d(hx, wr.half().float(), br, padding=1) + cr.half().float())
+    rh = (r * net.half().float()).half().float()
+    q = torch.tanh(F.conv2d(torch.cat([rh, x.half().float()], 1), wq.half().float(), bq, padding=1) + cq.half().float())
+    ref = (1 - z) * net.half().float() + z * q
+
+    net_h = nhwc(net).half()
+    ctx = nhwc(torch.cat([cz, cr, cq], 1)).half()
+    xh = nhwc(x).half()
+    wqx = wq.clone()
+    wqx[:, :hd] = 0
+    wzrq, kpad, _ = O.pack_conv_weight(torch.cat([wz, wr, wqx], 0))
+    wqh, kph, _ = O.pack_conv_weight(wq[:, :hd].contiguous())
+    zb = torch.empty(n, h, w, hd, device=DEV, dtype=torch.float16)
+    rhb = torch.empty_like(zb)
+    qx = torch.empty_like(zb)
+    ws = O.splitk_workspace(1 << 22, 4096) if splitk != 1 else None
+    O.conv2d([net_h, xh], wzrq, kpad, 3 * hd, 3, 3, bias=torch.cat([bz, br, bq]).contiguous(), out=qx,
+             epi="gru_zrq", ctx=ctx, aux=zb, hbuf=net_h, rh=rhb, tile_cfg=cfg, splitk=splitk, workspace=ws)
+    O.conv2d([rhb], wqh, kph, hd, 3, 3, out=net_h, epi="gru_q", res=qx, aux=zb, hbuf=net_h, tile_cfg=cfg)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(zb), z) < 3e-3
+    assert rel_err(nchw(net_h), ref) < 4e-3
+
+
 def test_conv2d_flow_acc_and_stats():
     O = ops()
     torch.manual_seed(4)

@@ -19,14 +19,23 @@ MODES = [
     ("pipeline1", {"SA_RAFT_PIPELINE": "1"}),
     ("pipeline2", {"SA_RAFT_PIPELINE": "2"}),
     ("pipeline3", {"SA_RAFT_PIPELINE": "3"}),
+    ("pipeline4", {"SA_RAFT_PIPELINE": "4"}),
     ("unfused-motion-encoder", {"SA_RAFT_PARALLEL": "0", "SA_RAFT_FUSE_MENC": "0"}),
 ]
 TOL = {"unfused-motion-encoder": 1e-2}
 KNOBS = ("SA_RAFT_PARALLEL", "SA_RAFT_PIPELINE", "SA_RAFT_FUSE_MENC")
 
 
-@pytest.mark.parametrize("batch", [1, 2])
-def test_raft_schedules_bitwise_equal(batch, tmp_path, monkeypatch):
+RT_MODES = [
+    ("serial", {"SA_RAFT_PARALLEL": "0"}),
+    ("parallel", {"SA_RAFT_PIPELINE": "0"}),
+    ("pipeline3", {"SA_RAFT_PIPELINE": "3"}),
+]
+
+
+@pytest.mark.parametrize("model,batch", [("raftstereo-sceneflow", 1), ("raftstereo-sceneflow", 2),
+                                         ("raftstereo-realtime", 1)])
+def test_raft_schedules_bitwise_equal(model, batch, tmp_path, monkeypatch):
     monkeypatch.setenv("SA_PLAN_DIR", str(tmp_path))
     from stereoalgorithms_amd.models.engine import NativeStereoEngine
     from stereoalgorithms_amd.utils.synthetic import batch_pairs
@@ -34,12 +43,12 @@ def test_raft_schedules_bitwise_equal(batch, tmp_path, monkeypatch):
     l, r = batch_pairs(batch, H, W, seed=0)
     left, right = torch.from_numpy(l).cuda(), torch.from_numpy(r).cuda()
     ref = None
-    for name, env in MODES:
+    for name, env in (MODES if model == "raftstereo-sceneflow" else RT_MODES):
         for k in KNOBS:
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
-        eng = NativeStereoEngine("raftstereo-sceneflow", None, H, W, batch=batch)
+        eng = NativeStereoEngine(model, None, H, W, batch=batch)
         out = [eng.run(left, right).clone() for _ in range(2)]
         torch.cuda.synchronize()
         assert torch.equal(out[0], out[1]), f"{name}: replays differ"
