@@ -162,6 +162,10 @@ int sa_proj_stencil(const float* P, int nslices, long plane, int N, int H, int W
 // w16 fp16 [16][C] (taps >= 9 zero), C % 32 == 0, C <= 256, flow fp32 [N][H][W].
 int sa_flow_head_tail(const void* y, int ys, int C, const void* w16, const float* bias, float* flow, int N, int H,
                       int W, hipStream_t stream);
+// the same for a 3x3 C -> oc (1 or 2) conv: flow [N][H][W][oc] fp32 += bias[o] + taps, w16 fp16 [16 or 32][C] with
+// row (ky*3+kx)*oc + o (rows >= 9 oc zero)
+int sa_flow_head_tail_oc(const void* y, int ys, int C, const void* w16, int oc, const float* bias, float* flow, int N,
+                         int H, int W, hipStream_t stream);
 int sa_tap_proj(const void* x, int xs, long M, int C, const void* w, int ntaps, float* P, long plane,
                 hipStream_t stream);
 

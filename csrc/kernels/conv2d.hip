@@ -83,8 +83,16 @@ enum : int {
   kPingM = 8,  // kPing with the DMA pieces issued between the MFMAs of the compute slot (an LDS-DMA issue costs
                // ~60 cycles among bare MFMAs, 100-185 beside a slot's ds_reads: MI355X_MICROARCH.md), leaving only
                // the fragment reads in the read slot
+  kHalo = 9,    // 3x3 / stride 1 convs with halo reuse: the output tile is a TH x TW patch of one image (8 x 32),
+                // the K loop runs channel-chunk-major (64 channels, then the 9 taps), and each chunk's input patch
+                // (TH+2) x (TW+2) x 64 is DMA'd into LDS ONCE and read by all 9 taps at shifted offsets -- the im2col
+                // gather fetches it 9 times.  Per 64-deep k-step the L2 -> LDS traffic drops from 48 KB (256x128
+                // im2col tile) to ~21 KB (weights + 1/9 of the patch), below the per-CU LDS-DMA gather rate that
+                // bounds the im2col tiles (MI355X_MICROARCH.md 'Indexed rows: gather into LDS': 66-73 GB/s per CU)
+  kHalo16 = 10,  // kHalo with 16 x 16 output patches (narrow images: the 1/8 and 1/16 GRU levels)
 };
 __host__ __device__ constexpr bool is_glds(int mode) { return mode == kGlds3 || mode == kGldsDeep; }
+__host__ __device__ constexpr bool is_halo(int mode) { return mode == kHalo || mode == kHalo16; }
 
 template <int BM, int BN, int WM, int WN, int MODE = kRegK32>
 struct ConvCfg {
@@ -107,8 +115,15 @@ struct ConvCfg {
   // kPing: as deep as 144 KB allows, at most 6 (256x256: 4 stages, 256x128: 6; a 5-deep 256x256 ring measured
   // the same)
   static constexpr int PING_NS = 147456 / (A_BYTES + B_BYTES) < 6 ? 147456 / (A_BYTES + B_BYTES) : 6;
-  static constexpr int NSTAGE = MODE == kGlds3 ? 3 : MODE == kGldsDeep ? DEEP_NS : PING ? PING_NS : (WIDE ? 4 : 2);
-  static constexpr int STAGE_BYTES = NSTAGE * (A_BYTES + B_BYTES);
+  static constexpr bool HALO = is_halo(MODE);
+  static constexpr int NSTAGE = MODE == kGlds3 || HALO ? 3 : MODE == kGldsDeep ? DEEP_NS : PING ? PING_NS : (WIDE ? 4 : 2);
+  // kHalo: output patch TH x TW, input patch (TH+2) x (TW+2) pixels of 128 B (one 64-channel chunk) in 1-KB DMA
+  // pieces of 8 pixels, HALO_NA pieces per wave; two patch buffers + a 3-deep ring of weight stages
+  static constexpr int TW = MODE == kHalo16 ? 16 : 32;
+  static constexpr int HALO_PIX = (BM / TW + 2) * (TW + 2);
+  static constexpr int HALO_NA = HALO ? ((HALO_PIX + 7) / 8 + NW - 1) / NW : 1;
+  static constexpr int A_PATCH = HALO_NA * NW * 1024;
+  static constexpr int STAGE_BYTES = HALO ? 2 * A_PATCH + NSTAGE * B_BYTES : NSTAGE * (A_BYTES + B_BYTES);
   // fp32 C tile, unpadded rows; columns XOR-swizzled in 16-float blocks (cswz) so the MFMA
   // write-out (4 row groups x 16 lanes) hits 64 distinct banks; aliases the stage buffers.
   // kWide stages it in bands of CROWS rows (128 KB of fp32 per band)
@@ -116,7 +131,8 @@ struct ConvCfg {
   static constexpr int CROWS = BANDED ? (32768 / BN < BM ? 32768 / BN : BM) : BM;
   static constexpr int C_BYTES = CROWS * CST * 4;
   static constexpr int SMEM = STAGE_BYTES > C_BYTES ? STAGE_BYTES : C_BYTES;
-  static_assert(WM * WN == 4 || (WM * WN == 8 && (is_glds(MODE) || WIDE || PING)), "4 waves (8 for kGlds3; 4 or 8 for kWide) per workgroup");
+  static_assert(WM * WN == 4 || (WM * WN == 8 && (is_glds(MODE) || WIDE || PING || HALO)), "4 waves (8 for kGlds3; 4 or 8 for kWide) per workgroup");
+  static_assert(!HALO || (BM % TW == 0 && TM % 16 == 0 && TW % 16 == 0 && BK == 64), "halo tiles: 16-pixel fragments inside one output row");
   static_assert(!PING || (WM == 2 && WN == 4 && BM == 256), "kPing: 2 x 4 waves, one 128-row half of the tile per wave group");
   static_assert(!is_glds(MODE) || NSTAGE >= 3, "DMA rings keep at least one stage in flight across the barrier");
   static_assert(TM % 16 == 0 && TN % 16 == 0, "wave tile must be 16-aligned");
@@ -215,7 +231,12 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
   const int KD = p.KD > 0 ? p.KD : 1, Di = p.Di > 0 ? p.Di : 1, Do = p.Do > 0 ? p.Do : 1;
   const int sd = p.sd > 0 ? p.sd : 1;
   const int M = p.N * Do * HWo;
-  const int m0 = bx * BM;
+  // kHalo: bx enumerates (image, patch row, patch column); m0 is the image's first pixel (statistics bookkeeping)
+  const int halo_tx = C::HALO ? (p.Wo + C::TW - 1) / C::TW : 1, halo_ty = C::HALO ? (p.Ho + BM / C::TW - 1) / (BM / C::TW) : 1;
+  const int halo_img = C::HALO ? bx / (halo_tx * halo_ty) : 0;
+  const int halo_oy0 = C::HALO ? ((bx - halo_img * halo_tx * halo_ty) / halo_tx) * (BM / C::TW) : 0;
+  const int halo_ox0 = C::HALO ? ((bx - halo_img * halo_tx * halo_ty) % halo_tx) * C::TW : 0;
+  const int m0 = C::HALO ? halo_img * HWo : bx * BM;
   const int n0 = by * BN;
   const int khw = p.KH * p.KW;
   const int taps = KD * khw;
@@ -355,6 +376,137 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
       if (kt + 1 < nk) store_tile(cur ^ 1);
       __syncthreads();
     }
+  } else if constexpr (C::HALO) {
+    // ---------------- 3x3 halo patch + weight ring via global->LDS DMA, channel-chunk-major K ----------------
+    // Step s = (chunk c = s / 9, tap t = s % 9) over the whole K (never split).  LDS: patch buffers [2][A_PATCH]
+    // (pixel q = row-major in the (TH+2) x (TW+2) patch, 128 B per pixel, chunk XOR ((q >> 1) & 7) on the SOURCE
+    // side and on the fragment reads: the 16 pixels of a fragment's lane group hit 16 distinct bank slots), then
+    // the weight ring [3][BN][128 B] (rows swizzled the same way as kGlds3).
+    // Issue order inside a step: the next chunk's patch (first tap of a chunk only), then the weights of step
+    // s + 2, so waiting for the weights of step s with vmcnt(#pieces issued in step s - 1) also covers the patch
+    // of step s's chunk (issued before them).  One raw barrier per step: afterwards every wave's DMA for step s
+    // has landed and every wave has finished reading step s - 1's weight stage and, at a chunk's first tap, the
+    // previous chunk's patch buffer, which the issues of this step then refill.
+    constexpr int TW = C::TW, TH = BM / TW, PW = TW + 2, RP = C::HALO_PIX;
+    constexpr int NAH = C::HALO_NA;
+    constexpr int NB = BN * 8 / NT;
+    static_assert(NB * NT == BN * 8 && NB >= 1, "whole-wave weight DMA pieces");
+    constexpr int APB = C::A_PATCH, BST = BN * 128;
+    static_assert(2 * APB + 3 * BST <= C::SMEM, "halo buffers fit");
+    char* const abuf0 = smem;
+    char* const bbuf0 = smem + 2 * APB;
+    const int Cin = p.Cin;
+    const int nchunk = Cin >> 6;
+    const int nsteps = 9 * nchunk;
+    int apix[NAH], alch[NAH];
+    bool aok[NAH];
+#pragma unroll
+    for (int i = 0; i < NAH; ++i) {
+      const int q = (wave * NAH + i) * 8 + (lane >> 3);
+      const int qy = q / PW, qx = q - qy * PW;
+      const int iy = halo_oy0 - 1 + qy, ix = halo_ox0 - 1 + qx;
+      aok[i] = q < RP && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+      apix[i] = aok[i] ? (halo_img * p.H + iy) * p.W + ix : 0;
+      alch[i] = ((lane & 7) ^ ((q >> 1) & 7)) << 3;
+    }
+    const int sb1 = p.src[0].channels;
+    const int sb2 = sb1 + (p.nsrc > 1 ? p.src[1].channels : 0);
+    const int sb3 = sb2 + (p.nsrc > 2 ? p.src[2].channels : 0);
+    const f16* sp0 = reinterpret_cast<const f16*>(p.src[0].ptr);
+    const f16* sp1 = reinterpret_cast<const f16*>(p.src[p.nsrc > 1 ? 1 : 0].ptr);
+    const f16* sp2 = reinterpret_cast<const f16*>(p.src[p.nsrc > 2 ? 2 : 0].ptr);
+    const f16* sp3 = reinterpret_cast<const f16*>(p.src[p.nsrc > 3 ? 3 : 0].ptr);
+    const int ss0 = p.src[0].stride, ss1 = p.src[p.nsrc > 1 ? 1 : 0].stride;
+    const int ss2 = p.src[p.nsrc > 2 ? 2 : 0].stride, ss3 = p.src[p.nsrc > 3 ? 3 : 0].stride;
+    const f16* wrow[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int row = (wave * NB + j) * 8 + (lane >> 3);
+      const int lch = (lane & 7) ^ ((row >> 1) & 7);
+      wrow[j] = reinterpret_cast<const f16*>(p.weight) + (size_t)(n0 + row) * p.Kpad + lch * 8;
+    }
+    const void* zero_src = g_zero16;
+    auto issue_a = [&](int c, int buf) {
+      const int ci = c << 6;
+      const f16* sp;
+      int sst;
+      if (ci < sb1) { sp = sp0 + ci; sst = ss0; }
+      else if (ci < sb2) { sp = sp1 + (ci - sb1); sst = ss1; }
+      else if (ci < sb3) { sp = sp2 + (ci - sb2); sst = ss2; }
+      else { sp = sp3 + (ci - sb3); sst = ss3; }
+      char* dst = abuf0 + buf * APB;
+#pragma unroll
+      for (int i = 0; i < NAH; ++i) {
+        const void* g = aok[i] ? (const void*)(sp + (size_t)apix[i] * sst + alch[i]) : zero_src;
+        __builtin_amdgcn_global_load_lds(g, (lds_void_t*)(dst + (wave * NAH + i) * 1024), 16, 0, 0);
+      }
+    };
+    auto issue_b = [&](int st, int buf) {
+      const int c = st / 9, t = st - c * 9;
+      const int koff = t * Cin + (c << 6);
+      char* dst = bbuf0 + buf * BST;
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        __builtin_amdgcn_global_load_lds((const void*)(wrow[j] + koff), (lds_void_t*)(dst + (wave * NB + j) * 1024), 16,
+                                         0, 0);
+    };
+    const int frow = lane & 15;
+    // A fragment rows of this wave: output pixel (py, px) of fragment i, lane row frow
+    int aq0[C::FM];
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i) {
+      const int r = wm * C::TM + i * 16 + frow;
+      aq0[i] = (r / TW) * PW + (r % TW);
+    }
+    issue_a(0, 0);
+    issue_b(0, 0);
+    if (nsteps > 1) issue_b(1, 1);
+    int prev = nsteps > 1 ? NB : 0;  // DMA pieces issued after the weights of the step about to be waited for
+    int bcur = 0;
+    for (int st = 0; st < nsteps; ++st) {
+      if (prev == NAH + NB) wait_vmcnt<NAH + NB>();
+      else if (prev == NB) wait_vmcnt<NB>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const int c = st / 9, t = st - c * 9;
+      int issued = 0;
+      if (t == 0 && c + 1 < nchunk) {
+        issue_a(c + 1, (c + 1) & 1);
+        issued += NAH;
+      }
+      if (st + 2 < nsteps) {
+        issue_b(st + 2, bcur == 0 ? 2 : bcur - 1);
+        issued += NB;
+      }
+      prev = issued;
+      const char* sa = abuf0 + (c & 1) * APB;
+      const char* sb = bbuf0 + bcur * BST;
+      const int ky = t / 3, kx = t - ky * 3;
+      const int toff = ky * PW + kx;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int lc = (lane >> 4) + 4 * kk;
+        half8 af[C::FM], bf[C::FN];
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+          const int q = aq0[i] + toff;
+          af[i] = *reinterpret_cast<const half8*>(sa + q * 128 + ((lc ^ ((q >> 1) & 7)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) {
+          const int row = wn * C::TN + j * 16 + frow;
+          bf[j] = *reinterpret_cast<const half8*>(sb + row * 128 + ((lc ^ ((row >> 1) & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int j = 0; j < C::FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
+      bcur = bcur == 2 ? 0 : bcur + 1;
+    }
+    __syncthreads();  // all fragment reads done before the epilogue reuses LDS
   } else if constexpr (is_glds(MODE)) {
     // ---------------- uniform-k im2col via global->LDS DMA, 3-deep LDS ring, BK = 64 -------------
     // Stage image per operand: [rows][64 halfs] (128-B rows), lane-linear per wave instruction
@@ -1347,8 +1499,15 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
   // rows [r0, r1) of the tile, their C values staged in LDS at row - cbase
   auto epi_rows = [&](const int r0, const int r1, const int cbase) {
     for (int row = r0 + tid / CPR; row < r1; row += RPI) {
-      const int m = m0 + row;
-      if (m >= M) break;
+      int m;
+      if constexpr (C::HALO) {  // patch pixel -> image pixel; patches may overhang the right / bottom edge
+        const int oy = halo_oy0 + row / C::TW, ox = halo_ox0 + row % C::TW;
+        if (oy >= p.Ho || ox >= p.Wo) continue;
+        m = m0 + oy * p.Wo + ox;
+      } else {
+        m = m0 + row;
+        if (m >= M) break;
+      }
       float v[8];
       const int crow = row - cbase;
       const float* cp = ct + crow * C::CST + cswz(crow, cc * 8);
@@ -1680,7 +1839,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
     }
     return;
   }
-  if constexpr (is_glds(MODE) || MODE == kWide) {
+  if constexpr (is_glds(MODE) || MODE == kWide || is_halo(MODE)) {
     const int nwg = gridDim.x * gridDim.y;
     const int bid = blockIdx.y * gridDim.x + blockIdx.x;
     const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
@@ -1832,6 +1991,25 @@ int launch_glds3(const SaConvArgs* a, hipStream_t stream, bool forced) {
   return (int)hipGetLastError();
 }
 
+// kHalo launcher (8 waves, 1 block per CU, never split): 3x3 / stride 1 / pad 1 / dilation 1 2-D convs whose
+// sources are multiples of 64 channels, K unpadded.  Returns 1 when the shape does not qualify.
+template <int MODE>
+int launch_halo(const SaConvArgs* a, hipStream_t stream) {
+  constexpr int BM = 256, BN = 128;
+  bool ok = a->KD <= 0 && a->KH == 3 && a->KW == 3 && a->sh == 1 && a->sw == 1 && a->ph == 1 && a->pw == 1 &&
+            a->dh == 1 && a->dw == 1 && a->up == 0 && a->Cin % 64 == 0 && a->Kpad == 9 * a->Cin &&
+            a->Ho == a->H && a->Wo == a->W && a->splitk <= 1 && a->epi != SA_EPI_PROJ;
+  for (int i = 0; i < a->nsrc; ++i) ok = ok && a->src[i].channels % 64 == 0;
+  if (!ok) return 1;
+  using C = ConvCfg<BM, BN, 4, 2, MODE>;
+  const int th = BM / C::TW;
+  const long tiles = (long)a->N * ((a->Ho + th - 1) / th) * ((a->Wo + C::TW - 1) / C::TW);
+  if (tiles >= (1L << 31) || (long)a->N * a->H * a->W >= (1L << 31)) return 1;
+  note_split(1, 0, 0);
+  launch_kernel<BM, BN, 4, 2, MODE>(dim3((unsigned)tiles, (a->Cout + BN - 1) / BN, 1), a, stream);
+  return (int)hipGetLastError();
+}
+
 // kWide launcher (8 waves, 1 block per CU, never split): uniform-k gather, no projection epilogue.
 // Returns 1 when the shape does not qualify.
 template <int BM, int BN, int WM, int WN>
@@ -1918,7 +2096,7 @@ int pick_cfg(const SaConvArgs* a) {
 int cfg_bn(int cfg) {
   switch (cfg) {
     case 10: case 12: case 18: case 20: return 256;
-    case 0: case 4: case 6: case 7: case 11: case 13: case 15: case 19: case 21: return 128;
+    case 0: case 4: case 6: case 7: case 11: case 13: case 15: case 19: case 21: case 26: case 27: return 128;
     case 1: case 3: case 5: case 8: case 9: case 14: case 16: case 17: return 64;
     case 2: return 16;
     default: return 0;
@@ -2039,6 +2217,11 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
                               : launch_wide<512, 128, 4, 1>(a, stream);
       return r == 1 ? -5 : r;
     }
+    case 26: case 27: {
+      // halo-reuse 3x3 tiles: 8 x 32 (26) / 16 x 16 (27) output patches x 128 channels
+      const int r = cfg == 26 ? launch_halo<kHalo>(a, stream) : launch_halo<kHalo16>(a, stream);
+      return r == 1 ? -5 : r;
+    }
     case 18: case 19: case 20: case 21: {
       // 8-wave ping-pong: 256x256 (4-deep ring) / 256x128 (6-deep ring); 18 / 19 issue the DMA in the read
       // slot (kPing), 20 / 21 between the MFMAs of the compute slot (kPingM)
@@ -2137,11 +2320,13 @@ namespace {
 // following conv's zero padding), then the 9-tap stencil + bias accumulated into the fp32 flow.  Replaces
 // tap_proj + proj_stencil (two launches and an HBM round trip of the 9 planes) on every GRU iteration's critical
 // path; the halo recompute (2.1x at 2 x 32 tiles, 1.5x at 4 x 64) only re-reads activations.
-template <int TH, int TW>
+template <int TH, int TW, int OC>
 __global__ __launch_bounds__(256) void flow_head_tail_kernel(const f16* __restrict__ y, int ys, int C,
                                                              const f16* __restrict__ w16, const float* __restrict__ bias,
                                                              float* __restrict__ flow, int N, int H, int W) {
-  constexpr int RH = TH + 2, RW = TW + 2, R = RH * RW, NF = (R + 15) / 16, PS = 9;
+  // OC output channels (RAFT: the x flow; CREStereo: x and y): 9 * OC projection taps, tap j = (ky*3+kx)*OC + o,
+  // in NB 16-column MFMA tiles; flow is [N][H][W][OC] fp32
+  constexpr int RH = TH + 2, RW = TW + 2, R = RH * RW, NF = (R + 15) / 16, PS = 9 * OC, NB = (PS + 15) / 16;
   __shared__ float P[NF * 16 * PS];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int frow = lane & 15, kq = lane >> 4;
@@ -2151,10 +2336,12 @@ __global__ __launch_bounds__(256) void flow_head_tail_kernel(const f16* __restri
   const int y0 = ty * TH - 1, x0 = tx * TW - 1;
   const int ks = C >> 5;
   const half8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
-  half8 b[8];  // B = the 16 (9 used) tap rows of the projection, column frow, k = kq*8 .. of each 32-deep step
+  half8 b[NB][8];  // B = 16 tap rows of the projection per tile, column frow, k = kq*8 .. of each 32-deep step
 #pragma unroll
-  for (int k = 0; k < 8; ++k)
-    b[k] = k < ks ? *reinterpret_cast<const half8*>(w16 + (size_t)frow * C + k * 32 + kq * 8) : zero8;
+  for (int j = 0; j < NB; ++j)
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      b[j][k] = k < ks ? *reinterpret_cast<const half8*>(w16 + (size_t)(16 * j + frow) * C + k * 32 + kq * 8) : zero8;
   for (int f = wave; f < NF; f += 4) {
     const int q = f * 16 + frow;  // halo pixel of this lane's A row
     const int hy = q / RW, hx = q - hy * RW;
@@ -2164,46 +2351,62 @@ __global__ __launch_bounds__(256) void flow_head_tail_kernel(const f16* __restri
     half8 a[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) a[k] = (ok && k < ks) ? *reinterpret_cast<const half8*>(src + k * 32) : zero8;
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (k < ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[k], b[k], acc, 0, 0, 0);
-    // acc[r]: halo pixel f*16 + kq*4 + r, tap frow
-    if (frow < PS)
+    for (int j = 0; j < NB; ++j) {
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) P[(f * 16 + kq * 4 + r) * PS + frow] = acc[r];
+      for (int k = 0; k < 8; ++k)
+        if (k < ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[k], b[j][k], acc, 0, 0, 0);
+      // acc[r]: halo pixel f*16 + kq*4 + r, tap 16 j + frow
+      const int tap = 16 * j + frow;
+      if (tap < PS)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) P[(f * 16 + kq * 4 + r) * PS + tap] = acc[r];
+    }
   }
   __syncthreads();
-  const float b0 = bias ? bias[0] : 0.f;
-  for (int o = threadIdx.x; o < TH * TW; o += 256) {
-    const int oy = o / TW, ox = o - oy * TW;
+  for (int o = threadIdx.x; o < TH * TW * OC; o += 256) {
+    const int c = o % OC, px = o / OC;
+    const int oy = px / TW, ox = px - oy * TW;
     const int gy = ty * TH + oy, gx = tx * TW + ox;
     if (gy >= H || gx >= W) continue;
-    float s = b0;
+    float s = bias ? bias[c] : 0.f;
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) s += P[((oy + ky) * RW + ox + kx) * PS + ky * 3 + kx];
-    flow[((size_t)n * H + gy) * W + gx] += s;
+      for (int kx = 0; kx < 3; ++kx) s += P[((oy + ky) * RW + ox + kx) * PS + (ky * 3 + kx) * OC + c];
+    flow[(((size_t)n * H + gy) * W + gx) * OC + c] += s;
   }
 }
 }  // namespace
 
-extern "C" int sa_flow_head_tail(const void* y, int ys, int C, const void* w16, const float* bias, float* flow, int N,
-                                 int H, int W, hipStream_t stream) {
-  if (C % 32 || C > 256 || C < 32 || ys < C || ys % 8 || N < 1 || H < 1 || W < 1) return -2;
+extern "C" int sa_flow_head_tail_oc(const void* y, int ys, int C, const void* w16, int oc, const float* bias,
+                                    float* flow, int N, int H, int W, hipStream_t stream) {
+  if (C % 32 || C > 256 || C < 32 || ys < C || ys % 8 || N < 1 || H < 1 || W < 1 || (oc != 1 && oc != 2)) return -2;
   const long M = (long)N * H * W;
   // small frames (batch 1 at 1/4 resolution): 2 x 32 tiles, enough blocks to cover the CUs; else 4 x 64 (less halo)
-  if (M <= 40000) {
-    const long tiles = (long)N * ((H + 1) / 2) * ((W + 31) / 32);
-    hipLaunchKernelGGL((flow_head_tail_kernel<2, 32>), dim3((unsigned)tiles), dim3(256), 0, stream, (const f16*)y, ys,
-                       C, (const f16*)w16, bias, flow, N, H, W);
-  } else {
-    const long tiles = (long)N * ((H + 3) / 4) * ((W + 63) / 64);
-    hipLaunchKernelGGL((flow_head_tail_kernel<4, 64>), dim3((unsigned)tiles), dim3(256), 0, stream, (const f16*)y, ys,
-                       C, (const f16*)w16, bias, flow, N, H, W);
-  }
+  const bool small = M <= 40000;
+  const long tiles = small ? (long)N * ((H + 1) / 2) * ((W + 31) / 32) : (long)N * ((H + 3) / 4) * ((W + 63) / 64);
+  const f16* yy = (const f16*)y;
+  const f16* ww = (const f16*)w16;
+  if (oc == 1 && small)
+    hipLaunchKernelGGL((flow_head_tail_kernel<2, 32, 1>), dim3((unsigned)tiles), dim3(256), 0, stream, yy, ys, C, ww,
+                       bias, flow, N, H, W);
+  else if (oc == 1)
+    hipLaunchKernelGGL((flow_head_tail_kernel<4, 64, 1>), dim3((unsigned)tiles), dim3(256), 0, stream, yy, ys, C, ww,
+                       bias, flow, N, H, W);
+  else if (small)
+    hipLaunchKernelGGL((flow_head_tail_kernel<2, 32, 2>), dim3((unsigned)tiles), dim3(256), 0, stream, yy, ys, C, ww,
+                       bias, flow, N, H, W);
+  else
+    hipLaunchKernelGGL((flow_head_tail_kernel<4, 64, 2>), dim3((unsigned)tiles), dim3(256), 0, stream, yy, ys, C, ww,
+                       bias, flow, N, H, W);
   return (int)hipGetLastError();
+}
+
+extern "C" int sa_flow_head_tail(const void* y, int ys, int C, const void* w16, const float* bias, float* flow, int N,
+                                 int H, int W, hipStream_t stream) {
+  return sa_flow_head_tail_oc(y, ys, C, w16, 1, bias, flow, N, H, W, stream);
 }
 
 extern "C" int sa_tap_proj(const void* x, int xs, long M, int C, const void* w, int ntaps, float* P, long plane,

@@ -108,6 +108,7 @@ struct Level {
     net = make_tensor(a, B, h, w, 128);
     xin = make_tensor(a, B, h, w, 256);  // [inp 128 | motion 126 | flow 2]
     corr = make_tensor(a, B, h, w, 40);
+    HIP_CHECK(hipMemset(corr.ptr, 0, corr.nbytes()));  // the zero tail (36..39) the AGCL never writes
     cor1 = make_tensor(a, B, h, w, 256);
     corflo = make_tensor(a, B, h, w, 256);  // [cor 192 | flo 64]
     flo1 = make_tensor(a, B, h, w, 128);
@@ -152,7 +153,6 @@ class CreStereo : public StereoEngine {
   bool fh2_proj_ = !std::getenv("SA_CRE_FH2_PROJ") || std::atoi(std::getenv("SA_CRE_FH2_PROJ")) != 0;
   void* fh2_w16_ = nullptr;
   float* fh2_b_ = nullptr;
-  float* tap_p_ = nullptr;
   float *flowup4_ = nullptr, *flowup2_ = nullptr, *pe_ = nullptr;
 };
 
@@ -263,7 +263,6 @@ void CreStereo::build(WeightSource& src) {
     HIP_CHECK(hipMemcpy(fh2_w16_, w16.data(), w16.size() * 2, hipMemcpyHostToDevice));
     fh2_b_ = (float*)a.alloc(2 * 4);
     HIP_CHECK(hipMemcpy(fh2_b_, b2.data.data(), 2 * 4, hipMemcpyHostToDevice));
-    tap_p_ = (float*)a.alloc((size_t)18 * B * h4 * w4 * 4);  // largest level (1/4)
   }
   mask2_.build(a, ws, {u + "mask.2"}, {{256, 256}}, s1, {}, 0.25f);
 
@@ -296,7 +295,7 @@ void CreStereo::update(hipStream_t s, Level& L, const Tensor& f1, const Tensor& 
   ag.iter_mode = iter_mode;
   ag.out = L.corr.ptr;
   ag.out_stride = L.corr.stride;
-  ag.out_channels = L.corr.c;
+  ag.out_channels = 36;  // channels 36..39 of the 40-channel pixel were zeroed at build and nothing writes them
   check(sa_agcl_corr(&ag, s), "agcl");
   const long P = (long)B * L.h * L.w;
   check(sa_flow_features(L.flow, 2, P, L.flowfeat.ptr, L.flowfeat.stride, 8, L.xin.slice_c(254, 2).ptr,
@@ -350,9 +349,9 @@ void CreStereo::update(hipStream_t s, Level& L, const Tensor& f1, const Tensor& 
   if (want_mask) fh1mask_.run(s, {L.net}, L.fh, SA_ACT_RELU);
   else fh1_.run(s, {L.net}, L.fh.slice_c(0, 256), SA_ACT_RELU);
   if (fh2_proj_) {
-    const long M = (long)B * L.h * L.w;
-    check(sa_tap_proj(L.fh.ptr, L.fh.stride, M, 256, fh2_w16_, 18, tap_p_, M, s), "flow-head taps");
-    check(sa_proj_stencil(tap_p_, 1, M, B, L.h, L.w, 3, 3, 2, fh2_b_, L.flow, 2, 1, s), "flow-head stencil");
+    // tap projections over a halo tile + 3x3 stencil into the (x, y) flow, one launch (sa_flow_head_tail_oc)
+    check(sa_flow_head_tail_oc(L.fh.ptr, L.fh.stride, 256, fh2_w16_, 2, fh2_b_, L.flow, B, L.h, L.w, s),
+          "flow-head tail");
   } else {
     SaConvArgs fa = fh2_.args({L.fh.slice_c(0, 256)}, Tensor{L.flow, B, L.h, L.w, 2, 2, DT::F32});
     fa.epi = SA_EPI_FLOW_ACC;

@@ -615,11 +615,13 @@ void RaftStereo::forward(hipStream_t s) {
   const int f = 1 << rc_.n_downsample;
   // 0 = off, 1 = G32 ahead, 2 = G32 + G16 ahead (default below batch 4)
   const int pmode = pipeline_mode_ >= 0 ? pipeline_mode_ : 2;
-  SA_REQUIRE(pmode >= 0 && pmode <= 4, "SA_RAFT_PIPELINE=%d (0..4)", pmode);
+  SA_REQUIRE(pmode >= 0 && pmode <= 2, "SA_RAFT_PIPELINE=%d (0..2)", pmode);
   const bool pipe = par && pmode > 0 && rc_.n_gru == 3 && !rc_.slow_fast;
-  // realtime preset (2 levels, slow-fast): the chain G08(t) -> pool -> G16 -> G16 -> interp -> G08(t + 1) on the
-  // main stream, flow head + motion encoder beside it (the same structure as pipeline mode 4)
-  const bool rt_pipe = par && pmode >= 3 && rc_.n_gru == 2 && rc_.slow_fast;
+  // realtime preset (2 levels, slow-fast): the recurrence G08(t) -> pool -> G16 -> G16 -> interp -> G08(t + 1) stays
+  // on the main stream, the flow head and next motion encoder run beside it (side stream), so per iteration only
+  // max(G16 chain, flow head + motion encoder) follows G08.  b1 network 2.10 -> 1.92 ms (GRU split on); on unless
+  // SA_RAFT_PIPELINE=0.
+  const bool rt_pipe = par && pmode > 0 && rc_.n_gru == 2 && rc_.slow_fast;
   // finest GRU (interp + z/r + q) and flow head as two halves, for the deeper pipeline
   auto fine = [&]() {
     interp(s, 0);
@@ -659,115 +661,6 @@ void RaftStereo::forward(hipStream_t s) {
         ScopedSplitK k1(&splitk_side_);
         wait(side_, 4);
         head(side_, last);
-        if (!last) motion(side_);
-        rec(side_, last ? 1 : 3);
-      }
-    }
-    wait(s, 1);
-  } else if (pipe && pmode == 4) {
-    // Mode 3's dependencies, captured so that at every fork of the chain the on-chain successor is captured
-    // before the off-chain one (in the b1 timeline the successor captured second started ~13 us after its
-    // producer, the first ~5 us): the interp of net1(t) forks G08(t) (main) and G32(t + 1) (side2); G08 q(t)
-    // forks G16(t + 1) (main) and FH(t) + M(t + 1) (side).
-    auto fh = [&](hipStream_t st, bool last) {
-      if (last) fh1mask_.run(st, {net_[0]}, fh_, SA_ACT_RELU);
-      else fh1_.run(st, {net_[0]}, fh_.slice_c(0, 256), SA_ACT_RELU);
-      check(sa_flow_head_tail(fh_.ptr, fh_.stride, 256, fh2_w16_, proj_b_, flow_, Bn, h0, w0, st), "flow-head tail");
-      if (last) mask2_.run(st, {fh_.slice_c(256, 256)}, mask_);
-    };
-    SA_REQUIRE(fh2_proj_ && fh_tail_, "pipeline mode 4 needs the flow-head tail kernel");
-    rec(s, 0);
-    rec(s, 4);
-    {
-      ScopedSplitK k2(&splitk_side2_);
-      wait(side2_, 0);
-      gru32(side2_);
-      rec(side2_, 2);
-    }
-    {
-      ScopedSplitK k1(&splitk_side_);
-      wait(side_, 4);
-      motion(side_);
-      rec(side_, 3);
-    }
-    wait(s, 2);
-    gru16(s);
-    for (int it = 0; it < rc_.iters; ++it) {
-      const bool last = it == rc_.iters - 1;
-      interp(s, 0);
-      rec(s, 0);
-      wait(s, 3);
-      gru(s, 0, {motion_, interp_[0]});
-      rec(s, 4);
-      if (!last) {
-        {
-          ScopedSplitK k2(&splitk_side2_);
-          wait(side2_, 0);
-          gru32(side2_);
-          rec(side2_, 2);
-        }
-        wait(s, 2);
-        gru16(s);
-      }
-      {
-        ScopedSplitK k1(&splitk_side_);
-        wait(side_, 4);
-        fh(side_, last);
-        if (!last) motion(side_);
-        rec(side_, last ? 1 : 3);
-      }
-    }
-    wait(s, 1);
-  } else if (pipe && pmode == 3) {
-    // Critical-chain schedule (b1 timeline, profiles/timeline_r03.md).  The update's inherent recurrence is
-    // G16(t) -> G08(t) -> G16(t + 1) (the 1/8 level pools net0(t), the 1/4 level interpolates net1(t)), so that
-    // chain stays on ONE stream -- consecutive kernels of one queue start back to back, a cross-stream event edge
-    // costs ~10-20 us of dispatch latency on this chip -- and the off-chain work hangs off it:
-    //   main : [wait G32(t)] pool_interp, G16 zr, q (t); rec 0; interp; [wait M(t)] G08 zr, q (t); rec 4
-    //   side2: [wait 0] G32(t + 1)    (reads net1(t); overwrites net2, read by pool_interp(t) before event 0)
-    //   side : [wait 4] FH(t), M(t + 1)  (FH reads net0(t); M overwrites motion, read by G08(t) before event 4)
-    // G08 q(t + 1) rewrites net0 only after waiting for M(t + 1), which follows FH(t) on side: no WAR hazard.
-    // Events: 0 = G16 done, 2 = G32 done, 3 = M done, 4 = G08 done, 1 = last FH done.
-    auto fh = [&](hipStream_t st, bool last) {
-      if (last) fh1mask_.run(st, {net_[0]}, fh_, SA_ACT_RELU);
-      else fh1_.run(st, {net_[0]}, fh_.slice_c(0, 256), SA_ACT_RELU);
-      check(sa_flow_head_tail(fh_.ptr, fh_.stride, 256, fh2_w16_, proj_b_, flow_, Bn, h0, w0, st), "flow-head tail");
-      if (last) mask2_.run(st, {fh_.slice_c(256, 256)}, mask_);
-    };
-    SA_REQUIRE(fh2_proj_ && fh_tail_, "pipeline mode 3 needs the flow-head tail kernel");
-    rec(s, 0);
-    rec(s, 4);
-    {
-      ScopedSplitK k2(&splitk_side2_);
-      wait(side2_, 0);
-      gru32(side2_);
-      rec(side2_, 2);
-    }
-    {
-      ScopedSplitK k1(&splitk_side_);
-      wait(side_, 4);
-      motion(side_);
-      rec(side_, 3);
-    }
-    for (int it = 0; it < rc_.iters; ++it) {
-      const bool last = it == rc_.iters - 1;
-      wait(s, 2);
-      gru16(s);
-      rec(s, 0);
-      if (!last) {
-        ScopedSplitK k2(&splitk_side2_);
-        wait(side2_, 0);
-        gru32(side2_);
-        rec(side2_, 2);
-      }
-      interp(s, 0);
-      wait(s, 3);
-      gru(s, 0, {motion_, interp_[0]});
-      rec(s, 4);
-      {
-        ScopedSplitK k1(&splitk_side_);
-        wait(side_, 4);
-        fh(side_, last);
         if (!last) motion(side_);
         rec(side_, last ? 1 : 3);
       }

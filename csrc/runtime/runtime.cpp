@@ -747,7 +747,7 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
   const bool can_split = a.ws && a.counters && !a.stats;
   // (cfgs 12 / 13, the 4-wave wide tiles, lose everywhere on MI355X (tools/conv_bench.py): not timed;
   // 14-17 are the deep DMA rings, 18 / 19 the 8-wave ping-pong tiles)
-  for (int cfg = 0; cfg <= 25; ++cfg) {
+  for (int cfg = 0; cfg <= 27; ++cfg) {
     if (cfg == 12 || cfg == 13) continue;
     if (cfg == 2 && a.Cout > 32) continue;  // 256x16 tile: narrow outputs only
     if (cfg == 6) continue;                 // 128x128 / 4 waves: never competitive (conv_bench)

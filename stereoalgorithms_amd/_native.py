@@ -135,6 +135,7 @@ def _declare_dev(lib):
         "sa_proj_stencil": (_i, [_p, _i, C.c_long, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p]),
         "sa_tap_proj": (_i, [_p, _i, C.c_long, _i, _p, _i, _p, C.c_long, _p]),
         "sa_flow_head_tail": (_i, [_p, _i, _i, _p, _p, _p, _i, _i, _i, _p]),
+        "sa_flow_head_tail_oc": (_i, [_p, _i, _i, _p, _i, _p, _p, _i, _i, _i, _p]),
         "sa_instnorm_apply": (_i, [C.POINTER(SaNormArgs), _p]),
         "sa_stats_reduce": (_i, [_p, _i, C.c_long, _p]),
         "sa_avgpool3s2": (_i, [_p, _i, _p, _i, _i, _i, _i, _i, _p]),

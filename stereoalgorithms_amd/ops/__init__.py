@@ -84,6 +84,18 @@ def flow_head_tail(y, w, bias, flow):
     return flow
 
 
+def flow_head_tail2(y, w, bias, flow):
+    """Two-channel variant (CREStereo's flow head conv2 256 -> 2): ``w`` [2, C, 3, 3], fp32 ``flow`` [n,h,w,2]
+    += bias + conv(y) in place."""
+    n, h, wd, c = y.shape
+    w16 = torch.zeros(32, c, dtype=torch.float16, device=y.device)
+    w16[:18] = w.permute(2, 3, 0, 1).reshape(18, c).to(torch.float16)  # row (ky*3+kx)*2 + o
+    assert flow.dtype == torch.float32 and flow.is_contiguous() and flow.shape == (n, h, wd, 2)
+    N.check(N.dev().sa_flow_head_tail_oc(y.data_ptr(), _pix_stride(y), c, w16.data_ptr(), 2, bias.data_ptr(),
+                                         flow.data_ptr(), n, h, wd, _stream()), "sa_flow_head_tail_oc")
+    return flow
+
+
 def raft_motion_head(pyr_buf, flow, b, h, w1, w2, convc1_w, convc1_b, convf1_w, convf1_b, levels=4, radius=4):
     """Fused lookup + relu(convc1) + relu(convf1 on [flow_x, 0]): returns (cor1, flo1, flowcopy) fp16
     NHWC.  ``convc1_w`` [64, L*(2r+1), 1, 1], ``convf1_w`` [64, 2, 7, 7] (torch layouts)."""

@@ -333,6 +333,23 @@ def test_flow_head_tail(n, hw):
     assert rel_err(flow - flow0, ref) < 2e-3
 
 
+@pytest.mark.parametrize("n,hw", [(1, (120, 160)), (1, (30, 40)), (2, (37, 70))])
+def test_flow_head_tail_two_channels(n, hw):
+    """CREStereo's flow-head conv2 (256 -> 2, 3x3) as one halo-tiled launch == F.conv2d in fp32 on the same fp16
+    operands, accumulated into the interleaved (x, y) flow."""
+    O = ops()
+    torch.manual_seed(48)
+    y = torch.randn(n, *hw, 256, device=DEV).half()
+    w2 = torch.randn(2, 256, 3, 3, device=DEV) / 48
+    b2 = torch.randn(2, device=DEV) * 0.1
+    flow0 = torch.randn(n, *hw, 2, device=DEV)
+    flow = flow0.clone()
+    O.flow_head_tail2(y, w2, b2.contiguous(), flow)
+    torch.cuda.synchronize()
+    ref = F.conv2d(y.float().permute(0, 3, 1, 2), w2.half().float(), b2, padding=1).permute(0, 2, 3, 1)
+    assert rel_err(flow - flow0, ref) < 2e-3
+
+
 @pytest.mark.parametrize("n,hw,c,xs,oc", [(2, (24, 40), 256, 512, 1), (1, (13, 21), 256, 256, 1),
                                             (1, (7, 9), 96, 104, 1), (2, (11, 30), 256, 512, 2)])
 def test_tap_proj_skinny_conv(n, hw, c, xs, oc):
@@ -632,6 +649,78 @@ def test_conv2d_gru_zrq_split(cfg, splitk):
     torch.cuda.synchronize()
     assert rel_err(nchw(zb), z) < 3e-3
     assert rel_err(nchw(net_h), ref) < 4e-3
+
+
+@pytest.mark.parametrize("cfg", [26, 27])
+@pytest.mark.parametrize("srcs,cout,hw,n", [
+    ((128, 256), 256, (120, 160), 1),   # RAFT 1/4 z/r (two sources, 2 n-tiles), patches tile the image exactly
+    ((128,), 128, (60, 80), 2),          # 1/8 level: 8x32 patches overhang the right edge
+    ((64, 64, 128), 384, (30, 40), 1),   # three sources, 3 n-tiles, patches overhang both edges
+    ((64,), 128, (13, 21), 2),           # tiny image: one partial patch per image
+])
+def test_conv2d_halo_vs_torch(srcs, cout, hw, n, cfg):
+    """Halo-reuse 3x3 tiles (cfg 26: 8 x 32 output patches, 27: 16 x 16): the input patch of each 64-channel chunk
+    is loaded once and read by all 9 taps; must equal F.conv2d (zero padding at every image border, multi-source
+    concatenation, bias + activation epilogue, run twice)."""
+    O = ops()
+    torch.manual_seed(21)
+    xs = [torch.randn(n, c, *hw, device=DEV) for c in srcs]
+    cin = sum(srcs)
+    w = torch.randn(cout, cin, 3, 3, device=DEV) / math.sqrt(cin * 9)
+    b = torch.randn(cout, device=DEV) * 0.1
+    ref = F.leaky_relu(F.conv2d(torch.cat([x.half().float() for x in xs], 1), w.half().float(), b, padding=1), 0.1)
+    wp, kpad, _ = O.pack_conv_weight(w)
+    for _ in range(2):
+        out = O.conv2d([nhwc(x).half() for x in xs], wp, kpad, cout, 3, 3, bias=b.contiguous(), act="leaky",
+                       alpha=0.1, tile_cfg=cfg)
+        torch.cuda.synchronize()
+        assert rel_err(nchw(out), ref) < 2e-3
+
+
+@pytest.mark.parametrize("cfg", [26, 27])
+def test_conv2d_halo_gru_and_stats(cfg):
+    """Halo tiles with the fused epilogues: the ZRQ / Q GRU pair and per-(image, channel) instance-norm statistics
+    (patch rows map to image pixels, so the statistics must still be exact)."""
+    O = ops()
+    torch.manual_seed(22)
+    n, hd, h, w = 2, 128, 24, 40
+    net = torch.randn(n, hd, h, w, device=DEV).tanh()
+    x = torch.randn(n, 256, h, w, device=DEV)
+    cz, cr, cq = (torch.randn(n, hd, h, w, device=DEV) * 0.5 for _ in range(3))
+    wz, wr, wq = (torch.randn(hd, hd + 256, 3, 3, device=DEV) / math.sqrt((hd + 256) * 9) for _ in range(3))
+    bz, br, bq = (torch.randn(hd, device=DEV) * 0.1 for _ in range(3))
+    hx = torch.cat([net, x], 1).half().float()
+    z = torch.sigmoid(F.conv2d(hx, wz.half().float(), bz, padding=1) + cz.half().float())
+    r = torch.sigmoid(F.conv2d(hx, wr.half().float(), br, padding=1) + cr.half().float())
+    rh = (r * net.half().float()).half().float()
+    q = torch.tanh(F.conv2d(torch.cat([rh, x.half().float()], 1), wq.half().float(), bq, padding=1) + cq.half().float())
+    ref = (1 - z) * net.half().float() + z * q
+    net_h = nhwc(net).half()
+    ctx = nhwc(torch.cat([cz, cr, cq], 1)).half()
+    xh = nhwc(x).half()
+    wqx = wq.clone()
+    wqx[:, :hd] = 0
+    wzrq, kpad, _ = O.pack_conv_weight(torch.cat([wz, wr, wqx], 0))
+    wqh, kph, _ = O.pack_conv_weight(wq[:, :hd].contiguous())
+    zb = torch.empty(n, h, w, hd, device=DEV, dtype=torch.float16)
+    rhb, qx = torch.empty_like(zb), torch.empty_like(zb)
+    O.conv2d([net_h, xh], wzrq, kpad, 3 * hd, 3, 3, bias=torch.cat([bz, br, bq]).contiguous(), out=qx,
+             epi="gru_zrq", ctx=ctx, aux=zb, hbuf=net_h, rh=rhb, tile_cfg=cfg)
+    O.conv2d([rhb], wqh, kph, hd, 3, 3, out=net_h, epi="gru_q", res=qx, aux=zb, hbuf=net_h, tile_cfg=cfg)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(zb), z) < 3e-3
+    assert rel_err(nchw(net_h), ref) < 4e-3
+    # statistics: sum / sum of squares per (image, channel) of the stored output
+    xin = torch.randn(n, 128, h, w, device=DEV)
+    ws = torch.randn(128, 128, 3, 3, device=DEV) / math.sqrt(128 * 9)
+    wsp, kps, _ = O.pack_conv_weight(ws)
+    st = torch.zeros(16, n, 128, 2, dtype=torch.int64, device=DEV)
+    out = O.conv2d(nhwc(xin).half(), wsp, kps, 128, 3, 3, stats=st, stats_slots=16, tile_cfg=cfg)
+    torch.cuda.synchronize()
+    o = out.float()
+    tot = st.sum(0).double() / 16777216.0
+    assert torch.allclose(tot[..., 0], o.sum((1, 2)).double(), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(tot[..., 1], (o * o).sum((1, 2)).double(), rtol=1e-3, atol=1e-2)
 
 
 def test_conv2d_flow_acc_and_stats():
