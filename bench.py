@@ -309,9 +309,22 @@ def main(argv=None) -> int:
     # batch-1 latency block: single-process GPU runs only (in a multi-rank job the other ranks would sit in
     # process-group teardown while rank 0 builds and tunes more engines)
     plan_b8 = None if cpu else eng.plan_status
+    dev_bytes_b8 = eng.device_bytes
+
+    def release_step():
+        """Tear the throughput step down in dependency order: the prefetcher's copies ride the engine's side stream,
+        so its buffers and events must go before the engine (and with it that stream) is destroyed -- left to
+        interpreter shutdown, the order is arbitrary and torch may touch the destroyed stream (segfault at exit)."""
+        nonlocal eng, dp, h2d
+        sync()
+        dp, h2d = None, None
+        if not cpu:
+            eng.close()
+        eng = None
+
+    h2d = None if cpu else h2d
     if rank == 0 and world == 1 and not args.no_latency and not cpu:
-        dev_bytes_b8 = eng.device_bytes
-        del eng
+        release_step()
         from stereoalgorithms_amd.models.engine import NativeStereoEngine
         for preset in ("raftstereo-sceneflow", "raftstereo-realtime", *OTHER_MS):
             # timed engine without stage stamps (they add serialising nodes to the frame graph)
@@ -346,8 +359,8 @@ def main(argv=None) -> int:
                              "plan_loaded": e1.plan_status["loaded"], "plan_saved": e1.plan_status["saved"],
                              "device_stages_ms": {k: round(v, 3) for k, v in e1.stage_times()}}
             e1.close()
-    else:
-        dev_bytes_b8 = eng.device_bytes
+    if eng is not None:
+        release_step()
     if rank == 0:
         base_fps = 1000.0 / BASELINE_MS[args.model]
         lat = extra.get(args.model, {}).get("latency_ms_mean")

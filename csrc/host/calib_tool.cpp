@@ -405,6 +405,11 @@ bool is_xcorner(const FImg& img, double cx, double cy, double rad) {
 }  // namespace
 
 // ------------------------------------------------------------------ cornerSubPix
+// Attribution: this follows OpenCV's cornerSubPix (modules/imgproc/src/cornersubpix.cpp, OpenCV, Apache-2.0 /
+// BSD-3-Clause, Copyright (C) Intel Corporation, Willow Garage, OpenCV Foundation et al.): the same Gaussian window
+// mask, the normal-equation accumulators (a, b, c, bb1, bb2), the stop rules and the fallback to the input corner
+// when a refined position leaves the search window -- the reference tool calls cv::cornerSubPix
+// (Stereo_Calibration/Stereo_Calibration.cpp:108-120) and the calibration tests compare against its behaviour.
 void corner_subpix(const Mat& gray, std::vector<std::array<double, 2>>& corners, int win, int iters, double eps) {
   const FImg img = to_float(gray);
   const int ww = 2 * win + 1;

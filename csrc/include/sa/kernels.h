@@ -29,8 +29,7 @@ enum SaEpi {
   SA_EPI_GRU_Q = 2,     // q = tanh(acc+b+cq) ; h = (1-z)h + zq  (in place on h)
   SA_EPI_FLOW_ACC = 3,  // fp32 out[m*out_stride + c] += acc*scale + bias for c < min(Cout, out_stride)
   SA_EPI_STORE_F32 = 4,  // y = act(acc*scale + bias) -> fp32
-  SA_EPI_PROJ = 5,       // y = act(acc*scale + bias) projected onto the taps of a following conv
-                         // (proj_* fields; y itself is stored only when out != NULL)
+  // 5: retired (projection epilogue; the flow-head conv2 is sa_flow_head_tail now)
   SA_EPI_GRU_ZRQ = 6     // Cout = 3 Hd stacked [convz | convr | convq restricted to the x inputs]: z -> aux,
                          // r*h -> rh as SA_EPI_GRU_ZR, and the x half of q's pre-activation (acc + bias + cq)
                          // -> out (fp16); the following SA_EPI_GRU_Q conv over r*h alone adds it back (res)
@@ -86,16 +85,6 @@ typedef struct {
   // broadcast over depth
   const void* gate;
   int32_t gate_stride;
-  // SA_EPI_PROJ: fuse a following (proj_taps = kh*kw)-tap conv with proj_oc output channels into
-  // this conv's epilogue.  Every output pixel m of an n-tile (slice = n0 / BN) writes
-  //   proj_out[(slice * proj_taps * proj_oc + t * proj_oc + o) * proj_plane + m]
-  //     = sum_{c in tile} y[m][c] * proj_w[(t * proj_oc + o) * Cout + c]
-  // and sa_proj_stencil() sums slices and taps (with the zero padding of the following conv).
-  // proj_taps * proj_oc <= 9; Cout a multiple of the chosen n-tile (64 suffices).
-  const float* proj_w;
-  float* proj_out;
-  int32_t proj_taps, proj_oc;
-  int64_t proj_plane;
   // instance-norm statistics spread over `stats_slots` copies of [N][Cout][2] (block b adds into
   // copy b % slots): atomics of the thousands of blocks of one image no longer pile onto one row of
   // addresses.  sa_stats_reduce() folds the copies into copy 0 before the statistics are read.
@@ -103,32 +92,22 @@ typedef struct {
   // real input channels when the single source is zero-padded beyond them (0 = all channels real); lets
   // the 7x7 stem kernel (tile_cfg 22) stage only the real channels
   int32_t cin_real;
-  // input instance norm fused into the conv's input staging (tile_cfg 23 only): the source is the raw previous
-  // conv output and every in-image pixel is replaced by in_act((x - mean) * rstd) before the GEMM, mean / rstd from
-  // in_stats [N][Cin][2] (fixed point, slots already folded), eps 1e-5; padding stays zero
-  const sa_stat_t* in_stats;
-  int32_t in_act;
 } SaConvArgs;
 
 int sa_conv2d(const SaConvArgs* a, hipStream_t stream);
-// Direct 3x3 / stride 1 / pad 1 conv, 64 -> 64 channels, weights ([>=64][kpad >= 576] packed fp16)
-// resident in LDS, persistent 2x64-pixel output tiles; bias / act / slotted IN statistics epilogue.
-// Also reachable through sa_conv2d with tile_cfg = 9.
-int sa_conv3x3_c64_direct(const void* x, int xs, const void* w, int kpad, const float* bias, void* out, int os,
-                          int N, int H, int W, int act, float alpha, sa_stat_t* stats, int slots, int max_blocks,
-                          hipStream_t stream);
 // 7x7 / pad 3 / stride 1 or 2 stem conv, <= 4 real input channels (pixel stride xs, 8-B aligned) -> 64
 // channels, weights packed [>=64][kpad] with K ordered (kh, kw, ci < cpad); act none / relu / leaky; optional
 // slotted IN statistics.  Also reachable through sa_conv2d with tile_cfg = 22.
 int sa_conv7x7_stem(const void* x, int xs, int creal, const void* w, int kpad, int cpad, const float* bias, void* out,
                     int os, int N, int H, int W, int stride, int act, float alpha, sa_stat_t* stats, int slots,
                     hipStream_t stream);
-// Same conv, two waves per SIMD (8-wave workgroups, channel-split stationary weights, register epilogue with
-// buffer stores, optional residual y = act2(act(acc + bias) + res) without statistics); tile_cfg = 23.  -5 when the output span exceeds 32-bit buffer offsets.
+// Direct 3x3 / stride 1 / pad 1 conv, 64 -> 64 channels (8-wave persistent workgroups over 2x64-pixel tiles,
+// channel-split weights stationary in registers, DMA ring, register epilogue with buffer stores): bias / act,
+// optional slotted IN statistics or residual y = act2(act(acc + bias) + res) (not both); tile_cfg = 23.
+// -5 when the output span exceeds 32-bit buffer offsets.
 int sa_conv3x3_c64_direct2(const void* x, int xs, const void* w, int kpad, const float* bias, void* out, int os,
                            int N, int H, int W, int act, float alpha, sa_stat_t* stats, int slots, const void* res,
-                           int rs, int act2, const sa_stat_t* in_stats, int in_act, int max_blocks,
-                           hipStream_t stream);
+                           int rs, int act2, int max_blocks, hipStream_t stream);
 // Direct 3x3 / pad 1 conv to 96 channels: 96 -> 96 at stride 1 or 64 -> 96 at stride 2 (12-wave persistent
 // tiles, weights stationary in registers, DMA ring); act none / relu / leaky, optional slotted IN statistics or
 // residual (not both); tile_cfg = 24.  -5 for other shapes or an output span past 32-bit buffer offsets.
@@ -141,23 +120,11 @@ int sa_conv3x3_c96_direct(const void* x, int xs, int cin, int stride, const void
 int sa_conv1x1_point(const void* x, int xs, int cin, const void* w, int kpad, const float* bias, void* out, int os,
                      int cout, int N, int H, int W, int stride, int act, float alpha, sa_stat_t* stats, int slots,
                      hipStream_t stream);
-// Number of n-tiles (projection slices) sa_conv2d() will use for these args.
-int sa_conv2d_nslices(const SaConvArgs* a);
 // split-K footprint of the calling thread's last successful sa_conv2d launch: slab floats and tile
 // counters it used (0, 0 when it did not split)
 void sa_conv2d_last_split(long* ws_floats, long* tiles);
-// Following-conv stencil of SA_EPI_PROJ: out[n][y][x][o] (fp32, pixel stride out_stride) gets
-// (accumulate ? out + : ) bias[o] + sum_{s < nslices, (ky,kx)} P[s][(ky*kw+kx)*oc + o][n][y+ky-ph][x+kx-pw]
-// (zero outside the image).  Stride-1 'same' convs only.
-int sa_proj_stencil(const float* P, int nslices, long plane, int N, int H, int W, int kh, int kw,
-                    int oc, const float* bias, float* out, int out_stride, int accumulate,
-                    hipStream_t stream);
-// Skinny-conv front half (a conv with <= 32 output taps x channels, e.g. the RAFT / CREStereo flow-head
-// conv2 256 -> 1 or 2, 3x3): P[t][m] = sum_c x[m][c] * w[t][c] for t < ntaps, as one MFMA GEMM that reads
-// the fp16 input exactly once (the implicit-GEMM conv re-reads it per tap).  x: fp16, pixel stride xs,
-// C % 32 == 0, C <= 256; w: fp16 [16][C] (ntaps <= 16) or [32][C], taps >= ntaps zero.
-// sa_proj_stencil() then forms the conv (tap index (ky*kw+kx)*oc + o).
-// tap_proj + proj_stencil of a 3x3 C -> 1 conv in one launch (halo-tiled, planes in LDS):
+// Flow-head conv2 (3x3 C -> 1, the RAFT flow head) in one launch: MFMA tap projections of a halo-tiled region
+// (planes in LDS) + the 9-tap stencil, accumulated into the flow:
 // flow[n][y][x] += bias[0] + sum_{ky,kx} sum_c y[n][y+ky-1][x+kx-1][c] * w16[ky*3+kx][c] (zero padding);
 // w16 fp16 [16][C] (taps >= 9 zero), C % 32 == 0, C <= 256, flow fp32 [N][H][W].
 int sa_flow_head_tail(const void* y, int ys, int C, const void* w16, const float* bias, float* flow, int N, int H,
@@ -166,8 +133,6 @@ int sa_flow_head_tail(const void* y, int ys, int C, const void* w16, const float
 // row (ky*3+kx)*oc + o (rows >= 9 oc zero)
 int sa_flow_head_tail_oc(const void* y, int ys, int C, const void* w16, int oc, const float* bias, float* flow, int N,
                          int H, int W, hipStream_t stream);
-int sa_tap_proj(const void* x, int xs, long M, int C, const void* w, int ntaps, float* P, long plane,
-                hipStream_t stream);
 
 // ---- normalisation / elementwise ------------------------------------------------------------
 // Instance-norm apply (biased var, eps): y = act(norm(x)); if res: y = act2(resnorm(res) + y)

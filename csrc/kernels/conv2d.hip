@@ -60,7 +60,6 @@ __device__ __forceinline__ void store8(f16* p, const float* v) {
 // Main-loop staging modes
 enum : int {
   kRegK32 = 0,  // register-staged, BK = 32 (K not a multiple of 64)
-  kDmaK64 = 1,  // global->LDS DMA (global_load_lds_dwordx4), BK = 64 (opt-in, SA_CONV_GLDS=1)
   kRegK64 = 2,  // register-staged, BK = 64: 8 x 16-B loads in flight per thread, one barrier per 64-deep step
   kFastK64 = 3,  // kRegK64 when every source's channel count is a multiple of 64: the (tap, source,
                  // channel) position of a k-step is wave-uniform, so the im2col gather is one
@@ -80,9 +79,6 @@ enum : int {
               // 6-deep LDS ring, waves 0-3 (one per SIMD) and 4-7 offset by one barrier so that on every SIMD
               // one wave runs a 16x16x32 MFMA cluster while the other reads its next fragments and issues DMA
               // (cdna_hip_programming.md §5 "256^2 8-phase template", T3-T5)
-  kPingM = 8,  // kPing with the DMA pieces issued between the MFMAs of the compute slot (an LDS-DMA issue costs
-               // ~60 cycles among bare MFMAs, 100-185 beside a slot's ds_reads: MI355X_MICROARCH.md), leaving only
-               // the fragment reads in the read slot
   kHalo = 9,    // 3x3 / stride 1 convs with halo reuse: the output tile is a TH x TW patch of one image (8 x 32),
                 // the K loop runs channel-chunk-major (64 channels, then the 9 taps), and each chunk's input patch
                 // (TH+2) x (TW+2) x 64 is DMA'd into LDS ONCE and read by all 9 taps at shifted offsets -- the im2col
@@ -96,9 +92,8 @@ __host__ __device__ constexpr bool is_halo(int mode) { return mode == kHalo || m
 
 template <int BM, int BN, int WM, int WN, int MODE = kRegK32>
 struct ConvCfg {
-  static constexpr bool GL = MODE == kDmaK64;
   static constexpr bool WIDE = MODE == kWide;
-  static constexpr bool PING = MODE == kPing || MODE == kPingM;
+  static constexpr bool PING = MODE == kPing;
   static constexpr bool BANDED = WIDE || PING;  // C tile staged through LDS in row bands
   static constexpr int BK = (MODE == kRegK32 || WIDE || PING) ? 32 : 64;
   static constexpr int KCH = BK / 8;  // 16-byte chunks per row per stage
@@ -159,20 +154,6 @@ __device__ __attribute__((aligned(16))) const unsigned char g_zero16[64] = {0};
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-// one recursive-halving step of the projection reduce-scatter over K live values: lanes whose bit O
-// is set keep the upper half and receive the partner's copy of it (partner = DPP control CTRL)
-template <int K, int O, int CTRL>
-__device__ __forceinline__ void rs_step(float* y, int cc) {
-  const bool up = (cc & O) != 0;
-#pragma unroll
-  for (int i = 0; i < K / 2; ++i) {
-    const float give = up ? y[i] : y[i + K / 2];
-    const float keep = up ? y[i + K / 2] : y[i];
-    const int g = __builtin_amdgcn_update_dpp(0, __float_as_int(give), CTRL, 0xF, 0xF, false);
-    y[i] = keep + __int_as_float(g);
-  }
-}
-
 #define SA_STR2(x) #x
 #define SA_STR(x) SA_STR2(x)
 // s_waitcnt vmcnt(N) with a compile-time N (the asm string needs a literal)
@@ -202,8 +183,6 @@ __device__ __forceinline__ void wait_stages(int s) {
   }
 }
 
-// PROJ: the SA_EPI_PROJ epilogue is compiled only into its own instantiations -- its registers
-// (hoisted tap weights, 16 partials) would otherwise cost every other conv its occupancy
 // One (tile, k-range) work item of the implicit GEMM: the output tile (bx, by) over k-steps [kt0, kt0 + nk).
 // S > 1: this item is contributor z of the S items of tile `ctr`; it writes its partial sums to its slab and
 // the last contributor to arrive (counter ctr) sums the S contributors' slabs in contributor order and runs
@@ -211,7 +190,7 @@ __device__ __forceinline__ void wait_stages(int s) {
 // skI k-steps): contributor c is block b = slab_base + c, and since only a block's first and last segments
 // can be partial tiles its slab is 2b (the segment starts the block's range) or 2b + 1, so 2G slabs cover
 // any tile count.  Called once per block (grid tiling / split-K) or once per segment of a stream-K block.
-template <int BM, int BN, int WM, int WN, int MODE, bool PROJ>
+template <int BM, int BN, int WM, int WN, int MODE>
 __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const int bx, const int by, const int kt0,
                                           const int nk, const int S, const int z, const int slab_base,
                                           const int ctr, const int skG, const long skI) {
@@ -458,53 +437,99 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
       const int r = wm * C::TM + i * 16 + frow;
       aq0[i] = (r / TW) * PW + (r % TW);
     }
+    // fragment reads of k-half kk of step st (patch buffer of its chunk, tap offset, weight slot st % 3)
+    auto frag_addr_a = [&](int st, int i, int kk) {
+      const int c = st / 9, t = st - c * 9;
+      const int q = aq0[i] + (t / 3) * PW + (t - (t / 3) * 3);
+      const int lc = (lane >> 4) + 4 * kk;
+      return abuf0 + (c & 1) * APB + q * 128 + ((lc ^ ((q >> 1) & 7)) << 4);
+    };
+    auto frag_addr_b = [&](int st, int j, int kk) {
+      const int row = wn * C::TN + j * 16 + frow;
+      const int lc = (lane >> 4) + 4 * kk;
+      return bbuf0 + (st % 3) * BST + row * 128 + ((lc ^ ((row >> 1) & 7)) << 4);
+    };
+    auto read_half = [&](int st, int kk, half8* af, half8* bf) {
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) af[i] = *reinterpret_cast<const half8*>(frag_addr_a(st, i, kk));
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) bf[j] = *reinterpret_cast<const half8*>(frag_addr_b(st, j, kk));
+    };
+    auto mfma_half = [&](const half8* af, const half8* bf) {
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    };
+    // the MFMAs of one k-half with the fragment reads of another interleaved one read per MFMA (as kGlds3)
+    auto mfma_read = [&](const half8* am, const half8* bm, int st, int kk, half8* ar, half8* br) {
+#pragma unroll
+      for (int tt = 0; tt < C::FM * C::FN; ++tt) {
+        const int i = tt / C::FN, j = tt - (tt / C::FN) * C::FN;
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(am[i], bm[j], acc[i][j], 0, 0, 0);
+        if (tt < C::FM) ar[tt] = *reinterpret_cast<const half8*>(frag_addr_a(st, tt, kk));
+        else if (tt < C::FM + C::FN) br[tt - C::FM] = *reinterpret_cast<const half8*>(frag_addr_b(st, tt - C::FM, kk));
+      }
+      static_assert(C::FM + C::FN <= C::FM * C::FN, "one read per MFMA slot");
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+#pragma unroll
+      for (int tt = 0; tt < C::FM + C::FN; ++tt) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, C::FM * C::FN - C::FM - C::FN - 1, 0);
+    };
+    // Schedule (kGlds3's, with a 3-slot weight ring and two patch buffers).  Iteration st:
+    //   [A] MFMAs of half 0 of step st + fragment reads of its half 1
+    //   lgkmcnt(0); vmcnt(<= pieces issued in iteration st - 1); raw s_barrier -- step st + 1's weights (and, at
+    //       a chunk boundary, its patch) have landed for every wave, and every wave is done reading step st
+    //   [B] MFMAs of half 1 of step st + fragment reads of half 0 of step st + 1
+    //   refill: the patch of chunk c + 2 into chunk c's buffer when st is chunk c's last step, then the weights
+    //       of step st + 3 into slot st % 3 (patch first, so waiting for a step's weights covers its patch)
+    // Prologue: patch 0, weights 0, 1, 2, patch 1.
     issue_a(0, 0);
     issue_b(0, 0);
     if (nsteps > 1) issue_b(1, 1);
-    int prev = nsteps > 1 ? NB : 0;  // DMA pieces issued after the weights of the step about to be waited for
-    int bcur = 0;
+    if (nsteps > 2) issue_b(2, 2);
+    if (nchunk > 1) issue_a(1, 1);
+    // pieces issued after the weights of step 0 / step 1 (the first two waits)
+    const int after0 = (nsteps > 1 ? NB : 0) + (nsteps > 2 ? NB : 0) + (nchunk > 1 ? NAH : 0);
+    if (after0 >= 2 * NB + NAH) wait_vmcnt<2 * NB + NAH>();
+    else if (after0 >= NB + NAH) wait_vmcnt<NB + NAH>();
+    else if (after0 >= 2 * NB) wait_vmcnt<2 * NB>();
+    else if (after0 >= NB) wait_vmcnt<NB>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    half8 a0[C::FM], b0[C::FN], a1[C::FM], b1[C::FN];
+    read_half(0, 0, a0, b0);
+    int prev = (nsteps > 2 ? NB : 0) + (nchunk > 1 ? NAH : 0);  // issued after step 1's weights
     for (int st = 0; st < nsteps; ++st) {
-      if (prev == NAH + NB) wait_vmcnt<NAH + NB>();
-      else if (prev == NB) wait_vmcnt<NB>();
-      else wait_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      const int c = st / 9, t = st - c * 9;
-      int issued = 0;
-      if (t == 0 && c + 1 < nchunk) {
-        issue_a(c + 1, (c + 1) & 1);
-        issued += NAH;
-      }
-      if (st + 2 < nsteps) {
-        issue_b(st + 2, bcur == 0 ? 2 : bcur - 1);
-        issued += NB;
-      }
-      prev = issued;
-      const char* sa = abuf0 + (c & 1) * APB;
-      const char* sb = bbuf0 + bcur * BST;
-      const int ky = t / 3, kx = t - ky * 3;
-      const int toff = ky * PW + kx;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int lc = (lane >> 4) + 4 * kk;
-        half8 af[C::FM], bf[C::FN];
-#pragma unroll
-        for (int i = 0; i < C::FM; ++i) {
-          const int q = aq0[i] + toff;
-          af[i] = *reinterpret_cast<const half8*>(sa + q * 128 + ((lc ^ ((q >> 1) & 7)) << 4));
+      mfma_read(a0, b0, st, 1, a1, b1);
+      if (st + 1 < nsteps) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (prev >= NB + NAH) wait_vmcnt<NB + NAH>();
+        else if (prev >= NB) wait_vmcnt<NB>();
+        else if (prev >= NAH) wait_vmcnt<NAH>();
+        else wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        mfma_read(a1, b1, st + 1, 0, a0, b0);
+        const int c = st / 9, t = st - c * 9;
+        int issued = 0;
+        if (t == 8 && c + 2 < nchunk) {
+          issue_a(c + 2, c & 1);
+          issued += NAH;
         }
-#pragma unroll
-        for (int j = 0; j < C::FN; ++j) {
-          const int row = wn * C::TN + j * 16 + frow;
-          bf[j] = *reinterpret_cast<const half8*>(sb + row * 128 + ((lc ^ ((row >> 1) & 7)) << 4));
+        if (st + 3 < nsteps) {
+          issue_b(st + 3, st % 3);
+          issued += NB;
         }
-#pragma unroll
-        for (int i = 0; i < C::FM; ++i)
-#pragma unroll
-          for (int j = 0; j < C::FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        prev = issued;
+      } else {
+        mfma_half(a1, b1);
       }
-      bcur = bcur == 2 ? 0 : bcur + 1;
     }
     __syncthreads();  // all fragment reads done before the epilogue reuses LDS
   } else if constexpr (is_glds(MODE)) {
@@ -883,109 +908,7 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
         if (t < nk) issue(t);
       if (nk > 0) wait_stages<NAB, NS - 2>((nk - 1 < NS - 2 ? nk - 1 : NS - 2));
       bar();
-      if constexpr (MODE == kPingM) {
-        // The compute slot of stage s also issues this wave's pieces of stage s + NS - 1 (into the buffer of
-        // stage s - 1, whose last reads (G1, slot 2s - 2) were retired before the barrier opening slot 2s),
-        // one piece after every few MFMAs:
-        //   slot 2s:   G0 MFMA(s) + DMA(s+NS-1)   G1 read(s)
-        //   slot 2s+1: G0 read(s+1)               G1 MFMA(s) + DMA(s+NS-1)
-        // Before the barrier opening slot 2s+1 stage s+1 must have landed: G0 has issued through s+NS-1 at
-        // that point, G1 through s+NS-2.
-        constexpr int GAP = C::FM * C::FN / NAB;  // MFMAs between two pieces
-        static_assert(GAP >= 2, "MFMA slots per DMA piece");
-        auto mfma_dma = [&](int buf) {
-          char* sa = smem + buf * STG;
-          char* sb = sa + BM * 64;
-          const f16* sp;
-          int sst;
-          if (ci0 < sb1) { sp = sp0 + ci0; sst = ss0; }
-          else if (ci0 < sb2) { sp = sp1 + (ci0 - sb1); sst = ss1; }
-          else if (ci0 < sb3) { sp = sp2 + (ci0 - sb2); sst = ss2; }
-          else { sp = sp3 + (ci0 - sb3); sst = ss3; }
-          const int koff = tap * p.Cin + ci0;
-          __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-          for (int t = 0; t < C::FM * C::FN; ++t) {
-            const int i = t / C::FN, j = t % C::FN;
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-            if (t % GAP == 0 && t / GAP < NAB) {
-              const int q = t / GAP;
-              if (q < NA) {
-                const bool v = (vmask[q] >> tap) & 1ull;
-                const f16* ga = sp + ((pixb[q] + toff) * sst + lcho[q]);
-                __builtin_amdgcn_global_load_lds(v ? (const void*)ga : zero_src,
-                                                 (lds_void_t*)(sa + (wave * NA + q) * 1024), 16, 0, 0);
-              } else {
-                __builtin_amdgcn_global_load_lds((const void*)(wrow[q - NA] + koff),
-                                                 (lds_void_t*)(sb + (wave * NB + q - NA) * 1024), 16, 0, 0);
-              }
-            }
-          }
-          __builtin_amdgcn_s_setprio(0);
-          ++tap;
-          ++kw_;
-          toff += p.dw;
-          if (kw_ == KW) {
-            kw_ = 0;
-            toff += p.dh * p.W - KW * p.dw;
-            ++kh_;
-            if (kh_ == KH) {
-              kh_ = 0;
-              toff += p.H * p.W - KH * p.dh * p.W;
-            }
-          }
-          if (tap == taps_all) {
-            tap = 0;
-            toff = 0;
-            ci0 += 32;
-          }
-        };
-        int rbuf = 0, ibuf = NS - 1;
-        if (g == 0) {
-          if (nk > 0) read_stage(0);
-          rbuf = 1;
-          lgkm0();
-          bar();
-          for (int s = 0; s < nk; ++s) {
-            if (s + NS - 1 < nk) {
-              mfma_dma(ibuf);
-              ibuf = ibuf == NS - 1 ? 0 : ibuf + 1;
-            } else {
-              mfma_stage();
-            }
-            if (s + 1 < nk) {
-              const int last = s + NS - 1 < nk - 1 ? s + NS - 1 : nk - 1;
-              wait_stages<NAB, NS - 2>(last - (s + 1));
-            }
-            bar();
-            if (s + 1 < nk) {
-              read_stage(rbuf);
-              rbuf = rbuf == NS - 1 ? 0 : rbuf + 1;
-            }
-            lgkm0();
-            bar();
-          }
-        } else {
-          bar();
-          for (int s = 0; s < nk; ++s) {
-            read_stage(rbuf);
-            rbuf = rbuf == NS - 1 ? 0 : rbuf + 1;
-            lgkm0();
-            if (s + 1 < nk) {
-              const int last = s + NS - 2 < nk - 1 ? s + NS - 2 : nk - 1;
-              wait_stages<NAB, NS - 3>(last - (s + 1));
-            }
-            bar();
-            if (s + NS - 1 < nk) {
-              mfma_dma(ibuf);
-              ibuf = ibuf == NS - 1 ? 0 : ibuf + 1;
-            } else {
-              mfma_stage();
-            }
-            bar();
-          }
-        }
-      } else if (g == 0) {
+      if (g == 0) {
         int rbuf = 0;       // buffer of the next stage to read (s + 1 after the first read)
         int ibuf = NS - 1;  // buffer of the next stage to issue
         if (nk > 0) read_stage(0);
@@ -1114,113 +1037,6 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
     }
     __syncthreads();  // all fragment reads done before the epilogue reuses LDS
     }  // kWide schedule
-  } else if constexpr (C::GL) {
-    // ---------------- DMA staging: [rows][64 halfs] (128 B) per stage, chunk XOR-swizzled ----------
-    // LDS image is lane-linear per wave instruction (q*16 = row*128 + pch*16); the swizzle lives on
-    // the SOURCE side: slot q fetches logical chunk lch = pch ^ ((row>>1)&7), so the fragment reads
-    // (16 rows x one chunk per ds_read_b128 lane group) hit 16 distinct 16-B bank slots.
-    // 16-B chunks per thread per stage (>= 1 so every config instantiates; BN < 32 never takes
-    // this path, see launch_cfg)
-    constexpr int NA = BM / 32 > 0 ? BM / 32 : 1, NB = BN / 32 > 0 ? BN / 32 : 1;
-    const int sb1 = p.src[0].channels;
-    const int sb2 = sb1 + (p.nsrc > 1 ? p.src[1].channels : 0);
-    const int sb3 = sb2 + (p.nsrc > 2 ? p.src[2].channels : 0);
-    int a_ih0[NA], a_iw0[NA], a_nb[NA], a_d0[NA], a_tap[NA], a_ci[NA];
-    bool a_ok[NA];
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int q = (wave * NA + i) * 64 + lane;
-      const int row = q >> 3, pch = q & 7;
-      const int lch = pch ^ ((row >> 1) & 7);
-      const int m = m0 + row;
-      a_ok[i] = m < M;
-      const int mm = a_ok[i] ? m : 0;
-      const int img = mm / HWo;
-      const int r = mm - img * HWo;
-      const int oh = r / p.Wo, ow = r - oh * p.Wo;
-      const int n = img / Do, od = img - n * Do;
-      a_ih0[i] = oh * p.sh - p.ph;
-      a_iw0[i] = ow * p.sw - p.pw;
-      a_d0[i] = od * sd - p.pd;
-      a_nb[i] = n * Di + a_d0[i];  // input slice index for kd = 0
-      const int kc = kt0 * C::BK + lch * 8;
-      a_tap[i] = kc / p.Cin;
-      a_ci[i] = kc - a_tap[i] * p.Cin;
-    }
-    const f16* wbase[NB];
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int q = (wave * NB + i) * 64 + lane;
-      const int row = q >> 3, pch = q & 7;
-      const int lch = pch ^ ((row >> 1) & 7);
-      wbase[i] = reinterpret_cast<const f16*>(p.weight) + (size_t)(n0 + row) * p.Kpad + (size_t)kt0 * C::BK + lch * 8;
-    }
-    const void* zero_src = g_zero16;
-    auto issue = [&](int kt, int buf) {
-      char* sa = smem + buf * (C::A_BYTES + C::B_BYTES);
-      char* sb = sa + C::A_BYTES;
-#pragma unroll
-      for (int i = 0; i < NA; ++i) {
-        const int tap = a_tap[i], ci = a_ci[i];
-        const int kd = tap / khw, t2 = tap - kd * khw;
-        const int kh = t2 / p.KW, kw = t2 - kh * p.KW;
-        const int ih = a_ih0[i] + kh * p.dh, iw = a_iw0[i] + kw * p.dw, dd = a_d0[i] + kd;
-        const bool ok = a_ok[i] && tap < taps && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W && dd >= 0 && dd < Di;
-        const int s = (ci >= sb1) + (ci >= sb2) + (ci >= sb3);
-        const int cbase = s == 0 ? 0 : (s == 1 ? sb1 : (s == 2 ? sb2 : sb3));
-        const void* g = zero_src;
-        if (ok) {
-          const size_t pix = ((size_t)(a_nb[i] + kd) * p.H + ih) * p.W + iw;
-          g = reinterpret_cast<const f16*>(p.src[s].ptr) + pix * p.src[s].stride + (ci - cbase);
-        }
-        __builtin_amdgcn_global_load_lds(g, (lds_void_t*)(sa + (wave * NA + i) * 1024), 16, 0, 0);
-        // next k-step of this chunk
-        int nci = ci + C::BK, ntap = tap;
-        while (nci >= p.Cin) {
-          nci -= p.Cin;
-          ++ntap;
-        }
-        a_ci[i] = nci;
-        a_tap[i] = ntap;
-      }
-#pragma unroll
-      for (int i = 0; i < NB; ++i)
-        // (explicit void* source: a typed _Float16* argument makes the host pass drop the kernel stub)
-        __builtin_amdgcn_global_load_lds((const void*)(wbase[i] + (size_t)kt * C::BK),
-                                         (lds_void_t*)(sb + (wave * NB + i) * 1024), 16, 0, 0);
-    };
-    // fragment read: row = lane&15 (+16 i), logical chunk = (lane>>4) + 4*kk
-    const int frow = lane & 15;
-    if (nk > 0) issue(0, 0);
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();  // stage kt landed for every wave; buffer cur^1 no longer read
-      if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
-      const char* sa = smem + cur * (C::A_BYTES + C::B_BYTES);
-      const char* sb = sa + C::A_BYTES;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        half8 af[C::FM], bf[C::FN];
-        const int lc = (lane >> 4) + 4 * kk;
-#pragma unroll
-        for (int i = 0; i < C::FM; ++i) {
-          const int row = wm * C::TM + i * 16 + frow;
-          af[i] = *reinterpret_cast<const half8*>(sa + row * 128 + ((lc ^ ((row >> 1) & 7)) << 4));
-        }
-#pragma unroll
-        for (int j = 0; j < C::FN; ++j) {
-          const int row = wn * C::TN + j * 16 + frow;
-          bf[j] = *reinterpret_cast<const half8*>(sb + row * 128 + ((lc ^ ((row >> 1) & 7)) << 4));
-        }
-#pragma unroll
-        for (int i = 0; i < C::FM; ++i)
-#pragma unroll
-          for (int j = 0; j < C::FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
-      }
-    }
-    __syncthreads();  // all fragment reads done before the epilogue reuses LDS
   } else {
   // ---------------- per-thread A-row precompute ----------------
   const int cth = tid % C::KCH;  // chunk index this thread loads (constant over k)
@@ -1434,7 +1250,7 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
   constexpr int RPI = NT / CPR;  // rows per pass
   const int cc = tid % CPR;
   const int co = n0 + cc * 8;
-  const bool do_stats = !PROJ && p.stats != nullptr;
+  const bool do_stats = p.stats != nullptr;
   // Instance-norm statistics: per-thread partial sums for the (at most) two images a BM-row tile
   // can straddle, reduced across the block in LDS, then ONE double atomic per (block, image,
   // channel).  Per-thread atomics to the same N*C addresses serialise at the memory side
@@ -1482,20 +1298,6 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
     __syncthreads();
   }
 
-  // SA_EPI_PROJ: this thread's 8 channels of the projection taps, hoisted out of the row loop
-  constexpr int kProjMax = PROJ ? 9 : 1;
-  float pw8[kProjMax][8];
-  if (PROJ) {
-    const int np = p.proj_taps * p.proj_oc;
-    // opaque base pointer: keeps the compiler from hoisting these loads above the main loop (72
-    // registers live across it would cost every conv kernel of this template its occupancy)
-    const float* pwb = p.proj_w + co;
-    asm volatile("" : "+v"(pwb));
-#pragma unroll
-    for (int t = 0; t < kProjMax; ++t)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) pw8[t][j] = (t < np && j < nvalid) ? pwb[(size_t)t * p.Cout + j] : 0.f;
-  }
   // rows [r0, r1) of the tile, their C values staged in LDS at row - cbase
   auto epi_rows = [&](const int r0, const int r1, const int cbase) {
     for (int row = r0 + tid / CPR; row < r1; row += RPI) {
@@ -1591,42 +1393,6 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
               ssq[j] += v[j] * v[j];
             }
           }
-        }
-      } else if (PROJ) {
-        // flow-head fusion: project this row's channels onto the taps of the following conv.
-        // The CPR lanes holding one row (consecutive, CPR-aligned) reduce-scatter their 16 tap
-        // partials (taps padded with zeros) with 15 xor shuffles for CPR = 16: afterwards lane cc
-        // holds the totals of taps PF*cc .. PF*cc + PF-1 (PF = 16 / CPR)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], p.act, p.alpha);
-        if (p.out) {
-          f16* op = reinterpret_cast<f16*>(p.out) + (size_t)m * p.out_stride + co;
-          if (full) store8(op, v);
-          else for (int j = 0; j < nvalid; ++j) op[j] = (f16)v[j];
-        }
-        float y[16];
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-          y[t] = 0.f;
-          if (t < kProjMax) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) y[t] += v[j] * pw8[t][j];
-          }
-        }
-        // partners via DPP (VALU lane permutes, no LDS crossbar): bit 3 = row mirror, bit 2 = half-row
-        // mirror, bits 1 / 0 = quad permutes; each pairs lanes that differ in that bit and agree in
-        // the higher ones, which is all recursive halving needs
-        if constexpr (CPR >= 16) rs_step<16, 8, 0x140>(y, cc);
-        if constexpr (CPR >= 8) rs_step<16 * 8 / CPR, 4, 0x141>(y, cc);
-        if constexpr (CPR >= 4) rs_step<16 * 4 / CPR, 2, 0x4E>(y, cc);
-        if constexpr (CPR >= 2) rs_step<16 * 2 / CPR, 1, 0xB1>(y, cc);
-        constexpr int PF = 16 / CPR;
-        const int np = p.proj_taps * p.proj_oc;
-        float* pout = p.proj_out + (size_t)by * np * p.proj_plane + m;
-#pragma unroll
-        for (int j = 0; j < PF; ++j) {
-          const int t = PF * cc + j;
-          if (t < np) pout[(size_t)t * p.proj_plane] = y[j];
         }
       } else if (p.epi == SA_EPI_GRU_ZR || p.epi == SA_EPI_GRU_ZRQ) {
         const int Hd = p.epi == SA_EPI_GRU_ZR ? p.Cout >> 1 : p.Cout / 3;
@@ -1767,7 +1533,7 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
 // blocks are finished by the last contributor (conv_tile's split-K path, 2G partial slabs).
 // Every block does the same amount of MFMA work whatever T is, so grids of 150 or 600 tiles no longer leave
 // CUs idle in the last wave (Osama et al., "Stream-K", PPoPP'23).
-template <int BM, int BN, int WM, int WN, int MODE, bool PROJ = false>
+template <int BM, int BN, int WM, int WN, int MODE>
 __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_streamk_kernel(const SaConvArgs p) {
   static_assert(MODE == kGlds3, "stream-K is built for the DMA-ring family");
   using C = ConvCfg<BM, BN, WM, WN, MODE>;
@@ -1797,13 +1563,13 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_streamk_kernel(const 
     const int bl = (int)((((long)(t + 1) * nk_all) * G + I - 1) / I) - 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("" : "+s"(pp));
-    conv_tile<BM, BN, WM, WN, MODE, PROJ>(*(const SaConvArgs*)pp, smem, t / gy, t % gy, kb, ke - kb, bl - bf + 1, b - bf, bf, t, G, I);
+    conv_tile<BM, BN, WM, WN, MODE>(*(const SaConvArgs*)pp, smem, t / gy, t % gy, kb, ke - kb, bl - bf + 1, b - bf, bf, t, G, I);
     it += ke - kb;
     __syncthreads();  // the next segment's DMA reuses the LDS this segment's epilogue read
   }
 }
 
-template <int BM, int BN, int WM, int WN, int MODE, bool PROJ = false>
+template <int BM, int BN, int WM, int WN, int MODE>
 __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvArgs p) {
   using C = ConvCfg<BM, BN, WM, WN, MODE>;
   __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
@@ -1828,14 +1594,14 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
       const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
       bx = lin / gy;
       by = lin - bx * gy;
-      conv_tile<BM, BN, WM, WN, MODE, PROJ>(p, smem, bx, by, 0, nk_all, 1, 0, 0, 0, 0, 0);
+      conv_tile<BM, BN, WM, WN, MODE>(p, smem, bx, by, 0, nk_all, 1, 0, 0, 0, 0, 0);
     } else {
       const int b2 = bid - full, t = b2 / S, z = b2 - t * S;
       bx = (full + t) / gy;
       by = full + t - bx * gy;
       const int kt0 = (int)((long)z * nk_all / S);
       const int nk = (int)((long)(z + 1) * nk_all / S) - kt0;
-      conv_tile<BM, BN, WM, WN, MODE, PROJ>(p, smem, bx, by, kt0, nk, S, z, t * S, t, 0, 0);
+      conv_tile<BM, BN, WM, WN, MODE>(p, smem, bx, by, kt0, nk, S, z, t * S, t, 0, 0);
     }
     return;
   }
@@ -1852,15 +1618,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
   const int kt0 = (int)((long)z * nk_all / S);
   const int nk = (int)((long)(z + 1) * nk_all / S) - kt0;
   const int tile = by * gridDim.x + bx;
-  conv_tile<BM, BN, WM, WN, MODE, PROJ>(p, smem, bx, by, kt0, nk, S, z, tile * S, tile, 0, 0);
+  conv_tile<BM, BN, WM, WN, MODE>(p, smem, bx, by, kt0, nk, S, z, tile * S, tile, 0, 0);
 }
 
 template <int BM, int BN, int WM, int WN, int MODE>
 void launch_kernel(dim3 grid, const SaConvArgs* a, hipStream_t stream) {
-  if (a->epi == SA_EPI_PROJ)
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, MODE, true>), grid, dim3(64 * WM * WN), 0, stream, *a);
-  else
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, MODE, false>), grid, dim3(64 * WM * WN), 0, stream, *a);
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, MODE>), grid, dim3(64 * WM * WN), 0, stream, *a);
 }
 
 thread_local long g_split_floats = 0, g_split_tiles = 0;
@@ -1883,33 +1646,17 @@ int device_cus() {
 
 template <int BM, int BN, int WM, int WN>
 int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
-  // DMA path (opt-in, SA_CONV_GLDS=1): measured 14% slower than register staging on the RAFT-SF
-  // batch-8 frame (108 vs 95 ms, one vmcnt(0)+barrier per 64-deep k-step), kept for tuning.
-  constexpr bool can_gl = BN >= 32 && BM >= 32;  // whole-wave DMA instructions per stage
-  static const bool want_gl = [] {
-    const char* e = std::getenv("SA_CONV_GLDS");
-    return e && e[0] == '1';
-  }();
-  const bool gl = can_gl && want_gl && a->Kpad % 64 == 0;
-  static const bool k32_only = [] {
-    const char* e = std::getenv("SA_CONV_K32");
-    return e && e[0] == '1';
-  }();
+  // register-staged family (the DMA-ring tiles live in launch_glds3 / launch_halo / launch_wide / launch_ping).
   // BK = 64 doubles the staging LDS: only for tiles whose C tile needs that LDS anyway (BN >= 64)
-  const bool k64 = BN >= 64 && !gl && !k32_only && a->Kpad % 64 == 0;
+  const bool k64 = BN >= 64 && a->Kpad % 64 == 0;
   // uniform-k fast gather: every source a multiple of 64 channels, K unpadded, <= 64 taps
   const int taps = (a->KD > 0 ? a->KD : 1) * a->KH * a->KW;
   bool fast = k64 && taps <= 64 && (long)taps * a->Cin == a->Kpad;
   for (int i = 0; i < a->nsrc; ++i) fast = fast && a->src[i].channels % 64 == 0;
-  static const bool no_fast = [] {
-    const char* e = std::getenv("SA_CONV_NOFAST");
-    return e && e[0] == '1';
-  }();
-  fast = fast && !no_fast;
   const int M = a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
   const int gx = (M + BM - 1) / BM, gy = (a->Cout + BN - 1) / BN;
   const long tiles = (long)gx * gy;
-  const int nk = a->Kpad / (gl || k64 ? 64 : 32);
+  const int nk = a->Kpad / (k64 ? 64 : 32);
   if (a->splitk < 0) return -4;  // stream-K exists for the DMA-ring (kGlds3) family only
   int S = a->splitk;
   if (S == 0) {
@@ -1919,7 +1666,7 @@ int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
     if (a->ws && a->counters && !a->stats && tiles < 320) {
       S = (int)((640 + tiles - 1) / tiles);
       if (S > 8) S = 8;
-      if (S > nk / (k64 || gl ? 2 : 4)) S = nk / (k64 || gl ? 2 : 4);
+      if (S > nk / (k64 ? 2 : 4)) S = nk / (k64 ? 2 : 4);
       while (S > 1 && ((long)S * tiles * BM * BN > a->ws_floats || tiles > a->n_counters)) --S;
       if (S < 1) S = 1;
     }
@@ -1929,8 +1676,7 @@ int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
     return -4;
   dim3 grid(gx, gy, S);
   note_split(S, tiles, BM * BN);
-  if (gl) launch_kernel<BM, BN, WM, WN, kDmaK64>(grid, a, stream);
-  else if (fast) launch_kernel<BM, BN, WM, WN, kFastK64>(grid, a, stream);
+  if (fast) launch_kernel<BM, BN, WM, WN, kFastK64>(grid, a, stream);
   else if (k64) launch_kernel<BM, BN, WM, WN, kRegK64>(grid, a, stream);
   else launch_kernel<BM, BN, WM, WN, kRegK32>(grid, a, stream);
   return (int)hipGetLastError();
@@ -1963,12 +1709,8 @@ int launch_glds3(const SaConvArgs* a, hipStream_t stream, bool forced) {
       return forced ? -4 : 1;
     g_split_floats = slabs * BM * BN;
     g_split_tiles = tiles;
-    if (a->epi == SA_EPI_PROJ)
-      hipLaunchKernelGGL((conv_igemm_streamk_kernel<BM, BN, WM, WN, kGlds3, true>), dim3((unsigned)G), dim3(C::NT), 0,
-                         stream, *a);
-    else
-      hipLaunchKernelGGL((conv_igemm_streamk_kernel<BM, BN, WM, WN, kGlds3, false>), dim3((unsigned)G), dim3(C::NT),
-                         0, stream, *a);
+    hipLaunchKernelGGL((conv_igemm_streamk_kernel<BM, BN, WM, WN, kGlds3>), dim3((unsigned)G), dim3(C::NT), 0, stream,
+                       *a);
     return (int)hipGetLastError();
   }
   int S = a->splitk;
@@ -1998,7 +1740,7 @@ int launch_halo(const SaConvArgs* a, hipStream_t stream) {
   constexpr int BM = 256, BN = 128;
   bool ok = a->KD <= 0 && a->KH == 3 && a->KW == 3 && a->sh == 1 && a->sw == 1 && a->ph == 1 && a->pw == 1 &&
             a->dh == 1 && a->dw == 1 && a->up == 0 && a->Cin % 64 == 0 && a->Kpad == 9 * a->Cin &&
-            a->Ho == a->H && a->Wo == a->W && a->splitk <= 1 && a->epi != SA_EPI_PROJ;
+            a->Ho == a->H && a->Wo == a->W && a->splitk <= 1;
   for (int i = 0; i < a->nsrc; ++i) ok = ok && a->src[i].channels % 64 == 0;
   if (!ok) return 1;
   using C = ConvCfg<BM, BN, 4, 2, MODE>;
@@ -2010,15 +1752,15 @@ int launch_halo(const SaConvArgs* a, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-// kWide launcher (8 waves, 1 block per CU, never split): uniform-k gather, no projection epilogue.
+// kWide launcher (8 waves, 1 block per CU, never split): uniform-k gather.
 // Returns 1 when the shape does not qualify.
 template <int BM, int BN, int WM, int WN>
 int launch_wide(const SaConvArgs* a, hipStream_t stream) {
-  if (!glds3_eligible(a) || a->epi == SA_EPI_PROJ || a->splitk > 1) return 1;
+  if (!glds3_eligible(a) || a->splitk > 1) return 1;
   const int M = a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
   const int gx = (M + BM - 1) / BM, gy = (a->Cout + BN - 1) / BN;
   note_split(1, 0, 0);
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, kWide, false>), dim3(gx, gy, 1), dim3(64 * WM * WN), 0,
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, kWide>), dim3(gx, gy, 1), dim3(64 * WM * WN), 0,
                      stream, *a);
   return (int)hipGetLastError();
 }
@@ -2027,16 +1769,15 @@ int launch_wide(const SaConvArgs* a, hipStream_t stream) {
 // qualify.
 int device_cus();
 
-template <int BM, int BN, int MODE = kPing>
+template <int BM, int BN>
 int launch_ping(const SaConvArgs* a, hipStream_t stream) {
-  // (the projection epilogue's row reduce-scatter covers at most 16 channel chunks: BN <= 128)
-  if (!glds3_eligible(a) || a->splitk > 1 || a->splitk < 0 || (BN > 128 && a->epi == SA_EPI_PROJ)) return 1;
+  if (!glds3_eligible(a) || a->splitk > 1 || a->splitk < 0) return 1;
   const int M = a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
   const int gx = (M + BM - 1) / BM, gy = (a->Cout + BN - 1) / BN;
   const long T = (long)gx * gy;
   // splitk 0 (auto): split the tiles of the last, partial round over the CUs (all tiles when T < CUs);
   // splitk 1: whole tiles only
-  using C = ConvCfg<BM, BN, 2, 4, MODE>;
+  using C = ConvCfg<BM, BN, 2, 4, kPing>;
   const int nk = a->Kpad / C::BK;
   const int cus = device_cus();
   const long rem = T % cus;
@@ -2050,14 +1791,7 @@ int launch_ping(const SaConvArgs* a, hipStream_t stream) {
   b.splitk = S;
   const long nb = S > 1 ? T - rem + S * rem : T;
   note_split(S, S > 1 ? rem : 0, BM * BN);
-  if constexpr (BN <= 128) {
-    if (a->epi == SA_EPI_PROJ)
-      hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 2, 4, MODE, true>), dim3((unsigned)nb), dim3(512), 0, stream, b);
-    else
-      hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 2, 4, MODE, false>), dim3((unsigned)nb), dim3(512), 0, stream, b);
-  } else {
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 2, 4, MODE, false>), dim3((unsigned)nb), dim3(512), 0, stream, b);
-  }
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 2, 4, kPing>), dim3((unsigned)nb), dim3(512), 0, stream, b);
   return (int)hipGetLastError();
 }
 
@@ -2071,13 +1805,8 @@ bool glds3_eligible(const SaConvArgs* a) {
 
 int pick_cfg(const SaConvArgs* a) {
   if (a->tile_cfg >= 0) return a->tile_cfg;
-  if (a->in_stats) return 23;  // the fused input norm exists in the direct 64-channel conv only
-  static const int glds3_mode = [] {  // SA_CONV_GLDS3: 0 = never, 1 = auto (default)
-    const char* e = std::getenv("SA_CONV_GLDS3");
-    return e ? std::atoi(e) : 1;
-  }();
   const int M = a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
-  if (glds3_mode == 1 && a->Cout > 64 && glds3_eligible(a) && (a->splitk <= 1 || a->ws)) {
+  if (a->Cout > 64 && glds3_eligible(a) && (a->splitk <= 1 || a->ws)) {
     // measured on MI355X (tools/conv_bench.py): 256x128 / 8 waves wins once its grid covers the
     // chip >= 2x (RAFT batch-8 GRU, flow head, motion encoder); 128x64 / 4 waves (2 blocks per CU)
     // wins for deep K (GRU convs at any batch) and for grids the register path would split
@@ -2093,16 +1822,6 @@ int pick_cfg(const SaConvArgs* a) {
   return tiles128 >= 512 ? 0 : 1;
 }
 
-int cfg_bn(int cfg) {
-  switch (cfg) {
-    case 10: case 12: case 18: case 20: return 256;
-    case 0: case 4: case 6: case 7: case 11: case 13: case 15: case 19: case 21: case 26: case 27: return 128;
-    case 1: case 3: case 5: case 8: case 9: case 14: case 16: case 17: return 64;
-    case 2: return 16;
-    default: return 0;
-  }
-}
-
 }  // namespace
 
 extern "C" void sa_conv2d_last_split(long* ws_floats, long* tiles) {
@@ -2110,43 +1829,27 @@ extern "C" void sa_conv2d_last_split(long* ws_floats, long* tiles) {
   *tiles = g_split_tiles;
 }
 
-extern "C" int sa_conv2d_nslices(const SaConvArgs* a) {
-  const int bn = cfg_bn(pick_cfg(a));
-  return bn > 0 ? (a->Cout + bn - 1) / bn : -3;
-}
-
 extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
   if (a->Kpad % 32 != 0 || a->Cin % 8 != 0 || a->nsrc < 1 || a->nsrc > 4) return -2;
   const int cfg = pick_cfg(a);
-  if (a->in_stats && cfg != 23) return -5;
-  // the projection epilogue reduces whole rows of an n-tile: every tile must be full
-  if (a->epi == SA_EPI_PROJ && (cfg_bn(cfg) == 0 || a->Cout % cfg_bn(cfg) != 0 || !a->proj_w || !a->proj_out ||
-                                a->proj_taps * a->proj_oc > 9 || a->proj_taps * a->proj_oc < 1))
-    return -6;
   switch (cfg) {
     case 0: return launch_cfg<128, 128, 2, 2>(a, stream);
     case 1: return launch_cfg<128, 64, 2, 2>(a, stream);
     case 2: return launch_cfg<256, 16, 4, 1>(a, stream);
     case 3: return launch_cfg<64, 64, 2, 2>(a, stream);
-    case 9: case 23: {
-      // direct conv: one 64-channel source, 64 outputs, 3x3 / stride 1 / pad 1, plain store epilogue
+    case 23: {
+      // direct conv (conv_direct.hip): one 64-channel source, 64 outputs, 3x3 / stride 1 / pad 1, store epilogue
+      // with optional IN statistics or residual
       const bool ok = a->nsrc == 1 && a->src[0].channels == 64 && a->Cin == 64 && a->Cout == 64 && a->KH == 3 &&
                       a->KW == 3 && a->sh == 1 && a->sw == 1 && a->ph == 1 && a->pw == 1 && a->dh == 1 &&
-                      a->dw == 1 && a->KD <= 0 && a->up == 0 && !a->gate && (!a->res || cfg == 23) &&
-                      a->epi == SA_EPI_STORE &&
-                      a->Kpad >= 576 && a->out_stride % 8 == 0 && a->src[0].stride % 8 == 0 && a->Ho == a->H &&
-                      a->Wo == a->W;
+                      a->dw == 1 && a->KD <= 0 && a->up == 0 && !a->gate && a->epi == SA_EPI_STORE &&
+                      a->scale == 1.f && a->Kpad >= 576 && a->out_stride % 8 == 0 && a->src[0].stride % 8 == 0 &&
+                      a->Ho == a->H && a->Wo == a->W;
       if (!ok) return -5;
       note_split(1, 0, 0);
-      if (cfg == 23)
-        return a->scale != 1.f ? -5
-                               : sa_conv3x3_c64_direct2(a->src[0].ptr, a->src[0].stride, a->weight, a->Kpad, a->bias,
-                                                        a->out, a->out_stride, a->N, a->H, a->W, a->act, a->alpha,
-                                                        a->stats, a->stats_slots, a->res, a->res_stride, a->act2,
-                                                        a->in_stats, a->in_act, 0, stream);
-      return sa_conv3x3_c64_direct(a->src[0].ptr, a->src[0].stride, a->weight, a->Kpad, a->bias, a->out,
-                                   a->out_stride, a->N, a->H, a->W, a->act, a->alpha, a->stats, a->stats_slots, 0,
-                                   stream);
+      return sa_conv3x3_c64_direct2(a->src[0].ptr, a->src[0].stride, a->weight, a->Kpad, a->bias, a->out,
+                                    a->out_stride, a->N, a->H, a->W, a->act, a->alpha, a->stats, a->stats_slots,
+                                    a->res, a->res_stride, a->act2, 0, stream);
     }
     case 24: {
       // direct 3x3 -> 96 (conv_direct96.hip): one 96-channel source at stride 1 or a 64-channel one at stride 2,
@@ -2191,10 +1894,9 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
                              a->out_stride, a->N, a->H, a->W, a->sh, a->act, a->alpha, a->stats, a->stats_slots,
                              stream);
     }
-    case 4: case 5: case 6: case 7: case 8: {
+    case 4: case 5: case 7: case 8: {
       const int r = cfg == 4 ? launch_glds3<256, 128, 4, 2>(a, stream, true)
                   : cfg == 5 ? launch_glds3<128, 64, 2, 2>(a, stream, true)
-                  : cfg == 6 ? launch_glds3<128, 128, 2, 2>(a, stream, true)
                   : cfg == 7 ? launch_glds3<128, 128, 2, 4>(a, stream, true)
                              : launch_glds3<256, 64, 4, 2>(a, stream, true);
       return r == 1 ? -5 : r;
@@ -2208,13 +1910,9 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
                               : launch_glds3<256, 64, 4, 2, kGldsDeep>(a, stream, true);
       return r == 1 ? -5 : r;
     }
-    case 10: case 11: case 12: case 13: {
-      // 10 / 11: 8 waves of 128x64 (2 per SIMD); 12 / 13: 4 waves of 128x128 (1 per SIMD, 512-VGPR budget,
-      // a third less LDS read traffic per MFMA)
-      const int r = cfg == 10 ? launch_wide<256, 256, 2, 4>(a, stream)
-                  : cfg == 11 ? launch_wide<512, 128, 4, 2>(a, stream)
-                  : cfg == 12 ? launch_wide<256, 256, 2, 2>(a, stream)
-                              : launch_wide<512, 128, 4, 1>(a, stream);
+    case 10: case 11: {
+      // 8 waves of 128x64 (2 per SIMD): 256x256 (10) / 512x128 (11)
+      const int r = cfg == 10 ? launch_wide<256, 256, 2, 4>(a, stream) : launch_wide<512, 128, 4, 2>(a, stream);
       return r == 1 ? -5 : r;
     }
     case 26: case 27: {
@@ -2222,104 +1920,21 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
       const int r = cfg == 26 ? launch_halo<kHalo>(a, stream) : launch_halo<kHalo16>(a, stream);
       return r == 1 ? -5 : r;
     }
-    case 18: case 19: case 20: case 21: {
-      // 8-wave ping-pong: 256x256 (4-deep ring) / 256x128 (6-deep ring); 18 / 19 issue the DMA in the read
-      // slot (kPing), 20 / 21 between the MFMAs of the compute slot (kPingM)
-      const int r = cfg == 18   ? launch_ping<256, 256>(a, stream)
-                    : cfg == 19 ? launch_ping<256, 128>(a, stream)
-                    : cfg == 20 ? launch_ping<256, 256, kPingM>(a, stream)
-                                : launch_ping<256, 128, kPingM>(a, stream);
+    case 18: case 19: {
+      // 8-wave ping-pong (kPing): 256x256 (4-deep ring) / 256x128 (6-deep ring), DMA issued in the read slot
+      const int r = cfg == 18 ? launch_ping<256, 256>(a, stream) : launch_ping<256, 128>(a, stream);
       return r == 1 ? -5 : r;
     }
     default: return -3;
   }
 }
 
-// ---------------- SA_EPI_PROJ stencil: the following conv's tap sum ----------------
-namespace {
-__global__ __launch_bounds__(256) void proj_stencil_kernel(const float* __restrict__ P, int nslices, long plane,
-                                                           int N, int H, int W, int kh, int kw, int oc,
-                                                           const float* __restrict__ bias, float* out,
-                                                           int out_stride, int accumulate) {
-  const long M = (long)N * H * W;
-  const long m = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= M) return;
-  const int x = (int)(m % W);
-  const long r = m / W;
-  const int y = (int)(r % H);
-  const int ph = kh / 2, pw = kw / 2;
-  const int np = kh * kw * oc;
-  for (int o = 0; o < oc; ++o) {
-    float acc = bias ? bias[o] : 0.f;
-    for (int s = 0; s < nslices; ++s) {
-      const float* ps = P + (size_t)s * np * plane;
-      for (int ky = 0; ky < kh; ++ky) {
-        const int yy = y + ky - ph;
-        if (yy < 0 || yy >= H) continue;
-        for (int kx = 0; kx < kw; ++kx) {
-          const int xx = x + kx - pw;
-          if (xx < 0 || xx >= W) continue;
-          const long q = m + (long)(ky - ph) * W + (kx - pw);
-          acc += ps[(size_t)((ky * kw + kx) * oc + o) * plane + q];
-        }
-      }
-    }
-    float* op = out + m * out_stride + o;
-    *op = accumulate ? *op + acc : acc;
-  }
-}
-
-// Per-pixel tap projections of a skinny conv: each wave owns 16-row tiles of the [M x C] input, the
-// [16*NT x C] tap weights stay in registers as B fragments (NT 16-column tiles), all A fragments of a
-// tile are loaded before its chained MFMAs (v_mfma_f32_16x16x32_f16), and results are written tap-major.
-template <int NT>
-__global__ __launch_bounds__(256) void tap_proj_kernel(const f16* __restrict__ x, int xs, long M, int C,
-                                                       const f16* __restrict__ w, int ntaps,
-                                                       float* __restrict__ P, long plane) {
-  const int lane = threadIdx.x & 63;
-  const int r16 = lane & 15, kofs = (lane >> 4) * 8;
-  const int ks = C >> 5;
-  const half8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
-  half8 b[NT][8];
-#pragma unroll
-  for (int j = 0; j < NT; ++j)
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      b[j][k] = k < ks ? *reinterpret_cast<const half8*>(w + (size_t)(16 * j + r16) * C + k * 32 + kofs) : zero8;
-  const long ntile = (M + 15) >> 4;
-  const long nw = (long)gridDim.x * 4;
-  for (long t = (long)blockIdx.x * 4 + (threadIdx.x >> 6); t < ntile; t += nw) {
-    const long row = t * 16 + r16;
-    const bool ok = row < M;
-    half8 a[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      a[k] = (ok && k < ks) ? *reinterpret_cast<const half8*>(x + row * xs + k * 32 + kofs) : zero8;
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (k < ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[k], b[j][k], acc, 0, 0, 0);
-      const int tap = 16 * j + r16;
-      if (tap < ntaps) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const long m = t * 16 + (lane >> 4) * 4 + r;
-          if (m < M) P[(size_t)tap * plane + m] = acc[r];
-        }
-      }
-    }
-  }
-}
-}  // namespace
-
 namespace {
 // Flow-head tail in one launch: the per-pixel 3x3-tap projections of a C -> 1 conv over a (TH+2) x (TW+2) halo
 // region (MFMA, fp32 planes in LDS; halo pixels outside the image project zero activations, which is exactly the
-// following conv's zero padding), then the 9-tap stencil + bias accumulated into the fp32 flow.  Replaces
-// tap_proj + proj_stencil (two launches and an HBM round trip of the 9 planes) on every GRU iteration's critical
-// path; the halo recompute (2.1x at 2 x 32 tiles, 1.5x at 4 x 64) only re-reads activations.
+// following conv's zero padding), then the 9-tap stencil + bias accumulated into the fp32 flow.  One launch and
+// no HBM round trip of the 9 tap planes on every GRU iteration's critical path; the halo recompute (2.1x at
+// 2 x 32 tiles, 1.5x at 4 x 64) only re-reads activations.
 template <int TH, int TW, int OC>
 __global__ __launch_bounds__(256) void flow_head_tail_kernel(const f16* __restrict__ y, int ys, int C,
                                                              const f16* __restrict__ w16, const float* __restrict__ bias,
@@ -2407,30 +2022,4 @@ extern "C" int sa_flow_head_tail_oc(const void* y, int ys, int C, const void* w1
 extern "C" int sa_flow_head_tail(const void* y, int ys, int C, const void* w16, const float* bias, float* flow, int N,
                                  int H, int W, hipStream_t stream) {
   return sa_flow_head_tail_oc(y, ys, C, w16, 1, bias, flow, N, H, W, stream);
-}
-
-extern "C" int sa_tap_proj(const void* x, int xs, long M, int C, const void* w, int ntaps, float* P, long plane,
-                           hipStream_t stream) {
-  if (C % 32 || C > 256 || C < 32 || ntaps < 1 || ntaps > 32 || xs < C || xs % 8 || plane < M || M < 1)
-    return -2;
-  const long ntile = (M + 15) / 16;
-  long blocks = (ntile + 3) / 4;
-  if (blocks > 2048) blocks = 2048;  // grid-stride beyond 8 waves per CU
-  if (ntaps <= 16)
-    hipLaunchKernelGGL(tap_proj_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, stream, (const f16*)x, xs, M, C,
-                       (const f16*)w, ntaps, P, plane);
-  else
-    hipLaunchKernelGGL(tap_proj_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, stream, (const f16*)x, xs, M, C,
-                       (const f16*)w, ntaps, P, plane);
-  return (int)hipGetLastError();
-}
-
-extern "C" int sa_proj_stencil(const float* P, int nslices, long plane, int N, int H, int W, int kh, int kw,
-                               int oc, const float* bias, float* out, int out_stride, int accumulate,
-                               hipStream_t stream) {
-  const long M = (long)N * H * W;
-  if (nslices < 1 || plane < M || oc < 1 || (kh & 1) == 0 || (kw & 1) == 0) return -2;
-  hipLaunchKernelGGL(proj_stencil_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, stream, P, nslices,
-                     plane, N, H, W, kh, kw, oc, bias, out, out_stride, accumulate);
-  return (int)hipGetLastError();
 }

@@ -1,27 +1,22 @@
-// Direct 3x3 convolution, 64 -> 64 channels, stride 1, pad 1, with the weights resident in LDS and
-// persistent output tiles (gfx950).
+// Direct 3x3 convolution, 64 -> 64 channels, stride 1, pad 1, weight-stationary with persistent output tiles
+// (gfx950; tile_cfg 23).
 //
 // The implicit-GEMM kernels (conv2d.hip) gather every im2col row from L2 once per tap: for the
 // full-resolution 64-channel layers of the RAFT-Stereo / CREStereo feature encoders (K = 576, only 9
 // 64-deep k-steps) that is 9 reads of every input pixel per conv and the per-block prologue / epilogue
-// dominate.  Here one persistent workgroup per CU (4 waves, one per SIMD) is weight-stationary: each
-// wave holds the whole 64 x 576 weight matrix as MFMA B fragments in VGPRs (288 registers, loaded once)
-// and the block walks output tiles of 2 rows x 64 columns:
-//   * the input tile with its halo (4 x 66 pixels x 64 channels) is DMA'd global->LDS
-//     (global_load_lds_dwordx4, source-side XOR swizzle of the 16-B channel chunks by pixel) into a
-//     4-deep LDS ring, three tiles ahead of the one computing (~100 KB in flight per CU: the kernel
-//     is HBM-latency bound with fewer bytes in flight);
-//   * every tap's A fragment is read from that tile (each input pixel crosses L2 ~2x instead of 9x);
-//   * v_mfma_f32_16x16x32_f16, each wave owns 32 pixels x 64 output channels, the A fragments of the
-//     next k-step prefetched into a second register set under the current MFMAs;
-//   * the epilogue stages the fp32 tile through the (finished) input buffer, applies bias +
-//     activation, stores 16-B fp16 chunks, and accumulates instance-norm statistics in registers
-//     across tiles of the same image (wave-reduced, slotted fixed-point atomics on image change).
+// dominate.  Here one persistent workgroup per CU holds the whole 64 x 576 weight matrix as MFMA fragments in
+// VGPRs (loaded once) and walks output tiles of 2 rows x 64 columns: the input tile with its halo (4 x 66
+// pixels x 64 channels) is DMA'd global->LDS (global_load_lds_dwordx4) into a ring several tiles ahead, and
+// every tap's fragment is read from that tile (each input pixel crosses L2 ~2x instead of 9x).
+//
+// A first version ran one wave per SIMD (4 waves, 288 weight VGPRs each, LDS-staged epilogue); its ablations on
+// the RAFT-SF b8 full-resolution layer put the MFMA + LDS-read loop alone at 0.83 PFLOP/s and the whole kernel
+// at 0.40 (profiles/direct_conv_r02.txt): one wave per SIMD exposes every DMA wait, barrier and the epilogue.
+// The kernel below replaced it.
+
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
 
-#include <cstdlib>
-#include <type_traits>
 
 #include "sa/kernels.h"
 
@@ -38,10 +33,6 @@ constexpr int KTOT = 576;                     // 3 * 3 * 64
 constexpr int IN_BYTES = IR * IC * 128;       // 33792
 constexpr int IN_PIECES = IR * IC * 8;        // 16-B pieces per input tile (2112)
 constexpr int IN_INSTR = (IN_PIECES + 63) / 64;  // wave-instructions per tile (33)
-constexpr int NWAVE = 4;
-constexpr int IN_PER_WAVE = (IN_INSTR + NWAVE - 1) / NWAVE;  // 9 (waves 0-2: 9, wave 3: 6)
-constexpr int NBUF = 4;                       // input tiles: current + 3 in flight
-constexpr int SMEM = NBUF * IN_BYTES;         // 135168
 
 __device__ __attribute__((aligned(16))) const unsigned char g_zero16d[64] = {0};
 
@@ -68,229 +59,8 @@ __device__ __forceinline__ float act_apply(float v, int act, float alpha) {
   }
 }
 
-struct DirectArgs {
-  const f16* x;
-  int xs;  // pixel stride (elements)
-  const f16* w;
-  int kpad;
-  const float* bias;
-  f16* out;
-  int os;
-  int N, H, W;
-  int act;
-  float alpha;
-  sa_stat_t* stats;
-  int slots;
-  int abl;  // ablation (profiling only, SA_DIRECT_ABL): 1 = no MFMA, 2 = no epilogue, 4 = no input DMA,
-            // 8 = no output stores, 16 = no C-tile LDS writes
-};
-
-__global__ __launch_bounds__(256) void conv3x3_c64_direct_kernel(const DirectArgs p) {
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tiles_x = (p.W + TC - 1) / TC, tiles_y = (p.H + TR - 1) / TR;
-  const int tiles_img = tiles_x * tiles_y;
-  const int ntiles = p.N * tiles_img;
-  const void* zero = g_zero16d;
-
-  // ---- input tile DMA: piece g -> pixel pp = g / 8, slot s = g % 8 holds chunk s ^ (pp & 7)
-  auto issue_tile = [&](int t, int buf) {
-    const int n = t / tiles_img, r = t - n * tiles_img;
-    const int ty = r / tiles_x, tx = r - ty * tiles_x;
-    const int y0 = ty * TR - 1, x0 = tx * TC - 1;
-    char* ib = smem + buf * IN_BYTES;
-#pragma unroll
-    for (int i = 0; i < IN_PER_WAVE; ++i) {
-      const int ins = wave * IN_PER_WAVE + i;
-      if (ins < IN_INSTR) {
-        const int g = ins * 64 + lane;
-        const int pp = g >> 3, s = g & 7;
-        const int q = s ^ (pp & 7);
-        const int iy = y0 + pp / IC, ix = x0 + pp % IC;
-        const void* src = zero;
-        if (g < IN_PIECES && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W)
-          src = p.x + ((size_t)((size_t)n * p.H + iy) * p.W + ix) * p.xs + q * 8;
-        __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(ib + ins * 1024), 16, 0, 0);
-      }
-    }
-  };
-
-  // per-thread epilogue mapping: channel chunk cc = tid & 7, pixels (tid >> 3) + 32 * i
-  const int cc = tid & 7;
-  float bias8[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) bias8[j] = p.bias ? p.bias[cc * 8 + j] : 0.f;
-  float ssum[8], ssq[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ssum[j] = ssq[j] = 0.f;
-  int stat_img = -1;
-  sa_stat_t* const st_blk = p.stats ? p.stats + (size_t)(blockIdx.x % (p.slots > 1 ? p.slots : 1)) * p.N * 64 * 2
-                                    : nullptr;
-  auto flush_stats = [&]() {
-    // lanes sharing a channel chunk: lane bits 3..5
-#pragma unroll
-    for (int off = 8; off < 64; off <<= 1)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        ssum[j] += __shfl_xor(ssum[j], off);
-        ssq[j] += __shfl_xor(ssq[j], off);
-      }
-    if (lane < 8 && stat_img >= 0) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        unsigned long long* sp =
-            reinterpret_cast<unsigned long long*>(st_blk) + ((size_t)stat_img * 64 + cc * 8 + j) * 2;
-        atomicAdd(sp, (unsigned long long)__double2ll_rn((double)ssum[j] * SA_STAT_SCALE));
-        atomicAdd(sp + 1, (unsigned long long)__double2ll_rn((double)ssq[j] * SA_STAT_SCALE));
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) ssum[j] = ssq[j] = 0.f;
-  };
-
-  // wave w: 32 output pixels (row w >> 1, columns (w & 1) * 32 .. +32) x all 64 output channels
-  const int wrow = wave >> 1, wcol = (wave & 1) * 32;
-  const int frow = lane & 15, kq = lane >> 4;
-  // stationary B fragments: k-step ks, n-fragment j -> W[cout = 16 j + frow][ks*32 + kq*8 .. +8]
-  half8 breg[KTOT / 32][4];
-#pragma unroll
-  for (int ks = 0; ks < KTOT / 32; ++ks)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      breg[ks][j] = *reinterpret_cast<const half8*>(p.w + (size_t)(j * 16 + frow) * p.kpad + ks * 32 + kq * 8);
-  const int G = gridDim.x;
-  int t = blockIdx.x;
-  // prologue: the first three tiles in flight
-#pragma unroll
-  for (int k = 0; k < NBUF - 1; ++k)
-    if (t + k * G < ntiles && !(p.abl & 4)) issue_tile(t + k * G, k);
-  int cur = 0;
-
-  for (; t < ntiles; t += G) {
-    const int tn = t + (NBUF - 1) * G;
-    if (tn < ntiles && !(p.abl & 4)) issue_tile(tn, (cur + NBUF - 1) % NBUF);
-    // tiles issued after t by this wave: ahead = min(3, remaining); wait until t's pieces landed
-    const int ahead = (t + G < ntiles) + (t + 2 * G < ntiles) + (t + 3 * G < ntiles);
-    static_assert(IN_PER_WAVE == 9 && IN_INSTR == 33, "vmcnt literals below assume 9, 9, 9, 6 pieces");
-    if (wave < 3) {
-      if (ahead == 3) asm volatile("s_waitcnt vmcnt(27)" ::: "memory");
-      else if (ahead == 2) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
-      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      if (ahead == 3) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
-      else if (ahead == 2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const char* ib = smem + cur * IN_BYTES;
-
-    floatx4 acc[2][4];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    auto load = [&](int ks, half8* af) {
-      const int tap = ks >> 1, kh = tap / 3, kw = tap - kh * 3;
-      const int q = (ks & 1) * 4 + kq;  // channel chunk of this lane's 8 k values
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int pp = (wrow + kh) * IC + wcol + i * 16 + frow + kw;
-        af[i] = *reinterpret_cast<const half8*>(ib + pp * 128 + ((q ^ (pp & 7)) << 4));
-      }
-    };
-    // A fragments of k-step ks+1 in flight under the MFMAs of ks
-    half8 a0[2], a1[2];
-    load(0, a0);
-#pragma unroll
-    for (int ks = 0; ks < (p.abl & 1 ? 0 : KTOT / 32); ks += 2) {
-      load(ks + 1, a1);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[i], breg[ks][j], acc[i][j], 0, 0, 0);
-      if (ks + 2 < KTOT / 32) load(ks + 2, a0);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[i], breg[ks + 1][j], acc[i][j], 0, 0, 0);
-    }
-    if (p.abl & 2) {
-      asm volatile("" :: "v"(acc[0][0]), "v"(acc[1][3]));
-      lds_barrier();
-      cur = (cur + 1) % NBUF;
-      continue;
-    }
-    lds_barrier();  // every wave finished reading the input tile: reuse it for the C tile
-    float* ct = reinterpret_cast<float*>(smem + cur * IN_BYTES);
-    if (!(p.abl & 16))
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int pix = wrow * TC + wcol + i * 16 + kq * 4 + r;  // 0..127
-          const int col = j * 16 + frow;
-          ct[pix * 64 + (col ^ (((pix >> 2) & 3) << 4))] = acc[i][j][r];
-        }
-    lds_barrier();
-    const int n = t / tiles_img, rr = t - n * tiles_img;
-    const int ty = rr / tiles_x, tx = rr - ty * tiles_x;
-    if (p.stats && n != stat_img) {
-      if (stat_img >= 0) flush_stats();
-      stat_img = n;
-    }
-    // activation resolved once per tile (a per-element switch costs more than the stores)
-    auto store_tile = [&](auto actc) {
-      constexpr int ACT = decltype(actc)::value;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int pix = (tid >> 3) + 32 * i;
-        const int oy = ty * TR + pix / TC, ox = tx * TC + pix % TC;
-        if (oy < p.H && ox < p.W) {
-          const float* cp = ct + pix * 64 + ((cc * 8) ^ (((pix >> 2) & 3) << 4));
-          const floatx4 c0 = *reinterpret_cast<const floatx4*>(cp);
-          const floatx4 c1 = *reinterpret_cast<const floatx4*>(cp + 4);
-          float v[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
-          half8 h;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            v[j] = act_apply(v[j] + bias8[j], ACT, p.alpha);
-            h[j] = (f16)v[j];
-            ssum[j] += v[j];
-            ssq[j] += v[j] * v[j];
-          }
-          if (p.abl & 8) asm volatile("" :: "v"(h));
-          else *reinterpret_cast<half8*>(p.out + ((size_t)((size_t)n * p.H + oy) * p.W + ox) * p.os + cc * 8) = h;
-        }
-      }
-    };
-    switch (p.act) {
-      case SA_ACT_RELU: store_tile(std::integral_constant<int, SA_ACT_RELU>{}); break;
-      case SA_ACT_LEAKY: store_tile(std::integral_constant<int, SA_ACT_LEAKY>{}); break;
-      case SA_ACT_TANH: store_tile(std::integral_constant<int, SA_ACT_TANH>{}); break;
-      case SA_ACT_SIGMOID: store_tile(std::integral_constant<int, SA_ACT_SIGMOID>{}); break;
-      case SA_ACT_RELU6: store_tile(std::integral_constant<int, SA_ACT_RELU6>{}); break;
-      default: store_tile(std::integral_constant<int, SA_ACT_NONE>{}); break;
-    }
-    lds_barrier();  // C tile consumed before this buffer receives tile t + 4 * gridDim
-    cur = (cur + 1) % NBUF;
-  }
-  if (p.stats && stat_img >= 0) flush_stats();
-}
-
-
 // ---------------------------------------------------------------------------------------------------
-// Version 2 (tile_cfg 23): two waves per SIMD.  The ablations of the kernel above on the RAFT-SF b8
-// full-resolution layer (tools/conv_bench.py fr8, SA_DIRECT_ABL; profiles/direct_conv_r02.txt) put its
-// MFMA + LDS-read loop alone at 0.83 PFLOP/s and the whole kernel at 0.40: one wave per SIMD exposes
-// every DMA wait, barrier and the LDS-staged epilogue.  Here
+// Two waves per SIMD:
 //   * 8 waves per workgroup, one workgroup per CU: wave w owns 32 pixels (pixel group w & 3 of the
 //     2 x 64 tile) x 32 output channels (half w >> 2), so the stationary weights are 144 VGPRs and two
 //     waves share each SIMD (one computes while the other waits or stores);
@@ -317,8 +87,7 @@ struct V2Lds {
   static constexpr int BIAS = DUMMY + 1024;
   static constexpr int ST = BIAS + 256;
   static constexpr int RED = ST + (STATS ? 512 * 64 : 0);  // flush: [8 waves][4 kq][16] wave totals
-  static constexpr int NRM = RED + (STATS ? 8 * 4 * 16 * 4 : 0);  // fused input norm: fp16 scale[64] | shift[64]
-  static constexpr int SMEM = NRM + 256;
+  static constexpr int SMEM = RED + (STATS ? 8 * 4 * 16 * 4 : 0);
 };
 
 // sum over the 16 lanes of a DPP row (every lane gets the row total)
@@ -360,16 +129,12 @@ struct DirectArgs2 {
   const f16* res;  // optional residual (RES): y = act2(act(acc + bias) + res)
   int rs;
   int act2;
-  int abl;  // profiling only (SA_DIRECT2_ABL): 1 = no per-tile statistics, 2 = no flush, 4 = non-stats kernel with
-            // the statistics variant's 3-deep ring
-  const sa_stat_t* in_stats;  // fused input instance norm (INN): folded fixed-point sums [N][64][2]
-  int in_act;
 };
 
-template <int ACT, bool STATS, bool RES, int NBO = 0, bool INN = false>
+template <int ACT, bool STATS, bool RES>
 __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const DirectArgs2 p) {
   using L = V2Lds<STATS>;
-  constexpr int NB = NBO ? NBO : L::NB;
+  constexpr int NB = L::NB;
   __shared__ __attribute__((aligned(16))) char smem[L::SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -510,53 +275,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const Direc
     // every wave is past tile k-1: its buffer takes tile k+NB-1
     if (k + NB - 1 < kb) issue_tile(t + NB - 1, (k + NB - 1) % NB);
     const char* ib = smem + cur * IN_BYTES;
-    if constexpr (INN) {
-      // fused input instance norm: this image's per-channel fp16 scale / shift (same mean / rstd as
-      // instnorm_apply), then every in-image staged pixel x -> act(x * scale + shift) in place (packed fp16
-      // FMA); halo pixels outside the image stay zero, which is the normalised tensor's zero padding
-      _Float16* nrm = reinterpret_cast<_Float16*>(smem + L::NRM);
-      if (tid < 64) {
-        const sa_stat_t* sp = p.in_stats + ((size_t)n * 64 + tid) * 2;
-        const double inv = 1.0 / ((double)p.H * p.W * SA_STAT_SCALE);
-        const double m = (double)sp[0] * inv, var = (double)sp[1] * inv - m * m;
-        const float rstd = rsqrtf((float)(var > 0.0 ? var : 0.0) + 1e-5f);
-        nrm[tid] = (_Float16)rstd;
-        nrm[64 + tid] = (_Float16)(-(float)m * rstd);
-      }
-      lds_barrier();
-      const int y0 = ty * TR - 1, x0 = tx * TC - 1;
-      // interior tiles (every staged pixel inside the image) skip the per-piece coordinate test
-      const bool interior = y0 >= 0 && y0 + IR <= p.H && x0 >= 0 && x0 + IC <= p.W;
-      char* ibw = smem + cur * IN_BYTES;
-      int tl = tid;
-      asm volatile("" : "+v"(tl));  // tile-invariant piece decomposition: recomputed, not held across the loop
-      for (int g = tl; g < IN_PIECES; g += 512) {
-        const int pp = g >> 3, q = (g & 7) ^ v2_swz(pp);
-        if (!interior) {
-          const int iy = y0 + pp / IC, ix = x0 + pp % IC;
-          if (iy < 0 || iy >= p.H || ix < 0 || ix >= p.W) continue;
-        }
-        half8 v = *reinterpret_cast<const half8*>(ibw + g * 16);
-        const half8 sc = *reinterpret_cast<const half8*>(nrm + q * 8);
-        const half8 sh = *reinterpret_cast<const half8*>(nrm + 64 + q * 8);
-        v = v * sc + sh;
-        if (p.in_act == SA_ACT_RELU) {
-          const half8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-          v = __builtin_elementwise_max(v, z);
-        }
-        *reinterpret_cast<half8*>(ibw + g * 16) = v;
-      }
-      lds_barrier();
-    }
-
     floatx4 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    // (fused input norm: its piece loop leaves no room for the 36 hoisted fragment addresses -> recompute per tile)
-    int fr = frow, kql = kq;
-    if constexpr (INN) asm volatile("" : "+v"(fr), "+v"(kql));
+    const int fr = frow, kql = kq;
     auto load = [&](int ks, half8* bf) {
       const int tap = ks >> 1, kh = tap / 3, kw = tap - kh * 3;
       const int q = (ks & 1) * 4 + kql;
@@ -586,7 +310,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const Direc
 
     if constexpr (STATS) {
       if (n != stat_img) {
-        if (stat_img >= 0 && !(p.abl & 2)) flush_stats();
+        if (stat_img >= 0) flush_stats();
         stat_img = n;
       }
     }
@@ -625,7 +349,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const Direc
       typedef unsigned uint4v __attribute__((ext_vector_type(4)));
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, h), orsrc, off, 0, 0);
     }
-    if (STATS && !(p.abl & 1)) {
+    if constexpr (STATS) {
       st_lane[0] += floatx4{tsum[0], tsum[1], tsum[2], tsum[3]};
       st_lane[1] += floatx4{tsum[4], tsum[5], tsum[6], tsum[7]};
       st_lane[2] += floatx4{tsq[0], tsq[1], tsq[2], tsq[3]};
@@ -639,14 +363,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const Direc
 
 template <bool STATS, bool RES>
 void launch_direct2(const DirectArgs2& a, int act, unsigned g, hipStream_t s) {
-  if (STATS && !RES && a.in_stats) {  // fused input norm: the instance-norm trunk's second block conv only
-    hipLaunchKernelGGL((conv3x3_c64_direct2_kernel<SA_ACT_NONE, true, false, 0, true>), dim3(g), dim3(512), 0, s, a);
-    return;
-  }
-  if (!STATS && !RES && (a.abl & 4)) {
-    hipLaunchKernelGGL((conv3x3_c64_direct2_kernel<SA_ACT_NONE, false, false, 3>), dim3(g), dim3(512), 0, s, a);
-    return;
-  }
   switch (act) {
     case SA_ACT_RELU:
       hipLaunchKernelGGL((conv3x3_c64_direct2_kernel<SA_ACT_RELU, STATS, RES>), dim3(g), dim3(512), 0, s, a);
@@ -662,37 +378,18 @@ void launch_direct2(const DirectArgs2& a, int act, unsigned g, hipStream_t s) {
 
 }  // namespace
 
-extern "C" int sa_conv3x3_c64_direct(const void* x, int xs, const void* w, int kpad, const float* bias, void* out,
-                                     int os, int N, int H, int W, int act, float alpha, sa_stat_t* stats,
-                                     int slots, int max_blocks, hipStream_t stream) {
-  if (kpad < KTOT || xs < 64 || os < 64 || xs % 8 || os % 8) return -2;
-  static const int abl = std::getenv("SA_DIRECT_ABL") ? std::atoi(std::getenv("SA_DIRECT_ABL")) : 0;
-  DirectArgs a{(const f16*)x, xs, (const f16*)w, kpad, bias, (f16*)out, os, N, H, W, act, alpha, stats, slots, abl};
-  const long ntiles = (long)N * ((H + TR - 1) / TR) * ((W + TC - 1) / TC);
-  long g = max_blocks > 0 ? max_blocks : 256;
-  if (g > ntiles) g = ntiles;
-  if (g < 1) return 0;
-  hipLaunchKernelGGL(conv3x3_c64_direct_kernel, dim3((unsigned)g), dim3(256), 0, stream, a);
-  return (int)hipGetLastError();
-}
-
 extern "C" int sa_conv3x3_c64_direct2(const void* x, int xs, const void* w, int kpad, const float* bias, void* out,
                                       int os, int N, int H, int W, int act, float alpha, sa_stat_t* stats, int slots,
-                                      const void* res, int rs, int act2, const sa_stat_t* in_stats, int in_act,
-                                      int max_blocks, hipStream_t stream) {
+                                      const void* res, int rs, int act2, int max_blocks, hipStream_t stream) {
   if (kpad < KTOT || xs < 64 || os < 64 || xs % 8 || os % 8 ||
       (act != SA_ACT_NONE && act != SA_ACT_RELU && act != SA_ACT_LEAKY))
     return -2;
   if (res && (stats || rs < 64 || rs % 8 || (act2 != SA_ACT_NONE && act2 != SA_ACT_RELU))) return -5;
-  // fused input norm: statistics variant with a plain (pre-norm) output only
-  if (in_stats && (!stats || res || act != SA_ACT_NONE || (in_act != SA_ACT_NONE && in_act != SA_ACT_RELU))) return -5;
   const size_t span = (((size_t)N * H - 1) * W + (W - 1)) * (size_t)os * 2 + 128;  // last pixel's 64 channels
   const size_t rspan = res ? (((size_t)N * H - 1) * W + (W - 1)) * (size_t)rs * 2 + 128 : 0;
   if (span >= 0xFFFFFF00ull || rspan >= 0xFFFFFF00ull) return -5;  // 32-bit buffer offsets
   DirectArgs2 a{(const f16*)x, xs, (const f16*)w, kpad, bias, (f16*)out, os, (unsigned)span, (unsigned)rspan, N, H, W,
-                alpha, stats, slots, (const f16*)res, rs, act2, 0, in_stats, in_act};
-  static const int abl = std::getenv("SA_DIRECT2_ABL") ? std::atoi(std::getenv("SA_DIRECT2_ABL")) : 0;
-  a.abl = abl;
+                alpha, stats, slots, (const f16*)res, rs, act2};
   const long ntiles = (long)N * ((H + TR - 1) / TR) * ((W + TC - 1) / TC);
   long g = max_blocks > 0 ? max_blocks : 256;
   if (g > ntiles) g = ntiles;

@@ -153,97 +153,7 @@ __global__ void corr_lookup_kernel(const float* __restrict__ pyr, const float* _
 // and wave 0 also writes the [flow_x, 0] tail of the motion features.  Weights are fp32 [k][64]
 // (k-major, so a wave's 16 outputs of one k are one scalar load); the corr features never leave
 // the chip and three launches per GRU iteration become one.
-__global__ __launch_bounds__(256) void raft_motion_head_kernel(
-    const float* __restrict__ pyr, const float* __restrict__ flow, int total, int H, int W1, int W2,
-    int levels, int radius, long lvl_off1, long lvl_off2, long lvl_off3, const float* __restrict__ wc,
-    const float* __restrict__ bc, const float* __restrict__ wf, const float* __restrict__ bf,
-    f16* __restrict__ cor, int cstride, f16* __restrict__ flo, int fstride, f16* __restrict__ fcopy,
-    int fcstride) {
-  __shared__ float corr_s[64][37];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int q = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int pixi = blockIdx.x * 64 + lane;  // total < 2^31 (host-checked): 32-bit index math
-  const long pix = pixi;
-  const bool ok = pixi < total;
-  const int ntap = 2 * radius + 1;
-  const int w1 = ok ? pixi % W1 : 0;
-  const float fx = ok ? flow[pix] : 0.f;
-  if (q < levels && ok) {
-    const long off = q == 0 ? 0 : (q == 1 ? lvl_off1 : (q == 2 ? lvl_off2 : lvl_off3));
-    const int Wl = W2 >> q;
-    const float* row = pyr + off + pix * Wl;
-    const float xl = ((float)w1 + fx) / (float)(1 << q) - (float)radius;
-    const float x0f = floorf(xl);
-    const float a = xl - x0f;
-    const int x0 = (int)x0f;
-    float prev = (x0 >= 0 && x0 < Wl) ? row[x0] : 0.f;
-    for (int k = 0; k < ntap; ++k) {
-      const int xi = x0 + k + 1;
-      const float nxt = (xi >= 0 && xi < Wl) ? row[xi] : 0.f;
-      corr_s[lane][q * ntap + k] = lerp_tap(prev, nxt, a);
-      prev = nxt;
-    }
-  }
-  __syncthreads();
-  if (!ok) return;
-  const int nc = levels * ntap;
-  float acc[16];
-#pragma unroll
-  for (int o = 0; o < 16; ++o) acc[o] = bc[q * 16 + o];
-#pragma unroll 12
-  for (int k = 0; k < nc; ++k) {
-    const float v = corr_s[lane][k];
-    const float* w = wc + k * 64 + q * 16;
-#pragma unroll
-    for (int o = 0; o < 16; ++o) acc[o] += v * w[o];
-  }
-  half8 h0, h1;
-#pragma unroll
-  for (int o = 0; o < 8; ++o) {
-    h0[o] = (f16)fmaxf(acc[o], 0.f);
-    h1[o] = (f16)fmaxf(acc[8 + o], 0.f);
-  }
-  f16* cp = cor + pix * cstride + q * 16;
-  *reinterpret_cast<half8*>(cp) = h0;
-  *reinterpret_cast<half8*>(cp + 8) = h1;
-
-  const int y = (pixi / W1) % H;
-#pragma unroll
-  for (int o = 0; o < 16; ++o) acc[o] = bf[q * 16 + o];
-  // all 49 taps' loads issued up front (zero outside the image; a masked tap adds exactly 0, so the
-  // accumulation order and result match the per-tap branchy loop), then the FMAs: the loads overlap
-  // instead of paying one global-load latency per tap
-  float fv[49];
-#pragma unroll
-  for (int ky = 0; ky < 7; ++ky) {
-    const bool rok = (unsigned)(y + ky - 3) < (unsigned)H;
-#pragma unroll
-    for (int kx = 0; kx < 7; ++kx) {
-      const bool tok = rok && (unsigned)(w1 + kx - 3) < (unsigned)W1;
-      fv[ky * 7 + kx] = tok ? flow[pix + (long)(ky - 3) * W1 + (kx - 3)] : 0.f;
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < 49; ++t) {
-    const float* w = wf + t * 64 + q * 16;
-#pragma unroll
-    for (int o = 0; o < 16; ++o) acc[o] += fv[t] * w[o];
-  }
-#pragma unroll
-  for (int o = 0; o < 8; ++o) {
-    h0[o] = (f16)fmaxf(acc[o], 0.f);
-    h1[o] = (f16)fmaxf(acc[8 + o], 0.f);
-  }
-  f16* fp = flo + pix * fstride + q * 16;
-  *reinterpret_cast<half8*>(fp) = h0;
-  *reinterpret_cast<half8*>(fp + 8) = h1;
-  if (q == 0 && fcopy) {
-    fcopy[pix * fcstride] = (f16)fx;
-    fcopy[pix * fcstride + 1] = (f16)0.f;
-  }
-}
-
-// MFMA form of the same head.  The block's 64 pixels become a [64 x 96] fp16 A tile in LDS (k < nc:
+// MFMA form: the block's 64 pixels become a [64 x 96] fp16 A tile in LDS (k < nc:
 // the bilinear correlation taps, wave l gathering level l; nc <= k < nc + 49: the 7x7 flow_x taps, 13
 // per wave; rest zero) and both 1x1 / 7x7 convs are ONE GEMM against a block-diagonal [96 x 128]
 // B (cols 0-63 convc1 on the corr rows, 64-127 convf1 on the flow rows), 6 fp16 B fragments per wave
@@ -375,8 +285,7 @@ extern "C" int sa_corr1d_pyramid(const void* f1, const void* f2, int stride, int
   // one workgroup per image row fills the chip at batch 8 (960 rows); at batch 1 (120 rows) the row's 32-row
   // slabs go to separate workgroups (each re-reads the row's right features from L2)
   const int nslab = (W1 + CORR_ROWS - 1) / CORR_ROWS;
-  const char* e = std::getenv("SA_CORR_SPLIT");  // 0 = one workgroup per row always (A/B; read at capture)
-  const int split = (B * H >= 512 || (e && e[0] == '0')) ? 1 : nslab;
+  const int split = B * H >= 512 ? 1 : nslab;
   hipLaunchKernelGGL(corr_pyramid_kernel, dim3(B * H, split), dim3(256), smem, stream, (const f16*)f1,
                      (const f16*)f2, stride, H, W1, W2, C, levels, off[1], off[2], off[3], pyr);
   return (int)hipGetLastError();
@@ -421,11 +330,8 @@ extern "C" int sa_raft_motion_head(const float* pyr, const float* flow, int B, i
   }
   if ((long)B * H * W1 >= (1L << 31) - 64) return -2;
   const int total = B * H * W1;
-  // SA_MH_VALU=1: the fp32 VALU kernel (A/B and numerics reference); default the MFMA kernel
-  const char* ve = std::getenv("SA_MH_VALU");  // read per launch (launches are captured once per engine)
-  const bool valu = ve && ve[0] == '1';
   if (((uintptr_t)cor | (uintptr_t)flo) & 15) return -2;
-  hipLaunchKernelGGL(valu ? raft_motion_head_kernel : raft_motion_head_mfma_kernel, dim3((total + 63) / 64),
+  hipLaunchKernelGGL(raft_motion_head_mfma_kernel, dim3((total + 63) / 64),
                      dim3(256), 0, stream, pyr, flow, total, H, W1, W2, levels, radius, off[1], off[2], off[3], wc,
                      bc, wf, bf, (f16*)cor, cstride, (f16*)flo, fstride, (f16*)fcopy, fcstride);
   return (int)hipGetLastError();

@@ -333,9 +333,9 @@ extern "C" int sa_hitnet_hyp_init(const float* dinit, const void* desc, int ds, 
 template <int C>
 int launch_warp(int T, dim3 g, const f16* el, int els, const f16* er, int ers, int B, int H, int W, const float* hyp,
                 int ncand, int th, int tw, f16* out, int ostride, int ccand, hipStream_t stream) {
-  const char* knob = getenv("SA_HIT_WARP_PX");  // "0": one thread per (candidate, tile) (A/B)
+  // one thread per (candidate, pixel); one per (candidate, tile) past 32-bit indexing
   const long px_total = (long)ncand * B * H * W;
-  if (!(knob && knob[0] == '0') && px_total < (1L << 31)) {
+  if (px_total < (1L << 31)) {
     const dim3 gp(grid_for(px_total, 256));
     switch (T) {
       case 4:

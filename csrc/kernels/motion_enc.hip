@@ -491,11 +491,7 @@ extern "C" int sa_raft_motion_encoder(const float* pyr, const float* flow, int B
   a.out = (f16*)out;
   a.os = os;
   a.stamps = g_stamps;
-  // SA_MENC_WAVES=4|8 (default 4: 8 waves measured no faster at batch 1 and 1 % slower at batch 8), read per
-  // launch (a frame graph captures it once)
-  const char* e = std::getenv("SA_MENC_WAVES");
-  const int nw = e && e[0] == '8' ? 8 : 4;
-  if (nw == 4) hipLaunchKernelGGL(raft_motion_encoder_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
-  else hipLaunchKernelGGL(raft_motion_encoder_kernel<8>, dim3((unsigned)blocks), dim3(512), 0, stream, a);
+  // 4 waves (an 8-wave variant measured no faster at batch 1 and 1 % slower at batch 8)
+  hipLaunchKernelGGL(raft_motion_encoder_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }

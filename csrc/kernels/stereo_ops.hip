@@ -361,8 +361,8 @@ extern "C" int sa_agcl_corr(const SaAgclArgs* a, hipStream_t stream) {
   if (a->C % 32 || a->out_channels < 36) return -2;
   const long total = (long)a->N * a->H * a->W * 36;
   if (total >= (1L << 31)) return -2;  // 32-bit index math in the kernel
-  const char* e = std::getenv("SA_AGCL8");  // 0 = one thread per tap (A/B; read at launch / graph capture)
-  if (a->C == 256 && total * 8 < (1L << 31) && !(e && e[0] == '0'))
+  // 8 threads per pixel for the 256-channel CREStereo features; one thread per tap otherwise
+  if (a->C == 256 && total * 8 < (1L << 31))
     hipLaunchKernelGGL(agcl8_kernel, dim3(grid_for(total * 8)), dim3(256), 0, stream, *a);
   else
     hipLaunchKernelGGL(agcl_kernel, dim3(grid_for(total)), dim3(256), 0, stream, *a);

@@ -401,9 +401,8 @@ extern "C" int sa_dwconv3x3(const void* x, int xs, const float* w, const float* 
   if (C % 8 || xs % 8 || os % 8) return -2;
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
   const long total = (long)N * Ho * Wo * (C / 8);
-  const char* knob = getenv("SA_DWCONV_LDS");  // "0": the one-thread-per-chunk kernel above (A/B)
-  const bool lds_path = !(knob && knob[0] == '0');
-  if (lds_path && C <= kDwMaxC && total < (1L << 31) && (long)N * H * W * xs < (1L << 31)) {
+  // LDS-staged weights for <= kDwMaxC channels; the one-thread-per-chunk kernel above otherwise
+  if (C <= kDwMaxC && total < (1L << 31) && (long)N * H * W * xs < (1L << 31)) {
     // <= 8 workgroups per CU so every workgroup's one-time weight staging is amortised over several tiles
     long g = (total + 255) / 256;
     if (g > 2048) g = 2048;
@@ -419,8 +418,8 @@ extern "C" int sa_dwconv3x3(const void* x, int xs, const float* w, const float* 
 extern "C" int sa_norm_corr_volume(const void* l, int ls, const void* r, int rs, int N, int H, int W, int C, int D,
                                    void* out, int os, hipStream_t stream) {
   if (C % 8 || os < 8 || os % 8) return -2;
-  const char* knob = getenv("SA_NORM_CORR8");  // "0": the per-plane kernel (A/B)
-  if (C == 48 && !(knob && knob[0] == '0') && (long)N * D * H * W < (1L << 31)) {
+  // 8 disparity planes per thread for the Fast-ACVNet+ 48-channel features; the per-plane kernel otherwise
+  if (C == 48 && (long)N * D * H * W < (1L << 31)) {
     hipLaunchKernelGGL(norm_corr8_kernel<6>, dim3(grid_for((long)N * ((D + 7) / 8) * H * W)), dim3(256), 0, stream,
                        (const f16*)l, ls, (const f16*)r, rs, N, H, W, D, (f16*)out, os);
     return (int)hipGetLastError();
@@ -443,8 +442,8 @@ extern "C" int sa_topk_disparity(const void* att, int as, int N, int D, int H, i
 extern "C" int sa_concat_volume(const void* l, int ls, const void* r, int rs, const float* prob, const float* disp,
                                 int N, int H, int W, int Cl, int K, void* out, int os, hipStream_t stream) {
   if (Cl % 8 || os < 2 * Cl) return -2;
-  const char* knob = getenv("SA_CONCAT_CHUNK");  // "0": one thread per volume row (A/B, profiles/concat_chunk_r02.txt)
-  if (!(knob && knob[0] == '0') && Cl % 8 == 0 && (long)N * K * H * W * (Cl / 8) < (1L << 31)) {
+  // 8-channel chunks per thread (profiles/concat_chunk_r02.txt); one thread per volume row past 32-bit indexing
+  if (Cl % 8 == 0 && (long)N * K * H * W * (Cl / 8) < (1L << 31)) {
     hipLaunchKernelGGL(concat_volume_chunk_kernel, dim3(grid_for((long)N * K * H * W * (Cl / 8))), dim3(256), 0,
                        stream, (const f16*)l, ls, (const f16*)r, rs, prob, disp, N, H, W, Cl, K, (f16*)out, os);
     return (int)hipGetLastError();

@@ -39,16 +39,9 @@ void instnorm(hipStream_t s, const Tensor& x, const sa_stat_t* stats, const Tens
   SA_LAUNCH_CHECK(s);
 }
 
-// SA_FUSE_IN=1: conv2 of the 64 -> 64 instance-norm blocks stages conv1's raw output and normalises it in LDS
-// (direct conv v2, tactic 23) instead of reading a materialised relu(IN(conv1)).  Off by default: the in-LDS
-// transform is a serial phase between two barriers (~250 us of the 520 us conv at b8), which eats the saved
-// HBM pass -- measured neutral (b8 44.66 vs 44.58 ms/step, b1 9.09 vs 9.12 ms, profiles/fused_input_norm_r02.txt)
-// while normalising in fp16 instead of fp32.
-static bool fused_input_norm(int in_planes, int planes) {
-  // read at every call (engine build and graph capture): tools/ab_engine.py sets it per engine
-  const bool on = std::getenv("SA_FUSE_IN") && std::getenv("SA_FUSE_IN")[0] == '1';
-  return on && in_planes == 64 && planes == 64;
-}
+// The instance-norm blocks materialise relu(IN(conv1)) before conv2.  Normalising conv1's raw output inside
+// conv2's LDS staging instead was measured neutral in round 2 (the in-LDS transform is a serial phase between
+// two barriers that eats the saved HBM pass; profiles/fused_input_norm_r02.txt) and has been removed.
 
 void ResBlock::build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std::string& p,
                      int in_planes, int planes, int stride, Norm nrm, int N, int H, int W, ActPlan* plan,
@@ -88,10 +81,7 @@ void ResBlock::build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std
     if (norm == Norm::Instance) {
       plan->use(x), plan->def(&y1, N, Ho, Wo, planes), plan->next();                   // c1(x) -> y1
       plan->use(&y1), plan->def(&a1, N, Ho, Wo, planes), plan->next();                 // IN -> a1
-      // c2(a1) -> y2; with the fused input norm c2 reads y1 itself, which must outlive the step (y2 must not
-      // take its memory)
-      if (fused_input_norm(planes, planes)) plan->use(&y1);
-      plan->use(&a1), plan->def(&y2, N, Ho, Wo, planes), plan->next();
+      plan->use(&a1), plan->def(&y2, N, Ho, Wo, planes), plan->next();                 // c2(a1) -> y2
       if (has_down) plan->use(x), plan->def(&yd, N, Ho, Wo, planes), plan->next();     // down(x) -> yd
       plan->use(&y2), plan->use(has_down ? &yd : x), plan->def(&out, N, Ho, Wo, planes), plan->next();
     } else {
@@ -114,22 +104,8 @@ void ResBlock::build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std
 void ResBlock::run(hipStream_t s, const StatsPool& sp, const Tensor& x) const {
   if (norm == Norm::Instance) {
     c1.run(s, {x}, y1, SA_ACT_NONE, nullptr, SA_ACT_NONE, sp.resolve(st1));
-    if (fused_input_norm(c2.cin_padded(), c2.cout())) {
-      // 64-channel blocks (full-resolution layer1): conv2 stages y1 and normalises it in LDS (direct conv v2,
-      // tactic 23) -- one HBM pass over the largest activations of the trunk fewer
-      int rc = sa_stats_reduce(sp.resolve(st1), kStatSlots, (long)y1.n * y1.c * 2, s);
-      SA_REQUIRE(rc == 0, "stats reduce failed");
-      SaConvArgs a = c2.args({y1}, y2);
-      a.act = SA_ACT_NONE;
-      a.stats = sp.resolve(st2);
-      a.stats_slots = kStatSlots;
-      a.in_stats = sp.resolve(st1);
-      a.in_act = SA_ACT_RELU;
-      c2.launch(s, a);
-    } else {
-      instnorm(s, y1, sp.resolve(st1), a1, SA_ACT_RELU);
-      c2.run(s, {a1}, y2, SA_ACT_NONE, nullptr, SA_ACT_NONE, sp.resolve(st2));
-    }
+    instnorm(s, y1, sp.resolve(st1), a1, SA_ACT_RELU);
+    c2.run(s, {a1}, y2, SA_ACT_NONE, nullptr, SA_ACT_NONE, sp.resolve(st2));
     if (has_down) {
       down.run(s, {x}, yd, SA_ACT_NONE, nullptr, SA_ACT_NONE, sp.resolve(std_));
       instnorm(s, y2, sp.resolve(st2), out, SA_ACT_RELU, &yd, sp.resolve(std_), SA_ACT_RELU);

@@ -143,14 +143,14 @@ class CreStereo : public StereoEngine {
   Trunk fnet_;
   ConvLayer fconv2_, offc8_, offc16_;
   AttnLayer self_, cross_;
-  ConvLayer convc1_, convc2_, convf1_, convf2_, mconv_, zr_[2], q_[2], fh1_, fh1mask_, fh2_, mask2_;
+  ConvLayer convc1_, convc2_, convf1_, convf2_, mconv_, zr_[2], q_[2], fh1_, fh1mask_, mask2_;
   // SepConvGRU with q's x-input half hoisted into the z/r conv (SA_EPI_GRU_ZRQ; see raft_stereo.cpp gzrq_): the q
-  // conv on the recurrent chain reads r*h alone (K = 5 x 128 instead of 5 x 384).  SA_CRE_GRU_SPLIT=0: z/r + q.
+  // conv on the recurrent chain reads r*h alone (K = 5 x 128 instead of 5 x 384); b1 iter10 network 6.86 -> 6.58 ms.
+  // On for batch <= 2 (the hoisted columns cost +11 % MACs, a throughput loss at large batch); SA_CRE_GRU_SPLIT=0/1.
   ConvLayer zrq_[2], qh_[2];
-  bool gru_split_ = !std::getenv("SA_CRE_GRU_SPLIT") || std::atoi(std::getenv("SA_CRE_GRU_SPLIT")) != 0;
+  int gru_split_mode_ = std::getenv("SA_CRE_GRU_SPLIT") ? std::atoi(std::getenv("SA_CRE_GRU_SPLIT")) : -1;
+  bool gru_split_ = false;
   Level lv_[3];  // 0: 1/4, 1: 1/8, 2: 1/16
-  // SA_CRE_FH2_PROJ=0: flow-head conv2 as the N=2 implicit GEMM instead of tap projection + stencil
-  bool fh2_proj_ = !std::getenv("SA_CRE_FH2_PROJ") || std::atoi(std::getenv("SA_CRE_FH2_PROJ")) != 0;
   void* fh2_w16_ = nullptr;
   float* fh2_b_ = nullptr;
   float *flowup4_ = nullptr, *flowup2_ = nullptr, *pe_ = nullptr;
@@ -210,6 +210,7 @@ void CreStereo::build(WeightSource& src) {
   src.conv(u + "encoder.convf2", 64, 128, 3, 3);
   src.conv(u + "encoder.conv", 126, 256, 3, 3);
   const WeightStore& ws = *src.ws;
+  gru_split_ = gru_split_mode_ >= 0 ? gru_split_mode_ != 0 : B <= 2;
   convc1_.build(a, ws, {u + "encoder.convc1"}, {{36, 40}}, s1);
   convc2_.build(a, ws, {u + "encoder.convc2"}, {{256, 256}}, s3);
   convf1_.build(a, ws, {u + "encoder.convf1"}, {{2, 8}}, s3);
@@ -249,10 +250,9 @@ void CreStereo::build(WeightSource& src) {
   src.conv(u + "mask.2", 144, 256, 1, 1);
   fh1_.build(a, ws, {u + "flow_head.conv1"}, {{128, 128}}, s3);
   fh1mask_.build(a, ws, {u + "flow_head.conv1", u + "mask.0"}, {{128, 128}}, s3);
-  fh2_.build(a, ws, {u + "flow_head.conv2"}, {{256, 256}}, s3);
   {
-    // flow-head conv2 (256 -> 2, 3x3) as an MFMA tap projection + stencil (sa_tap_proj): tap row
-    // (ky*3+kx)*2 + o of a [32][256] fp16 matrix, rows 18..31 zero
+    // flow-head conv2 (256 -> 2, 3x3) as MFMA tap projections + stencil in one launch (sa_flow_head_tail_oc):
+    // tap row (ky*3+kx)*2 + o of a [32][256] fp16 matrix, rows 18..31 zero
     const HostTensor& w2 = ws.get(u + "flow_head.conv2.weight");  // [2][256][3][3]
     const HostTensor& b2 = ws.get(u + "flow_head.conv2.bias");
     std::vector<_Float16> w16(32 * 256, (_Float16)0.f);
@@ -348,15 +348,9 @@ void CreStereo::update(hipStream_t s, Level& L, const Tensor& f1, const Tensor& 
   }
   if (want_mask) fh1mask_.run(s, {L.net}, L.fh, SA_ACT_RELU);
   else fh1_.run(s, {L.net}, L.fh.slice_c(0, 256), SA_ACT_RELU);
-  if (fh2_proj_) {
-    // tap projections over a halo tile + 3x3 stencil into the (x, y) flow, one launch (sa_flow_head_tail_oc)
-    check(sa_flow_head_tail_oc(L.fh.ptr, L.fh.stride, 256, fh2_w16_, 2, fh2_b_, L.flow, B, L.h, L.w, s),
-          "flow-head tail");
-  } else {
-    SaConvArgs fa = fh2_.args({L.fh.slice_c(0, 256)}, Tensor{L.flow, B, L.h, L.w, 2, 2, DT::F32});
-    fa.epi = SA_EPI_FLOW_ACC;
-    fh2_.launch(s, fa);
-  }
+  // tap projections over a halo tile + 3x3 stencil into the (x, y) flow, one launch
+  check(sa_flow_head_tail_oc(L.fh.ptr, L.fh.stride, 256, fh2_w16_, 2, fh2_b_, L.flow, B, L.h, L.w, s),
+        "flow-head tail");
   if (want_mask) mask2_.run(s, {L.fh.slice_c(256, 256)}, L.mask);
 }
 

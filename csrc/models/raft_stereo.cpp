@@ -92,26 +92,31 @@ class RaftStereo : public StereoEngine {
   // ConvGRU with q's x-input half hoisted into the z/r conv (SA_EPI_GRU_ZRQ): gzrq_ = [convz | convr | convq with
   // its h-input taps zeroed] over [h, x] (Cout 3 hd), gqh_ = convq's h-input taps over r*h alone (K = 9 hd instead
   // of 9 (hd + x)), qx_ = the hoisted x half of q's pre-activation.  Same sums, regrouped: the q conv on the
-  // recurrent chain gets 3x shorter, the z/r conv gets a third more columns (more workgroups at batch 1).
-  // SA_RAFT_GRU_SPLIT=0 restores the z/r + q pair.
+  // recurrent chain gets 3x shorter, the z/r conv gets a third more columns (more workgroups at batch 1).  The
+  // hoisted columns still run the h-input taps (zero weights), +11 % MACs: a latency win at batch <= 2 (b1 network
+  // SF 9.05 -> 8.42 ms, RT 2.25 -> 2.10 ms, profiles/timeline_r03.md), a throughput loss at batch 8, so it is on
+  // for batch <= 2.  SA_RAFT_GRU_SPLIT=0/1 forces it.
   ConvLayer gzrq_[3], gqh_[3];
   Tensor qx_[3];
-  bool gru_split_ = !std::getenv("SA_RAFT_GRU_SPLIT") || std::atoi(std::getenv("SA_RAFT_GRU_SPLIT")) != 0;
-  ConvLayer fh1_, fh1mask_, fh2_, mask2_;
+  int gru_split_mode_ = std::getenv("SA_RAFT_GRU_SPLIT") ? std::atoi(std::getenv("SA_RAFT_GRU_SPLIT")) : -1;
+  bool gru_split_ = false;
+  ConvLayer fh1_, fh1mask_, mask2_;
   Tensor corr_feat_, flow_feat_, cor1_, flo1_, corflo_, motion_;
   Tensor z_[3], rh_[3];
   Tensor pool_[2], interp_[2];  // pool_[i] = pool2x(net[i]) at level i+1; interp_[i] = interp(net[i+1]) at level i
   Tensor fh_, mask_;
-  // flow-head fusion (SA_EPI_PROJ): conv2's x-channel taps [9][256] fp32, its bias, the per-n-tile
-  // tap planes [<=4][9][M] written by conv1's epilogue
-  float* proj_w_ = nullptr;
-  float* proj_b_ = nullptr;
-  float* proj_p_ = nullptr;
+  // flow head conv2 (256 -> 1, 3x3; only the x component of the flow is used): bias, and its taps as fp16 [16][256]
+  // (taps 9..15 zero) for sa_flow_head_tail, which projects conv1's output onto the 9 taps over a halo tile and
+  // adds the stencil into the flow in one launch (round 2 A/Bs of the alternatives -- conv2 as an N = 1 implicit
+  // GEMM, fused into conv1's epilogue, or tap projection + stencil as two launches -- all lost:
+  // profiles/flow_head_tail_r02.txt)
+  float* fh2_b_ = nullptr;
+  void* fh2_w16_ = nullptr;
   // fused lookup + convc1 + convf1 (sa_raft_motion_head): fp32 [k][64] weights and biases
   float *mh_wc_ = nullptr, *mh_bc_ = nullptr, *mh_wf_ = nullptr, *mh_bf_ = nullptr;
   void* me_w1_ = nullptr;  // fused motion encoder stage-1 weights (fp16 [128][96]) and bias [128]
   float* me_b1_ = nullptr;
-  bool fuse_motion_ = !(std::getenv("SA_RAFT_FUSE_MOTION") && std::getenv("SA_RAFT_FUSE_MOTION")[0] == '0');
+  bool fuse_motion_ = true;  // the fused head kernels exist for levels * (2 radius + 1) <= 36 correlation planes
   // the whole motion encoder (head + convc2/convf2 + conv) as one kernel (sa_raft_motion_encoder): bitwise the
   // same output as the head kernel + three convs (same fp16 operands, same k order), 4 launches -> 1 per
   // iteration.  Measured in-process (tools/ab_engine.py): b1 9.94 vs 10.57 ms, b8 53.61 vs 55.75 ms/step.
@@ -128,21 +133,6 @@ class RaftStereo : public StereoEngine {
   // (profiles/pipeline_b8_r02.txt), so mode 2 is now the default at every batch.
   // SA_RAFT_PIPELINE=0/1/2 forces a mode (1: G32 one iteration ahead; 2: G32 and G16 ahead, see forward()).
   int pipeline_mode_ = std::getenv("SA_RAFT_PIPELINE") ? std::atoi(std::getenv("SA_RAFT_PIPELINE")) : -1;
-  // SA_RAFT_FUSE_FH: 0 = off, 1 = on, unset = auto.  With conv2 as a separate tap projection
-  // (sa_tap_proj, below) the unfused head wins at every batch, measured in-process on MI355X
-  // (tools/ab_engine.py): b8 56.6 vs 58.1 ms/step unfused vs fused; b1 tap projection vs the N=1
-  // implicit GEMM 12.0 vs 12.5 ms.  Auto = fused only when the tap projection is disabled and B >= 4.
-  int fuse_fh_mode_ = std::getenv("SA_RAFT_FUSE_FH") ? std::atoi(std::getenv("SA_RAFT_FUSE_FH")) : -1;
-  bool fuse_fh_ = false;
-  // unfused flow-head conv2 (256 -> 1, 3x3) as tap projection (one MFMA pass over the 256-channel
-  // activation, sa_tap_proj) + 9-tap stencil instead of an N=1 implicit GEMM that re-reads the
-  // activation once per tap.  SA_RAFT_FH2_PROJ=0 restores the implicit GEMM.
-  bool fh2_proj_ = !std::getenv("SA_RAFT_FH2_PROJ") || std::atoi(std::getenv("SA_RAFT_FH2_PROJ")) != 0;
-  void* fh2_w16_ = nullptr;  // fp16 [16][256], taps 9..15 zero
-  // tap projection + stencil as one halo-tiled launch (sa_flow_head_tail); SA_RAFT_FH_TAIL=0 restores the two
-  bool fh_tail_ = !std::getenv("SA_RAFT_FH_TAIL") || std::atoi(std::getenv("SA_RAFT_FH_TAIL")) != 0;
-  bool pool_interp_ = !std::getenv("SA_RAFT_POOL_INTERP") || std::atoi(std::getenv("SA_RAFT_POOL_INTERP")) != 0;
-  float* tap_p_ = nullptr;   // [9][B*h0*w0]
   float* pyr_ = nullptr;
   float* flow_ = nullptr;
   int lh_[3], lw_[3];
@@ -286,6 +276,7 @@ void RaftStereo::build(WeightSource& src) {
   }
   mconv_.build(a, ws, {u + "encoder.conv"}, {{128, 128}}, s3);
 
+  gru_split_ = gru_split_mode_ >= 0 ? gru_split_mode_ != 0 : Bn <= 2;
   const char* gnames[3] = {"gru08", "gru16", "gru32"};
   for (int i = 0; i < rc_.n_gru; ++i) {
     int xin;
@@ -331,24 +322,16 @@ void RaftStereo::build(WeightSource& src) {
   fh1_.build(a, ws, {u + "flow_head.conv1"}, {{hd, hd}}, s3);
   fh1mask_.build(a, ws, {u + "flow_head.conv1", u + "mask.0"}, {{hd, hd}}, s3);
   {
-    // only the x component of delta_flow is used (upstream zeroes delta_flow[:,1])
-    const HostTensor& w2 = ws.get(u + "flow_head.conv2.weight");
+    // only the x component of delta_flow is used (upstream zeroes delta_flow[:,1]): conv2's x-output taps
+    const HostTensor& w2 = ws.get(u + "flow_head.conv2.weight");  // [2][256][3][3]
     const HostTensor& b2 = ws.get(u + "flow_head.conv2.bias");
-    std::vector<float> wx(w2.data.begin(), w2.data.begin() + 256 * 9);
-    std::vector<float> bx = {b2.data[0]};
-    fh2_.build_raw(a, wx, bx, 1, 256, {{256, 256}}, s3);
-    // the same taps as [tap][c] for the fused projection
-    std::vector<float> pw(9 * 256);
-    for (int c = 0; c < 256; ++c)
-      for (int t = 0; t < 9; ++t) pw[t * 256 + c] = w2.data[c * 9 + t];
-    proj_w_ = (float*)a.alloc(pw.size() * 4);
-    proj_b_ = (float*)a.alloc(4);
-    HIP_CHECK(hipMemcpy(proj_w_, pw.data(), pw.size() * 4, hipMemcpyHostToDevice));
-    HIP_CHECK(hipMemcpy(proj_b_, bx.data(), 4, hipMemcpyHostToDevice));
     std::vector<_Float16> w16(16 * 256, (_Float16)0.f);
-    for (int i = 0; i < 9 * 256; ++i) w16[i] = (_Float16)pw[i];
+    for (int c = 0; c < 256; ++c)
+      for (int t = 0; t < 9; ++t) w16[t * 256 + c] = (_Float16)w2.data[c * 9 + t];
     fh2_w16_ = a.alloc(w16.size() * 2);
     HIP_CHECK(hipMemcpy(fh2_w16_, w16.data(), w16.size() * 2, hipMemcpyHostToDevice));
+    fh2_b_ = (float*)a.alloc(4);
+    HIP_CHECK(hipMemcpy(fh2_b_, b2.data.data(), 4, hipMemcpyHostToDevice));
   }
   mask2_.build(a, ws, {u + "mask.2"}, {{256, 256}}, s1, {}, 0.25f);
 
@@ -360,9 +343,6 @@ void RaftStereo::build(WeightSource& src) {
   corflo_ = make_tensor(a, Bn, h0, w0, 128);
   motion_ = make_tensor(a, Bn, h0, w0, 128);
   fh_ = make_tensor(a, Bn, h0, w0, 512);
-  fuse_fh_ = fuse_fh_mode_ > 0 || (fuse_fh_mode_ < 0 && !fh2_proj_ && Bn >= 4);
-  if (fuse_fh_) proj_p_ = (float*)a.alloc((size_t)4 * 9 * Bn * h0 * w0 * 4);  // <= 4 n-tiles of 64 channels
-  if (fh2_proj_) tap_p_ = (float*)a.alloc((size_t)9 * Bn * h0 * w0 * 4);
   mask_ = make_tensor(a, Bn, h0, w0, round_up(f * f * 9, 8));
   for (int i = 0; i + 1 < rc_.n_gru; ++i) {
     pool_[i] = make_tensor(a, Bn, lh_[i + 1], lw_[i + 1], hd);
@@ -514,16 +494,11 @@ void RaftStereo::forward(hipStream_t s) {
   };
   auto gru16 = [&](hipStream_t st) {
     if (rc_.n_gru == 3) {
-      // pool2x(net[0]) and interp(net[2]) as one launch (SA_RAFT_POOL_INTERP=0: two)
-      if (pool_interp_) {
-        check(sa_pool_interp(net_[0].ptr, net_[0].stride, pool_[0].ptr, pool_[0].stride, Bn, lh_[0], lw_[0], hd,
-                             net_[2].ptr, net_[2].stride, interp_[1].ptr, interp_[1].stride, Bn, lh_[2], lw_[2], hd,
-                             lh_[1], lw_[1], 1, 1.f, st),
-              "pool2x + interp");
-      } else {
-        pool(st, 0);
-        interp(st, 1);
-      }
+      // pool2x(net[0]) and interp(net[2]) as one launch (disjoint block ranges)
+      check(sa_pool_interp(net_[0].ptr, net_[0].stride, pool_[0].ptr, pool_[0].stride, Bn, lh_[0], lw_[0], hd,
+                           net_[2].ptr, net_[2].stride, interp_[1].ptr, interp_[1].stride, Bn, lh_[2], lw_[2], hd,
+                           lh_[1], lw_[1], 1, 1.f, st),
+            "pool2x + interp");
       gru(st, 1, {pool_[0], interp_[1]});
     } else {
       pool(st, 0);
@@ -564,7 +539,15 @@ void RaftStereo::forward(hipStream_t s) {
     convf2_.run(ms, {flo1_}, corflo_.slice_c(64, 64), SA_ACT_RELU);
     mconv_.run(ms, {corflo_}, motion_.slice_c(0, 126), SA_ACT_RELU);
   };
-  // finest GRU + flow head (+ mask head on the last iteration), coords1 += delta (x only)
+  // flow head: conv1 (+ the mask head's conv on the last iteration), then conv2's taps + stencil into the flow
+  // (x only) in one launch; mask head 1x1 on the last iteration
+  auto head = [&](hipStream_t st, bool last) {
+    if (last) fh1mask_.run(st, {net_[0]}, fh_, SA_ACT_RELU);
+    else fh1_.run(st, {net_[0]}, fh_.slice_c(0, 256), SA_ACT_RELU);
+    check(sa_flow_head_tail(fh_.ptr, fh_.stride, 256, fh2_w16_, fh2_b_, flow_, Bn, h0, w0, st), "flow-head tail");
+    if (last) mask2_.run(st, {fh_.slice_c(256, 256)}, mask_);
+  };
+  // finest GRU + flow head
   auto fine_and_head = [&](bool last, bool head_only = false) {
     if (head_only) {
       // (the finest GRU was enqueued by the caller)
@@ -574,42 +557,7 @@ void RaftStereo::forward(hipStream_t s) {
     } else {
       gru(s, 0, {motion_});
     }
-    if (last || !fuse_fh_) {
-      if (last) fh1mask_.run(s, {net_[0]}, fh_, SA_ACT_RELU);
-      else fh1_.run(s, {net_[0]}, fh_.slice_c(0, 256), SA_ACT_RELU);
-      if (fh2_proj_) {
-        const long M = (long)Bn * h0 * w0;
-        if (fh_tail_) {
-          check(sa_flow_head_tail(fh_.ptr, fh_.stride, 256, fh2_w16_, proj_b_, flow_, Bn, h0, w0, s), "flow-head tail");
-        } else {
-          check(sa_tap_proj(fh_.ptr, fh_.stride, M, 256, fh2_w16_, 9, tap_p_, M, s), "flow-head taps");
-          check(sa_proj_stencil(tap_p_, 1, M, Bn, h0, w0, 3, 3, 1, proj_b_, flow_, 1, 1, s), "flow-head stencil");
-        }
-      } else {
-        SaConvArgs fa = fh2_.args({fh_.slice_c(0, 256)}, Tensor{flow_, Bn, h0, w0, 1, 1, DT::F32});
-        fa.epi = SA_EPI_FLOW_ACC;
-        fh2_.launch(s, fa);
-      }
-      if (last) mask2_.run(s, {fh_.slice_c(256, 256)}, mask_);
-    } else {
-      // conv2 (256 -> 1, 3x3) fused into conv1's epilogue: per-pixel tap projections, then a
-      // 9-tap stencil adds bias + taps into the flow; the 256-channel activation never hits memory
-      SaConvArgs pa = fh1_.args({net_[0]}, fh_.slice_c(0, 256));
-      pa.out = nullptr;
-      pa.act = SA_ACT_RELU;
-      pa.epi = SA_EPI_PROJ;
-      pa.proj_w = proj_w_;
-      pa.proj_out = proj_p_;
-      pa.proj_taps = 9;
-      pa.proj_oc = 1;
-      pa.proj_plane = (long)Bn * h0 * w0;
-      conv_apply_plan(pa, s);  // the tuned tile fixes the n-tile count (= projection slices)
-      const int nsl = sa_conv2d_nslices(&pa);
-      SA_REQUIRE(nsl >= 1 && nsl <= 4, "flow-head projection slices %d", nsl);
-      fh1_.launch(s, pa);
-      check(sa_proj_stencil(proj_p_, nsl, pa.proj_plane, Bn, h0, w0, 3, 3, 1, proj_b_, flow_, 1, 1, s),
-            "flow-head stencil");
-    }
+    head(s, last);
   };
 
   const int f = 1 << rc_.n_downsample;
@@ -635,13 +583,6 @@ void RaftStereo::forward(hipStream_t s) {
       gru(s, 1, {pool_[0]});
       gru(s, 1, {pool_[0]});
     };
-    auto head = [&](hipStream_t st, bool last) {
-      if (last) fh1mask_.run(st, {net_[0]}, fh_, SA_ACT_RELU);
-      else fh1_.run(st, {net_[0]}, fh_.slice_c(0, 256), SA_ACT_RELU);
-      check(sa_flow_head_tail(fh_.ptr, fh_.stride, 256, fh2_w16_, proj_b_, flow_, Bn, h0, w0, st), "flow-head tail");
-      if (last) mask2_.run(st, {fh_.slice_c(256, 256)}, mask_);
-    };
-    SA_REQUIRE(fh2_proj_ && fh_tail_, "realtime pipeline needs the flow-head tail kernel");
     rec(s, 4);
     {
       ScopedSplitK k1(&splitk_side_);

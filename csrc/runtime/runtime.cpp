@@ -680,7 +680,6 @@ std::string plan_key(const SaConvArgs& a) {
   char buf[512];
   int n = std::snprintf(buf, sizeof(buf), "%s|%d,%d,%d,%d|", g_arch.c_str(), a.N, a.H, a.W, a.Cin);
   for (int i = 0; i < a.nsrc; ++i) n += std::snprintf(buf + n, sizeof(buf) - n, "%d.", a.src[i].channels);
-  if (a.in_stats) n += std::snprintf(buf + n, sizeof(buf) - n, "|i%d", a.in_act);
   std::snprintf(buf + n, sizeof(buf) - n, "|k%dx%dx%d|s%d,%d,%d|p%d,%d,%d|d%d,%d|o%dx%d|D%d,%d|c%d,%d|e%d,%d,%d,%d,%d|w%d",
                 a.KD, a.KH, a.KW, a.sd, a.sh, a.sw, a.pd, a.ph, a.pw, a.dh, a.dw, a.Ho, a.Wo, a.Do, a.Di, a.Cout,
                 a.Kpad, a.epi, (int)(a.stats != nullptr), a.up, (int)(a.gate != nullptr), (int)(a.res != nullptr),
@@ -696,6 +695,48 @@ bool env_tune_on() {
   return on;
 }
 
+// The tactics the tuner times (sa_conv2d tile_cfg values), with the split-K modes each family supports and the
+// shapes it is worth timing on.  A tactic whose launcher rejects a shape returns -5 and is skipped.
+struct Tactic {
+  int cfg;
+  bool split;    // splitk 0 (auto in-launch split-K) is a candidate
+  bool streamk;  // splitk -1 (stream-K) is a candidate
+  int min_cout;  // only for Cout > min_cout ...
+  int max_cout;  // ... and Cout <= max_cout (0 = no limit)
+  int tile_m, tile_n;  // ... whose grid of tile_m x tile_n tiles still covers >= 256 CUs (0 = always)
+  const char* what;
+};
+constexpr Tactic kTactics[] = {
+    {0, true, false, 0, 0, 0, 0, "128x128 register-staged"},
+    {1, true, false, 0, 0, 0, 0, "128x64 register-staged"},
+    {2, true, false, 0, 32, 0, 0, "256x16 register-staged (narrow outputs)"},
+    {3, true, false, 0, 0, 0, 0, "64x64 register-staged"},
+    {4, true, true, 0, 0, 0, 0, "256x128 DMA ring, 8 waves"},
+    {5, true, true, 0, 0, 0, 0, "128x64 DMA ring, 4 waves"},
+    {7, true, true, 0, 0, 0, 0, "128x128 DMA ring, 8 waves"},
+    {8, true, true, 0, 0, 0, 0, "256x64 DMA ring, 8 waves"},
+    {10, false, false, 128, 0, 256, 256, "256x256 wide 32x32x16"},
+    {11, false, false, 0, 0, 512, 128, "512x128 wide 32x32x16"},
+    {14, false, false, 0, 0, 0, 0, "128x64 deep DMA ring"},
+    {15, false, false, 0, 0, 0, 0, "128x128 deep DMA ring"},
+    {16, false, false, 0, 0, 0, 0, "64x64 deep DMA ring"},
+    {17, false, false, 0, 0, 0, 0, "256x64 deep DMA ring"},
+    {18, true, false, 128, 0, 0, 0, "256x256 ping-pong"},
+    {19, true, false, 0, 0, 0, 0, "256x128 ping-pong"},
+    {22, false, false, 0, 0, 0, 0, "7x7 stem"},
+    {23, false, false, 0, 0, 0, 0, "direct 3x3 64 -> 64, 2 waves / SIMD"},
+    {24, false, false, 0, 0, 0, 0, "direct 3x3 -> 96"},
+    {25, false, false, 0, 0, 0, 0, "strided 1x1"},
+    {26, false, false, 0, 0, 0, 0, "3x3 halo patch 8x32"},
+    {27, false, false, 0, 0, 0, 0, "3x3 halo patch 16x16"},
+};
+
+bool tactic_applies(const Tactic& t, const SaConvArgs& a, long M) {
+  if (a.Cout <= t.min_cout || (t.max_cout > 0 && a.Cout > t.max_cout)) return false;
+  if (t.tile_m > 0 && ((M + t.tile_m - 1) / t.tile_m) * ((a.Cout + t.tile_n - 1) / t.tile_n) < 256) return false;
+  return true;
+}
+
 PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
   // scratch for everything the candidates write (real outputs / in-place state are untouched)
   const long M = (long)a.N * (a.Do > 0 ? a.Do : 1) * a.Ho * a.Wo;
@@ -704,9 +745,8 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
   const size_t out_bytes = (size_t)Mo * width * 4 + 256;
   const size_t stats_bytes =
       a.stats ? (size_t)std::max(1, a.stats_slots) * a.N * a.Cout * 2 * sizeof(sa_stat_t) + 256 : 0;
-  const size_t proj_bytes = a.proj_out ? (size_t)4 * std::max(1, a.proj_taps * a.proj_oc) * a.proj_plane * 4 + 256 : 0;
   char* scratch = nullptr;
-  const size_t all_bytes = out_bytes + stats_bytes + proj_bytes;
+  const size_t all_bytes = out_bytes + stats_bytes;
   HIP_CHECK(hipMalloc((void**)&scratch, all_bytes));
   SaConvArgs t = a;
   if (t.out) t.out = scratch;
@@ -737,30 +777,19 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
     HIP_CHECK(hipMalloc((void**)&res, 2 * sizeof(unsigned)));
   }
   bool have_ref = false;
-  int ref_cfg = -1, ref_sk = 0, ref_slices = 0;
+  int ref_cfg = -1, ref_sk = 0;
   if (t.stats) t.stats = reinterpret_cast<sa_stat_t*>(scratch + out_bytes);
-  if (t.proj_out) t.proj_out = reinterpret_cast<float*>(scratch + out_bytes + stats_bytes);
   hipEvent_t e0, e1;
   HIP_CHECK(hipEventCreate(&e0));
   HIP_CHECK(hipEventCreate(&e1));
   PlanEntry best{-1, 1, 1e30f};
   const bool can_split = a.ws && a.counters && !a.stats;
-  // (cfgs 12 / 13, the 4-wave wide tiles, lose everywhere on MI355X (tools/conv_bench.py): not timed;
-  // 14-17 are the deep DMA rings, 18 / 19 the 8-wave ping-pong tiles)
-  for (int cfg = 0; cfg <= 27; ++cfg) {
-    if (cfg == 12 || cfg == 13) continue;
-    if (cfg == 2 && a.Cout > 32) continue;  // 256x16 tile: narrow outputs only
-    if (cfg == 6) continue;                 // 128x128 / 4 waves: never competitive (conv_bench)
-    // wide tiles (one block per CU, never split): only where their grid still covers the chip
-    if ((cfg == 10 || cfg == 12) && (a.Cout <= 128 || ((M + 255) / 256) * ((a.Cout + 255) / 256) < 256)) continue;
-    if ((cfg == 11 || cfg == 13) && ((M + 511) / 512) * ((a.Cout + 127) / 128) < 256) continue;
-    // ping-pong tiles: 20 / 21 (DMA inside the MFMA slot) measured no better than 18 / 19 and 20 spills: A/B only
-    if (cfg == 20 || cfg == 21) continue;
-    if (cfg == 18 && a.Cout <= 128) continue;
+  for (const Tactic& tc : kTactics) {
+    const int cfg = tc.cfg;
+    if (!tactic_applies(tc, a, M)) continue;
     for (int sk : {1, 0, -1}) {
-      // (ping-pong tiles: splitk 0 = K-split only the tiles of the last, partial round)
-      if (sk == 0 && (!can_split || (cfg >= 9 && cfg < 18) || cfg >= 22)) continue;
-      if (sk == -1 && (!can_split || cfg < 4 || cfg > 8)) continue;  // stream-K: DMA-ring family only
+      if (sk == 0 && (!can_split || !tc.split)) continue;
+      if (sk == -1 && (!can_split || !tc.streamk)) continue;
       t.tile_cfg = cfg;
       t.splitk = sk;
       if (sa_conv2d(&t, s) != 0) {
@@ -775,16 +804,10 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
           have_ref = true;
           ref_cfg = cfg;
           ref_sk = sk;
-          ref_slices = proj_bytes ? sa_conv2d_nslices(&t) : 0;
         } else {
           HIP_CHECK(hipMemsetAsync(res, 0, 2 * sizeof(unsigned), s));
           HIP_CHECK((hipError_t)sa_absdiff_max(scratch, ref, (long)(out_bytes / (out_f32 ? 4 : 2)), out_f32 ? 1 : 0,
                                                res, s));
-          // projection planes are laid out per n-tile slice: only comparable between tactics of the same
-          // n-tile width (a 64-wide tile writes 4 slices where a 128-wide one writes 2 -- the stencil sums them)
-          if (proj_bytes && sa_conv2d_nslices(&t) == ref_slices)
-            HIP_CHECK((hipError_t)sa_absdiff_max(scratch + out_bytes + stats_bytes, ref + out_bytes + stats_bytes,
-                                                 (long)(proj_bytes / 4), 1, res, s));
           unsigned h[2];
           HIP_CHECK(hipMemcpyAsync(h, res, sizeof(h), hipMemcpyDeviceToHost, s));
           HIP_CHECK(hipStreamSynchronize(s));

@@ -82,9 +82,7 @@ class SaConvArgs(C.Structure):
         ("n_counters", C.c_int32),
         ("KD", C.c_int32), ("Di", C.c_int32), ("Do", C.c_int32), ("sd", C.c_int32), ("pd", C.c_int32),
         ("up", C.c_int32), ("cout_real", C.c_int32), ("gate", C.c_void_p), ("gate_stride", C.c_int32),
-        ("proj_w", C.c_void_p), ("proj_out", C.c_void_p), ("proj_taps", C.c_int32), ("proj_oc", C.c_int32),
-        ("proj_plane", C.c_int64), ("stats_slots", C.c_int32), ("cin_real", C.c_int32),
-        ("in_stats", C.c_void_p), ("in_act", C.c_int32),
+        ("stats_slots", C.c_int32), ("cin_real", C.c_int32),
     ]
 
 
@@ -120,7 +118,7 @@ class SaEwArgs(C.Structure):
 
 
 ACT = {"none": 0, "relu": 1, "leaky": 2, "tanh": 3, "sigmoid": 4, "relu6": 5}
-EPI = {"store": 0, "gru_zr": 1, "gru_q": 2, "flow_acc": 3, "store_f32": 4, "proj": 5, "gru_zrq": 6}
+EPI = {"store": 0, "gru_zr": 1, "gru_q": 2, "flow_acc": 3, "store_f32": 4, "gru_zrq": 6}
 PRE = {"raw": 0, "unit": 1, "imagenet": 2, "signed": 3}
 
 _i = C.c_int
@@ -131,9 +129,6 @@ _f = C.c_float
 def _declare_dev(lib):
     sig = {
         "sa_conv2d": (_i, [C.POINTER(SaConvArgs), _p]),
-        "sa_conv2d_nslices": (_i, [C.POINTER(SaConvArgs)]),
-        "sa_proj_stencil": (_i, [_p, _i, C.c_long, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p]),
-        "sa_tap_proj": (_i, [_p, _i, C.c_long, _i, _p, _i, _p, C.c_long, _p]),
         "sa_flow_head_tail": (_i, [_p, _i, _i, _p, _p, _p, _i, _i, _i, _p]),
         "sa_flow_head_tail_oc": (_i, [_p, _i, _i, _p, _i, _p, _p, _i, _i, _i, _p]),
         "sa_instnorm_apply": (_i, [C.POINTER(SaNormArgs), _p]),

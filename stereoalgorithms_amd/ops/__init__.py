@@ -15,7 +15,7 @@ import torch
 from .. import _native as N
 
 __all__ = [
-    "splitk_workspace", "pack_conv_weight", "conv2d", "proj_stencil", "tap_proj", "stats_reduce", "instnorm_apply", "avgpool3s2", "avgpool_k", "interp_bilinear",
+    "splitk_workspace", "pack_conv_weight", "conv2d", "flow_head_tail", "flow_head_tail2", "stats_reduce", "instnorm_apply", "avgpool3s2", "avgpool_k", "interp_bilinear",
     "corr1d_pyramid", "corr1d_lookup", "raft_motion_head", "convex_upsample", "preprocess", "remap_bgr", "reproject",
     "agcl_corr", "linear_attention", "layernorm", "ew", "interp_flow", "convex_upsample_c",
     "pack_conv3d_weight", "deconv_as_conv_weight", "conv3d", "dwconv3x3", "norm_corr_volume", "topk_disparity",
@@ -44,32 +44,6 @@ def stats_reduce(stats, slots):
     """Fold ``slots`` copies of instance-norm statistics into copy 0 (copies 1.. are cleared)."""
     N.check(N.dev().sa_stats_reduce(stats.data_ptr(), slots, stats.numel() // slots, _stream()), "sa_stats_reduce")
     return stats
-
-
-def proj_stencil(P, nslices, n, h, w, kh, kw, oc, bias=None, out=None, accumulate=False):
-    """Tap sum of a conv fused into the producer's epilogue (``conv2d(..., epi="proj")``): fp32
-    ``out[n, h, w, oc]`` (+)= bias + sum over slices and taps with zero padding."""
-    if out is None:
-        out = torch.zeros(n, h, w, oc, dtype=torch.float32, device=P.device)
-    assert out.dtype == torch.float32
-    N.check(N.dev().sa_proj_stencil(P.data_ptr(), nslices, P.shape[-1], n, h, w, kh, kw, oc,
-                                    bias.data_ptr() if bias is not None else None, out.data_ptr(),
-                                    _pix_stride(out), int(accumulate), _stream()), "sa_proj_stencil")
-    return out
-
-
-def tap_proj(x, w):
-    """Per-pixel tap projections of a skinny conv: fp16 NHWC ``x`` [n,h,w,C] (pixel stride may exceed C),
-    ``w`` [T<=32, C] -> fp32 P [T, n*h*w] with P[t, m] = sum_c x[m, c] * w[t, c]."""
-    n, h, wd, c = x.shape
-    T = w.shape[0]
-    m = n * h * wd
-    w16 = torch.zeros(16 if T <= 16 else 32, c, dtype=torch.float16, device=x.device)
-    w16[:T] = w.to(torch.float16)
-    P = torch.empty(T, m, dtype=torch.float32, device=x.device)
-    N.check(N.dev().sa_tap_proj(x.data_ptr(), _pix_stride(x), m, c, w16.data_ptr(), T, P.data_ptr(), m, _stream()),
-            "sa_tap_proj")
-    return P
 
 
 def flow_head_tail(y, w, bias, flow):
@@ -167,10 +141,8 @@ def pack_conv_weight(w: torch.Tensor, segs: Sequence[tuple[int, int]] | None = N
 def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1, act="none",
            act2="none", res=None, out=None, epi="store", scale=1.0, alpha=0.01, stats=None,
            ctx=None, aux=None, hbuf=None, rh=None, tile_cfg=-1, splitk=1, workspace=None, up=0, cout_real=0,
-           gate=None, proj=None, stats_slots=1, cin_real=0, in_stats=None, in_act="none"):
-    """NHWC fp16 implicit-GEMM conv.  ``proj = (w2 fp32 [taps*oc, cout], taps, oc)`` with
-    ``epi="proj"``: the epilogue projects the activated output onto the taps of a following conv
-    and the call returns ``(out_or_None, P, nslices)`` for :func:`proj_stencil`.  ``splitk``: 1 = off, 0 = auto, >1 = forced; needs
+           gate=None, stats_slots=1, cin_real=0):
+    """NHWC fp16 implicit-GEMM conv.  ``splitk``: 1 = off, 0 = auto, >1 = forced; needs
     ``workspace`` = (fp32 slab tensor, int32 counter tensor zero-initialised).  ``up`` = 2: transposed
     conv, the 4 parity classes (cout = 4 * cout_real) are scattered to a 2x output.  ``gate``: fp16
     NHWC multiplier applied after the activation."""
@@ -198,13 +170,10 @@ def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1
         cin += x.shape[3]
     a.nsrc = len(xs)
     a.cin_real = cin_real  # single zero-padded source: real channels (the 7x7 stem kernel stages only those)
-    if in_stats is not None:  # fused input instance norm (tile_cfg 23): folded fixed-point sums [n][cin][2]
-        assert in_stats.dtype == torch.int64
-        a.in_stats, a.in_act = in_stats.data_ptr(), N.ACT[in_act]
     a.N, a.H, a.W, a.Cin = n, h, w, cin
     a.KH, a.KW, a.sh, a.sw, a.ph, a.pw, a.dh, a.dw = kh, kw, sh, sw, ph, pw, dil, dil
     a.Ho, a.Wo = ho, wo
-    if out is None and epi != "proj":
+    if out is None:
         dt = torch.float32 if epi == "store_f32" else torch.float16
         if up:
             out = torch.empty(n, 2 * ho, 2 * wo, cout_real, dtype=dt, device=xs[0].device)
@@ -240,18 +209,7 @@ def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1
         ws, cnt = workspace
         assert ws.dtype == torch.float32 and cnt.dtype == torch.int32
         a.ws, a.counters, a.ws_floats, a.n_counters = ws.data_ptr(), cnt.data_ptr(), ws.numel(), cnt.numel()
-    P = None
-    if epi == "proj":
-        w2, taps, oc = proj
-        assert w2.dtype == torch.float32 and w2.is_contiguous() and w2.shape == (taps * oc, cout)
-        a.tile_cfg = tile_cfg
-        nsl = N.dev().sa_conv2d_nslices(C.byref(a))
-        assert nsl > 0
-        P = torch.empty(nsl, taps * oc, n * ho * wo, dtype=torch.float32, device=xs[0].device)
-        a.proj_w, a.proj_out, a.proj_taps, a.proj_oc, a.proj_plane = w2.data_ptr(), P.data_ptr(), taps, oc, n * ho * wo
     N.check(N.dev().sa_conv2d(C.byref(a), _stream()), "sa_conv2d")
-    if epi == "proj":
-        return out, P, P.shape[0]
     return out
 
 

@@ -99,9 +99,9 @@ def test_conv2d_splitk_gru_epilogue():
 
 
 @pytest.mark.parametrize("cfg", [0, 1, 3])
-def test_conv2d_register_vs_dma_paths(cfg, monkeypatch):
-    """K padded to 32 only (odd multiple) forces the register-staged BK=32 loop; 64-padded weights take
-    the global->LDS DMA path when SA_CONV_GLDS=1.  Both must equal the torch reference."""
+def test_conv2d_register_bk32_vs_bk64(cfg):
+    """K padded to 32 only (odd multiple) forces the register-staged BK=32 loop; 64-padded weights take the
+    BK=64 loop.  Both must equal the torch reference."""
     O = ops()
     torch.manual_seed(7)
     n, cin, cout, h, w = 2, 24, 128 if cfg == 0 else 64, 13, 21
@@ -148,7 +148,7 @@ def test_conv2d_multisource_concat_and_residual():
     ((128, 128, 128), 128, 3, 1, (24, 32), 1, 3),  # three sources + forced split-K
     ((64,), 128, 7, 1, (12, 12), 1, 1),         # 49 taps
 ])
-@pytest.mark.parametrize("cfg", [4, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21])
+@pytest.mark.parametrize("cfg", [4, 10, 11, 14, 15, 16, 17, 18, 19])
 def test_conv2d_glds3_vs_torch(srcs, cout, k, stride, hw, n, splitk, cfg):
     """8-wave global->LDS DMA kernels: 256x128 (cfg 4: 3-deep LDS ring, counted vmcnt, XCD-ordered
     tiles), the wide tiles 256x256 / 512x128 (cfg 10 / 11: BK 32 4-deep ring, 32x32x16 MFMA,
@@ -209,7 +209,7 @@ def test_conv2d_streamk_vs_torch(srcs, cout, k, hw, n, cfg):
     assert int(ws[1].abs().sum()) == 0, "tile counters not reset"
 
 
-@pytest.mark.parametrize("cfg,splitk", [(18, 1), (19, 1), (20, 1), (21, 1), (18, 0), (19, 0)])
+@pytest.mark.parametrize("cfg,splitk", [(18, 1), (19, 1), (18, 0), (19, 0)])
 def test_conv2d_ping_pong_full_size_race_screen(cfg, splitk):
     """Ping-pong tiles at the RAFT-SF batch-8 GRU z/r shape (600 / 1200 tiles, 108 ring stages per tile):
     matches torch and repeated launches are bitwise identical (a misplaced vmcnt / barrier shows up as rare
@@ -257,7 +257,7 @@ def test_conv2d_streamk_gru_zr_epilogue():
     assert rel_err(nchw(rhb), r * net.half().float()) < 3e-3
 
 
-@pytest.mark.parametrize("cfg", [4, 10, 11, 12, 13, 18, 19, 20, 21])
+@pytest.mark.parametrize("cfg", [4, 10, 11, 18, 19])
 def test_conv2d_glds3_gru_and_stats_epilogues(cfg):
     O = ops()
     torch.manual_seed(12)
@@ -288,31 +288,6 @@ def test_conv2d_glds3_gru_and_stats_epilogues(cfg):
     assert rel_err(nchw(y), yr) < 2e-3
     assert rel_err(stats[..., 0].double() / 2 ** 24, yr.sum((2, 3))) < 1e-2
     assert rel_err(stats[..., 1].double() / 2 ** 24, (yr * yr).sum((2, 3))) < 1e-2
-
-
-@pytest.mark.parametrize("n,hw,cfg,oc", [(1, (24, 40), -1, 1), (2, (13, 21), 4, 1), (1, (30, 17), 5, 1),
-                                            (1, (9, 11), 0, 1), (2, (13, 21), 19, 1), (1, (30, 17), 21, 1)])
-def test_conv2d_projection_epilogue_flow_head(n, hw, cfg, oc):
-    """RAFT flow head fused: conv1 (3x3 128->256, ReLU) with the 3x3 256->oc conv2 projected in its
-    epilogue and summed by the stencil == conv2(relu(conv1(x))) (+ the running flow)."""
-    O = ops()
-    torch.manual_seed(21)
-    x = torch.randn(n, 128, *hw, device=DEV)
-    w1 = torch.randn(256, 128, 3, 3, device=DEV) / math.sqrt(128 * 9)
-    b1 = torch.randn(256, device=DEV) * 0.1
-    w2 = torch.randn(oc, 256, 3, 3, device=DEV) / math.sqrt(256 * 9)
-    b2 = torch.randn(oc, device=DEV) * 0.1
-    y1 = F.relu(F.conv2d(x.half().float(), w1.half().float(), b1, padding=1))
-    flow0 = torch.randn(n, *hw, oc, device=DEV)
-    ref = F.conv2d(y1, w2, b2, padding=1).permute(0, 2, 3, 1) + flow0
-    wp, kpad, _ = O.pack_conv_weight(w1)
-    w2p = w2.permute(2, 3, 0, 1).reshape(9 * oc, 256).contiguous()  # [(ky*3+kx)*oc + o][c]
-    _, P, nsl = O.conv2d(nhwc(x).half(), wp, kpad, 256, 3, 3, bias=b1.contiguous(), act="relu", epi="proj",
-                         proj=(w2p, 9, oc), tile_cfg=cfg)
-    out = flow0.clone()
-    O.proj_stencil(P, nsl, n, hw[0], hw[1], 3, 3, oc, bias=b2.contiguous(), out=out, accumulate=True)
-    torch.cuda.synchronize()
-    assert rel_err(out - flow0, ref - flow0) < 3e-3
 
 
 @pytest.mark.parametrize("n,hw", [(1, (120, 160)), (8, (120, 160)), (2, (37, 70)), (1, (5, 3))])
@@ -350,34 +325,11 @@ def test_flow_head_tail_two_channels(n, hw):
     assert rel_err(flow - flow0, ref) < 2e-3
 
 
-@pytest.mark.parametrize("n,hw,c,xs,oc", [(2, (24, 40), 256, 512, 1), (1, (13, 21), 256, 256, 1),
-                                            (1, (7, 9), 96, 104, 1), (2, (11, 30), 256, 512, 2)])
-def test_tap_proj_skinny_conv(n, hw, c, xs, oc):
-    """Flow-head conv2 (3x3 c->oc; RAFT oc 1, CREStereo oc 2 = 18 taps, two MFMA column tiles): MFMA tap
-    projection (one pass over the fp16 input, strided pixels) + stencil == F.conv2d in fp32 on the same
-    fp16-rounded operands, added to the running flow."""
-    O = ops()
-    torch.manual_seed(5)
-    base = torch.randn(n, *hw, xs, device=DEV).half()
-    x = base[..., :c]
-    w2 = torch.randn(oc, c, 3, 3, device=DEV) / math.sqrt(c * 9)
-    b2 = torch.randn(oc, device=DEV) * 0.1
-    taps = w2.permute(2, 3, 0, 1).reshape(9 * oc, c)  # [(ky*3+kx)*oc + o][c]
-    P = O.tap_proj(x, taps)
-    flow0 = torch.randn(n, *hw, oc, device=DEV)
-    out = flow0.clone()
-    O.proj_stencil(P, 1, n, hw[0], hw[1], 3, 3, oc, bias=b2.contiguous(), out=out, accumulate=True)
-    torch.cuda.synchronize()
-    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w2.half().float(), b2, padding=1).permute(0, 2, 3, 1)
-    assert rel_err(out - flow0, ref) < 2e-3
-
-
-@pytest.mark.parametrize("cfg", [9, 23])
 @pytest.mark.parametrize("n,hw,act,stats", [(2, (17, 70), "relu", False), (1, (48, 128), "none", True),
                                              (3, (5, 9), "leaky", True), (2, (33, 190), "none", True)])
-def test_conv3x3_c64_direct(n, hw, act, stats, cfg):
-    """Direct 3x3 64 -> 64 conv (tile_cfg 9: one wave per SIMD; 23: two waves per SIMD, buffer-store
-    epilogue): tails in both dims, several images per block, slotted statistics folded to the unsplit sums."""
+def test_conv3x3_c64_direct(n, hw, act, stats):
+    """Direct 3x3 64 -> 64 conv (tile_cfg 23: two waves per SIMD, buffer-store epilogue): tails in both dims,
+    several images per block, slotted statistics folded to the unsplit sums."""
     O = ops()
     torch.manual_seed(31)
     x = torch.randn(n, 64, *hw, device=DEV)
@@ -390,7 +342,7 @@ def test_conv3x3_c64_direct(n, hw, act, stats, cfg):
     if stats:
         st = torch.zeros(16, n, 64, 2, dtype=torch.int64, device=DEV)
         kw = dict(stats=st, stats_slots=16)
-    out = O.conv2d(nhwc(x).half(), wp, kpad, 64, 3, 3, bias=b.contiguous(), act=act, alpha=0.1, tile_cfg=cfg, **kw)
+    out = O.conv2d(nhwc(x).half(), wp, kpad, 64, 3, 3, bias=b.contiguous(), act=act, alpha=0.1, tile_cfg=23, **kw)
     torch.cuda.synchronize()
     assert rel_err(nchw(out), ref) < 2e-3
     if stats:
@@ -511,36 +463,6 @@ def test_conv1x1_point(cin, cout, n, hw, act, stats):
         y = nchw(out)
         assert rel_err(st[0, ..., 0].double() / 2 ** 24, y.sum((2, 3))) < 1e-3
         assert rel_err(st[0, ..., 1].double() / 2 ** 24, (y * y).sum((2, 3))) < 1e-3
-
-
-@pytest.mark.parametrize("n,hw", [(2, (17, 70)), (1, (48, 128)), (3, (5, 9))])
-def test_conv3x3_c64_direct2_input_norm(n, hw):
-    """Direct conv v2 with the input instance norm fused into its staging (tile_cfg 23, in_stats): conv2 of the
-    instance-norm ResidualBlock reads conv1's raw output y and its folded statistics; == F.conv2d on
-    relu(instance_norm(y)) with zero padding applied after the norm, and its own output statistics."""
-    O = ops()
-    torch.manual_seed(53)
-    y = (torch.randn(n, 64, *hw, device=DEV) * 2 + 0.7).half()
-    w = torch.randn(64, 64, 3, 3, device=DEV) / 24
-    b = torch.randn(64, device=DEV) * 0.1
-    yf = y.float()
-    mean = yf.mean((2, 3), keepdim=True)
-    var = yf.var((2, 3), unbiased=False, keepdim=True)
-    a = F.relu((yf - mean) / torch.sqrt(var + 1e-5))
-    ref = F.conv2d(a, w.half().float(), b, padding=1)
-    # fixed-point input statistics [n][64][2], folded (slot 0)
-    ist = torch.stack([yf.sum((2, 3)), (yf * yf).sum((2, 3))], -1).double() * 2 ** 24
-    ist = ist.round().to(torch.int64).contiguous()
-    wp, kpad, _ = O.pack_conv_weight(w)
-    st = torch.zeros(16, n, 64, 2, dtype=torch.int64, device=DEV)
-    out = O.conv2d(nhwc(y), wp, kpad, 64, 3, 3, bias=b.contiguous(), act="none", tile_cfg=23, stats=st,
-                   stats_slots=16, in_stats=ist, in_act="relu")
-    torch.cuda.synchronize()
-    assert rel_err(nchw(out), ref) < 5e-3  # the staged input is normalised in packed fp16
-    O.stats_reduce(st, 16)
-    torch.cuda.synchronize()
-    yo = nchw(out)
-    assert rel_err(st[0, ..., 0].double() / 2 ** 24, yo.sum((2, 3))) < 1e-3
 
 
 @pytest.mark.parametrize("n,hw,act2", [(2, (17, 70), "relu"), (1, (33, 190), "none")])
@@ -715,12 +637,13 @@ def test_conv2d_halo_gru_and_stats(cfg):
     ws = torch.randn(128, 128, 3, 3, device=DEV) / math.sqrt(128 * 9)
     wsp, kps, _ = O.pack_conv_weight(ws)
     st = torch.zeros(16, n, 128, 2, dtype=torch.int64, device=DEV)
-    out = O.conv2d(nhwc(xin).half(), wsp, kps, 128, 3, 3, stats=st, stats_slots=16, tile_cfg=cfg)
+    O.conv2d(nhwc(xin).half(), wsp, kps, 128, 3, 3, stats=st, stats_slots=16, tile_cfg=cfg)
     torch.cuda.synchronize()
-    o = out.float()
+    # the epilogue accumulates the fp32 values before their fp16 store
+    o = F.conv2d(xin.half().float(), ws.half().float(), padding=1).double()
     tot = st.sum(0).double() / 16777216.0
-    assert torch.allclose(tot[..., 0], o.sum((1, 2)).double(), rtol=1e-3, atol=1e-2)
-    assert torch.allclose(tot[..., 1], (o * o).sum((1, 2)).double(), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(tot[..., 0], o.sum((2, 3)), rtol=1e-4, atol=2e-3)
+    assert torch.allclose(tot[..., 1], (o * o).sum((2, 3)), rtol=1e-4, atol=2e-3)
 
 
 def test_conv2d_flow_acc_and_stats():
@@ -827,13 +750,11 @@ def test_raft_motion_head_vs_torch():
     assert torch.allclose(fc[..., 0].float(), flow, atol=1e-2) and fc[..., 1].abs().max().item() == 0
 
 
-@pytest.mark.parametrize("waves", ["4", "8"])
 @pytest.mark.parametrize("b,h,w", [(2, 7, 44), (1, 24, 32), (1, 13, 37)])
-def test_raft_motion_encoder_vs_torch(b, h, w, waves, monkeypatch):
+def test_raft_motion_encoder_vs_torch(b, h, w):
     """The whole motion encoder in one kernel == lookup -> convc1/convf1 -> convc2/convf2 -> conv (fp32 torch on
     the same fp16-rounded operands), including tiles that overhang the image (zero padding of every conv)."""
     from stereoalgorithms_amd.models.raft_stereo import CorrBlock1D, coords_grid
-    monkeypatch.setenv("SA_MENC_WAVES", waves)
     O = ops()
     torch.manual_seed(10)
     c = 256

@@ -13,24 +13,21 @@ def _pairs(b, h, w):
     return torch.from_numpy(l).cuda(), torch.from_numpy(r).cuda()
 
 
-@pytest.mark.parametrize("preset,iters,hw,fuse", [
+@pytest.mark.parametrize("preset,iters,hw,variant", [
     ("raftstereo-realtime", 7, (96, 160), ""),
-    ("raftstereo-sceneflow", 6, (96, 128), "0"),
-    ("raftstereo-sceneflow", 6, (96, 128), "1"),  # flow head conv2 fused into conv1's epilogue
-    ("raftstereo-sceneflow", 6, (96, 128), "nomotion"),  # unfused lookup / convc1 / convf1
-    ("raftstereo-sceneflow", 6, (96, 128), "fusein"),  # conv2 of the 64-channel IN blocks normalises its input
+    ("raftstereo-sceneflow", 6, (96, 128), ""),
+    ("raftstereo-sceneflow", 6, (96, 128), "nosplit"),  # z/r + q convs (the batch > 2 default)
+    ("raftstereo-sceneflow", 6, (96, 128), "nomenc"),  # motion head kernel + three convs instead of the fused encoder
 ])
-def test_engine_matches_oracle(tmp_path, monkeypatch, preset, iters, hw, fuse):
+def test_engine_matches_oracle(tmp_path, monkeypatch, preset, iters, hw, variant):
     from stereoalgorithms_amd.models import raft_stereo as R
     from stereoalgorithms_amd.models.engine import NativeStereoEngine
     from stereoalgorithms_amd.utils.weights import save_model
     h, w = hw
-    if fuse == "nomotion":
-        monkeypatch.setenv("SA_RAFT_FUSE_MOTION", "0")
-    elif fuse == "fusein":
-        monkeypatch.setenv("SA_FUSE_IN", "1")
-    elif fuse:
-        monkeypatch.setenv("SA_RAFT_FUSE_FH", fuse)
+    if variant == "nosplit":
+        monkeypatch.setenv("SA_RAFT_GRU_SPLIT", "0")
+    elif variant == "nomenc":
+        monkeypatch.setenv("SA_RAFT_FUSE_MENC", "0")
     m = R.build(preset, seed=0)
     path = save_model(m, tmp_path / "w.safetensors", preset)
     left, right = _pairs(2, h, w)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """In-process A/B of engine variants selected by an environment knob read at engine build time.
 
-    python3 tools/ab_engine.py --knob SA_RAFT_FUSE_FH --values 0,1 --model raftstereo-sceneflow --batch 8
+    python3 tools/ab_engine.py --knob SA_RAFT_GRU_SPLIT --values 0,1 --model raftstereo-sceneflow --batch 8
 
 Builds one engine per value (the knob is set while that engine is constructed), then times them in
 interleaved rounds (cdna_hip_programming.md §5.4 rule 24: cross-process numbers on different boxes

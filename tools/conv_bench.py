@@ -4,7 +4,6 @@
     python3 tools/conv_bench.py [--iters 50] [--shapes zr1,q1,...]
 
 Prints per shape: time per call (hipEvent, averaged), TFLOP/s, and the tile config the launcher chose.
-Env knobs of the kernel (SA_CONV_K32=1, SA_CONV_GLDS=1) select alternative main loops for A/B runs.
 """
 import argparse
 import os

@@ -26,8 +26,7 @@ def main():
     outs = [eng.run(L, R).clone() for _ in range(a.runs)]
     torch.cuda.synchronize()
     d = [float((o - outs[0]).abs().max()) for o in outs]
-    print(f"{a.model} b{a.batch} env FH2_PROJ={os.environ.get('SA_RAFT_FH2_PROJ')} "
-          f"NO_GRAPH={os.environ.get('SA_NO_GRAPH')}: max diff vs run0 {d}")
+    print(f"{a.model} b{a.batch} env NO_GRAPH={os.environ.get('SA_NO_GRAPH')}: max diff vs run0 {d}")
 
 
 if __name__ == "__main__":

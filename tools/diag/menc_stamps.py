@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Stage timing of the fused motion encoder from s_memrealtime marks (sa_raft_motion_encoder_stamps).
 
-    python tools/diag/menc_stamps.py [--batch 1] [--waves 4]
+    python tools/diag/menc_stamps.py [--batch 1]
 """
 import argparse
 import os
@@ -13,9 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1)
-    ap.add_argument("--waves", default="4")
     a = ap.parse_args()
-    os.environ["SA_MENC_WAVES"] = a.waves
     import torch
     from stereoalgorithms_amd import ops as O
     from stereoalgorithms_amd._native import dev
@@ -39,7 +37,7 @@ def main():
     t = st.view(blocks, 8, 64)[:, :7, 0].double()
     d = (t[:, 1:] - t[:, :-1]) / 100.0  # s_memrealtime ticks at 100 MHz -> us
     names = ["flow patch", "lookup+flow taps", "stage-1 GEMM", "stage-2 convs", "stage-3 loop", "epilogue+store"]
-    print(f"batch {b}, {blocks} workgroups, {a.waves} waves: mean / max us per stage")
+    print(f"batch {b}, {blocks} workgroups: mean / max us per stage")
     for i, n in enumerate(names):
         print(f"  {n:18s} {d[:, i].mean().item():8.2f} {d[:, i].max().item():8.2f}")
     tot = (t[:, 6] - t[:, 0]) / 100.0
