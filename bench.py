@@ -32,6 +32,7 @@ RAFTStereo/src/TRTRAFTStereo.cpp:119-146) for every model preset.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import socket
@@ -313,11 +314,15 @@ def main(argv=None) -> int:
 
     def release_step():
         """Tear the throughput step down in dependency order: the prefetcher's copies ride the engine's side stream,
-        so its buffers and events must go before the engine (and with it that stream) is destroyed -- left to
-        interpreter shutdown, the order is arbitrary and torch may touch the destroyed stream (segfault at exit)."""
-        nonlocal eng, dp, h2d
+        and torch's pinned-host allocator records an event on every stream that used a pinned block when that block
+        is FREED -- so the pinned inputs, the prefetcher's buffers and events must go before the engine (and with it
+        that stream) is destroyed.  Left to interpreter shutdown, the pinned blocks are freed after the stream is
+        gone and the event record segfaults the exit."""
+        nonlocal eng, dp, h2d, left_h, right_h
         sync()
-        dp, h2d = None, None
+        dp, h2d, left_h, right_h = None, None, None, None
+        gc.collect()
+        sync()
         if not cpu:
             eng.close()
         eng = None

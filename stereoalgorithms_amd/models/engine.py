@@ -63,7 +63,9 @@ class NativeStereoEngine:
     @property
     def copy_stream(self) -> torch.cuda.ExternalStream:
         """The engine's side stream as a torch stream: idle outside graph capture, so callers stage their input
-        copies there (parallel.dp.H2DPrefetcher) instead of creating a stream of their own."""
+        copies there (parallel.dp.H2DPrefetcher) instead of creating a stream of their own.  The stream dies with
+        the engine: free pinned host tensors that were copied on it BEFORE close() (torch's pinned-host allocator
+        records an event on every stream that used a block when the block is freed)."""
         return torch.cuda.ExternalStream(self._lib.sa_engine_copy_stream(self._h), device=self.device)
 
     @property
