@@ -73,8 +73,12 @@ class StereoEngine {
   // The engine's side stream.  It only carries work while a frame is being captured (graph replays run every
   // branch from the instantiated graph), so between frames it is free for the caller's input copies: the
   // data-parallel step issues its H2D prefetch there instead of on a stream of its own, keeping a rank within
-  // GPU_MAX_HW_QUEUES = 4 (engine, copy/side, caller, RCCL).
-  hipStream_t copy_stream() const { return side_; }
+  // GPU_MAX_HW_QUEUES = 4 (engine, copy/side, caller, RCCL).  Once handed out, the stream outlives the engine
+  // (see ~StereoEngine).
+  hipStream_t copy_stream() const {
+    side_exported_ = true;
+    return side_;
+  }
   size_t device_bytes() const { return arena_.bytes(); }
   // tuned-plan file used by this engine ("" = none) and how many conv shapes it had to time
   const std::string& plan_path() const { return plan_path_; }
@@ -150,6 +154,7 @@ class StereoEngine {
   int plan_loaded_ = -3, plan_saved_ = -1;
   SplitKWorkspace splitk_;
   hipStream_t side_ = nullptr;
+  mutable bool side_exported_ = false;  // copy_stream() was handed to a caller
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
   SplitKWorkspace splitk_side_;
   hipStream_t side2_ = nullptr;  // third stream for pipelined schedules

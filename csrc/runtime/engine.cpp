@@ -89,7 +89,13 @@ StereoEngine::~StereoEngine() {
   if (ev_out_) (void)hipEventDestroy(ev_out_);
   if (ev_fork_) (void)hipEventDestroy(ev_fork_);
   if (ev_join_) (void)hipEventDestroy(ev_join_);
-  if (side_) (void)hipStreamDestroy(side_);
+  if (side_) {
+    // An exported copy stream stays alive: torch's pinned-host allocator records an event on every stream a
+    // pinned block was copied on when that block is FREED, which may be long after the engine is gone (a
+    // destroyed stream there is a use-after-free at interpreter exit).  One stream per such engine is leaked.
+    if (side_exported_) (void)hipStreamSynchronize(side_);
+    else (void)hipStreamDestroy(side_);
+  }
   if (side2_) (void)hipStreamDestroy(side2_);
   for (hipEvent_t e : ev_dep_)
     if (e) (void)hipEventDestroy(e);
