@@ -561,7 +561,7 @@ void RaftStereo::forward(hipStream_t s) {
   };
 
   const int f = 1 << rc_.n_downsample;
-  // 0 = off, 1 = G32 ahead, 2 = G32 + G16 ahead (default below batch 4)
+  // 0 = off, 1 = G32 ahead, 2 = G32 + G16 ahead (the default at every batch, profiles/pipeline_b8_r02.txt)
   const int pmode = pipeline_mode_ >= 0 ? pipeline_mode_ : 2;
   SA_REQUIRE(pmode >= 0 && pmode <= 2, "SA_RAFT_PIPELINE=%d (0..2)", pmode);
   const bool pipe = par && pmode > 0 && rc_.n_gru == 3 && !rc_.slow_fast;
@@ -608,7 +608,7 @@ void RaftStereo::forward(hipStream_t s) {
     }
     wait(s, 1);
   } else if (pipe && pmode == 2) {
-    // Deeper cross-iteration pipeline (sceneflow at batch < 4).  Per iteration t:
+    // Deeper cross-iteration pipeline (sceneflow, every batch).  Per iteration t:
     //   side2: G32(t); then G16(t) once the finest q conv of t-1 is done (needs net0(t-1); the finest
     //          interp of t-1, the last reader of net1(t-1), ran before it)
     //   side : M(t) after FH(t-1) (needs flow(t-1); overwrites motion read by G08(t-1))
