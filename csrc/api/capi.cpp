@@ -29,6 +29,18 @@ int guarded(F&& f) {
 extern "C" {
 
 const char* sa_version(void) { return SA_VERSION_STRING; }
+
+// sizeof of the launch-argument structs the Python ctypes layer mirrors (checked when the library is loaded, so a
+// field added on one side only fails at import instead of shifting every later field)
+long sa_struct_size(const char* name) {
+  const std::string n = name ? name : "";
+  if (n == "SaConvArgs") return (long)sizeof(SaConvArgs);
+  if (n == "SaNormArgs") return (long)sizeof(SaNormArgs);
+  if (n == "SaAgclArgs") return (long)sizeof(SaAgclArgs);
+  if (n == "SaEwArgs") return (long)sizeof(SaEwArgs);
+  if (n == "SaConvSrc") return (long)sizeof(SaConvSrc);
+  return -1;
+}
 const char* sa_last_error(void) { return g_err.c_str(); }
 
 void* sa_engine_create(const char* model, const char* weights, int height, int width, int batch,

@@ -187,6 +187,14 @@ def _declare_dev(lib):
             continue
         fn.restype = res
         fn.argtypes = args
+    size = getattr(lib, "sa_struct_size", None)
+    if size is not None:
+        size.restype, size.argtypes = C.c_long, [C.c_char_p]
+        for st in (SaConvSrc, SaConvArgs, SaNormArgs, SaAgclArgs, SaEwArgs):
+            n = size(st.__name__.encode())
+            if n != C.sizeof(st):
+                raise RuntimeError(f"{st.__name__}: ctypes layout {C.sizeof(st)} B != native {n} B "
+                                   "(stereoalgorithms_amd/_native.py out of sync with csrc/include/sa/kernels.h)")
 
 
 def _declare_host(lib):
