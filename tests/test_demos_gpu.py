@@ -54,6 +54,22 @@ def test_demo_writes_outputs(demo, tmp_path):
 
 
 @pytest.mark.gpu
+def test_demo_stream_list(tmp_path):
+    """--list: several pairs streamed through the host frame pipeline (decode / write threads beside the engine)."""
+    lst = tmp_path / "pairs.txt"
+    lst.write_text("".join(f"{os.path.join(FX, 'left0.jpg')} {os.path.join(FX, 'right0.jpg')}\n" for _ in range(4)))
+    r = subprocess.run([os.path.join(BIN, "raft_stereo_demo"), "--model", "raftstereo-realtime", "--list", str(lst),
+                        "--save-all", "--calib", os.path.join(FX, "StereoCalibration.yml"), "--out", str(tmp_path)],
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "stream frames 4" in r.stdout
+    for i in range(4):
+        assert _jpeg_size(tmp_path / f"disparity_{i}.jpg") == (W, H)
+    assert _jpeg_size(tmp_path / "heatmap.jpg") == (W, H)
+    assert len((tmp_path / "pointcloud.txt").read_text().splitlines()) == H * W
+
+
+@pytest.mark.gpu
 def test_c_abi_contract():
     r = subprocess.run([os.path.join(BIN, "abi_check"), LIB, os.path.join(FX, "left0.jpg"), os.path.join(FX, "right0.jpg"),
                         os.path.join(FX, "StereoCalibration.yml"), "2"], capture_output=True, text=True, timeout=110)

@@ -111,6 +111,20 @@ def test_hostcopy_pool_tsan(tmp_path):
     assert "ThreadSanitizer" not in r.stderr
 
 
+def test_frame_pipeline_tsan(tmp_path):
+    """The host frame pipeline (csrc/host/pipeline.cpp: loader thread -> engine thread -> writer thread with
+    recycled frames) under ThreadSanitizer: order and content through recycled buffers, and clean shutdown after a
+    failing Infer, a throwing Source / Sink and a frame cap."""
+    import shutil
+    if not shutil.which("g++"):
+        pytest.skip("g++ not available")
+    r = subprocess.run(["bash", str(ROOT / "tools" / "sanitize" / "pipeline_tsan.sh"), str(tmp_path), "400"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "pipeline_stress: 400 rounds ok" in r.stdout
+    assert "ThreadSanitizer" not in r.stderr
+
+
 def test_pmc_summary_busy_fraction(tmp_path):
     """tools/pmc_summary.py: per-dispatch counters summed over rows, medians per (kernel, grid), and the MFMA busy
     fraction at the held clock = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)."""
