@@ -167,8 +167,12 @@ def test_end_to_end_away_from_ties(run):
     costs or the two candidates' confidences within 1 %, models/hitnet.py near_tie_mask) may go either way;
     everywhere else >= 98 % of the pixels must agree within 1 px.  At 480x640 the oracle must be
     non-degenerate (mean disparity >= 5 px) and the near-tie share small enough for the check to mean
-    something."""
+    something.  Only the scaled-init graphs: at PyTorch's default init the coarse features are ~1e-7, in fp16's
+    subnormal range, so an fp16 implementation cannot track the fp32 oracle there (an fp16-rounded copy of the
+    oracle itself agrees on 39 % / 87 % of the pixels; those configurations are pinned by the chain tests)."""
     from stereoalgorithms_amd.models import hitnet as HN
+    if not run["full"]:
+        pytest.skip("default init: features in fp16's subnormal range (chain tests cover this configuration)")
     with torch.no_grad():
         ref, tie = HN.near_tie_mask(run["m"], run["x6"])
     disp = run["disp_graph"]
