@@ -150,6 +150,9 @@ int StereoAlgorithm::Run(Mat& left, Mat& right, float* pointcloud, Mat& disparit
   }
 }
 
+int StereoAlgorithm::height() const { return engine_ ? engine_->H() : 0; }
+int StereoAlgorithm::width() const { return engine_ ? engine_->W() : 0; }
+
 int StereoAlgorithm::Release() {
   engine_.reset();
   have_maps_ = false;

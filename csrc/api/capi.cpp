@@ -4,7 +4,9 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
+#include "sa/algorithm.h"
 #include "sa/capi.h"
 #include "sa/engine.h"
 
@@ -128,5 +130,53 @@ int sa_engine_stage_times(void* e, float* ms, const char** names, int max) {
   });
   return rc == 0 ? n : -1;
 }
+
+void* sa_algorithm_create(const char* model, int gpu_id, const char* calibration_path, const char* default_preset) {
+  auto* a = new sa::StereoAlgorithm();
+  if (a->Initialize(model ? model : "", gpu_id, calibration_path ? calibration_path : "",
+                    default_preset ? default_preset : "") != 0) {
+    g_err = a->last_error();
+    delete a;
+    return nullptr;
+  }
+  return a;
+}
+
+int sa_algorithm_frame_size(void* alg, int* rows, int* cols) {
+  auto* a = static_cast<sa::StereoAlgorithm*>(alg);
+  if (!a || !a->initialized()) {
+    g_err = "not initialized";
+    return -1;
+  }
+  *rows = a->height();
+  *cols = a->width();
+  return 0;
+}
+
+int sa_algorithm_run(void* alg, unsigned char* left, unsigned char* right, int rows, int cols, float* disparity,
+                     float* cloud, int rectify) {
+  auto* a = static_cast<sa::StereoAlgorithm*>(alg);
+  int rc = -1;
+  const int g = guarded([&] {
+    sa::Mat l(rows, cols, sa::SA_8UC3, left), r(rows, cols, sa::SA_8UC3, right), d;
+    std::vector<float> scratch;
+    float* pc = cloud;
+    if (!pc) {  // the facade always reprojects; a caller that does not want the cloud gets it discarded
+      scratch.resize((size_t)rows * cols * 6);
+      pc = scratch.data();
+    }
+    rc = a->Run(l, r, pc, d, rectify != 0);
+    if (rc != 0) {
+      g_err = a->last_error();
+      return;
+    }
+    for (int y = 0; y < rows; ++y) std::memcpy(disparity + (size_t)y * cols, d.ptr<float>(y), (size_t)cols * 4);
+  });
+  return g != 0 ? g : rc;
+}
+
+float sa_algorithm_last_ms(void* alg) { return static_cast<sa::StereoAlgorithm*>(alg)->last_ms(); }
+
+void sa_algorithm_destroy(void* alg) { delete static_cast<sa::StereoAlgorithm*>(alg); }
 
 }  // extern "C"

@@ -74,7 +74,9 @@ bool read_calibration(const std::string& path, CalibrationParam& p) {
     return false;
   };
   p.has_roi = roi("validROIL", p.validROIL) & roi("validROIR", p.validROIR);
-  return true;
+  // a file without any of the matrices is not a stereo calibration (OpenCV's FileStorage would already have
+  // refused most such files; ours is lenient about the format)
+  return !(p.Q.empty() && p.intrinsic_left.empty() && p.intrinsic_right.empty() && p.P1.empty() && p.P2.empty());
 }
 
 bool write_calibration(const std::string& path, const CalibrationParam& p) {

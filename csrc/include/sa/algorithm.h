@@ -37,6 +37,9 @@ class StereoAlgorithm {
   const std::string& last_error() const { return err_; }
   const CalibrationParam& calibration() const { return calib_; }
   float last_ms() const { return last_ms_; }
+  // frame size of the engine (0 before Initialize)
+  int height() const;
+  int width() const;
   std::string model() const { return model_; }
 
  private:

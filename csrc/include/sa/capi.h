@@ -33,6 +33,17 @@ void sa_conv_plan_clear(void);
 // ms[i] and names[i] (pointers valid for the engine's lifetime)
 int sa_engine_stage_times(void* engine, float* ms, const char** names, int max);
 
+// The per-model facade (sa::StereoAlgorithm, sa/algorithm.h): calibration YAML, rectification maps and the
+// reference's Run semantics.  create returns NULL on failure (message: sa_last_error).  run takes contiguous BGR
+// u8 [rows][cols][3] images (rectified in place when `rectify`), writes disparity [rows][cols] fp32 and, when
+// `cloud` is not NULL, the point cloud [rows][cols][6].
+void* sa_algorithm_create(const char* model, int gpu_id, const char* calibration_path, const char* default_preset);
+int sa_algorithm_run(void* alg, unsigned char* left, unsigned char* right, int rows, int cols, float* disparity,
+                     float* cloud, int rectify);
+int sa_algorithm_frame_size(void* alg, int* rows, int* cols);
+float sa_algorithm_last_ms(void* alg);
+void sa_algorithm_destroy(void* alg);
+
 #ifdef __cplusplus
 }
 #endif

@@ -180,6 +180,11 @@ def _declare_dev(lib):
         "sa_conv_tune_rejects": (C.c_long, []),
         "sa_conv_plan_clear": (None, []),
         "sa_engine_stage_times": (_i, [_p, C.POINTER(C.c_float), C.POINTER(C.c_char_p), _i]),
+        "sa_algorithm_create": (_p, [C.c_char_p, _i, C.c_char_p, C.c_char_p]),
+        "sa_algorithm_run": (_i, [_p, _p, _p, _i, _i, _p, _p, _i]),
+        "sa_algorithm_frame_size": (_i, [_p, C.POINTER(_i), C.POINTER(_i)]),
+        "sa_algorithm_last_ms": (_f, [_p]),
+        "sa_algorithm_destroy": (None, [_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name, None)
