@@ -2,6 +2,7 @@
 Stereo_Calibration/process_image.py) and the V4L2 capture app's argument / error handling
 (reference usb_test.py; no camera exists here, so only the paths that need none are exercised)."""
 import os
+import re
 import subprocess
 import sys
 from pathlib import Path
@@ -123,6 +124,35 @@ def test_frame_pipeline_tsan(tmp_path):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "pipeline_stress: 400 rounds ok" in r.stdout
     assert "ThreadSanitizer" not in r.stderr
+
+
+def test_timeline_critical_chain(tmp_path):
+    """tools/timeline.py on a synthetic two-frame trace: frame cut at the preprocess marker, busy / idle union,
+    iterations at the marker kernel and the critical chain (latest-ending predecessor) with its launch gaps."""
+    hdr = "Kernel_Name,Start_Timestamp,End_Timestamp,Grid_Size_X,Workgroup_Size_X\n"
+    rows = []
+    for f in range(3):
+        t = f * 1_000_000
+        rows += [("preprocess_kernel", t, t + 1000), ("enc_kernel", t + 1000, t + 5000),
+                 ("side_kernel", t + 1200, t + 2000)]  # a concurrent branch, off the chain
+        for it in range(3):
+            b = t + 6000 + it * 10000
+            rows += [("motion_encoder_kernel", b, b + 3000), ("gru_kernel", b + 3000, b + 8000)]
+    csv = tmp_path / "x_kernel_trace.csv"
+    csv.write_text(hdr + "".join(f"{n},{s},{e},256,256\n" for n, s, e in rows))
+    r = subprocess.run([sys.executable, str(ROOT / "tools" / "timeline.py"), str(csv), "--iter-marker",
+                        "motion_encoder", "--chain", "5"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    out = r.stdout
+    assert "3 iterations" in out
+    # frame: 0..34000 ns span, idle = the 1000 ns before iteration 0 plus 2000 ns between iterations
+    m = re.search(r"span\s+([\d.]+) us, busy\s+([\d.]+) us", out)
+    assert m and abs(float(m.group(1)) - 34.0) < 1e-6 and abs(float(m.group(2)) - 29.0) < 1e-6, out
+    chain = out[out.index("critical chain"):]
+    # the concurrent branch is off the chain; the chain accounts for the whole span (kernels + launch gaps)
+    assert "side_kernel" not in chain, out
+    m = re.search(r"([\d.]+) us in kernels \+ ([\d.]+) us of launch gaps = ([\d.]+) us", chain)
+    assert m and abs(float(m.group(1)) - 29.0) < 1e-6 and abs(float(m.group(3)) - 34.0) < 1e-6, chain
 
 
 def test_pmc_summary_busy_fraction(tmp_path):

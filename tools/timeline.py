@@ -134,7 +134,9 @@ def main():
     while True:
         s = fr[chain[-1]][0]
         p = bisect.bisect_right(ends, s + 1000) - 1
-        while p >= 0 and by_end[p] == chain[-1]:
+        # a predecessor started before this kernel did (the slack must not admit a concurrent branch that began
+        # after it and happened to end within the slack)
+        while p >= 0 and (by_end[p] == chain[-1] or fr[by_end[p]][0] >= s):
             p -= 1
         if p < 0:
             break
