@@ -112,6 +112,25 @@ long sa_engine_nonzero_splitk_counters(void* e) { return static_cast<sa::StereoE
 long sa_conv_tune_count(void) { return sa::conv_tune_count(); }
 long sa_conv_tune_rejects(void) { return sa::conv_tune_rejects(); }
 void sa_conv_plan_clear(void) { sa::conv_plan_clear(); }
+// plan-file round trip without a GPU (tests pin the on-disk format the native writer produces): put seeds the
+// in-process plan, save writes the entries of the newline-separated `keys`, load merges a file (-1 absent, -2 stale)
+void sa_conv_plan_put(const char* key, int cfg, int splitk, float us) { sa::conv_plan_put(key, cfg, splitk, us); }
+int sa_conv_plan_save(const char* file, const char* keys) {
+  std::vector<std::string> k;
+  std::string cur;
+  for (const char* p = keys; ; ++p) {
+    if (*p == '\n' || *p == 0) {
+      if (!cur.empty()) k.push_back(cur);
+      cur.clear();
+      if (*p == 0) break;
+    } else {
+      cur += *p;
+    }
+  }
+  return sa::conv_plan_save(file, k);
+}
+int sa_conv_plan_load(const char* file) { return sa::conv_plan_load(file); }
+long sa_conv_plan_entries(void) { return (long)sa::conv_plan_entries(); }
 
 void* sa_engine_stream(void* e) { return (void*)static_cast<sa::StereoEngine*>(e)->stream(); }
 
@@ -156,6 +175,10 @@ int sa_algorithm_frame_size(void* alg, int* rows, int* cols) {
 int sa_algorithm_run(void* alg, unsigned char* left, unsigned char* right, int rows, int cols, float* disparity,
                      float* cloud, int rectify) {
   auto* a = static_cast<sa::StereoAlgorithm*>(alg);
+  if (!a) {
+    g_err = "null algorithm handle";
+    return -1;
+  }
   int rc = -1;
   const int g = guarded([&] {
     sa::Mat l(rows, cols, sa::SA_8UC3, left), r(rows, cols, sa::SA_8UC3, right), d;
@@ -175,7 +198,13 @@ int sa_algorithm_run(void* alg, unsigned char* left, unsigned char* right, int r
   return g != 0 ? g : rc;
 }
 
-float sa_algorithm_last_ms(void* alg) { return static_cast<sa::StereoAlgorithm*>(alg)->last_ms(); }
+float sa_algorithm_last_ms(void* alg) {
+  if (!alg) {
+    g_err = "null algorithm handle";
+    return -1.f;
+  }
+  return static_cast<sa::StereoAlgorithm*>(alg)->last_ms();
+}
 
 void sa_algorithm_destroy(void* alg) { delete static_cast<sa::StereoAlgorithm*>(alg); }
 

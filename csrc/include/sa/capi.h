@@ -29,6 +29,10 @@ long sa_engine_nonzero_splitk_counters(void* engine);
 long sa_conv_tune_count(void);
 long sa_conv_tune_rejects(void);
 void sa_conv_plan_clear(void);
+void sa_conv_plan_put(const char* key, int cfg, int splitk, float us);
+int sa_conv_plan_save(const char* file, const char* keys);  // keys newline-separated; 0 or errno
+int sa_conv_plan_load(const char* file);                    // entries added, -1 absent, -2 another build / no header
+long sa_conv_plan_entries(void);
 // per-stage device times of the last frame (SA_STAGE_TIMES=1): returns the count (<= max), fills
 // ms[i] and names[i] (pointers valid for the engine's lifetime)
 int sa_engine_stage_times(void* engine, float* ms, const char** names, int max);

@@ -179,6 +179,9 @@ int conv_plan_load(const std::string& file);
 // write the plan entries of `keys` (atomic rename); 0 or the errno of the failing step
 int conv_plan_save(const std::string& file, const std::vector<std::string>& keys);
 const std::string& conv_plan_build_id();  // hash of the loaded kernel library (plan files carry it)
+// how many of `keys` have an in-process plan but no entry in `file` (all of them if the file is absent / stale)
+int conv_plan_missing(const std::string& file, const std::vector<std::string>& keys);
+void conv_plan_put(const std::string& key, int cfg, int splitk, float us);  // tests: seed the in-process plan
 // collects every plan key consulted by conv_apply_plan in this thread (the engine's own shapes)
 struct ScopedPlanCollect {
   std::vector<std::string>* prev;

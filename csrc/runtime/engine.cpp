@@ -201,7 +201,10 @@ void StereoEngine::init() {
       HIP_CHECK(hipStreamSynchronize(stream_));
     }
     tuned_shapes_ = conv_tune_count() - tuned0;
-    if (!plan_path_.empty() && tuned_shapes_ > 0) {
+    // Save whenever this engine's own plan file lacks a shape it consulted, not only when it tuned one: an engine
+    // whose shapes were all tuned by an earlier engine in the same process (crestereo-iter10 after iter2 / iter5)
+    // still gets its "<stem>_batch=1.engine"-style file, so a fresh process running it alone does not re-tune.
+    if (!plan_path_.empty() && (tuned_shapes_ > 0 || conv_plan_missing(plan_path_, keys) > 0)) {
       plan_saved_ = conv_plan_save(plan_path_, keys);
       if (plan_saved_ == 0) SA_LOGI("tactic plan saved to %s", plan_path_.c_str());
       else SA_LOGE("could not write tactic plan %s: %s", plan_path_.c_str(), std::strerror(plan_saved_));

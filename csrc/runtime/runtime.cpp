@@ -640,8 +640,13 @@ const std::string& build_id() {
   return id;
 }
 
-// Plan files: an optional "# sa-plan build=<id>" header, then "key cfg splitk us" lines.  Returns the entries read,
-// or -2 when the header names another build (nothing is taken from such a file).
+bool known_tactic(int cfg);
+
+// Plan files: a "# sa-plan build=<id>" header, then "key cfg splitk us" lines.  Returns the entries read, or -2 when
+// the file is not this build's: its header names another build, or it has no header at all (every plan written
+// before headers existed, whose tactic numbers may no longer exist).  Nothing is taken from such a file.  An entry
+// whose cfg is not one of this build's tactics (a hand-edited plan) is dropped, so its shape is re-tuned instead of
+// failing the launch.
 int load_plan_file(std::unordered_map<std::string, PlanEntry>& m, const std::string& f) {
   std::ifstream in(f);
   std::string line;
@@ -649,23 +654,32 @@ int load_plan_file(std::unordered_map<std::string, PlanEntry>& m, const std::str
   bool first = true;
   while (std::getline(in, line)) {
     if (line.empty()) continue;
-    if (line[0] == '#') {
+    if (first) {
       const size_t b = line.find("build=");
-      if (first && b != std::string::npos && line.substr(b + 6, 16) != build_id()) return -2;
+      if (line[0] != '#' || b == std::string::npos || line.substr(b + 6, 16) != build_id()) return -2;
       first = false;
       continue;
     }
-    first = false;
+    if (line[0] == '#') continue;
     std::istringstream ls(line);
     std::string key;
     PlanEntry e;
     if (ls >> key >> e.cfg >> e.splitk >> e.us) {
+      if (!known_tactic(e.cfg)) {
+        SA_LOGW("plan %s: entry with unknown tactic %d dropped (re-tuned): %s", f.c_str(), e.cfg, key.c_str());
+        continue;
+      }
       m[key] = e;
       ++n;
     }
   }
   return n;
 }
+
+// SA_PLAN_CACHE file state for appending: true once the file is known to carry this build's header.  A file left by
+// another build is truncated and restarted with this build's header, so appended entries are never filed under a
+// header every later process rejects (the file would grow without the cache ever taking effect).
+bool g_cache_file_ok = false;
 
 std::unordered_map<std::string, PlanEntry>& plan_map() {  // caller holds g_plan_mu
   if (!g_plan) {
@@ -730,6 +744,12 @@ constexpr Tactic kTactics[] = {
     {26, false, false, 0, 0, 0, 0, "3x3 halo patch 8x32"},
     {27, false, false, 0, 0, 0, 0, "3x3 halo patch 16x16"},
 };
+
+bool known_tactic(int cfg) {
+  for (const Tactic& t : kTactics)
+    if (t.cfg == cfg) return true;
+  return false;
+}
 
 bool tactic_applies(const Tactic& t, const SaConvArgs& a, long M) {
   if (a.Cout <= t.min_cout || (t.max_cout > 0 && a.Cout > t.max_cout)) return false;
@@ -898,6 +918,24 @@ int conv_plan_load(const std::string& file) {
 
 const std::string& conv_plan_build_id() { return build_id(); }
 
+void conv_plan_put(const std::string& key, int cfg, int splitk, float us) {
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  plan_map()[key] = PlanEntry{cfg, splitk, us};
+}
+
+int conv_plan_missing(const std::string& file, const std::vector<std::string>& keys) {
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  auto& m = plan_map();
+  std::unordered_map<std::string, PlanEntry> in_file;
+  if (load_plan_file(in_file, file) < 0) in_file.clear();
+  int missing = 0;
+  for (const std::string& k : keys) {
+    auto it = m.find(k);
+    if (it != m.end() && it->second.cfg >= 0 && !in_file.count(k)) ++missing;
+  }
+  return missing;
+}
+
 int conv_plan_save(const std::string& file, const std::vector<std::string>& keys) {
   std::lock_guard<std::mutex> lk(g_plan_mu);
   auto& m = plan_map();
@@ -959,9 +997,18 @@ void conv_apply_plan(SaConvArgs& a, hipStream_t s) {
     ++g_tuned;
     const std::string f = plan_file();
     if (!f.empty() && e.cfg >= 0) {
-      const bool fresh = !std::ifstream(f).good();
+      if (!g_cache_file_ok) {
+        const std::string header = "# sa-plan build=" + build_id();
+        std::string first;
+        {
+          std::ifstream in(f);
+          in >> std::ws;
+          std::getline(in, first);
+        }
+        if (first != header) std::ofstream(f, std::ios::trunc) << header << '\n';
+        g_cache_file_ok = true;
+      }
       std::ofstream out(f, std::ios::app);
-      if (fresh) out << "# sa-plan build=" << build_id() << '\n';
       out << key << ' ' << e.cfg << ' ' << e.splitk << ' ' << e.us << '\n';
     }
   }

@@ -52,6 +52,8 @@ class StereoAlgorithm:
     @property
     def last_ms(self) -> float:
         """Wall time of the last run's timed region (ms)."""
+        if self._h is None:
+            raise RuntimeError("StereoAlgorithm is released")
         return float(self._lib.sa_algorithm_last_ms(self._h))
 
     def close(self):

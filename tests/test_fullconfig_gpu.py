@@ -40,12 +40,12 @@ def _stats(disp, ref, tag):
 
 
 def _plan(path):
+    from stereoalgorithms_amd.utils.plan import read_plan
     if os.path.exists(path):
-        lines = open(path).read().splitlines()
-        print(f"tactic plan: {len(lines)} new entries")
-        for l in lines[:40]:
-            key, cfg, sk, us = l.rsplit(" ", 3)
-            print(f"  cfg {cfg} splitk {sk} {float(us):8.1f} us  {key}")
+        build, entries = read_plan(path)
+        print(f"tactic plan (build {build}): {len(entries)} new entries")
+        for e in entries[:40]:
+            print(f"  cfg {e.cfg} splitk {e.splitk} {e.us:8.1f} us  {e.key}")
 
 
 def _engine(tmp_path, monkeypatch, model, preset, batch, iters=-1):

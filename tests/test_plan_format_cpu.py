@@ -1,0 +1,60 @@
+"""The tuned-plan file format, pinned against the native writer on the CPU (a header added to
+the plan files broke the GPU harness's parser and stopped the driver's GPU suite at test 32).  The plan API of
+libstereo_amd.so needs no device: entries are seeded in-process, written by conv_plan_save
+(csrc/runtime/runtime.cpp), then read back by the Python reader every test uses and by the native loader.
+Also pins the loader's rejection rules: a file without a header or with another build's header is not
+trusted, and an entry naming a tactic this build does not have is dropped instead of failing the launch."""
+import pytest
+
+from stereoalgorithms_amd import _native as N
+from stereoalgorithms_amd.utils.plan import read_plan
+
+pytestmark = pytest.mark.skipif(not N.available(), reason="native library not built")
+
+KEYS = ["gfx950|1,120,160,384|128.256.|k1x3x3|s1,1,1|p0,1,1|d1,1|o120x160|D0,0|c256,3456|e1,0,0,0,0|w1",
+        "gfx950|1,60,80,256|256.|k1x1x1|s1,1,1|p0,0,0|d1,1|o60x80|D0,0|c128,256|e0,0,0,0,0|w0"]
+
+
+def _lib():
+    lib = N.dev()
+    lib.sa_conv_plan_clear()
+    return lib
+
+
+def test_native_writer_roundtrip(tmp_path):
+    lib = _lib()
+    lib.sa_conv_plan_put(KEYS[0].encode(), 26, 1, 41.5)
+    lib.sa_conv_plan_put(KEYS[1].encode(), 3, 0, 7.25)
+    lib.sa_conv_plan_put(b"gfx950|untuned", -1, 1, 1e30)  # no tactic found: never written
+    path = tmp_path / "x.plan"
+    assert lib.sa_conv_plan_save(str(path).encode(), "\n".join(KEYS + ["gfx950|untuned", KEYS[0]]).encode()) == 0
+    build, entries = read_plan(path)
+    assert build == lib.sa_plan_build_id().decode() and len(build) == 16
+    assert [(e.key, e.cfg, e.splitk, e.us) for e in entries] == [(KEYS[0], 26, 1, 41.5), (KEYS[1], 3, 0, 7.25)]
+    # the native loader reads its own file back
+    lib.sa_conv_plan_clear()
+    assert lib.sa_conv_plan_load(str(path).encode()) == 2
+    assert lib.sa_conv_plan_entries() == 2
+
+
+def test_loader_rejects_stale_and_headerless_files(tmp_path):
+    lib = _lib()
+    body = f"{KEYS[0]} 26 1 41.5\n"
+    stale = tmp_path / "stale.plan"
+    stale.write_text("# sa-plan build=0000000000000000\n" + body)
+    assert lib.sa_conv_plan_load(str(stale).encode()) == -2
+    legacy = tmp_path / "legacy.plan"  # a plan written before headers existed
+    legacy.write_text(body)
+    assert lib.sa_conv_plan_load(str(legacy).encode()) == -2
+    assert lib.sa_conv_plan_load(str(tmp_path / "absent.plan").encode()) == -1
+    assert lib.sa_conv_plan_entries() == 0
+
+
+def test_loader_drops_unknown_tactics(tmp_path):
+    lib = _lib()
+    build = lib.sa_plan_build_id().decode()
+    p = tmp_path / "edited.plan"
+    p.write_text(f"# sa-plan build={build}\n{KEYS[0]} 9 1 10.0\n# comment\n{KEYS[1]} 3 1 5.0\n")
+    assert lib.sa_conv_plan_load(str(p).encode()) == 1  # retired tactic 9 dropped, tactic 3 kept
+    _, entries = read_plan(p)
+    assert len(entries) == 2  # the reader itself is format-only
