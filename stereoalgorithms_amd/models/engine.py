@@ -35,6 +35,13 @@ class NativeStereoEngine:
         self.model = model
         self.has_q = False
 
+    @property
+    def _live(self):
+        """The native handle; a closed engine raises instead of passing NULL to the C API (which would crash)."""
+        if not getattr(self, "_h", None):
+            raise RuntimeError("engine is closed")
+        return self._h
+
     def close(self):
         if getattr(self, "_h", None):
             self._lib.sa_engine_destroy(self._h)
@@ -51,14 +58,14 @@ class NativeStereoEngine:
         [("encoders+corr", 1.2), ("gru_iterations", 11.0), ("network", 0.1), ("reproject", 0.05)]."""
         ms = (C.c_float * 16)()
         names = (C.c_char_p * 16)()
-        n = self._lib.sa_engine_stage_times(self._h, ms, names, 16)
+        n = self._lib.sa_engine_stage_times(self._live, ms, names, 16)
         if n < 0:
             raise RuntimeError(f"stage_times failed: {self._lib.sa_last_error().decode()}")
         return [(names[i].decode(), float(ms[i])) for i in range(n)]
 
     @property
     def device_bytes(self) -> int:
-        return int(self._lib.sa_engine_device_bytes(self._h))
+        return int(self._lib.sa_engine_device_bytes(self._live))
 
     @property
     def copy_stream(self) -> torch.cuda.ExternalStream:
@@ -66,41 +73,41 @@ class NativeStereoEngine:
         copies there (parallel.dp.H2DPrefetcher) instead of creating a stream of their own.  The stream dies with
         the engine: free pinned host tensors that were copied on it BEFORE close() (torch's pinned-host allocator
         records an event on every stream that used a block when the block is freed)."""
-        return torch.cuda.ExternalStream(self._lib.sa_engine_copy_stream(self._h), device=self.device)
+        return torch.cuda.ExternalStream(self._lib.sa_engine_copy_stream(self._live), device=self.device)
 
     @property
     def plan_path(self) -> str:
         """Tuned-plan cache file of this engine ('' when disabled: SA_PLAN_CACHE set, SA_PLAN_DIR='')."""
-        return self._lib.sa_engine_plan_path(self._h).decode()
+        return self._lib.sa_engine_plan_path(self._live).decode()
 
     @property
     def tuned_shapes(self) -> int:
         """Conv shapes this engine had to time at build (0 when its plan file covered everything)."""
-        return int(self._lib.sa_engine_tuned_shapes(self._h))
+        return int(self._lib.sa_engine_tuned_shapes(self._live))
 
     @property
     def plan_status(self) -> dict:
         """Tuned-plan cache at build: path, entries loaded (-1 absent, -2 written by another library build, -3 not
         consulted), save result (0 ok, errno of a failed write, -1 not attempted) and the library build id."""
         ld, sv = C.c_int(0), C.c_int(0)
-        self._lib.sa_engine_plan_status(self._h, C.byref(ld), C.byref(sv))
+        self._lib.sa_engine_plan_status(self._live, C.byref(ld), C.byref(sv))
         return {"path": self.plan_path, "loaded": ld.value, "saved": sv.value, "tuned_shapes": self.tuned_shapes,
                 "build": self._lib.sa_plan_build_id().decode()}
 
     def nonzero_splitk_counters(self) -> int:
         """Diagnostic: split-K tile counters left non-zero (0 after every correctly ordered frame)."""
-        return int(self._lib.sa_engine_nonzero_splitk_counters(self._h))
+        return int(self._lib.sa_engine_nonzero_splitk_counters(self._live))
 
     def set_Q(self, Q):
         q = np.ascontiguousarray(np.asarray(Q, dtype=np.float32).reshape(16))
-        N.check(self._lib.sa_engine_set_q(self._h, q.ctypes.data_as(C.c_void_p)), "set_Q")
+        N.check(self._lib.sa_engine_set_q(self._live, q.ctypes.data_as(C.c_void_p)), "set_Q")
         self.has_q = True
 
     def set_rectify_maps(self, map_left: np.ndarray, map_right: np.ndarray):
         ml = np.ascontiguousarray(map_left, dtype=np.float32)
         mr = np.ascontiguousarray(map_right, dtype=np.float32)
         assert ml.shape == (self.height, self.width, 2) and mr.shape == ml.shape
-        N.check(self._lib.sa_engine_set_rectify_maps(self._h, ml.ctypes.data_as(C.c_void_p),
+        N.check(self._lib.sa_engine_set_rectify_maps(self._live, ml.ctypes.data_as(C.c_void_p),
                                                      mr.ctypes.data_as(C.c_void_p)), "set_rectify_maps")
 
     def run(self, left: torch.Tensor, right: torch.Tensor, cloud: bool = False, rectify: bool = False,
@@ -121,7 +128,7 @@ class NativeStereoEngine:
         rr = torch.empty_like(right) if (rectify and rectified) else None
         stream = C.c_void_p(torch.cuda.current_stream(left.device).cuda_stream)
         N.check(self._lib.sa_engine_run_device(
-            self._h, C.c_void_p(left.data_ptr()), C.c_void_p(right.data_ptr()), C.c_void_p(disp.data_ptr()),
+            self._live, C.c_void_p(left.data_ptr()), C.c_void_p(right.data_ptr()), C.c_void_p(disp.data_ptr()),
             C.c_void_p(pc.data_ptr() if pc is not None else 0), int(rectify), stream,
             C.c_void_p(rl.data_ptr() if rl is not None else 0), C.c_void_p(rr.data_ptr() if rr is not None else 0)),
             "engine run")
@@ -139,7 +146,7 @@ class NativeStereoEngine:
         right = np.ascontiguousarray(right, dtype=np.uint8).reshape(b, h, w, 3)
         disp = np.empty((b, h, w), np.float32)
         pc = np.empty((b, h, w, 6), np.float32) if cloud else None
-        N.check(self._lib.sa_engine_run_host(self._h, left.ctypes.data_as(C.c_void_p), right.ctypes.data_as(C.c_void_p),
+        N.check(self._lib.sa_engine_run_host(self._live, left.ctypes.data_as(C.c_void_p), right.ctypes.data_as(C.c_void_p),
                                              disp.ctypes.data_as(C.c_void_p),
                                              pc.ctypes.data_as(C.c_void_p) if pc is not None else None,
                                              int(rectify)), "engine run_host")
@@ -147,5 +154,5 @@ class NativeStereoEngine:
 
     def low_res_flow(self) -> int:
         n = C.c_int(0)
-        self._lib.sa_engine_aux_output(self._h, C.byref(n))
+        self._lib.sa_engine_aux_output(self._live, C.byref(n))
         return n.value

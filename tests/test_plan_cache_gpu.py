@@ -86,9 +86,12 @@ def test_second_engine_same_shapes_gets_its_own_plan(tmp_path, monkeypatch):
     lib.sa_conv_plan_clear()
     e1 = NativeStereoEngine("raftstereo-realtime", None, 64, 96, batch=1, iters=2, seed=21)
     assert e1.tuned_shapes > 0 and e1.plan_status["saved"] == 0
+    p1 = e1.plan_path
     e1.close()
+    with pytest.raises(RuntimeError):
+        e1.plan_path  # a closed engine raises instead of handing NULL to the C API
     e2 = NativeStereoEngine("raftstereo-realtime", None, 64, 96, batch=1, iters=2, seed=22)
-    assert e2.plan_path != e1.plan_path
+    assert e2.plan_path != p1
     assert e2.tuned_shapes == 0, "same shapes: nothing left to tune"
     assert e2.plan_status["saved"] == 0 and os.path.exists(e2.plan_path)
     build, entries = read_plan(e2.plan_path)

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 T=${1:-r4}
 mkdir -p gpurun_out/$T
 PYTEST_ARGS=${PYTEST_ARGS:-"tests -m gpu"}
-timeout -k 10 1000 python3 -u -m pytest $PYTEST_ARGS -v -rfE --durations=25 --timeout 300 --timeout-method thread \
+timeout -k 10 1000 python3 -u -m pytest $PYTEST_ARGS -v -rfEP --durations=25 --timeout 300 --timeout-method thread \
     > gpurun_out/$T/pytest.log 2>&1
 prc=$?
 echo "pytest rc=$prc"; tail -40 gpurun_out/$T/pytest.log | grep -E "passed|failed|FAILED|ERROR" || true
