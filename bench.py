@@ -244,8 +244,11 @@ def main(argv=None) -> int:
             pass
     else:
         left_h, right_h = left_h.pin_memory(), right_h.pin_memory()
-        # the H2D prefetch rides the engine's side stream (idle between captures): engine + side + torch + RCCL
-        # streams = 4 = GPU_MAX_HW_QUEUES per rank
+        # Streams per rank: the engine's own stream is made torch's current stream, so frames launch there without a
+        # cross-stream event pair and the step adds no caller stream; the H2D prefetch rides the engine's copy
+        # stream (idle outside capture); RCCL's all-gather runs on the process group's stream.  That is 3 streams
+        # (plus whatever the graph runtime uses for the frame graph's parallel branches) within GPU_MAX_HW_QUEUES=4.
+        torch.cuda.set_stream(eng.main_stream)
         h2d = H2DPrefetcher([left_h, right_h], dev, stream=eng.copy_stream)
 
         def step():
@@ -324,6 +327,7 @@ def main(argv=None) -> int:
         gc.collect()
         sync()
         if not cpu:
+            torch.cuda.set_stream(torch.cuda.default_stream(dev))
             eng.close()
         eng = None
 

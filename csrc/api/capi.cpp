@@ -132,7 +132,7 @@ int sa_conv_plan_save(const char* file, const char* keys) {
 int sa_conv_plan_load(const char* file) { return sa::conv_plan_load(file); }
 long sa_conv_plan_entries(void) { return (long)sa::conv_plan_entries(); }
 
-void* sa_engine_stream(void* e) { return (void*)static_cast<sa::StereoEngine*>(e)->stream(); }
+void* sa_engine_stream(void* e) { return (void*)static_cast<sa::StereoEngine*>(e)->export_stream(); }
 
 int sa_engine_stage_times(void* e, float* ms, const char** names, int max) {
   static thread_local std::vector<std::string> keep;

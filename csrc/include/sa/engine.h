@@ -70,6 +70,12 @@ class StereoEngine {
   void run_host(uint8_t* left, uint8_t* right, float* disp, float* cloud, bool rectify);
 
   hipStream_t stream() const { return stream_; }
+  // The engine stream handed to a caller that makes it its current stream (bench.py's data-parallel step): like
+  // an exported copy stream it outlives the engine, since the caller's allocator may still hold blocks keyed to it.
+  hipStream_t export_stream() const {
+    main_exported_ = true;
+    return stream_;
+  }
   // The engine's side stream.  It only carries work while a frame is being captured (graph replays run every
   // branch from the instantiated graph), so between frames it is free for the caller's input copies: the
   // data-parallel step issues its H2D prefetch there instead of on a stream of its own, keeping a rank within
@@ -155,6 +161,7 @@ class StereoEngine {
   SplitKWorkspace splitk_;
   hipStream_t side_ = nullptr;
   mutable bool side_exported_ = false;  // copy_stream() was handed to a caller
+  mutable bool main_exported_ = false;  // export_stream() was handed to a caller
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
   SplitKWorkspace splitk_side_;
   hipStream_t side2_ = nullptr;  // third stream for pipelined schedules

@@ -100,7 +100,10 @@ StereoEngine::~StereoEngine() {
   for (hipEvent_t e : ev_dep_)
     if (e) (void)hipEventDestroy(e);
 
-  if (stream_) (void)hipStreamDestroy(stream_);
+  if (stream_) {
+    if (main_exported_) (void)hipStreamSynchronize(stream_);
+    else (void)hipStreamDestroy(stream_);
+  }
   arena_.release();
 }
 

@@ -76,6 +76,14 @@ class NativeStereoEngine:
         return torch.cuda.ExternalStream(self._lib.sa_engine_copy_stream(self._live), device=self.device)
 
     @property
+    def main_stream(self) -> torch.cuda.ExternalStream:
+        """The engine's own stream (where its frame graphs are captured and replayed) as a torch stream.  A caller
+        that makes it current (``torch.cuda.set_stream``) runs frames without the cross-stream event pair a foreign
+        caller stream needs, and adds no stream of its own: the data-parallel step then uses the engine stream, its
+        copy stream and RCCL's stream (parallel.dp, bench.py)."""
+        return torch.cuda.ExternalStream(self._lib.sa_engine_stream(self._live), device=self.device)
+
+    @property
     def plan_path(self) -> str:
         """Tuned-plan cache file of this engine ('' when disabled: SA_PLAN_CACHE set, SA_PLAN_DIR='')."""
         return self._lib.sa_engine_plan_path(self._live).decode()
