@@ -355,14 +355,19 @@ def main(argv=None) -> int:
             e1 = NativeStereoEngine(preset if wpath is None else "", wpath, H, W, batch=1, device=dev.index, seed=0)
             e1.set_Q(Q)
             l1, r1 = l_np[:1].copy(), r_np[:1].copy()
+            # caller-owned outputs allocated once outside the timed loop, as the reference's demo allocates its
+            # point cloud (RAFTStereo/test/main.cpp:20); the timed region still copies both out every frame
+            d_out = np.empty((1, H, W), np.float32)
+            c_out = np.empty((1, H, W, 6), np.float32)
             for _ in range(3):
-                e1.run_host(l1, r1, cloud=True)
+                e1.run_host(l1, r1, cloud=True, out=d_out, cloud_out=c_out)
             ts = []
             for _ in range(args.latency_frames):
                 t1 = time.perf_counter()
-                e1.run_host(l1, r1, cloud=True)
+                e1.run_host(l1, r1, cloud=True, out=d_out, cloud_out=c_out)
                 ts.append((time.perf_counter() - t1) * 1e3)
             ts = np.array(ts)
+            host_split = e1.host_times()  # last frame: input copies / enqueue / device wait + output copies
             dev_b1 = e1.device_bytes
             e1.close()
             # per-stage device times from a second engine with stamps in its graph (tactic plan cached)
@@ -379,6 +384,7 @@ def main(argv=None) -> int:
                              "baseline_ms_rtx3090": base,
                              "speedup_vs_baseline": round(base / float(ts.mean()), 3) if base else None,
                              "device_bytes": dev_b1,
+                             "host_split_ms_last_frame": host_split,
                              "weights": "scale_init (parity-tested graph)" if wpath else "seeded default init",
                              "plan_loaded": e1.plan_status["loaded"], "plan_saved": e1.plan_status["saved"],
                              "device_stages_ms": {k: round(v, 3) for k, v in e1.stage_times()}}

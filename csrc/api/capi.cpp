@@ -90,6 +90,15 @@ int sa_engine_run_host(void* e, void* left, void* right, float* disp, float* clo
   });
 }
 
+void sa_engine_host_buffers(void* e, void** left, void** right, float** disp, float** cloud) {
+  static_cast<sa::StereoEngine*>(e)->host_buffers((uint8_t**)left, (uint8_t**)right, disp, cloud);
+}
+int sa_engine_host_times(void* e, float* out, int max) {
+  const float* t = static_cast<sa::StereoEngine*>(e)->host_times();
+  int n = 0;
+  for (; n < max && n < 7; ++n) out[n] = t[n];
+  return n;
+}
 void* sa_engine_copy_stream(void* e) { return static_cast<sa::StereoEngine*>(e)->copy_stream(); }
 long long sa_engine_device_bytes(void* e) {
   return (long long)static_cast<sa::StereoEngine*>(e)->device_bytes();

@@ -19,6 +19,10 @@ int sa_engine_run_device(void* engine, const void* left, const void* right, floa
 int sa_engine_run_host(void* engine, void* left, void* right, float* disp, float* cloud,
                        int rectify);
 long long sa_engine_device_bytes(void* engine);
+// run_host's pinned staging (pass these pointers back to run_host to skip the host-side copies) and the timing
+// split of the last run_host (ms: total, input copies, enqueue, wait + output copies[, H2D, graph, D2H])
+void sa_engine_host_buffers(void* engine, void** left, void** right, float** disp, float** cloud);
+int sa_engine_host_times(void* engine, float* out, int max);
 const float* sa_engine_aux_output(void* engine, int* n);
 void* sa_engine_stream(void* engine);
 // tuned-plan cache: the engine's plan file ("" = none), the conv shapes it had to time at build,

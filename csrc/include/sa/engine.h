@@ -68,6 +68,14 @@ class StereoEngine {
   // Host-side frame = the reference's timed region (RAFTStereo/src/TRTRAFTStereo.cpp:119-146):
   // pinned staging, H2D, graph, D2H of disparity and point cloud, synchronise.
   void run_host(uint8_t* left, uint8_t* right, float* disp, float* cloud, bool rectify);
+  // The pinned host staging run_host uses: inputs u8 BGR [B][H][W][3] x 2, disparity fp32 [B][H][W], cloud fp32
+  // [B][H][W][6].  Passing these very pointers to run_host skips the pageable <-> pinned copies (a camera writes
+  // frames straight into pinned memory, the D2H lands where the caller reads).  Valid for the engine's lifetime;
+  // overwritten by the next run_host.
+  void host_buffers(uint8_t** left, uint8_t** right, float** disp, float** cloud) const;
+  // ms of the last run_host: [0] whole timed region, [1] input copies, [2] enqueue, [3] device wait + output
+  // copies; with SA_HOST_TIMES=1 at engine creation also the device-side [4] H2D, [5] frame graph, [6] D2H
+  const float* host_times() const { return host_times_; }
 
   hipStream_t stream() const { return stream_; }
   // The engine stream handed to a caller that makes it its current stream (bench.py's data-parallel step): like
@@ -179,6 +187,8 @@ class StereoEngine {
   // run_host: chunked D2H (one event per chunk) copied out by a small thread pool as the chunks land
   static constexpr int kCopyEvents = 8;
   hipEvent_t ev_copy_[kCopyEvents] = {};
+  hipEvent_t host_ev_[4] = {};  // SA_HOST_TIMES=1: timing events around H2D / graph / D2H
+  float host_times_[8] = {};
   std::unique_ptr<HostCopyPool> copy_pool_;
   long launches_per_frame_ = 0;
 };

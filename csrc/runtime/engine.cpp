@@ -3,6 +3,7 @@
 #include "sa/engine.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -82,6 +83,8 @@ StereoEngine::~StereoEngine() {
   graph_[1].reset();
   copy_pool_.reset();
   for (auto& e : ev_copy_)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : host_ev_)
     if (e) (void)hipEventDestroy(e);
   if (pin_in_) (void)hipHostFree(pin_in_);
   if (pin_out_) (void)hipHostFree(pin_out_);
@@ -164,6 +167,9 @@ void StereoEngine::init() {
   HIP_CHECK(hipHostMalloc((void**)&pin_in_, 2 * img, hipHostMallocDefault));
   HIP_CHECK(hipHostMalloc((void**)&pin_out_, (size_t)B() * H() * W() * 7 * 4 + 2 * img, hipHostMallocDefault));
   for (auto& e : ev_copy_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (const char* ht = std::getenv("SA_HOST_TIMES"))
+    if (ht[0] == '1')
+      for (auto& e : host_ev_) HIP_CHECK(hipEventCreate(&e));
   copy_pool_ = std::make_unique<HostCopyPool>(3);
   // generous split-K / stream-K workspaces for the tuning pass (128 MiB of fp32 slabs, 8192 tile counters);
   // right-sized to the tuned plan's high-water mark afterwards
@@ -419,26 +425,47 @@ void StereoEngine::run_device(const uint8_t* left, const uint8_t* right, float* 
   if (rectify && rect_right) HIP_CHECK(hipMemcpyAsync(rect_right, in_right_, img, hipMemcpyDeviceToDevice, s));
 }
 
+void StereoEngine::host_buffers(uint8_t** left, uint8_t** right, float** disp, float** cloud) const {
+  const size_t img = (size_t)B() * H() * W() * 3;
+  const size_t n = (size_t)B() * H() * W();
+  *left = pin_in_;
+  *right = pin_in_ + img;
+  *disp = pin_out_;
+  *cloud = pin_out_ + n;
+}
+
 void StereoEngine::run_host(uint8_t* left, uint8_t* right, float* disp, float* cloud, bool rectify) {
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
   HIP_CHECK(hipSetDevice(cfg_.device));
   hipStream_t s = stream_;
   const size_t img = (size_t)B() * H() * W() * 3;
   const size_t n = (size_t)B() * H() * W();
-  copy_pool_->run({{pin_in_, left, img, nullptr}, {pin_in_ + img, right, img, nullptr}});
+  // Buffers handed out by host_buffers() are the pinned staging itself: a caller that fills / reads them in place
+  // skips the pageable <-> pinned copies (the D2H lands in the caller's array directly).
+  std::vector<HostCopyPool::Task> in;
+  if (left != pin_in_) in.push_back({pin_in_, left, img, nullptr});
+  if (right != pin_in_ + img) in.push_back({pin_in_ + img, right, img, nullptr});
+  copy_pool_->run(in);
+  const auto t1 = clk::now();
+  if (host_ev_[0]) HIP_CHECK(hipEventRecord(host_ev_[0], s));
   uint8_t* dl = rectify ? raw_left_ : in_left_;
   uint8_t* dr = rectify ? raw_right_ : in_right_;
   HIP_CHECK(hipMemcpyAsync(dl, pin_in_, img, hipMemcpyHostToDevice, s));
   HIP_CHECK(hipMemcpyAsync(dr, pin_in_ + img, img, hipMemcpyHostToDevice, s));
+  if (host_ev_[1]) HIP_CHECK(hipEventRecord(host_ev_[1], s));
   launch_frame(s, rectify);
+  if (host_ev_[2]) HIP_CHECK(hipEventRecord(host_ev_[2], s));
   float* pd = pin_out_;
   float* pc = pin_out_ + n;
   uint8_t* pr = reinterpret_cast<uint8_t*>(pin_out_ + 7 * n);
   // outputs: each D2H piece gets an event; the pool copies a piece into the caller's array once it landed,
-  // overlapping the rest of the transfer
+  // overlapping the rest of the transfer (nothing to copy when the caller's array is the pinned buffer)
   std::vector<HostCopyPool::Task> out;
   int ev = 0;
   auto d2h = [&](void* dst, void* pinned, const void* dev, size_t bytes) {
     HIP_CHECK(hipMemcpyAsync(pinned, dev, bytes, hipMemcpyDeviceToHost, s));
+    if (dst == pinned) return;
     HIP_CHECK(hipEventRecord(ev_copy_[ev], s));
     out.push_back({dst, pinned, bytes, ev_copy_[ev]});
     ++ev;
@@ -458,8 +485,21 @@ void StereoEngine::run_host(uint8_t* left, uint8_t* right, float* disp, float* c
     d2h(right, pr + img, in_right_, img);
   }
   SA_REQUIRE(ev <= kCopyEvents, "run_host: %d copy events", ev);
+  if (host_ev_[3]) HIP_CHECK(hipEventRecord(host_ev_[3], s));
+  const auto t2 = clk::now();
   copy_pool_->run(out);
   HIP_CHECK(hipStreamSynchronize(s));
+  const auto t3 = clk::now();
+  auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<float, std::milli>(b - a).count(); };
+  host_times_[0] = ms(t0, t3);  // whole timed region
+  host_times_[1] = ms(t0, t1);  // caller -> pinned input copies
+  host_times_[2] = ms(t1, t2);  // enqueue (H2D, graph launch, D2H)
+  host_times_[3] = ms(t2, t3);  // wait for the device + pinned -> caller output copies
+  if (host_ev_[0]) {  // SA_HOST_TIMES=1: device-side split of the same frame
+    HIP_CHECK(hipEventElapsedTime(&host_times_[4], host_ev_[0], host_ev_[1]));  // H2D
+    HIP_CHECK(hipEventElapsedTime(&host_times_[5], host_ev_[1], host_ev_[2]));  // frame graph
+    HIP_CHECK(hipEventElapsedTime(&host_times_[6], host_ev_[2], host_ev_[3]));  // D2H
+  }
 }
 
 }  // namespace sa

@@ -168,6 +168,8 @@ def _declare_dev(lib):
         "sa_engine_run_device": (_i, [_p, _p, _p, _p, _p, _i, _p, _p, _p]),
         "sa_engine_run_host": (_i, [_p, _p, _p, _p, _p, _i]),
         "sa_engine_device_bytes": (C.c_longlong, [_p]),
+        "sa_engine_host_buffers": (None, [_p, _p, _p, _p, _p]),
+        "sa_engine_host_times": (_i, [_p, C.POINTER(C.c_float), _i]),
         "sa_engine_copy_stream": (C.c_void_p, [_p]),
         "sa_engine_aux_output": (_p, [_p, C.POINTER(_i)]),
         "sa_engine_stream": (_p, [_p]),

@@ -147,13 +147,43 @@ class NativeStereoEngine:
             res += [rl, rr]
         return res[0] if len(res) == 1 else tuple(res)
 
-    def run_host(self, left: np.ndarray, right: np.ndarray, cloud: bool = True, rectify: bool = False):
-        """The reference's timed region: host BGR in, host disparity (+cloud) out."""
+    def host_buffers(self) -> dict:
+        """The engine's pinned host staging as numpy views (valid while the engine lives, overwritten by the next
+        run_host): ``left`` / ``right`` u8 [B,H,W,3], ``disp`` fp32 [B,H,W], ``cloud`` fp32 [B,H,W,6].  Passing them to
+        run_host (inputs filled in place, ``out`` / ``cloud_out``) skips the pageable <-> pinned copies."""
+        b, h, w = self.batch, self.height, self.width
+        ptrs = [C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()]
+        self._lib.sa_engine_host_buffers(self._live, *[C.byref(p) for p in ptrs])
+
+        def view(p, shape, ctype, dtype):
+            n = int(np.prod(shape))
+            return np.ctypeslib.as_array((ctype * n).from_address(p.value)).view(dtype).reshape(shape)
+        return {"left": view(ptrs[0], (b, h, w, 3), C.c_uint8, np.uint8),
+                "right": view(ptrs[1], (b, h, w, 3), C.c_uint8, np.uint8),
+                "disp": view(ptrs[2], (b, h, w), C.c_float, np.float32),
+                "cloud": view(ptrs[3], (b, h, w, 6), C.c_float, np.float32)}
+
+    def host_times(self) -> dict:
+        """Timing split of the last run_host in ms (device-side entries need SA_HOST_TIMES=1 at creation)."""
+        t = (C.c_float * 8)()
+        n = self._lib.sa_engine_host_times(self._live, t, 8)
+        keys = ("total", "input_copies", "enqueue", "wait_and_output_copies", "h2d", "graph", "d2h")
+        return {k: round(float(t[i]), 4) for i, k in enumerate(keys[:n])}
+
+    def run_host(self, left: np.ndarray, right: np.ndarray, cloud: bool = True, rectify: bool = False,
+                 out: np.ndarray | None = None, cloud_out: np.ndarray | None = None):
+        """The reference's timed region: host BGR in, host disparity (+cloud) out.  ``out`` / ``cloud_out``: caller
+        arrays to write (the reference's caller-allocated point cloud, RAFTStereo/test/main.cpp:20), e.g. the
+        engine's own pinned buffers from host_buffers(); fresh arrays otherwise."""
         b, h, w = self.batch, self.height, self.width
         left = np.ascontiguousarray(left, dtype=np.uint8).reshape(b, h, w, 3)
         right = np.ascontiguousarray(right, dtype=np.uint8).reshape(b, h, w, 3)
-        disp = np.empty((b, h, w), np.float32)
-        pc = np.empty((b, h, w, 6), np.float32) if cloud else None
+        disp = out if out is not None else np.empty((b, h, w), np.float32)
+        assert disp.shape == (b, h, w) and disp.dtype == np.float32 and disp.flags["C_CONTIGUOUS"]
+        pc = None
+        if cloud:
+            pc = cloud_out if cloud_out is not None else np.empty((b, h, w, 6), np.float32)
+            assert pc.shape == (b, h, w, 6) and pc.dtype == np.float32 and pc.flags["C_CONTIGUOUS"]
         N.check(self._lib.sa_engine_run_host(self._live, left.ctypes.data_as(C.c_void_p), right.ctypes.data_as(C.c_void_p),
                                              disp.ctypes.data_as(C.c_void_p),
                                              pc.ctypes.data_as(C.c_void_p) if pc is not None else None,
