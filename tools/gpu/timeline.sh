@@ -5,7 +5,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-TAG=${1:-r3}
+TAG=${1:-r4}
 mkdir -p gpurun_out/tl
 run() {  # name model iter-marker
   local name=$1 model=$2 marker=$3
