@@ -36,6 +36,7 @@
 namespace {
 typedef _Float16 f16;
 typedef f16 half8 __attribute__((ext_vector_type(8)));
+typedef f16 half4 __attribute__((ext_vector_type(4)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int TH = 8, TW = 16;                 // output tile
@@ -124,7 +125,9 @@ __device__ __forceinline__ int sw(int pix, int chunk) { return pix * 256 + ((chu
 
 // NW waves per workgroup (4: one per SIMD, 2 x 16 output channels per wave in stages 2 / 3; 8: two per SIMD,
 // one 16-channel column tile per wave)
-template <int NW>
+// VEC: every pyramid row length is a multiple of 4 floats (W2 % 32 == 0), so each level's 10 taps come from four
+// aligned 16-B loads (one cache line per lane instead of ten scalar loads that each touch 64 lines per wave)
+template <int NW, bool VEC>
 __global__ __launch_bounds__(64 * NW) void raft_motion_encoder_kernel(const MotionEncArgs p) {
   constexpr int NT = 64 * NW, JN = 8 / NW;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
@@ -165,30 +168,68 @@ __global__ __launch_bounds__(64 * NW) void raft_motion_encoder_kernel(const Moti
     const int y = ty0 - 2 + r, x = tx0 - 2 + c;
     const bool in = (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
     const float fx = fl[(r + 3) * FW + (c + 3)];
-    float v[4][10], wa[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const long off = q == 0 ? 0 : (q == 1 ? p.lvl_off1 : (q == 2 ? p.lvl_off2 : p.lvl_off3));
-      const int Wl = p.W2 >> q;
-      const float* row = p.pyr + off + (img_base + (long)(in ? y : 0) * p.W + (in ? x : 0)) * Wl;
-      const float xl = ((float)x + fx) / (float)(1 << q) - 4.f;
-      const float x0f = floorf(xl);
-      wa[q] = xl - x0f;
-      const int x0 = (int)x0f;
-#pragma unroll
-      for (int k = 0; k < 10; ++k) {
-        const int xi = x0 + k;
-        v[q][k] = (in && xi >= 0 && xi < Wl) ? row[xi] : 0.f;
-      }
-    }
     half8 hv[12];
+    if constexpr (VEC) {
+      // level q: the 16 floats of row[b .. b + 16), b = x0 rounded down to a multiple of 4 (chunks lie wholly inside
+      // or wholly outside the row, so the zero padding is per chunk); tap k = lerp(x0 - b + k)
+      floatx4 f[4][4];
+      float wa[4];
+      int d[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < 4; ++q) {
+        const long off = q == 0 ? 0 : (q == 1 ? p.lvl_off1 : (q == 2 ? p.lvl_off2 : p.lvl_off3));
+        const int Wl = p.W2 >> q;
+        const float* row = p.pyr + off + (img_base + (long)(in ? y : 0) * p.W + (in ? x : 0)) * Wl;
+        const float xl = ((float)x + fx) / (float)(1 << q) - 4.f;
+        const float x0f = floorf(xl);
+        wa[q] = xl - x0f;
+        const int x0 = (int)x0f;
+        const int b = x0 & ~3;
+        d[q] = x0 - b;
 #pragma unroll
-      for (int k = 0; k < 9; ++k) {
-        const int kk = 9 * q + k;
-        hv[kk >> 3][kk & 7] = (f16)__fmaf_rn(wa[q], v[q][k + 1], __fmul_rn(1.f - wa[q], v[q][k]));  // = lerp_tap (corr.hip)
+        for (int t = 0; t < 4; ++t) {
+          const int c = b + 4 * t;
+          f[q][t] = (in && c >= 0 && c < Wl) ? *reinterpret_cast<const floatx4*>(row + c) : floatx4{0.f, 0.f, 0.f, 0.f};
+        }
       }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float g[13];
+#pragma unroll
+        for (int sidx = 0; sidx < 13; ++sidx)  // = lerp_tap (corr.hip) at offset sidx
+          g[sidx] = __fmaf_rn(wa[q], f[q][(sidx + 1) >> 2][(sidx + 1) & 3], __fmul_rn(1.f - wa[q], f[q][sidx >> 2][sidx & 3]));
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+          const int kk = 9 * q + k;
+          const float t = d[q] == 0 ? g[k] : (d[q] == 1 ? g[k + 1] : (d[q] == 2 ? g[k + 2] : g[k + 3]));
+          hv[kk >> 3][kk & 7] = (f16)t;
+        }
+      }
+    } else {
+      float v[4][10], wa[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const long off = q == 0 ? 0 : (q == 1 ? p.lvl_off1 : (q == 2 ? p.lvl_off2 : p.lvl_off3));
+        const int Wl = p.W2 >> q;
+        const float* row = p.pyr + off + (img_base + (long)(in ? y : 0) * p.W + (in ? x : 0)) * Wl;
+        const float xl = ((float)x + fx) / (float)(1 << q) - 4.f;
+        const float x0f = floorf(xl);
+        wa[q] = xl - x0f;
+        const int x0 = (int)x0f;
+#pragma unroll
+        for (int k = 0; k < 10; ++k) {
+          const int xi = x0 + k;
+          v[q][k] = (in && xi >= 0 && xi < Wl) ? row[xi] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+          const int kk = 9 * q + k;
+          hv[kk >> 3][kk & 7] = (f16)__fmaf_rn(wa[q], v[q][k + 1], __fmul_rn(1.f - wa[q], v[q][k]));  // = lerp_tap (corr.hip)
+        }
+    }
 #pragma unroll
     for (int t = 0; t < 49; ++t) {
       const int kk = 36 + t, ky = t / 7, kx = t % 7;
@@ -207,14 +248,14 @@ __global__ __launch_bounds__(64 * NW) void raft_motion_encoder_kernel(const Moti
   {
     constexpr int NT1 = P1 / 16;  // 15
     half8 bfr[JN][3];
-    float bias[JN];
 #pragma unroll
     for (int j = 0; j < JN; ++j) {
       const int n = 16 * (wave * JN + j) + r16;
-      bias[j] = p.b1[n];
 #pragma unroll
       for (int ks = 0; ks < 3; ++ks) bfr[j][ks] = *reinterpret_cast<const half8*>(p.w1 + n * KP + ks * 32 + kofs);
     }
+    // transposed product (weights as the A operand): lane (r16, g) holds output channels 4 g .. 4 g + 3 of pixel
+    // 16 i + r16, stored as one 8-byte LDS write instead of four 2-byte ones
     floatx4 acc[NT1][JN];
 #pragma unroll
     for (int i = 0; i < NT1; ++i)
@@ -226,22 +267,27 @@ __global__ __launch_bounds__(64 * NW) void raft_motion_encoder_kernel(const Moti
       for (int i = 0; i < NT1; ++i) {
         const half8 a = *reinterpret_cast<const half8*>(a1 + (16 * i + r16) * AS + ks * 32 + kofs);
 #pragma unroll
-        for (int j = 0; j < JN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bfr[j][ks], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < JN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bfr[j][ks], a, acc[i][j], 0, 0, 0);
       }
+    float bias4[JN][4];
 #pragma unroll
-    for (int i = 0; i < NT1; ++i)
+    for (int j = 0; j < JN; ++j)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int pix = 16 * i + (lane >> 4) * 4 + rr;
-        const int r = pix / R1W, c = pix - r * R1W;
-        const bool in = (unsigned)(ty0 - 2 + r) < (unsigned)p.H && (unsigned)(tx0 - 2 + c) < (unsigned)p.W;
+      for (int rr = 0; rr < 4; ++rr) bias4[j][rr] = p.b1[16 * (wave * JN + j) + 4 * (lane >> 4) + rr];
 #pragma unroll
-        for (int j = 0; j < JN; ++j) {
-          const int col = 16 * (wave * JN + j) + r16;
-          const float v = in ? fmaxf(acc[i][j][rr] + bias[j], 0.f) : 0.f;
-          *reinterpret_cast<f16*>(s1 + sw(pix, col >> 3) + (col & 7) * 2) = (f16)v;
-        }
+    for (int i = 0; i < NT1; ++i) {
+      const int pix = 16 * i + r16;
+      const int r = pix / R1W, c = pix - r * R1W;
+      const bool in = (unsigned)(ty0 - 2 + r) < (unsigned)p.H && (unsigned)(tx0 - 2 + c) < (unsigned)p.W;
+#pragma unroll
+      for (int j = 0; j < JN; ++j) {
+        const int col = 16 * (wave * JN + j) + 4 * (lane >> 4);
+        half4 h;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) h[rr] = (f16)(in ? fmaxf(acc[i][j][rr] + bias4[j][rr], 0.f) : 0.f);
+        *reinterpret_cast<half4*>(s1 + sw(pix, col >> 3) + (col & 7) * 2) = h;
       }
+    }
   }
   __syncthreads();
 
@@ -302,7 +348,7 @@ __global__ __launch_bounds__(64 * NW) void raft_motion_encoder_kernel(const Moti
 #pragma unroll
       for (int i = 0; i < NT2; ++i)
 #pragma unroll
-        for (int j = 0; j < JN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ac[i], bc[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < JN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bc[j], ac[i], acc[i][j], 0, 0, 0);
     };
 #pragma unroll
     for (int st = 0; st < RING - 1; ++st) br.issue(st);
@@ -322,24 +368,27 @@ __global__ __launch_bounds__(64 * NW) void raft_motion_encoder_kernel(const Moti
       if ((st - MAIN) % 2 == 0) step(st, st + RING - 1 < NS2, st + 1 < NS2, ahead, a0, b0, a1v, b1v);
       else step(st, st + RING - 1 < NS2, st + 1 < NS2, ahead, a1v, b1v, a0, b0);
     }
-    float bias[JN];
+    // transposed product: lane (r16, g) holds channels 4 g .. 4 g + 3 of S2 pixel 16 i + r16 (one 8-byte write)
+    float bias4[JN][4];
 #pragma unroll
-    for (int j = 0; j < JN; ++j) bias[j] = bsrc[nb + 16 * j + r16];
+    for (int j = 0; j < JN; ++j)
 #pragma unroll
-    for (int i = 0; i < NT2; ++i)
+      for (int rr = 0; rr < 4; ++rr) bias4[j][rr] = bsrc[nb + 16 * j + 4 * (lane >> 4) + rr];
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int q = 16 * i + (lane >> 4) * 4 + rr;
-        if (q >= P2) continue;
-        const int r = q / R2W, c = q - r * R2W;
-        const bool in = (unsigned)(ty0 - 1 + r) < (unsigned)p.H && (unsigned)(tx0 - 1 + c) < (unsigned)p.W;
+    for (int i = 0; i < NT2; ++i) {
+      const int q = 16 * i + r16;
+      if (q >= P2) continue;
+      const int r = q / R2W, c = q - r * R2W;
+      const bool in = (unsigned)(ty0 - 1 + r) < (unsigned)p.H && (unsigned)(tx0 - 1 + c) < (unsigned)p.W;
 #pragma unroll
-        for (int j = 0; j < JN; ++j) {
-          const int col = cb + nb + 16 * j + r16;
-          const float v = in ? fmaxf(acc[i][j][rr] + bias[j], 0.f) : 0.f;
-          *reinterpret_cast<f16*>(s2 + sw(q, col >> 3) + (col & 7) * 2) = (f16)v;
-        }
+      for (int j = 0; j < JN; ++j) {
+        const int col = cb + nb + 16 * j + 4 * (lane >> 4);
+        half4 h;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) h[rr] = (f16)(in ? fmaxf(acc[i][j][rr] + bias4[j][rr], 0.f) : 0.f);
+        *reinterpret_cast<half4*>(s2 + sw(q, col >> 3) + (col & 7) * 2) = h;
       }
+    }
   }
   __syncthreads();
 
@@ -395,7 +444,7 @@ __global__ __launch_bounds__(64 * NW) void raft_motion_encoder_kernel(const Moti
 #pragma unroll
       for (int i = 0; i < NT3; ++i)
 #pragma unroll
-        for (int j = 0; j < JN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ac[i], bc[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < JN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bc[j], ac[i], acc[i][j], 0, 0, 0);
     };
 #pragma unroll
     for (int st = 0; st < RING - 1; ++st) br.issue(st);
@@ -418,20 +467,26 @@ __global__ __launch_bounds__(64 * NW) void raft_motion_encoder_kernel(const Moti
     stamp(5);
     __syncthreads();  // every wave is done with its ring before the S1 area takes the output tile
     // bias + relu (channels < 126), [fx, 0] tail, staged in the (finished) S1 area
+    // transposed product: lane (r16, g) holds channels 4 g .. 4 g + 3 of output pixel 16 i + r16
     char* so = s1;
 #pragma unroll
     for (int j = 0; j < JN; ++j) {
-      const int col = nb + 16 * j + r16;
-      const float bj = col < 126 ? p.b3[col] : 0.f;
+      const int col0 = nb + 16 * j + 4 * (lane >> 4);
+      float bj[4];
 #pragma unroll
-      for (int i = 0; i < NT3; ++i)
+      for (int rr = 0; rr < 4; ++rr) bj[rr] = col0 + rr < 126 ? p.b3[col0 + rr] : 0.f;
+#pragma unroll
+      for (int i = 0; i < NT3; ++i) {
+        const int q = 16 * i + r16;
+        const float fx = fl[((q / TW) + 5) * FW + (q % TW) + 5];
+        half4 h;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-          const int q = 16 * i + (lane >> 4) * 4 + rr;
-          const float fx = fl[((q / TW) + 5) * FW + (q % TW) + 5];
-          const float v = col < 126 ? fmaxf(acc[i][j][rr] + bj, 0.f) : (col == 126 ? fx : 0.f);
-          *reinterpret_cast<f16*>(so + sw(q, col >> 3) + (col & 7) * 2) = (f16)v;
+          const int col = col0 + rr;
+          h[rr] = (f16)(col < 126 ? fmaxf(acc[i][j][rr] + bj[rr], 0.f) : (col == 126 ? fx : 0.f));
         }
+        *reinterpret_cast<half4*>(so + sw(q, col0 >> 3) + (col0 & 7) * 2) = h;
+      }
     }
     __syncthreads();
     for (int i = tid; i < TH * TW * 16; i += NT) {
@@ -492,6 +547,9 @@ extern "C" int sa_raft_motion_encoder(const float* pyr, const float* flow, int B
   a.os = os;
   a.stamps = g_stamps;
   // 4 waves (an 8-wave variant measured no faster at batch 1 and 1 % slower at batch 8)
-  hipLaunchKernelGGL(raft_motion_encoder_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+  if (W2 % 32 == 0 && ((uintptr_t)pyr & 15) == 0)
+    hipLaunchKernelGGL((raft_motion_encoder_kernel<4, true>), dim3((unsigned)blocks), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL((raft_motion_encoder_kernel<4, false>), dim3((unsigned)blocks), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }

@@ -100,6 +100,12 @@ class RaftStereo : public StereoEngine {
   Tensor qx_[3];
   int gru_split_mode_ = std::getenv("SA_RAFT_GRU_SPLIT") ? std::atoi(std::getenv("SA_RAFT_GRU_SPLIT")) : -1;
   bool gru_split_ = false;
+  // Pipeline mode 2 layout: motion encoder on the main stream and the finest interp on side2 (default), or round 3's
+  // layout with the motion encoder on a third stream (SA_RAFT_M2_MAIN=0).  Measured and dropped in round 4: the
+  // finest ZRQ conv split by input source into three convs so that only the motion third stays on the chain -- each
+  // batch-1 conv carries ~11 us of fixed cost (prologue, epilogue, launch) and the parts were ~3x less efficient per
+  // K step, so the frame got slower, serial schedule included (profiles/round4_notes.md).
+  bool m2_main_ = !(std::getenv("SA_RAFT_M2_MAIN") && std::getenv("SA_RAFT_M2_MAIN")[0] == '0');
   ConvLayer fh1_, fh1mask_, mask2_;
   Tensor corr_feat_, flow_feat_, cor1_, flo1_, corflo_, motion_;
   Tensor z_[3], rh_[3];
@@ -607,6 +613,32 @@ void RaftStereo::forward(hipStream_t s) {
       }
     }
     wait(s, 1);
+  } else if (pipe && pmode == 2 && m2_main_) {
+    // Mode 2, chain on one stream.  The batch-1 critical chain is q(t-1) -> FH(t-1) -> M(t) -> G08 z/r(t) -> q(t);
+    // the coarse levels and the finest interp run beside it.  Per iteration t:
+    //   side2: G32(t); G16(t) once q(t-1) is done; interp(t)           (event 0)
+    //   main : M(t); G08(t) once side2's interp(t) is done; FH(t)      (event 4 after the q conv)
+    // With M on the main stream the chain carries no cross-stream edge of its own (round 3's layout put M on a third
+    // stream: two event edges per iteration, ~12 us each on the timeline, and the interp on the chain); side2 ends
+    // before M does, so the one join (event 0) is normally already signalled when main reaches it.
+    rec(s, 4);
+    wait(side2_, 4);  // the first G32 reads the encoders' hidden states / context
+    for (int it = 0; it < rc_.iters; ++it) {
+      const bool last = it == rc_.iters - 1;
+      {
+        ScopedSplitK k2(&splitk_side2_);
+        gru32(side2_);
+        wait(side2_, 4);
+        gru16(side2_);
+        interp(side2_, 0);
+        rec(side2_, 0);
+      }
+      motion(s);
+      wait(s, 0);
+      gru(s, 0, {motion_, interp_[0]});
+      rec(s, 4);
+      head(s, last);
+    }
   } else if (pipe && pmode == 2) {
     // Deeper cross-iteration pipeline (sceneflow, every batch).  Per iteration t:
     //   side2: G32(t); then G16(t) once the finest q conv of t-1 is done (needs net0(t-1); the finest

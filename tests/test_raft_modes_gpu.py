@@ -19,9 +19,11 @@ MODES = [
     ("pipeline1", {"SA_RAFT_PIPELINE": "1"}),
     ("pipeline2", {"SA_RAFT_PIPELINE": "2"}),
     ("unfused-motion-encoder", {"SA_RAFT_PARALLEL": "0", "SA_RAFT_FUSE_MENC": "0"}),
+    # round 3's mode-2 layout (motion encoder on a third stream); the default runs it on the main stream
+    ("pipeline2-side-menc", {"SA_RAFT_PIPELINE": "2", "SA_RAFT_M2_MAIN": "0"}),
 ]
 TOL = {"unfused-motion-encoder": 1e-2}
-KNOBS = ("SA_RAFT_PARALLEL", "SA_RAFT_PIPELINE", "SA_RAFT_FUSE_MENC")
+KNOBS = ("SA_RAFT_PARALLEL", "SA_RAFT_PIPELINE", "SA_RAFT_FUSE_MENC", "SA_RAFT_M2_MAIN")
 
 
 RT_MODES = [
