@@ -86,9 +86,19 @@ enum : int {
                 // im2col tile) to ~21 KB (weights + 1/9 of the patch), below the per-CU LDS-DMA gather rate that
                 // bounds the im2col tiles (MI355X_MICROARCH.md 'Indexed rows: gather into LDS': 66-73 GB/s per CU)
   kHalo16 = 10,  // kHalo with 16 x 16 output patches (narrow images: the 1/8 and 1/16 GRU levels)
+  kHaloP = 11,   // kHalo with the input patch stored PLANAR in LDS: [8 planes of 8 channels][pixels][16 B], planes
+                 // 256-B aligned.  The 16 lanes of an A fragment read 16 consecutive pixels of one plane, which hit
+                 // 16 distinct 16-B bank slots at ANY start pixel, so a tap's shifted read needs no XOR swizzle: its
+                 // address is the lane's tap-0 address plus a wave-uniform offset.  kHalo's swizzled image costs
+                 // ~6 VALU per fragment address (3.7 VALU per MFMA on the b8 GRU conv, PMC) and 2-way conflicts
+                 // on odd tap shifts (SQ_LDS_BANK_CONFLICT above the LDS instruction count)
+  kHaloP16 = 12,  // kHaloP with 16 x 16 output patches
 };
 __host__ __device__ constexpr bool is_glds(int mode) { return mode == kGlds3 || mode == kGldsDeep; }
-__host__ __device__ constexpr bool is_halo(int mode) { return mode == kHalo || mode == kHalo16; }
+__host__ __device__ constexpr bool is_halop(int mode) { return mode == kHaloP || mode == kHaloP16; }
+__host__ __device__ constexpr bool is_halo(int mode) {
+  return mode == kHalo || mode == kHalo16 || is_halop(mode);
+}
 
 template <int BM, int BN, int WM, int WN, int MODE = kRegK32>
 struct ConvCfg {
@@ -114,9 +124,15 @@ struct ConvCfg {
   static constexpr int NSTAGE = MODE == kGlds3 || HALO ? 3 : MODE == kGldsDeep ? DEEP_NS : PING ? PING_NS : (WIDE ? 4 : 2);
   // kHalo: output patch TH x TW, input patch (TH+2) x (TW+2) pixels of 128 B (one 64-channel chunk) in 1-KB DMA
   // pieces of 8 pixels, HALO_NA pieces per wave; two patch buffers + a 3-deep ring of weight stages
-  static constexpr int TW = MODE == kHalo16 ? 16 : 32;
+  static constexpr int TW = (MODE == kHalo16 || MODE == kHaloP16) ? 16 : 32;
   static constexpr int HALO_PIX = (BM / TW + 2) * (TW + 2);
-  static constexpr int HALO_NA = HALO ? ((HALO_PIX + 7) / 8 + NW - 1) / NW : 1;
+  // kHaloP: plane length in pixels (a multiple of 16: planes start on 256-B boundaries); 8 planes of HALO_RPP 16-B
+  // slots fill HALO_RPP / 8 DMA instructions of 64 lanes
+  static constexpr bool HALOP = is_halop(MODE);
+  static constexpr int HALO_RPP = (HALO_PIX + 15) / 16 * 16;
+  static constexpr int HALO_NA = !HALO ? 1
+                                 : HALOP ? (HALO_RPP / 8 + NW - 1) / NW
+                                         : ((HALO_PIX + 7) / 8 + NW - 1) / NW;
   static constexpr int A_PATCH = HALO_NA * NW * 1024;
   static constexpr int STAGE_BYTES = HALO ? 2 * A_PATCH + NSTAGE * B_BYTES : NSTAGE * (A_BYTES + B_BYTES);
   // fp32 C tile, unpadded rows; columns XOR-swizzled in 16-float blocks (cswz) so the MFMA
@@ -379,15 +395,30 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
     const int nsteps = 9 * nchunk;
     int apix[NAH], alch[NAH];
     bool aok[NAH];
+    constexpr int RPP = C::HALO_RPP, APL = RPP * 16;  // kHaloP: plane length (pixels) and plane stride (bytes)
 #pragma unroll
     for (int i = 0; i < NAH; ++i) {
-      const int q = (wave * NAH + i) * 8 + (lane >> 3);
-      const int qy = q / PW, qx = q - qy * PW;
-      const int iy = halo_oy0 - 1 + qy, ix = halo_ox0 - 1 + qx;
-      aok[i] = q < RP && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
-      apix[i] = aok[i] ? (halo_img * p.H + iy) * p.W + ix : 0;
-      alch[i] = ((lane & 7) ^ ((q >> 1) & 7)) << 3;
+      if constexpr (C::HALOP) {
+        // DMA instruction (wave, i) fills the 64 LDS slots from 64 (wave * NAH + i): slot = plane * RPP + pixel;
+        // each lane loads its pixel's 8 channels of that plane
+        const int slot = (wave * NAH + i) * 64 + lane;
+        const int pl = slot / RPP, q = slot - pl * RPP;
+        const int qy = q / PW, qx = q - qy * PW;
+        const int iy = halo_oy0 - 1 + qy, ix = halo_ox0 - 1 + qx;
+        aok[i] = pl < 8 && q < RP && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+        apix[i] = aok[i] ? (halo_img * p.H + iy) * p.W + ix : 0;
+        alch[i] = pl << 3;
+      } else {
+        const int q = (wave * NAH + i) * 8 + (lane >> 3);
+        const int qy = q / PW, qx = q - qy * PW;
+        const int iy = halo_oy0 - 1 + qy, ix = halo_ox0 - 1 + qx;
+        aok[i] = q < RP && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+        apix[i] = aok[i] ? (halo_img * p.H + iy) * p.W + ix : 0;
+        alch[i] = ((lane & 7) ^ ((q >> 1) & 7)) << 3;
+      }
     }
+    static_assert(!C::HALOP || NAH * C::NW * 64 >= 8 * RPP, "kHaloP: the DMA instructions cover all 8 planes");
+    static_assert(!C::HALOP || (RPP % 16 == 0 && 4 * APL < 65536), "kHaloP: 256-B planes, immediate plane offsets");
     const int sb1 = p.src[0].channels;
     const int sb2 = sb1 + (p.nsrc > 1 ? p.src[1].channels : 0);
     const int sb3 = sb2 + (p.nsrc > 2 ? p.src[2].channels : 0);
@@ -437,18 +468,33 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
       const int r = wm * C::TM + i * 16 + frow;
       aq0[i] = (r / TW) * PW + (r % TW);
     }
+    // lane-constant parts of the fragment addresses.  B (swizzled rows): the row and chunk of (j, kk) never change,
+    // only the ring slot does.  kHaloP A: the tap-0 pixel of fragment i in plane (lane >> 4); a tap, a k-half and
+    // the chunk's patch buffer only add wave-uniform byte offsets.
+    int boff[C::FN][2], aoff[C::FM];
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int row = wn * C::TN + j * 16 + frow;
+        const int lc = (lane >> 4) + 4 * kk;
+        boff[j][kk] = row * 128 + ((lc ^ ((row >> 1) & 7)) << 4);
+      }
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i) aoff[i] = (lane >> 4) * APL + aq0[i] * 16;
     // fragment reads of k-half kk of step st (patch buffer of its chunk, tap offset, weight slot st % 3)
     auto frag_addr_a = [&](int st, int i, int kk) {
       const int c = st / 9, t = st - c * 9;
-      const int q = aq0[i] + (t / 3) * PW + (t - (t / 3) * 3);
-      const int lc = (lane >> 4) + 4 * kk;
-      return abuf0 + (c & 1) * APB + q * 128 + ((lc ^ ((q >> 1) & 7)) << 4);
+      if constexpr (C::HALOP) {
+        const int u = (c & 1) * APB + kk * 4 * APL + ((t / 3) * PW + (t - (t / 3) * 3)) * 16;  // wave-uniform
+        return abuf0 + aoff[i] + u;
+      } else {
+        const int q = aq0[i] + (t / 3) * PW + (t - (t / 3) * 3);
+        const int lc = (lane >> 4) + 4 * kk;
+        return abuf0 + (c & 1) * APB + q * 128 + ((lc ^ ((q >> 1) & 7)) << 4);
+      }
     };
-    auto frag_addr_b = [&](int st, int j, int kk) {
-      const int row = wn * C::TN + j * 16 + frow;
-      const int lc = (lane >> 4) + 4 * kk;
-      return bbuf0 + (st % 3) * BST + row * 128 + ((lc ^ ((row >> 1) & 7)) << 4);
-    };
+    auto frag_addr_b = [&](int st, int j, int kk) { return bbuf0 + (st % 3) * BST + boff[j][kk]; };
     auto read_half = [&](int st, int kk, half8* af, half8* bf) {
 #pragma unroll
       for (int i = 0; i < C::FM; ++i) af[i] = *reinterpret_cast<const half8*>(frag_addr_a(st, i, kk));
@@ -1915,9 +1961,13 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
       const int r = cfg == 10 ? launch_wide<256, 256, 2, 4>(a, stream) : launch_wide<512, 128, 4, 2>(a, stream);
       return r == 1 ? -5 : r;
     }
-    case 26: case 27: {
-      // halo-reuse 3x3 tiles: 8 x 32 (26) / 16 x 16 (27) output patches x 128 channels
-      const int r = cfg == 26 ? launch_halo<kHalo>(a, stream) : launch_halo<kHalo16>(a, stream);
+    case 26: case 27: case 28: case 29: {
+      // halo-reuse 3x3 tiles: 8 x 32 (26) / 16 x 16 (27) output patches x 128 channels; 28 / 29 the same with the
+      // planar patch image (kHaloP)
+      const int r = cfg == 26 ? launch_halo<kHalo>(a, stream)
+                  : cfg == 27 ? launch_halo<kHalo16>(a, stream)
+                  : cfg == 28 ? launch_halo<kHaloP>(a, stream)
+                              : launch_halo<kHaloP16>(a, stream);
       return r == 1 ? -5 : r;
     }
     case 18: case 19: {

@@ -743,6 +743,8 @@ constexpr Tactic kTactics[] = {
     {25, false, false, 0, 0, 0, 0, "strided 1x1"},
     {26, false, false, 0, 0, 0, 0, "3x3 halo patch 8x32"},
     {27, false, false, 0, 0, 0, 0, "3x3 halo patch 16x16"},
+    {28, false, false, 0, 0, 0, 0, "3x3 halo patch 8x32, planar image"},
+    {29, false, false, 0, 0, 0, 0, "3x3 halo patch 16x16, planar image"},
 };
 
 bool known_tactic(int cfg) {

@@ -573,7 +573,7 @@ def test_conv2d_gru_zrq_split(cfg, splitk):
     assert rel_err(nchw(net_h), ref) < 4e-3
 
 
-@pytest.mark.parametrize("cfg", [26, 27])
+@pytest.mark.parametrize("cfg", [26, 27, 28, 29])
 @pytest.mark.parametrize("srcs,cout,hw,n", [
     ((128, 256), 256, (120, 160), 1),   # RAFT 1/4 z/r (two sources, 2 n-tiles), patches tile the image exactly
     ((128,), 128, (60, 80), 2),          # 1/8 level: 8x32 patches overhang the right edge
@@ -599,7 +599,7 @@ def test_conv2d_halo_vs_torch(srcs, cout, hw, n, cfg):
         assert rel_err(nchw(out), ref) < 2e-3
 
 
-@pytest.mark.parametrize("cfg", [26, 27])
+@pytest.mark.parametrize("cfg", [26, 27, 28, 29])
 def test_conv2d_halo_gru_and_stats(cfg):
     """Halo tiles with the fused epilogues: the ZRQ / Q GRU pair and per-(image, channel) instance-norm statistics
     (patch rows map to image pixels, so the statistics must still be exact)."""
