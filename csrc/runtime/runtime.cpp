@@ -754,8 +754,11 @@ bool known_tactic(int cfg) {
 }
 
 bool tactic_applies(const Tactic& t, const SaConvArgs& a, long M) {
+  // SA_TUNE_MIN_TILES: the grid size below which the wide tiles are not timed (default 256 = one per CU)
+  const char* mt = std::getenv("SA_TUNE_MIN_TILES");  // read per shape (tuning is rare): in-process A/B knob
+  const long min_tiles = mt ? std::atol(mt) : 256L;
   if (a.Cout <= t.min_cout || (t.max_cout > 0 && a.Cout > t.max_cout)) return false;
-  if (t.tile_m > 0 && ((M + t.tile_m - 1) / t.tile_m) * ((a.Cout + t.tile_n - 1) / t.tile_n) < 256) return false;
+  if (t.tile_m > 0 && ((M + t.tile_m - 1) / t.tile_m) * ((a.Cout + t.tile_n - 1) / t.tile_n) < min_tiles) return false;
   return true;
 }
 

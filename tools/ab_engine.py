@@ -23,6 +23,8 @@ def main():
     p.add_argument("--batch", type=int, default=8)
     p.add_argument("--rounds", type=int, default=6)
     p.add_argument("--frames", type=int, default=5)
+    p.add_argument("--clear-plan", action="store_true",
+                   help="forget the in-process tactic plan before each engine (knobs that change what the tuner picks)")
     a = p.parse_args()
     import numpy as np
     import torch
@@ -34,6 +36,10 @@ def main():
     engines, outs = {}, {}
     for v in a.values.split(","):
         os.environ[a.knob] = v
+        if a.clear_plan:
+            os.environ["SA_PLAN_DIR"] = ""  # no plan files either: every engine tunes under its own knob value
+            from stereoalgorithms_amd import _native as N
+            N.require_native().sa_conv_plan_clear()
         e = NativeStereoEngine(a.model, None, 480, 640, batch=a.batch, seed=0)
         for _ in range(2):
             d = e.run(left, right)
