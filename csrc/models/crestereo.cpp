@@ -101,13 +101,10 @@ struct AttnLayer {
 struct Level {
   int h = 0, w = 0;
   Tensor net, xin, corr, cor1, corflo, flo1, flowfeat, z, rh, fh, mask, qx;
-  Tensor cst[2];  // per GRU direction: the constant context input's share of [z | r | q] pre-activations + biases
   float* flow = nullptr;
   void build(DeviceArena& a, int B, int h_, int w_) {
     h = h_;
     w = w_;
-    cst[0] = make_tensor(a, B, h, w, 384);
-    cst[1] = make_tensor(a, B, h, w, 384);
     net = make_tensor(a, B, h, w, 128);
     xin = make_tensor(a, B, h, w, 256);  // [inp 128 | motion 126 | flow 2]
     corr = make_tensor(a, B, h, w, 40);
@@ -151,7 +148,6 @@ class CreStereo : public StereoEngine {
   // conv on the recurrent chain reads r*h alone (K = 5 x 128 instead of 5 x 384); b1 iter10 network 6.86 -> 6.58 ms.
   // On for batch <= 2 (the hoisted columns cost +11 % MACs, a throughput loss at large batch); SA_CRE_GRU_SPLIT=0/1.
   ConvLayer zrq_[2], qh_[2];
-  ConvLayer cst_[2];  // the constant context input's share of each direction's [z | r | q] (+ biases), per level
   bool par_ = !(std::getenv("SA_CRE_PARALLEL") && std::getenv("SA_CRE_PARALLEL")[0] == '0');
   int gru_split_mode_ = std::getenv("SA_CRE_GRU_SPLIT") ? std::atoi(std::getenv("SA_CRE_GRU_SPLIT")) : -1;
   bool gru_split_ = false;
@@ -221,48 +217,31 @@ void CreStereo::build(WeightSource& src) {
   convf1_.build(a, ws, {u + "encoder.convf1"}, {{2, 8}}, s3);
   convf2_.build(a, ws, {u + "encoder.convf2"}, {{128, 128}}, s3);
   mconv_.build(a, ws, {u + "encoder.conv"}, {{256, 256}}, s3);
-  // SepConvGRU convs over [h | x] with x = [inp 128 | motion 126 | flow 2] (input channels 0:128 | 128:256 |
-  // 256:384).  inp (the context features) is the same on every iteration of a level, so its share of every gate's
-  // pre-activation -- plus the biases -- is computed once per level and frame (cst_: Level::cst, added through the
-  // GRU epilogues' context input); the per-iteration convs run over [h | motion, flow] only (K 5 x 256 instead of
-  // 5 x 384).  Same sums, regrouped; the constant share is rounded to fp16 once.
-  const int taps = 5;
-  auto slice = [&](const std::string& name, std::vector<std::pair<int, int>> ranges, bool bias, bool zero_h,
-                   const std::string& tag) {
-    const HostTensor& w = ws.get(name + ".weight");
-    int ci = 0;
-    for (auto& r : ranges) ci += r.second - r.first;
-    HostTensor o;
-    o.shape = {128, ci, w.shape[2], w.shape[3]};
-    o.data.assign((size_t)128 * ci * taps, 0.f);
-    for (int oc = 0; oc < 128; ++oc) {
-      int c2 = 0;
-      for (auto& r : ranges)
-        for (int c = r.first; c < r.second; ++c, ++c2)
-          for (int t = 0; t < taps; ++t)
-            o.data[((size_t)oc * ci + c2) * taps + t] = (zero_h && c < 128) ? 0.f : w.data[((size_t)oc * 384 + c) * taps + t];
-    }
-    src.ws->put(name + tag + ".weight", std::move(o));
-    if (bias) src.ws->put(name + tag + ".bias", ws.get(name + ".bias"));
-  };
   for (int d = 0; d < 2; ++d) {
     const std::string sfx = d == 0 ? "1" : "2";
     for (const char* g : {"convz", "convr", "convq"})
       src.conv(u + "gru." + g + sfx, 128, 384, d == 0 ? 1 : 5, d == 0 ? 5 : 1);
     ConvSpec sp;  // (1,5) pad (0,2) / (5,1) pad (2,0)
-    const std::string zn = u + "gru.convz" + sfx, rn = u + "gru.convr" + sfx, qn = u + "gru.convq" + sfx;
-    for (const std::string& n : {zn, rn, qn}) {
-      slice(n, {{128, 256}}, true, false, "#inp");
-      slice(n, {{0, 128}, {256, 384}}, false, false, "#hm");
-    }
-    cst_[d].build(a, ws, {zn + "#inp", rn + "#inp", qn + "#inp"}, {{128, 128}}, sp);
-    zr_[d].build(a, ws, {zn + "#hm", rn + "#hm"}, {{128, 128}, {128, 128}}, sp);
-    q_[d].build(a, ws, {qn + "#hm"}, {{128, 128}, {128, 128}}, sp);
+    zr_[d].build(a, ws, {u + "gru.convz" + sfx, u + "gru.convr" + sfx}, {{128, 128}, {256, 256}}, sp);
+    q_[d].build(a, ws, {u + "gru.convq" + sfx}, {{128, 128}, {256, 256}}, sp);
     if (gru_split_) {
-      // convq over [h | motion, flow] -> x part (h taps zeroed, in the z/r conv) and h part [128][128] (over r*h)
-      slice(qn, {{0, 128}, {256, 384}}, false, true, "@x#hm");
-      slice(qn, {{0, 128}}, false, false, "@h");
-      zrq_[d].build(a, ws, {zn + "#hm", rn + "#hm", qn + "@x#hm"}, {{128, 128}, {128, 128}}, sp);
+      // convq [128][384][kh][kw] -> x half (h taps zeroed, bias kept) and h half [128][128][kh][kw] (no bias)
+      const std::string qn = u + "gru.convq" + sfx;
+      const HostTensor& wq = ws.get(qn + ".weight");
+      const int taps = 5;
+      HostTensor qxw = wq, qhw;
+      qhw.shape = {128, 128, wq.shape[2], wq.shape[3]};
+      qhw.data.resize((size_t)128 * 128 * taps);
+      for (int o = 0; o < 128; ++o)
+        for (int c = 0; c < 128; ++c)
+          for (int t = 0; t < taps; ++t) {
+            qhw.data[((size_t)o * 128 + c) * taps + t] = wq.data[((size_t)o * 384 + c) * taps + t];
+            qxw.data[((size_t)o * 384 + c) * taps + t] = 0.f;
+          }
+      src.ws->put(qn + "@x.weight", std::move(qxw));
+      src.ws->put(qn + "@x.bias", ws.get(qn + ".bias"));
+      src.ws->put(qn + "@h.weight", std::move(qhw));
+      zrq_[d].build(a, ws, {u + "gru.convz" + sfx, u + "gru.convr" + sfx, qn + "@x"}, {{128, 128}, {256, 256}}, sp);
       qh_[d].build(a, ws, {qn + "@h"}, {{128, 128}}, sp);
     }
   }
@@ -320,7 +299,7 @@ void CreStereo::update(hipStream_t s, Level& L, const Tensor& f1, const Tensor& 
   ag.out_channels = 36;  // channels 36..39 of the 40-channel pixel were zeroed at build and nothing writes them
   // motion encoder -> xin[128:254].  Its flow branch (flow features -> convf1 -> convf2) and correlation branch
   // (AGCL -> convc1 -> convc2) are independent until the final conv: the flow branch runs on the side stream
-  // (SA_CRE_PARALLEL=0: one stream)
+  // (SA_CRE_PARALLEL=0: one stream; iter10 b1 6.45 -> 6.15 ms, profiles/round4_notes.md)
   const bool par = par_ && !tuning_pass_;
   const long P = (long)B * L.h * L.w;
   {
@@ -338,12 +317,9 @@ void CreStereo::update(hipStream_t s, Level& L, const Tensor& f1, const Tensor& 
   if (par) join(s);
   mconv_.run(s, {L.corflo}, L.xin.slice_c(128, 126), SA_ACT_RELU);
   // SepConvGRU: horizontal then vertical; z/r and q gates fused into the conv epilogues
-  const Tensor xmf = L.xin.slice_c(128, 128);  // [motion 126 | flow 2]; inp's share is in L.cst
   for (int d = 0; d < 2 && gru_split_; ++d) {
-    SaConvArgs za = zrq_[d].args({L.net, xmf}, L.qx);
+    SaConvArgs za = zrq_[d].args({L.net, L.xin}, L.qx);
     za.epi = SA_EPI_GRU_ZRQ;
-    za.ctx = L.cst[d].ptr;
-    za.ctx_stride = L.cst[d].stride;
     za.aux = L.z.ptr;
     za.aux_stride = L.z.stride;
     za.hbuf = L.net.ptr;
@@ -362,10 +338,8 @@ void CreStereo::update(hipStream_t s, Level& L, const Tensor& f1, const Tensor& 
     qh_[d].launch(s, qa);
   }
   for (int d = 0; d < 2 && !gru_split_; ++d) {
-    SaConvArgs za = zr_[d].args({L.net, xmf}, L.z);
+    SaConvArgs za = zr_[d].args({L.net, L.xin}, L.z);
     za.epi = SA_EPI_GRU_ZR;
-    za.ctx = L.cst[d].ptr;
-    za.ctx_stride = L.cst[d].stride;
     za.aux = L.z.ptr;
     za.aux_stride = L.z.stride;
     za.hbuf = L.net.ptr;
@@ -373,10 +347,8 @@ void CreStereo::update(hipStream_t s, Level& L, const Tensor& f1, const Tensor& 
     za.rh = L.rh.ptr;
     za.rh_stride = L.rh.stride;
     zr_[d].launch(s, za);
-    SaConvArgs qa = q_[d].args({L.rh, xmf}, L.net);
+    SaConvArgs qa = q_[d].args({L.rh, L.xin}, L.net);
     qa.epi = SA_EPI_GRU_Q;
-    qa.ctx = L.cst[d].slice_c(256, 128).ptr;
-    qa.ctx_stride = L.cst[d].stride;
     qa.aux = L.z.ptr;
     qa.aux_stride = L.z.stride;
     qa.hbuf = L.net.ptr;
@@ -427,9 +399,6 @@ void CreStereo::forward(hipStream_t s) {
     check(sa_avgpool_k(L4.net.ptr, L4.net.stride, lv_[l].net.ptr, lv_[l].net.stride, B, h4, w4, 128, k, s), "pool");
     check(sa_avgpool_k(L4.xin.ptr, L4.xin.stride, lv_[l].xin.ptr, lv_[l].xin.stride, B, h4, w4, 128, k, s), "pool");
   }
-  // the context input's constant share of the GRU pre-activations, once per level and direction
-  for (int l = 0; l < 3; ++l)
-    for (int d = 0; d < 2; ++d) cst_[d].run(s, {lv_[l].xin.slice_c(0, 128)}, lv_[l].cst[d]);
   // 1/16 tokens: pooled features + position encoding -> self attention (both images batched) ->
   // cross attention (left attends to right, then right to the updated left)
   {

@@ -512,10 +512,10 @@ void RaftStereo::forward(hipStream_t s) {
     }
   };
   // motion encoder: lookup -> convc1/convf1 -> convc2/convf2 -> conv (+ [flow, 0] tail)
-  // auto: fused once the frame has >= 128 of its 8x16 tiles (one workgroup each); the realtime preset's 1/8
-  // grid at batch 1 (40 tiles) runs the wider unfused kernels slightly faster (2.39 vs 2.41 ms)
-  const long menc_tiles = (long)Bn * ((h0 + 7) / 8) * ((w0 + 15) / 16);
-  const bool menc = fuse_motion_ && fuse_menc_ && (fuse_menc_mode_ >= 0 ? fuse_menc_mode_ != 0 : menc_tiles >= 128);
+  // fused by default at every size: round 3 measured the realtime preset's 1/8 grid at batch 1 (40 tiles) a little
+  // faster unfused (2.39 vs 2.41 ms); with round 4's motion-encoder kernel the fused path wins there too (1.961 ->
+  // 1.838 ms network, tools/ab_engine.py, profiles/round4_notes.md)
+  const bool menc = fuse_motion_ && fuse_menc_ && (fuse_menc_mode_ >= 0 ? fuse_menc_mode_ != 0 : true);
   auto motion = [&](hipStream_t ms) {
     if (menc) {
       const SaConvArgs c2 = convc2_.args({cor1_}, corflo_.slice_c(0, 64));
