@@ -368,6 +368,22 @@ def main(argv=None) -> int:
                 ts.append((time.perf_counter() - t1) * 1e3)
             ts = np.array(ts)
             host_split = e1.host_times()  # last frame: input copies / enqueue / device wait + output copies
+            # same timed region with the engine's pinned I/O buffers (host_buffers(): the camera writes its frame
+            # there, the caller reads disparity + cloud there): H2D from pinned memory, and the frame graph's
+            # reprojection writes both outputs to host memory itself, so no D2H copy and no pageable staging
+            hb = e1.host_buffers()
+            hb["left"][...] = l1
+            hb["right"][...] = r1
+            for _ in range(3):
+                e1.run_host(hb["left"], hb["right"], cloud=True, out=hb["disp"], cloud_out=hb["cloud"])
+            tp = []
+            for _ in range(args.latency_frames):
+                t1 = time.perf_counter()
+                e1.run_host(hb["left"], hb["right"], cloud=True, out=hb["disp"], cloud_out=hb["cloud"])
+                tp.append((time.perf_counter() - t1) * 1e3)
+            tp = np.array(tp)
+            pinned_ok = bool(np.array_equal(hb["disp"], d_out) and np.array_equal(hb["cloud"], c_out, equal_nan=True))
+            hb = None
             dev_b1 = e1.device_bytes
             e1.close()
             # per-stage device times from a second engine with stamps in its graph (tactic plan cached)
@@ -383,6 +399,9 @@ def main(argv=None) -> int:
                              "fps_b1": round(1000.0 / float(ts.mean()), 2),
                              "baseline_ms_rtx3090": base,
                              "speedup_vs_baseline": round(base / float(ts.mean()), 3) if base else None,
+                             "latency_ms_pinned_io_mean": round(float(tp.mean()), 3),
+                             "latency_ms_pinned_io_p99": round(float(np.percentile(tp, 99)), 3),
+                             "pinned_io_matches": pinned_ok,
                              "device_bytes": dev_b1,
                              "host_split_ms_last_frame": host_split,
                              "weights": "scale_init (parity-tested graph)" if wpath else "seeded default init",

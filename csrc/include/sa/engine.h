@@ -144,8 +144,9 @@ class StereoEngine {
   // stage boundary on the frame's main stream (no-op unless stage timing is on)
   void stage(hipStream_t s, const char* name);
 
-  void frame(hipStream_t s, bool rectify);  // the captured body
-  void launch_frame(hipStream_t s, bool rectify);
+  // the captured body; host_out: the reprojection writes the disparity and the cloud straight into pin_out_
+  void frame(hipStream_t s, bool rectify, bool host_out = false);
+  void launch_frame(hipStream_t s, bool rectify, bool host_out = false);
 
   EngineConfig cfg_;
   DeviceArena arena_;
@@ -161,7 +162,8 @@ class StereoEngine {
   float* rect_maps_ = nullptr;  // [2][H][W][2]
   float Q_[16];
   bool have_Q_ = false;
-  GraphExec graph_[2];  // [no rectify, rectify]
+  GraphExec graph_[4];  // [rectify + 2 * host_out]: host_out graphs reproject straight into the pinned outputs
+  float* pin_out_dev_ = nullptr;  // device address of pin_out_ (kernels write the zero-copy outputs through it)
   std::string default_plan_path() const;
   std::string plan_path_;
   long tuned_shapes_ = 0;

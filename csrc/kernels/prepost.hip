@@ -92,29 +92,58 @@ struct Q16 {
   float q[16];
 };
 
-__global__ void reproject_kernel(const float* __restrict__ din, int dstride, float sign,
-                                 const uint8_t* __restrict__ left, int B, int H, int W, Q16 Q,
-                                 float* __restrict__ dout, float* __restrict__ cloud) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * H * W) return;
-  const int pix = i % (H * W);
-  const int r = pix / W, c = pix - (pix / W) * W;
-  const float d = sign * din[(long)i * dstride];
-  if (dout) dout[i] = d;
-  if (!cloud) return;
-  const float* q = Q.q;
-  const float X = q[0] * c + q[1] * r + q[2] * d + q[3];
-  const float Y = q[4] * c + q[5] * r + q[6] * d + q[7];
-  const float Z = q[8] * c + q[9] * r + q[10] * d + q[11];
-  const float Wh = q[12] * c + q[13] * r + q[14] * d + q[15];
-  float* o = cloud + (long)i * 6;
-  o[0] = X / Wh;
-  o[1] = Y / Wh;
-  o[2] = Z / Wh;
-  const uint8_t* px = left + (long)i * 3;
-  o[3] = (float)px[2];
-  o[4] = (float)px[1];
-  o[5] = (float)px[0];
+// One thread per pixel computes its XYZRGB; the workgroup's 256 x 6 floats are staged in LDS and leave as
+// contiguous 16-B stores (the cloud and the disparity copy may live in pinned host memory: the engine's zero-copy
+// run_host path writes them straight over PCIe, where 4-B stores with a 24-B stride would cost a bus transaction
+// each).
+__global__ __launch_bounds__(256) void reproject_kernel(const float* __restrict__ din, int dstride, float sign,
+                                                        const uint8_t* __restrict__ left, int B, int H, int W, Q16 Q,
+                                                        float* __restrict__ dout, float* __restrict__ cloud) {
+  __shared__ __attribute__((aligned(16))) float st[256 * 6];
+  __shared__ __attribute__((aligned(16))) float sd[256];
+  const int total = B * H * W;
+  const long base = (long)blockIdx.x * 256;
+  const int i = (int)base + threadIdx.x;
+  const bool ok = i < total;
+  float d = 0.f;
+  if (ok) {
+    const int pix = i % (H * W);
+    const int r = pix / W, c = pix - (pix / W) * W;
+    d = sign * din[(long)i * dstride];
+    const float* q = Q.q;
+    const float X = q[0] * c + q[1] * r + q[2] * d + q[3];
+    const float Y = q[4] * c + q[5] * r + q[6] * d + q[7];
+    const float Z = q[8] * c + q[9] * r + q[10] * d + q[11];
+    const float Wh = q[12] * c + q[13] * r + q[14] * d + q[15];
+    float* o = st + threadIdx.x * 6;
+    o[0] = X / Wh;
+    o[1] = Y / Wh;
+    o[2] = Z / Wh;
+    const uint8_t* px = left + (long)i * 3;
+    o[3] = (float)px[2];
+    o[4] = (float)px[1];
+    o[5] = (float)px[0];
+  }
+  sd[threadIdx.x] = d;
+  __syncthreads();
+  const int n = total - (int)base < 256 ? total - (int)base : 256;  // pixels of this workgroup
+  if (cloud) {
+    float* cb = cloud + base * 6;
+    if (n == 256 && (((uintptr_t)cb) & 15) == 0) {
+      for (int k = threadIdx.x; k < 384; k += 256)
+        reinterpret_cast<float4*>(cb)[k] = reinterpret_cast<const float4*>(st)[k];
+    } else {
+      for (int k = threadIdx.x; k < n * 6; k += 256) cb[k] = st[k];
+    }
+  }
+  if (dout) {
+    float* db = dout + base;
+    if (n == 256 && (((uintptr_t)db) & 15) == 0) {
+      if (threadIdx.x < 64) reinterpret_cast<float4*>(db)[threadIdx.x] = reinterpret_cast<const float4*>(sd)[threadIdx.x];
+    } else if (threadIdx.x < n) {
+      db[threadIdx.x] = sd[threadIdx.x];
+    }
+  }
 }
 
 __global__ void convex_upsample_kernel(const f16* __restrict__ mask, int mstride,

@@ -79,8 +79,7 @@ StereoEngine::StereoEngine(const EngineConfig& cfg) : cfg_(cfg) {
 }
 
 StereoEngine::~StereoEngine() {
-  graph_[0].reset();
-  graph_[1].reset();
+  for (GraphExec& g : graph_) g.reset();
   copy_pool_.reset();
   for (auto& e : ev_copy_)
     if (e) (void)hipEventDestroy(e);
@@ -166,6 +165,7 @@ void StereoEngine::init() {
   cloud_ = (float*)arena_.alloc((size_t)B() * H() * W() * 6 * 4);
   HIP_CHECK(hipHostMalloc((void**)&pin_in_, 2 * img, hipHostMallocDefault));
   HIP_CHECK(hipHostMalloc((void**)&pin_out_, (size_t)B() * H() * W() * 7 * 4 + 2 * img, hipHostMallocDefault));
+  HIP_CHECK(hipHostGetDevicePointer((void**)&pin_out_dev_, pin_out_, 0));
   for (auto& e : ev_copy_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   if (const char* ht = std::getenv("SA_HOST_TIMES"))
     if (ht[0] == '1')
@@ -295,8 +295,7 @@ void StereoEngine::wait(hipStream_t s, int i) { HIP_CHECK(hipStreamWaitEvent(s, 
 void StereoEngine::set_Q(const float* q16) {
   std::memcpy(Q_, q16, sizeof(Q_));
   have_Q_ = true;
-  graph_[0].reset();  // Q is baked into the reprojection launch
-  graph_[1].reset();
+  for (GraphExec& g : graph_) g.reset();  // Q is baked into the reprojection launch
 }
 
 void StereoEngine::set_rectify_maps(const float* ml, const float* mr) {
@@ -357,7 +356,7 @@ std::vector<std::pair<std::string, float>> StereoEngine::stage_times() const {
   return out;
 }
 
-void StereoEngine::frame(hipStream_t s, bool rectify) {
+void StereoEngine::frame(hipStream_t s, bool rectify, bool host_out) {
   ScopedSplitK sk(&splitk_);
   nstage_ = 0;
   stage(s, "start");
@@ -373,15 +372,18 @@ void StereoEngine::frame(hipStream_t s, bool rectify) {
   forward(s);
   stage(s, "network");
   if (have_Q_) {
-    int rc = sa_reproject(disp_, 1, 1.f, in_left_, B(), H(), W(), Q_, nullptr, cloud_, s);
+    // host_out: disparity and cloud go straight into the pinned outputs (zero-copy run_host), no D2H copy
+    const size_t n = (size_t)B() * H() * W();
+    int rc = host_out ? sa_reproject(disp_, 1, 1.f, in_left_, B(), H(), W(), Q_, pin_out_dev_, pin_out_dev_ + n, s)
+                      : sa_reproject(disp_, 1, 1.f, in_left_, B(), H(), W(), Q_, nullptr, cloud_, s);
     SA_REQUIRE(rc == 0, "reproject failed");
     stage(s, "reproject");
   }
   SA_LAUNCH_CHECK(s);
 }
 
-void StereoEngine::launch_frame(hipStream_t s, bool rectify) {
-  GraphExec& g = graph_[rectify ? 1 : 0];
+void StereoEngine::launch_frame(hipStream_t s, bool rectify, bool host_out) {
+  GraphExec& g = graph_[(rectify ? 1 : 0) + (host_out ? 2 : 0)];
   // The frame always executes on the engine's own stream (where its graphs were captured); a
   // caller stream is ordered against it with events on both sides, so graph execs are never
   // replayed on a foreign (e.g. the legacy null) stream.
@@ -392,10 +394,10 @@ void StereoEngine::launch_frame(hipStream_t s, bool rectify) {
   }
   TraceRange tr("frame");
   if (cfg_.use_graph) {
-    if (!g.ready()) g.capture(stream_, [&] { frame(stream_, rectify); });
+    if (!g.ready()) g.capture(stream_, [&] { frame(stream_, rectify, host_out); });
     g.launch(stream_);
   } else {
-    frame(stream_, rectify);
+    frame(stream_, rectify, host_out);
   }
   static const bool sync_frame = [] {
     const char* v = std::getenv("SA_SYNC_FRAME");
@@ -454,7 +456,10 @@ void StereoEngine::run_host(uint8_t* left, uint8_t* right, float* disp, float* c
   HIP_CHECK(hipMemcpyAsync(dl, pin_in_, img, hipMemcpyHostToDevice, s));
   HIP_CHECK(hipMemcpyAsync(dr, pin_in_ + img, img, hipMemcpyHostToDevice, s));
   if (host_ev_[1]) HIP_CHECK(hipEventRecord(host_ev_[1], s));
-  launch_frame(s, rectify);
+  // zero-copy outputs: the caller reads the engine's pinned buffers (host_buffers()), so the frame graph's
+  // reprojection writes disparity and cloud there directly over PCIe and no D2H copy follows
+  const bool zero_copy = have_Q_ && disp == pin_out_ && cloud == pin_out_ + n;
+  launch_frame(s, rectify, zero_copy);
   if (host_ev_[2]) HIP_CHECK(hipEventRecord(host_ev_[2], s));
   float* pd = pin_out_;
   float* pc = pin_out_ + n;
@@ -470,8 +475,8 @@ void StereoEngine::run_host(uint8_t* left, uint8_t* right, float* disp, float* c
     out.push_back({dst, pinned, bytes, ev_copy_[ev]});
     ++ev;
   };
-  if (disp) d2h(disp, pd, disp_, n * 4);
-  if (cloud && have_Q_) {
+  if (disp && !zero_copy) d2h(disp, pd, disp_, n * 4);
+  if (cloud && have_Q_ && !zero_copy) {
     constexpr int kChunks = kCopyEvents - 3;
     const size_t total = n * 24, step = (total / kChunks + 4095) & ~(size_t)4095;
     for (size_t o = 0; o < total; o += step) {
@@ -488,7 +493,19 @@ void StereoEngine::run_host(uint8_t* left, uint8_t* right, float* disp, float* c
   if (host_ev_[3]) HIP_CHECK(hipEventRecord(host_ev_[3], s));
   const auto t2 = clk::now();
   copy_pool_->run(out);
-  HIP_CHECK(hipStreamSynchronize(s));
+  // SA_HOST_SPIN=1: poll the stream instead of the blocking wait (no wake-up latency; burns the calling core)
+  static const bool spin = [] {
+    const char* e = std::getenv("SA_HOST_SPIN");
+    return e && e[0] == '1';
+  }();
+  if (spin) {
+    hipError_t q;
+    while ((q = hipStreamQuery(s)) == hipErrorNotReady) {
+    }
+    HIP_CHECK(q);
+  } else {
+    HIP_CHECK(hipStreamSynchronize(s));
+  }
   const auto t3 = clk::now();
   auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<float, std::milli>(b - a).count(); };
   host_times_[0] = ms(t0, t3);  // whole timed region

@@ -68,6 +68,15 @@ def test_engine_cloud_and_rectify_roundtrip():
     # host path (reference timed region) agrees with the device path
     dh, ch, _, _ = eng.run_host(left.cpu().numpy(), right.cpu().numpy(), cloud=True)
     assert np.allclose(dh, d0.cpu().numpy(), atol=1e-5)
+    # zero-copy host path: the engine's pinned buffers in and out, the reprojection writes them over PCIe
+    hb = eng.host_buffers()
+    hb["left"][...] = left.cpu().numpy()
+    hb["right"][...] = right.cpu().numpy()
+    hb["disp"][...] = -1.0
+    hb["cloud"][...] = -1.0
+    eng.run_host(hb["left"], hb["right"], cloud=True, out=hb["disp"], cloud_out=hb["cloud"])
+    assert np.array_equal(hb["disp"], dh)
+    assert np.array_equal(hb["cloud"], ch, equal_nan=True)
 
 
 @pytest.mark.parametrize("graph", [True, False])
