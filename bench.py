@@ -251,10 +251,14 @@ def main(argv=None) -> int:
         torch.cuda.set_stream(eng.main_stream)
         h2d = H2DPrefetcher([left_h, right_h], dev, stream=eng.copy_stream)
 
+        h2d.prefetch([left_h, right_h])
+
         def step():
-            # every step copies its inputs H2D (copy stream, double-buffered: overlaps the previous step's
-            # frame graph); the all-gather of step t (RCCL's own stream) overlaps step t+1's frame graph
-            left, right = h2d.load([left_h, right_h])
+            # every step copies its inputs H2D on the copy stream, issued one step ahead (the copies of step t+1
+            # are enqueued before step t, so they run under step t's frame graph, see H2DPrefetcher); the
+            # all-gather of step t (RCCL's own stream) overlaps step t+1's frame graph
+            h2d.prefetch([left_h, right_h])
+            left, right = h2d.next()
             return dp.step_async(left, right)
 
         def sync():

@@ -188,19 +188,24 @@ def gather_clouds_to_rank0(cloud: torch.Tensor, world: int, rank: int):
 
 
 class H2DPrefetcher:
-    """Double-buffered host->device input staging on a copy stream.
+    """Multi-buffered host->device input staging on a copy stream.
 
-    ``load(host_tensors)`` enqueues the pinned-host -> device copies of the next step on a side stream
-    (the copy engine) and makes the current stream wait for them, so the inputs of step t+1 travel over
-    PCIe while step t's frame graph still runs.  A slot is only overwritten once the compute stream has
-    passed the step that read it (event recorded by the next ``load``).  Every step still copies its
-    own inputs; only the overlap changes.
+    ``prefetch(host_tensors)`` enqueues the pinned-host -> device copies of a FUTURE step on a side stream (the
+    copy engine); ``next()`` hands out the oldest prefetched slot and makes the current stream wait for its copies.
+    A slot is only overwritten once the compute stream has passed the step that read it (event recorded by the
+    following ``next``).  Every step still copies its own inputs; only the overlap changes.
+
+    Issue order matters on this hardware: streams share the GPU_MAX_HW_QUEUES = 4 hardware queues, and a copy's
+    stream-ordering barrier sits in its queue behind whatever was enqueued there before it.  Copied "just in time"
+    (``load``: copy step t, then run step t), the copy of step t lands behind the previous step's all-gather, which
+    waits for the previous frame, and frame t then waits for the copy: the copy runs between frames.  Prefetched one
+    step ahead (``prefetch`` of step t+1 BEFORE step t is enqueued; 3 slots), the copy only waits for the frame two
+    steps back and runs under the current one (profiles/dp_overlap_r04.txt).
     """
 
-    def __init__(self, host_tensors, device, slots: int = 2, stream=None):
+    def __init__(self, host_tensors, device, slots: int = 3, stream=None):
         """``stream``: the copy stream to use (e.g. ``NativeStereoEngine.copy_stream``, so the data-parallel step
-        adds no stream of its own: engine + its side stream + caller + RCCL stay within 4 hardware queues);
-        default a new stream."""
+        adds no stream of its own); default a new stream."""
         self.device = torch.device(device)
         self.stream = stream if stream is not None else torch.cuda.Stream(self.device)
         self.slots = slots
@@ -210,24 +215,42 @@ class H2DPrefetcher:
         # stream (without this, a recycled block can be overwritten under a not-yet-run read).
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         self.freed = [None] * slots  # compute-stream event after the step that consumed the slot
-        self._i = 0
+        self.ready = [None] * slots  # copy-stream event after the slot's copies
+        self._issued = 0  # slots handed to prefetch so far
+        self._taken = 0  # slots handed out by next so far
         self._last = None
 
-    def load(self, host_tensors):
-        cs = torch.cuda.current_stream(self.device)
-        if self._last is not None:  # the previous slot is consumed by everything queued so far
-            ev = torch.cuda.Event()
-            ev.record(cs)
-            self.freed[self._last] = ev
-        slot = self._i % self.slots
-        self._i += 1
+    def prefetch(self, host_tensors):
+        """Enqueue the copies of a future step (at most ``slots - 1`` ahead of the consumer)."""
+        if self._issued - self._taken >= self.slots - 1:
+            raise RuntimeError("H2DPrefetcher: prefetch queue full (call next() first)")
+        slot = self._issued % self.slots
+        self._issued += 1
         with torch.cuda.stream(self.stream):
             if self.freed[slot] is not None:
                 self.stream.wait_event(self.freed[slot])
             for d, h in zip(self.bufs[slot], host_tensors):
                 d.copy_(h, non_blocking=True)
-            ready = torch.cuda.Event()
-            ready.record(self.stream)
-        cs.wait_event(ready)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+            self.ready[slot] = ev
+
+    def next(self):
+        """Device buffers of the oldest prefetched step, ordered before the current stream's next work."""
+        if self._taken >= self._issued:
+            raise RuntimeError("H2DPrefetcher: next() without a prefetched step")
+        cs = torch.cuda.current_stream(self.device)
+        if self._last is not None:  # the previous slot is consumed by everything queued so far
+            ev = torch.cuda.Event()
+            ev.record(cs)
+            self.freed[self._last] = ev
+        slot = self._taken % self.slots
+        self._taken += 1
+        cs.wait_event(self.ready[slot])
         self._last = slot
         return self.bufs[slot]
+
+    def load(self, host_tensors):
+        """Just-in-time form: copy this step's inputs and hand them out."""
+        self.prefetch(host_tensors)
+        return self.next()

@@ -21,6 +21,30 @@ def test_h2d_prefetcher_slots_and_ordering():
 
 
 @pytest.mark.gpu
+def test_h2d_prefetcher_issue_ahead():
+    """bench.py's form: the copies of step i+1 are enqueued before step i runs; every step sees its own data and
+    no slot is overwritten under a pending read (3 slots, at most 2 steps in flight)."""
+    dev = torch.device("cuda", 0)
+    n = 7
+    hosts = [torch.full((1 << 22,), i, dtype=torch.uint8).pin_memory() for i in range(n + 1)]
+    pf = H2DPrefetcher([hosts[0]], dev)
+    pf.prefetch([hosts[0]])
+    seen = []
+    for i in range(n):
+        pf.prefetch([hosts[i + 1]])
+        (d,) = pf.next()
+        x = d.float()
+        for _ in range(4):  # keep the consumer busy so the next copy is in flight while it reads
+            x = x * 1.0 + 0.0
+        seen.append(x.sum())
+    with pytest.raises(RuntimeError):
+        pf.prefetch([hosts[0]])
+        pf.prefetch([hosts[0]])
+    torch.cuda.synchronize()
+    assert [int(s.item()) for s in seen] == [i * (1 << 22) for i in range(n)]
+
+
+@pytest.mark.gpu
 def test_dp_step_async_world1_engine():
     import stereoalgorithms_amd  # noqa: F401
     from stereoalgorithms_amd.models.engine import NativeStereoEngine

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 O=gpurun_out/ov; mkdir -p $O
 export SA_PLAN_DIR=/tmp/sa_plans
 timeout -k 10 300 python3 bench.py --steps 2 --warmup 1 --no-latency > /dev/null 2>&1 || exit 1  # tune once
-for r in 1 2; do
+for r in $([ "${SKIP_AB:-0}" = 1 ] || echo 1 2); do
   timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 --no-latency > $O/plain_$r.log 2>&1 || exit 1
   SA_DP_GATHER_WORLD1=1 timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 --no-latency > $O/gather_$r.log 2>&1 || exit 1
 done
@@ -18,4 +18,5 @@ rm -rf /tmp/ovp
 SA_DP_GATHER_WORLD1=1 timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
   -d /tmp/ovp -o run -- python3 bench.py --steps 6 --warmup 2 --no-latency > $O/trace.log 2>&1 || exit 1
 echo "== bench.py DP step, world 1, gather forced (HEAD defaults), last 6 steps"
-python3 tools/overlap_report.py /tmp/ovp --last-ms 250 | tee $O/overlap.txt
+python3 tools/overlap_report.py /tmp/ovp --last-ms 250 --dump $O/window.csv | tee $O/overlap.txt
+head -3 /tmp/ovp/*/*kernel_trace.csv > $O/kernel_trace_head.txt 2>/dev/null || head -3 /tmp/ovp/*kernel_trace.csv > $O/kernel_trace_head.txt

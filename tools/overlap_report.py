@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--last-ms", type=float, default=0.0,
                     help="only the final window of this length before the last kernel ends (steady-state steps; "
                          "0 = everything, engine build and tuning included)")
+    ap.add_argument("--dump", default="", help="write the window's kernels and copies to this CSV")
     a = ap.parse_args()
     kt = glob.glob(os.path.join(a.dir, "**", "*kernel_trace.csv"), recursive=True)
     mt = glob.glob(os.path.join(a.dir, "**", "*memory_copy_trace.csv"), recursive=True)
@@ -81,6 +82,18 @@ def main():
         h2d.append((s, e, d))
     for d in sorted(set(x[2] for x in h2d)):
         report(f"copies {d}", [x for x in h2d if x[2] == d])
+    if a.dump:
+        # compact window dump (start/end relative to the window, ns) for offline timeline analysis
+        with open(a.dump, "w") as f:
+            f.write("kind,start_ns,end_ns,queue,name\n")
+            for r in kern:
+                s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+                if e >= t0:
+                    f.write(f"k,{s - t0},{e - t0},{r.get('Queue_Id', '')},{r['Kernel_Name'][:60].replace(',', ';')}\n")
+            for r in copies:
+                s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+                if e >= t0:
+                    f.write(f"c,{s - t0},{e - t0},,{r.get('Direction', '')}\n")
     return 0
 
 
