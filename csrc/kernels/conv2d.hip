@@ -391,8 +391,10 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
     char* const abuf0 = smem;
     char* const bbuf0 = smem + 2 * APB;
     const int Cin = p.Cin;
-    const int nchunk = Cin >> 6;
-    const int nsteps = 9 * nchunk;
+    // k-steps [kt0, kt0 + nk) of the 9 * Cin / 64 (chunk-major, then tap): whole chunks (a split launch cuts K at
+    // chunk boundaries, conv_igemm_kernel), so chunk cb's patch is the first one DMA'd
+    const int cb = kt0 / 9, ce = (kt0 + nk) / 9;
+    const int s0 = kt0, s1 = kt0 + nk;
     int apix[NAH], alch[NAH];
     bool aok[NAH];
     constexpr int RPP = C::HALO_RPP, APL = RPP * 16;  // kHaloP: plane length (pixels) and plane stride (bytes)
@@ -534,13 +536,13 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
     //   refill: the patch of chunk c + 2 into chunk c's buffer when st is chunk c's last step, then the weights
     //       of step st + 3 into slot st % 3 (patch first, so waiting for a step's weights covers its patch)
     // Prologue: patch 0, weights 0, 1, 2, patch 1.
-    issue_a(0, 0);
-    issue_b(0, 0);
-    if (nsteps > 1) issue_b(1, 1);
-    if (nsteps > 2) issue_b(2, 2);
-    if (nchunk > 1) issue_a(1, 1);
+    issue_a(cb, cb & 1);
+    issue_b(s0, s0 % 3);
+    if (nk > 1) issue_b(s0 + 1, (s0 + 1) % 3);
+    if (nk > 2) issue_b(s0 + 2, (s0 + 2) % 3);
+    if (ce - cb > 1) issue_a(cb + 1, (cb + 1) & 1);
     // pieces issued after the weights of step 0 / step 1 (the first two waits)
-    const int after0 = (nsteps > 1 ? NB : 0) + (nsteps > 2 ? NB : 0) + (nchunk > 1 ? NAH : 0);
+    const int after0 = (nk > 1 ? NB : 0) + (nk > 2 ? NB : 0) + (ce - cb > 1 ? NAH : 0);
     if (after0 >= 2 * NB + NAH) wait_vmcnt<2 * NB + NAH>();
     else if (after0 >= NB + NAH) wait_vmcnt<NB + NAH>();
     else if (after0 >= 2 * NB) wait_vmcnt<2 * NB>();
@@ -549,11 +551,11 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     half8 a0[C::FM], b0[C::FN], a1[C::FM], b1[C::FN];
-    read_half(0, 0, a0, b0);
-    int prev = (nsteps > 2 ? NB : 0) + (nchunk > 1 ? NAH : 0);  // issued after step 1's weights
-    for (int st = 0; st < nsteps; ++st) {
+    read_half(s0, 0, a0, b0);
+    int prev = (nk > 2 ? NB : 0) + (ce - cb > 1 ? NAH : 0);  // issued after step 1's weights
+    for (int st = s0; st < s1; ++st) {
       mfma_read(a0, b0, st, 1, a1, b1);
-      if (st + 1 < nsteps) {
+      if (st + 1 < s1) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (prev >= NB + NAH) wait_vmcnt<NB + NAH>();
         else if (prev >= NB) wait_vmcnt<NB>();
@@ -564,11 +566,11 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
         mfma_read(a1, b1, st + 1, 0, a0, b0);
         const int c = st / 9, t = st - c * 9;
         int issued = 0;
-        if (t == 8 && c + 2 < nchunk) {
+        if (t == 8 && c + 2 < ce) {
           issue_a(c + 2, c & 1);
           issued += NAH;
         }
-        if (st + 3 < nsteps) {
+        if (st + 3 < s1) {
           issue_b(st + 3, st % 3);
           issued += NB;
         }
@@ -1651,6 +1653,31 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
     }
     return;
   }
+  if constexpr (is_halo(MODE)) {
+    if (p.splitk > 1) {
+      // tail split (launch_halo): a 1-D grid whose first `full` dispatch ids are whole tiles (XCD-aware order) and
+      // whose remaining ones cut each of the last T - full tiles into S K-ranges of whole 64-channel chunks, so a
+      // tile count just above a multiple of the CU count does not leave most CUs idle in the last round
+      constexpr int TH = BM / C::TW;
+      const int gy = (p.Cout + BN - 1) / BN;
+      const int T = p.N * ((p.Ho + TH - 1) / TH) * ((p.Wo + C::TW - 1) / C::TW) * gy;
+      const int S = p.splitk, nchunk = p.Cin >> 6;
+      const int nb = gridDim.x;
+      const int full = (S * T - nb) / (S - 1);
+      const int bid = blockIdx.x;
+      if (bid < full) {
+        const int q = full >> 3, r = full & 7, xcd = bid & 7;
+        const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+        conv_tile<BM, BN, WM, WN, MODE>(p, smem, lin / gy, lin % gy, 0, nk_all, 1, 0, 0, 0, 0, 0);
+      } else {
+        const int b2 = bid - full, t = b2 / S, z = b2 - t * S;
+        const int c0 = z * nchunk / S, c1 = (z + 1) * nchunk / S;
+        conv_tile<BM, BN, WM, WN, MODE>(p, smem, (full + t) / gy, (full + t) % gy, 9 * c0, 9 * (c1 - c0), S, z, t * S,
+                                        t, 0, 0);
+      }
+      return;
+    }
+  }
   if constexpr (is_glds(MODE) || MODE == kWide || is_halo(MODE)) {
     const int nwg = gridDim.x * gridDim.y;
     const int bid = blockIdx.y * gridDim.x + blockIdx.x;
@@ -1786,15 +1813,39 @@ int launch_halo(const SaConvArgs* a, hipStream_t stream) {
   constexpr int BM = 256, BN = 128;
   bool ok = a->KD <= 0 && a->KH == 3 && a->KW == 3 && a->sh == 1 && a->sw == 1 && a->ph == 1 && a->pw == 1 &&
             a->dh == 1 && a->dw == 1 && a->up == 0 && a->Cin % 64 == 0 && a->Kpad == 9 * a->Cin &&
-            a->Ho == a->H && a->Wo == a->W && a->splitk <= 1;
+            a->Ho == a->H && a->Wo == a->W && a->splitk >= 0 && a->splitk <= 1;
   for (int i = 0; i < a->nsrc; ++i) ok = ok && a->src[i].channels % 64 == 0;
   if (!ok) return 1;
   using C = ConvCfg<BM, BN, 4, 2, MODE>;
   const int th = BM / C::TW;
   const long tiles = (long)a->N * ((a->Ho + th - 1) / th) * ((a->Wo + C::TW - 1) / C::TW);
-  if (tiles >= (1L << 31) || (long)a->N * a->H * a->W >= (1L << 31)) return 1;
+  const int gy = (a->Cout + BN - 1) / BN;
+  if (tiles * gy >= (1L << 31) || (long)a->N * a->H * a->W >= (1L << 31)) return 1;
+  // splitk 0 (auto): the tiles of the last, partial round are split into S K-ranges of whole 64-channel chunks over
+  // the idle CUs (conv_igemm_kernel's tail split); splitk 1: whole tiles only
+  const long T = tiles * gy;
+  const int cus = device_cus();
+  const long rem = T % cus;
+  const int nchunk = a->Cin / 64;
+  int S = 1;
+  if (a->splitk == 0 && a->ws && a->counters && !a->stats && rem > 0 && 2 * rem <= cus) {
+    S = (int)(cus / rem);
+    if (S > 4) S = 4;
+    if (S > nchunk) S = nchunk;
+    while (S > 1 && ((long)S * rem * BM * BN > a->ws_floats || rem > a->n_counters)) --S;
+  }
+  if (S > 1) {
+    SaConvArgs b = *a;
+    b.splitk = S;
+    note_split(S, rem, BM * BN);
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 4, 2, MODE>), dim3((unsigned)(T - rem + S * rem)), dim3(C::NT), 0,
+                       stream, b);
+    return (int)hipGetLastError();
+  }
+  SaConvArgs b = *a;
+  b.splitk = 1;
   note_split(1, 0, 0);
-  launch_kernel<BM, BN, 4, 2, MODE>(dim3((unsigned)tiles, (a->Cout + BN - 1) / BN, 1), a, stream);
+  launch_kernel<BM, BN, 4, 2, MODE>(dim3((unsigned)tiles, gy, 1), &b, stream);
   return (int)hipGetLastError();
 }
 

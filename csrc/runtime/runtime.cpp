@@ -741,10 +741,10 @@ constexpr Tactic kTactics[] = {
     {23, false, false, 0, 0, 0, 0, "direct 3x3 64 -> 64, 2 waves / SIMD"},
     {24, false, false, 0, 0, 0, 0, "direct 3x3 -> 96"},
     {25, false, false, 0, 0, 0, 0, "strided 1x1"},
-    {26, false, false, 0, 0, 0, 0, "3x3 halo patch 8x32"},
-    {27, false, false, 0, 0, 0, 0, "3x3 halo patch 16x16"},
-    {28, false, false, 0, 0, 0, 0, "3x3 halo patch 8x32, planar image"},
-    {29, false, false, 0, 0, 0, 0, "3x3 halo patch 16x16, planar image"},
+    {26, true, false, 0, 0, 0, 0, "3x3 halo patch 8x32"},
+    {27, true, false, 0, 0, 0, 0, "3x3 halo patch 16x16"},
+    {28, true, false, 0, 0, 0, 0, "3x3 halo patch 8x32, planar image"},
+    {29, true, false, 0, 0, 0, 0, "3x3 halo patch 16x16, planar image"},
 };
 
 bool known_tactic(int cfg) {
@@ -814,6 +814,13 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
     if (!tactic_applies(tc, a, M)) continue;
     for (int sk : {1, 0, -1}) {
       if (sk == 0 && (!can_split || !tc.split)) continue;
+      // halo tiles' tail split (splitk 0) is a candidate unless SA_TUNE_HALO_SPLIT=0 (read per shape: in-process A/B
+      // knob).  Same-process A/B, round 4: RAFT-SF b8 43.54 -> 43.33 ms/step, b1 8.58 -> 8.47, CREStereo iter10
+      // 6.37 -> 6.30 (profiles/round4_notes.md)
+      if (sk == 0 && cfg >= 26 && cfg <= 29) {
+        const char* hs = std::getenv("SA_TUNE_HALO_SPLIT");
+        if (hs && hs[0] == '0') continue;
+      }
       if (sk == -1 && (!can_split || !tc.streamk)) continue;
       t.tile_cfg = cfg;
       t.splitk = sk;

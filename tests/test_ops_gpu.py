@@ -599,6 +599,45 @@ def test_conv2d_halo_vs_torch(srcs, cout, hw, n, cfg):
         assert rel_err(nchw(out), ref) < 2e-3
 
 
+@pytest.mark.parametrize("cfg", [26, 28])
+def test_conv2d_halo_tail_split(cfg):
+    """splitk 0 on the halo tiles: 300 tiles on 256 CUs, so the last 44 are cut into K-ranges of whole 64-channel
+    chunks (uneven: 6 chunks over 4 ranges) reduced by the last arriver.  Must equal F.conv2d and the unsplit launch
+    to fp32-summation-order noise, for the store epilogue and the GRU q epilogue (in-place hidden-state update)."""
+    O = ops()
+    torch.manual_seed(23)
+    n, h, w = 4, 120, 160
+    xs = [torch.randn(n, 128, h, w, device=DEV) for _ in range(3)]
+    wt = torch.randn(128, 384, 3, 3, device=DEV) / math.sqrt(384 * 9)
+    b = torch.randn(128, device=DEV) * 0.1
+    ref = F.leaky_relu(F.conv2d(torch.cat([x.half().float() for x in xs], 1), wt.half().float(), b, padding=1), 0.1)
+    wp, kpad, _ = O.pack_conv_weight(wt)
+    ws = O.splitk_workspace(1 << 24, 4096)
+    xh = [nhwc(x).half() for x in xs]
+    whole = O.conv2d(xh, wp, kpad, 128, 3, 3, bias=b.contiguous(), act="leaky", alpha=0.1, tile_cfg=cfg, splitk=1)
+    for _ in range(2):
+        out = O.conv2d(xh, wp, kpad, 128, 3, 3, bias=b.contiguous(), act="leaky", alpha=0.1, tile_cfg=cfg, splitk=0,
+                       workspace=ws)
+        torch.cuda.synchronize()
+        assert rel_err(nchw(out), ref) < 2e-3
+        assert (out.float() - whole.float()).abs().max().item() < 2e-2
+    # GRU q epilogue (net <- (1 - z) net + z tanh(conv(r*h) + qx)) over a 2-chunk input: split in two
+    hd = 128
+    net = torch.randn(n, hd, h, w, device=DEV).tanh()
+    rh = torch.randn(n, hd, h, w, device=DEV) * 0.5
+    qx = torch.randn(n, hd, h, w, device=DEV) * 0.5
+    z = torch.rand(n, hd, h, w, device=DEV)
+    wq = torch.randn(hd, hd, 3, 3, device=DEV) / math.sqrt(hd * 9)
+    q = torch.tanh(F.conv2d(rh.half().float(), wq.half().float(), padding=1) + qx.half().float())
+    refn = (1 - z.half().float()) * net.half().float() + z.half().float() * q
+    wqp, kq, _ = O.pack_conv_weight(wq)
+    net_h = nhwc(net).half()
+    O.conv2d([nhwc(rh).half()], wqp, kq, hd, 3, 3, out=net_h, epi="gru_q", res=nhwc(qx).half(), aux=nhwc(z).half(),
+             hbuf=net_h, tile_cfg=cfg, splitk=0, workspace=ws)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(net_h), refn) < 4e-3
+
+
 @pytest.mark.parametrize("cfg", [26, 27, 28, 29])
 def test_conv2d_halo_gru_and_stats(cfg):
     """Halo tiles with the fused epilogues: the ZRQ / Q GRU pair and per-(image, channel) instance-norm statistics
