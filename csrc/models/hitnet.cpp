@@ -108,6 +108,10 @@ class HitNet : public StereoEngine {
 
  private:
   HitCfg hc_;
+  // two-chain schedule (forward): SA_HIT_PARALLEL=0 keeps everything on one stream
+  bool par_ = !(std::getenv("SA_HIT_PARALLEL") && std::getenv("SA_HIT_PARALLEL")[0] == '0');
+  void init_level(hipStream_t s, int l);
+  void prop_level(hipStream_t s, int l);
   Tensor img_;
   std::vector<ConvLayer> down_[kLevels];
   std::vector<Tensor> dt_[kLevels];  // per-conv outputs of the down path (last = d_l)
@@ -213,8 +217,57 @@ void HitNet::build(WeightSource& src) {
   }
 }
 
+// Tile hypotheses of level l from its features alone: tile features, initial matching cost / disparity, descriptor,
+// the level's own candidate (last slot of cand)
+void HitNet::init_level(hipStream_t s, int l) {
+  const int B = this->B();
+  Lvl& L = lv_[l];
+  const Tensor el = e_[l].slice_n(0, B), er = e_[l].slice_n(B, B);
+  const long P = (long)B * L.th * L.tw;
+  L.tile_l.run(s, {el}, L.tl);
+  L.tile_r.run(s, {er}, L.tr);
+  tap(s, ("tl" + std::to_string(l)).c_str(), L.tl);
+  tap(s, ("tr" + std::to_string(l)).c_str(), L.tr);
+  check(sa_hitnet_tile_init(L.tl.ptr, L.tl.stride, L.tr.ptr, L.tr.stride, B, L.th, L.tw, L.wr, hc_.maxdisp >> l,
+                            L.cmin.ptr, L.cmin.stride, L.dinit, s),
+        "tile init");
+  L.desc.run(s, {L.cmin, L.tl}, L.dsc, SA_ACT_LEAKY, nullptr, SA_ACT_NONE, nullptr, kSlope);
+  // own init goes to the last candidate slot; slot 0 = upsampled coarser hypothesis
+  float* init_slot = L.cand + (size_t)(L.ncand - 1) * P * 16;
+  check(sa_hitnet_hyp_init(L.dinit, L.dsc.ptr, L.dsc.stride, P, init_slot, s), "hyp init");
+}
+
+// Propagation of level l: the coarser level's winner upsampled into slot 0, warped costs, update net, selection
+void HitNet::prop_level(hipStream_t s, int l) {
+  const int B = this->B();
+  Lvl& L = lv_[l];
+  const Tensor el = e_[l].slice_n(0, B), er = e_[l].slice_n(B, B);
+  const long P = (long)B * L.th * L.tw;
+  if (L.ncand > 1) {
+    const Lvl& C = lv_[l + 1];
+    check(sa_hitnet_upsample(C.hyp, B, C.th, C.tw, L.cand, s), "hyp upsample");
+  }
+  const UpdateNet& U = L.prop;
+  check(sa_hitnet_warp_cost(el.ptr, el.stride, er.ptr, er.stride, B, e_[l].h, e_[l].w, hc_.ch[l], 4, L.cand, L.ncand,
+                            U.x.ptr, U.x.stride, U.cin_pad, s),
+        "warp cost");
+  U.run(s);
+  check(sa_hitnet_select(L.cand, L.ncand, P, (const float*)U.delta.ptr, U.delta.stride, U.nout, 1, L.hyp, s),
+        "select");
+  tap_f32(s, ("cand" + std::to_string(l)).c_str(), L.cand, L.ncand * B, L.th, L.tw, 16);
+  tap(s, ("cost" + std::to_string(l)).c_str(), U.x);
+  tap(s, ("delta" + std::to_string(l)).c_str(), U.delta);
+  tap_f32(s, ("hyp" + std::to_string(l)).c_str(), L.hyp, B, L.th, L.tw, 16);
+}
+
+// Two chains once the coarsest decoder level exists (b1: every conv of the coarse levels is a 5-75 workgroup,
+// latency-bound launch, so a single stream leaves the chip mostly idle):
+//   main: decoder levels 2, 1, 0 and, after each, that level's tile init (events 2, 1, 0)
+//   side: init + propagation of the coarsest level, then propagation of each finer level once its init is done,
+//         the two refinement stages and the final expansion; joined into main at the end
 void HitNet::forward(hipStream_t s) {
   const int B = this->B();
+  const bool par = par_ && !tuning_pass_;
   check(sa_preprocess(in_left_, B, H(), W(), SA_PRE_UNIT, img_.ptr, 8, 0, 8, s), "preprocess");
   check(sa_preprocess(in_right_, B, H(), W(), SA_PRE_UNIT, img_.slice_n(B, B).ptr, 8, 0, 8, s), "preprocess");
   const Tensor* x = &img_;
@@ -223,67 +276,58 @@ void HitNet::forward(hipStream_t s) {
       down_[l][i].run(s, {*x}, dt_[l][i], SA_ACT_LEAKY, nullptr, SA_ACT_NONE, nullptr, kSlope);
       x = &dt_[l][i];
     }
-  for (int l = 3; l >= 0; --l) {
+  auto up = [&](int l) {
     up_deconv_[l].run(s, {e_[l + 1]}, up_t_[l], SA_ACT_LEAKY, nullptr, SA_ACT_NONE, nullptr, kSlope);
     up_merge_[l].run(s, {up_t_[l], dt_[l].back()}, up_m_[l], SA_ACT_LEAKY, nullptr, SA_ACT_NONE, nullptr, kSlope);
     up_conv_[l].run(s, {up_m_[l]}, e_[l], SA_ACT_LEAKY, nullptr, SA_ACT_NONE, nullptr, kSlope);
-  }
-  for (int l = 0; l < kLevels; ++l) tap(s, ("e" + std::to_string(l)).c_str(), e_[l]);
-  for (int l = kHypLevels - 1; l >= 0; --l) {
-    Lvl& L = lv_[l];
-    const Tensor el = e_[l].slice_n(0, B), er = e_[l].slice_n(B, B);
-    const long P = (long)B * L.th * L.tw;
-    L.tile_l.run(s, {el}, L.tl);
-    L.tile_r.run(s, {er}, L.tr);
-    tap(s, ("tl" + std::to_string(l)).c_str(), L.tl);
-    tap(s, ("tr" + std::to_string(l)).c_str(), L.tr);
-    check(sa_hitnet_tile_init(L.tl.ptr, L.tl.stride, L.tr.ptr, L.tr.stride, B, L.th, L.tw, L.wr, hc_.maxdisp >> l,
-                              L.cmin.ptr, L.cmin.stride, L.dinit, s),
-          "tile init");
-    L.desc.run(s, {L.cmin, L.tl}, L.dsc, SA_ACT_LEAKY, nullptr, SA_ACT_NONE, nullptr, kSlope);
-    // own init goes to the last candidate slot; slot 0 = upsampled coarser hypothesis
-    float* init_slot = L.cand + (size_t)(L.ncand - 1) * P * 16;
-    check(sa_hitnet_hyp_init(L.dinit, L.dsc.ptr, L.dsc.stride, P, init_slot, s), "hyp init");
-    if (L.ncand > 1) {
-      const Lvl& C = lv_[l + 1];
-      check(sa_hitnet_upsample(C.hyp, B, C.th, C.tw, L.cand, s), "hyp upsample");
+    tap(s, ("e" + std::to_string(l)).c_str(), e_[l]);
+  };
+  tap(s, "e4", e_[4]);
+  constexpr int top = kHypLevels - 1;
+  for (int l = kLevels - 2; l >= top; --l) up(l);
+  hipStream_t hs = s;  // the hypothesis chain
+  if (par) {
+    hs = fork(s);
+    for (int l = top - 1; l >= 0; --l) {
+      up(l);
+      init_level(s, l);
+      rec(s, l);
     }
-    const UpdateNet& U = L.prop;
-    check(sa_hitnet_warp_cost(el.ptr, el.stride, er.ptr, er.stride, B, e_[l].h, e_[l].w, hc_.ch[l], 4, L.cand,
-                              L.ncand, U.x.ptr, U.x.stride, U.cin_pad, s),
-          "warp cost");
-    U.run(s);
-    check(sa_hitnet_select(L.cand, L.ncand, P, (const float*)U.delta.ptr, U.delta.stride, U.nout, 1, L.hyp, s),
-          "select");
-    tap_f32(s, ("cand" + std::to_string(l)).c_str(), L.cand, L.ncand * B, L.th, L.tw, 16);
-    tap(s, ("cost" + std::to_string(l)).c_str(), U.x);
-    tap(s, ("delta" + std::to_string(l)).c_str(), U.delta);
-    tap_f32(s, ("hyp" + std::to_string(l)).c_str(), L.hyp, B, L.th, L.tw, 16);
   }
-  // final refinement on the level-0 (full-resolution) features
-  const Tensor e0l = e_[0].slice_n(0, B), e0r = e_[0].slice_n(B, B);
-  const float* prev = lv_[0].hyp;
-  int pth = lv_[0].th, ptw = lv_[0].tw, pt = 4;
-  for (int j = 0; j < 2; ++j) {
-    const Refine& R = rf_[j];
-    const long P = (long)B * R.th * R.tw;
-    check(sa_hitnet_split(prev, B, pth, ptw, pt, R.cand, s), "hyp split");
-    const UpdateNet& U = R.net;
-    check(sa_hitnet_warp_cost(e0l.ptr, e0l.stride, e0r.ptr, e0r.stride, B, H(), W(), hc_.ch[0], R.t, R.cand, 1,
-                              U.x.ptr, U.x.stride, U.cin_pad, s),
-          "warp cost");
-    U.run(s);
-    check(sa_hitnet_select(R.cand, 1, P, (const float*)U.delta.ptr, U.delta.stride, U.nout, 0, R.hyp, s), "refine");
-    tap_f32(s, ("rcand" + std::to_string(j)).c_str(), R.cand, B, R.th, R.tw, 16);
-    tap(s, ("rcost" + std::to_string(j)).c_str(), U.x);
-    tap(s, ("rdelta" + std::to_string(j)).c_str(), U.delta);
-    tap_f32(s, ("rhyp" + std::to_string(j)).c_str(), R.hyp, B, R.th, R.tw, 16);
-    prev = R.hyp;
-    pth = R.th;
-    ptw = R.tw;
-    pt = R.t;
+  {
+    ScopedSplitK sk(par ? &splitk_side_ : current_splitk());
+    for (int l = top; l >= 0; --l) {
+      if (!par && l < top) up(l);
+      if (!par || l == top) init_level(hs, l);
+      if (par && l < top) wait(hs, l);
+      prop_level(hs, l);
+    }
+    // final refinement on the level-0 (full-resolution) features
+    const Tensor e0l = e_[0].slice_n(0, B), e0r = e_[0].slice_n(B, B);
+    const float* prev = lv_[0].hyp;
+    int pth = lv_[0].th, ptw = lv_[0].tw, pt = 4;
+    for (int j = 0; j < 2; ++j) {
+      const Refine& R = rf_[j];
+      const long P = (long)B * R.th * R.tw;
+      check(sa_hitnet_split(prev, B, pth, ptw, pt, R.cand, hs), "hyp split");
+      const UpdateNet& U = R.net;
+      check(sa_hitnet_warp_cost(e0l.ptr, e0l.stride, e0r.ptr, e0r.stride, B, H(), W(), hc_.ch[0], R.t, R.cand, 1,
+                                U.x.ptr, U.x.stride, U.cin_pad, hs),
+            "warp cost");
+      U.run(hs);
+      check(sa_hitnet_select(R.cand, 1, P, (const float*)U.delta.ptr, U.delta.stride, U.nout, 0, R.hyp, hs), "refine");
+      tap_f32(hs, ("rcand" + std::to_string(j)).c_str(), R.cand, B, R.th, R.tw, 16);
+      tap(hs, ("rcost" + std::to_string(j)).c_str(), U.x);
+      tap(hs, ("rdelta" + std::to_string(j)).c_str(), U.delta);
+      tap_f32(hs, ("rhyp" + std::to_string(j)).c_str(), R.hyp, B, R.th, R.tw, 16);
+      prev = R.hyp;
+      pth = R.th;
+      ptw = R.tw;
+      pt = R.t;
+    }
+    check(sa_hitnet_expand(prev, B, pth, ptw, 1, disp_, hs), "expand");
   }
-  check(sa_hitnet_expand(prev, B, pth, ptw, 1, disp_, s), "expand");
+  if (par) join(s);
 }
 
 }  // namespace
