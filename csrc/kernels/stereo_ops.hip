@@ -175,6 +175,110 @@ __global__ void agcl8_kernel(const SaAgclArgs a) {
   }
 }
 
+// Same op, one wave per pixel: lane l holds channels 4l .. 4l+3 of the 256 (group l >> 4), so the left features are
+// read once per pixel (agcl8 re-reads them for each of the 9 taps) and every corner of a tap is one coalesced 512-B
+// row of the right features.  In the plain window modes (no learned offsets, not iter mode) the 9 taps share their
+// bilinear corners -- a 1x9 window touches 2 rows x 10 columns, a 3x3 one 4 x 4 -- so those are loaded once into
+// registers and reused (36 corner rows -> 20 / 16).  Per-tap group sums: xor shuffles inside the 16 lanes of a
+// group; lane 16g + k stores tap k of group g.
+// SPX: 0 = per-tap corners (offset / iter modes), 9 = shared 1 x 9 window, 3 = shared 3 x 3 window
+template <int SPX>
+__global__ __launch_bounds__(256) void agclw_kernel(const SaAgclArgs a) {
+  constexpr bool SHARED = SPX != 0;
+  constexpr int ntap = 9;
+  typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+  typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const long P = (long)a.N * a.H * a.W;
+  const long pix = (long)blockIdx.x * 4 + wave;
+  if (pix >= P) return;
+  const int w = (int)(pix % a.W);
+  const long hw = pix / a.W;
+  const int h = (int)(hw % a.H);
+  const int n = (int)(hw / a.H);
+  const int px = SHARED ? SPX : (a.small_patch ? 3 : 9), py = SHARED ? (SPX == 3 ? 3 : 1) : (a.small_patch ? 3 : 1);
+  const half4 l4 = *reinterpret_cast<const half4*>(reinterpret_cast<const f16*>(a.f1) + pix * a.f1_stride + lane * 4);
+  const f16* f2 = reinterpret_cast<const f16*>(a.f2) + (long)n * a.H * a.W * a.f2_stride + lane * 4;
+  auto dot4 = [&](const half4 r) {
+    float s = __builtin_amdgcn_fdot2(half2v{l4[0], l4[1]}, half2v{r[0], r[1]}, 0.f, false);
+    return __builtin_amdgcn_fdot2(half2v{l4[2], l4[3]}, half2v{r[2], r[3]}, s, false);
+  };
+  auto corner = [&](int xx, int yy) -> float {  // zero padding outside the image
+    if (xx < 0 || xx >= a.W || yy < 0 || yy >= a.H) return 0.f;
+    return dot4(*reinterpret_cast<const half4*>(f2 + ((long)yy * a.W + xx) * a.f2_stride));
+  };
+  float res = 0.f;  // lane 16 g + k keeps tap k of group g
+  auto emit = [&](int k, float v) {
+    v += __shfl_xor(v, 1);
+    v += __shfl_xor(v, 2);
+    v += __shfl_xor(v, 4);
+    v += __shfl_xor(v, 8);
+    if ((lane & 15) == k) res = v;
+  };
+  if constexpr (SHARED) {
+    // sample (w + f + dx, h + f + dy): one fractional part for every tap
+    const float* f = a.flow + pix * 2;
+    const float sx0 = (float)w + f[0] - (float)(px / 2), sy0 = (float)h + f[1] - (float)(py / 2);
+    const bool finite = isfinite(sx0) && isfinite(sy0);
+    const float x0f = finite ? floorf(sx0) : 0.f, y0f = finite ? floorf(sy0) : 0.f;
+    const int x0 = (int)x0f, y0 = (int)y0f;
+    const float ax = sx0 - x0f, ay = sy0 - y0f;
+    // corner dot products of the (py + 1) x (px + 1) patch, row by row (each row's px + 1 corners once)
+    constexpr int PX = SPX, PY = SPX == 3 ? 3 : 1;
+    float prev[PX + 1];
+#pragma unroll
+    for (int r = 0; r <= PY; ++r) {
+      float cur[PX + 1];
+#pragma unroll
+      for (int c = 0; c <= PX; ++c) cur[c] = finite ? corner(x0 + c, y0 + r) : 0.f;
+      if (r > 0) {
+#pragma unroll
+        for (int c = 0; c < PX; ++c) {
+          const float v = (1.f - ay) * ((1.f - ax) * prev[c] + ax * prev[c + 1]) + ay * ((1.f - ax) * cur[c] + ax * cur[c + 1]);
+          emit((r - 1) * PX + c, v);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c <= PX; ++c) prev[c] = cur[c];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < ntap; ++k) {
+      const int dx = k % px - px / 2, dy = k / px - py / 2;
+      float sx, sy;
+      if (a.iter_mode) {
+        int hh = h + dy, ww = w + dx;
+        hh = hh < 0 ? 0 : (hh >= a.H ? a.H - 1 : hh);
+        ww = ww < 0 ? 0 : (ww >= a.W ? a.W - 1 : ww);
+        const float* f = a.flow + (((long)n * a.H + hh) * a.W + ww) * 2;
+        sx = (float)ww + f[0];
+        sy = (float)hh + f[1];
+      } else {
+        const float* f = a.flow + pix * 2;
+        sx = (float)w + f[0] + (float)dx;
+        sy = (float)h + f[1] + (float)dy;
+        if (a.offset) {
+          const f16* o = reinterpret_cast<const f16*>(a.offset) + pix * a.offset_stride + k * 2;
+          sx += (float)o[0];
+          sy += (float)o[1];
+        }
+      }
+      float v = 0.f;
+      if (isfinite(sx) && isfinite(sy)) {
+        const float x0f = floorf(sx), y0f = floorf(sy);
+        const int x0 = (int)x0f, y0 = (int)y0f;
+        const float ax = sx - x0f, ay = sy - y0f;
+        v = (1.f - ay) * ((1.f - ax) * corner(x0, y0) + ax * corner(x0 + 1, y0)) +
+            ay * ((1.f - ax) * corner(x0, y0 + 1) + ax * corner(x0 + 1, y0 + 1));
+      }
+      emit(k, v);
+    }
+  }
+  if ((lane & 15) < ntap)
+    reinterpret_cast<f16*>(a.out)[pix * a.out_stride + (lane >> 4) * ntap + (lane & 15)] = (f16)(res * (1.f / 64.f));
+}
+
 __global__ void zero_tail_kernel(f16* out, int stride, long P, int c0, int c1) {
   const int n = c1 - c0;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < P * n; i += (long)gridDim.x * blockDim.x)
@@ -361,13 +465,21 @@ extern "C" int sa_agcl_corr(const SaAgclArgs* a, hipStream_t stream) {
   if (a->C % 32 || a->out_channels < 36) return -2;
   const long total = (long)a->N * a->H * a->W * 36;
   if (total >= (1L << 31)) return -2;  // 32-bit index math in the kernel
-  // 8 threads per pixel for the 256-channel CREStereo features; one thread per tap otherwise
-  if (a->C == 256 && total * 8 < (1L << 31))
+  // 256-channel CREStereo features: one wave per pixel (SA_AGCL_KERNEL=8: 8 lanes per tap); one thread per tap
+  // otherwise
+  const char* ak = std::getenv("SA_AGCL_KERNEL");  // per launch (captured once per graph): in-process A/B knob
+  const bool use8 = ak && ak[0] == '8';
+  const long P = (long)a->N * a->H * a->W;
+  if (a->C == 256 && !use8 && (P + 3) / 4 < (1L << 31)) {
+    const dim3 g((unsigned)((P + 3) / 4));
+    if (a->iter_mode || a->offset) hipLaunchKernelGGL(agclw_kernel<0>, g, dim3(256), 0, stream, *a);
+    else if (a->small_patch) hipLaunchKernelGGL(agclw_kernel<3>, g, dim3(256), 0, stream, *a);
+    else hipLaunchKernelGGL(agclw_kernel<9>, g, dim3(256), 0, stream, *a);
+  } else if (a->C == 256 && total * 8 < (1L << 31))
     hipLaunchKernelGGL(agcl8_kernel, dim3(grid_for(total * 8)), dim3(256), 0, stream, *a);
   else
     hipLaunchKernelGGL(agcl_kernel, dim3(grid_for(total)), dim3(256), 0, stream, *a);
   if (a->out_channels > 36) {
-    const long P = (long)a->N * a->H * a->W;
     hipLaunchKernelGGL(zero_tail_kernel, dim3(grid_for(P * (a->out_channels - 36))), dim3(256), 0, stream,
                        (f16*)a->out, a->out_stride, P, 36, a->out_channels);
   }

@@ -177,10 +177,17 @@ struct Hourglass {
     ag1 = make_volume(a, N, D / 2, h / 2, w / 2, 2 * c);
     out = make_volume(a, N, D, h, w, 1);
   }
-  void run(hipStream_t s, const Tensor& x, const Tensor& x8, const Tensor& x16) const {
+  // the three image-guided gates depend on the 2-D features only (a side branch in FastAcvNet::forward)
+  void run_gates(hipStream_t s, const Tensor& x8, const Tensor& x16) const {
     att8.run(s, {x8});
     att16.run(s, {x16});
     attup8.run(s, {x8});
+  }
+  void run(hipStream_t s, const Tensor& x, const Tensor& x8, const Tensor& x16) const {
+    run_gates(s, x8, x16);
+    run_body(s, x);
+  }
+  void run_body(hipStream_t s, const Tensor& x) const {
     run_gated(s, c1a, {x}, v1a, nullptr);
     run_gated(s, c1b, {v1a}, v1b, &att8);
     run_gated(s, c2a, {v1b}, v2a, nullptr);
@@ -198,6 +205,8 @@ class FastAcvNet : public StereoEngine {
   const char* name() const override { return "FastACVNet_plus"; }
 
  protected:
+  // two-stream schedule (forward): SA_FACV_PARALLEL=0 keeps everything on one stream
+  bool par_ = !(std::getenv("SA_FACV_PARALLEL") && std::getenv("SA_FACV_PARALLEL")[0] == '0');
   void build(WeightSource& src) override;
   void forward(hipStream_t s) override;
 
@@ -342,11 +351,26 @@ void FastAcvNet::build(WeightSource& src) {
   spxo_ = make_tensor(a, B, H(), W(), 16);
 }
 
+// Two streams (b1: most launches here are latency-bound, 19-600 workgroups):
+//   stems (image -> 1/2 -> 1/4) on the side stream beside the MobileNetV2 backbone + FPN on main (join);
+//   then every branch that depends on the 2-D features only -- the six hourglass gates, the two volume gates, the
+//   concatenation features and the whole spx branch -- on the side stream beside the correlation volume and the
+//   attention hourglass on main (events 0 / 1 hand over the gates and the concatenation features, the final join the
+//   spx logits).
 void FastAcvNet::forward(hipStream_t s) {
   const int B = this->B();
   const int h = H() / 4, w = W() / 4;
+  const bool par = par_ && !tuning_pass_;
   check(sa_preprocess(in_left_, B, H(), W(), SA_PRE_IMAGENET, img_.ptr, 8, 0, 8, s), "preprocess");
   check(sa_preprocess(in_right_, B, H(), W(), SA_PRE_IMAGENET, img_.slice_n(B, B).ptr, 8, 0, 8, s), "preprocess");
+  {
+    hipStream_t ss = par ? fork(s) : s;
+    ScopedSplitK sk(par ? &splitk_side_ : current_splitk());
+    st2a_.run(ss, {img_}, st2t_, SA_ACT_LEAKY);
+    st2b_.run(ss, {st2t_}, st2_, SA_ACT_RELU);
+    st4a_.run(ss, {st2_}, st4t_, SA_ACT_LEAKY);
+    st4b_.run(ss, {st4t_}, st4_, SA_ACT_RELU);
+  }
   // backbone
   stem_conv_.run(s, {img_}, s0_, SA_ACT_RELU6);
   b0dw_.run(s, s0_, b0t_, SA_ACT_RELU6);
@@ -366,6 +390,7 @@ void FastAcvNet::forward(hipStream_t s) {
   up8_1_.run(s, {x8u_}, d4_, SA_ACT_LEAKY);
   up8_2_.run(s, {d4_, x4}, x4c_, SA_ACT_LEAKY);
   conv4_.run(s, {x4c_}, x4u_, SA_ACT_LEAKY);
+  if (par) join(s);
   tap(s, "x4", x4);
   tap(s, "x8", x8);
   tap(s, "x16", x16);
@@ -373,55 +398,75 @@ void FastAcvNet::forward(hipStream_t s) {
   tap(s, "x16u", x16u_);
   tap(s, "x8u", x8u_);
   tap(s, "x4u", x4u_);
-  // stems
-  st2a_.run(s, {img_}, st2t_, SA_ACT_LEAKY);
-  st2b_.run(s, {st2t_}, st2_, SA_ACT_RELU);
-  st4a_.run(s, {st2_}, st4t_, SA_ACT_LEAKY);
-  st4b_.run(s, {st4t_}, st4_, SA_ACT_RELU);
   tap(s, "stem2", st2_);
   tap(s, "stem4", st4_);
   const std::vector<Tensor> f0 = {x4u_, st4_};
   const std::vector<Tensor> f0l = {x4u_.slice_n(0, B), st4_.slice_n(0, B)};
+  const Tensor x8l = x8u_.slice_n(0, B), x16l = x16u_.slice_n(0, B);
+  hipStream_t ss = par ? fork(s) : s;
+  auto side_gates = [&]() {  // -> event 0
+    ScopedSplitK sk(par ? &splitk_side_ : current_splitk());
+    gcorr_.run(ss, f0l);
+    hg_att_.run_gates(ss, x8l, x16l);
+    if (par) rec(ss, 0);
+  };
+  auto side_concat = [&]() {  // -> event 1
+    ScopedSplitK sk(par ? &splitk_side_ : current_splitk());
+    cf0_.run(ss, f0, cft_, SA_ACT_LEAKY);
+    cf1_.run(ss, {cft_}, cfeat_);
+    gconcat_.run(ss, f0l);
+    hg_.run_gates(ss, x8l, x16l);
+    if (par) rec(ss, 1);
+  };
+  auto side_spx = [&]() {  // joined at the end
+    ScopedSplitK sk(par ? &splitk_side_ : current_splitk());
+    spx4a_.run(ss, f0l, sx4t_, SA_ACT_LEAKY);
+    spx4b_.run(ss, {sx4t_}, sx4_, SA_ACT_RELU);
+    spx2c1_.run(ss, {sx4_}, sxu_, SA_ACT_LEAKY);
+    spx2c2_.run(ss, {sxu_, st2_.slice_n(0, B)}, sx2_, SA_ACT_LEAKY);
+    spx_.run(ss, {sx2_}, spxo_);
+  };
+  if (par) {
+    side_gates();
+    side_concat();
+    side_spx();
+  }
   // matching descriptors + normalised correlation volume
   mconv_.run(s, f0, m48_, SA_ACT_LEAKY);
   mdesc_.run(s, {m48_}, match_);
   tap(s, "match", match_);
   const int D = kMaxDisp / 4;
   check(sa_norm_corr_volume(match_.ptr, 48, match_.slice_n(B, B).ptr, 48, B, h, w, 48, D, cvol_.ptr, 8, s), "corr vol");
-  gcorr_.run(s, f0l);
+  if (par) wait(s, 0);
+  else side_gates();
   run_gated(s, corr_stem_, {cvol_}, cost0_, &gcorr_);
   tap(s, "corr_vol", cvol_);
   tap(s, "corr_gate", gcorr_.g);
   tap(s, "cost0", cost0_);
-  const Tensor x8l = x8u_.slice_n(0, B), x16l = x16u_.slice_n(0, B);
-  hg_att_.run(s, cost0_, x8l, x16l);
+  hg_att_.run_body(s, cost0_);
   tap(s, "hga_conv1", hg_att_.v1b);
   tap(s, "hga_conv2", hg_att_.v2b);
   tap(s, "hga_agg", hg_att_.ag1);
   tap(s, "att_weights", hg_att_.out);
   check(sa_topk_disparity(hg_att_.out.ptr, hg_att_.out.stride, B, D, h, w, kTopK, prob_, dsamp_, s), "topk");
   // attention-weighted concatenation volume at the sampled disparities
-  cf0_.run(s, f0, cft_, SA_ACT_LEAKY);
-  cf1_.run(s, {cft_}, cfeat_);
+  if (par) wait(s, 1);
+  else side_concat();
   tap_f32(s, "prob", prob_, B, h, w, kTopK);
   tap_f32(s, "samples", dsamp_, B, h, w, kTopK);
   tap(s, "concat_feat", cfeat_);
   check(sa_concat_volume(cfeat_.ptr, 16, cfeat_.slice_n(B, B).ptr, 16, prob_, dsamp_, B, h, w, 16, kTopK, cvol2_.ptr,
                          32, s),
         "concat volume");
-  gconcat_.run(s, f0l);
   run_gated(s, concat_stem_, {cvol2_}, cost1_, &gconcat_);
-  hg_.run(s, cost1_, x8l, x16l);
+  hg_.run_body(s, cost1_);
   tap(s, "concat_vol", cvol2_);
   tap(s, "cost1", cost1_);
   tap(s, "cost", hg_.out);
   check(sa_topk_regress(hg_.out.ptr, hg_.out.stride, dsamp_, B, kTopK, h, w, 2, pred_, s), "regress");
   // spx upsampling
-  spx4a_.run(s, f0l, sx4t_, SA_ACT_LEAKY);
-  spx4b_.run(s, {sx4t_}, sx4_, SA_ACT_RELU);
-  spx2c1_.run(s, {sx4_}, sxu_, SA_ACT_LEAKY);
-  spx2c2_.run(s, {sxu_, st2_.slice_n(0, B)}, sx2_, SA_ACT_LEAKY);
-  spx_.run(s, {sx2_}, spxo_);
+  if (par) join(s);
+  else side_spx();
   tap_f32(s, "pred", pred_, B, h, w, 1);
   tap(s, "spx4", sx4_);
   tap(s, "spx2", sx2_);
