@@ -465,12 +465,13 @@ extern "C" int sa_agcl_corr(const SaAgclArgs* a, hipStream_t stream) {
   if (a->C % 32 || a->out_channels < 36) return -2;
   const long total = (long)a->N * a->H * a->W * 36;
   if (total >= (1L << 31)) return -2;  // 32-bit index math in the kernel
-  // 256-channel CREStereo features: one wave per pixel (SA_AGCL_KERNEL=8: 8 lanes per tap); one thread per tap
-  // otherwise
+  // 256-channel CREStereo features: 8 lanes per (pixel, group, tap); SA_AGCL_KERNEL=w: one wave per pixel (same-process
+  // A/B on CREStereo iter10 b1: 6.423 ms with the 8-lane kernel, 6.528 with the wave kernel -- a quarter of the
+  // threads, each walking 9 dependent flow -> corner loads); one thread per tap otherwise
   const char* ak = std::getenv("SA_AGCL_KERNEL");  // per launch (captured once per graph): in-process A/B knob
-  const bool use8 = ak && ak[0] == '8';
+  const bool wave = ak && ak[0] == 'w';
   const long P = (long)a->N * a->H * a->W;
-  if (a->C == 256 && !use8 && (P + 3) / 4 < (1L << 31)) {
+  if (a->C == 256 && wave && (P + 3) / 4 < (1L << 31)) {
     const dim3 g((unsigned)((P + 3) / 4));
     if (a->iter_mode || a->offset) hipLaunchKernelGGL(agclw_kernel<0>, g, dim3(256), 0, stream, *a);
     else if (a->small_patch) hipLaunchKernelGGL(agclw_kernel<3>, g, dim3(256), 0, stream, *a);

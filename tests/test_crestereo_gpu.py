@@ -26,10 +26,12 @@ def rel_err(a, b):
 
 @pytest.mark.parametrize("small_patch", [False, True])
 @pytest.mark.parametrize("mode", ["offset", "iter", "window"])
-def test_agcl_vs_oracle(small_patch, mode):
+@pytest.mark.parametrize("kernel", ["8", "w"])
+def test_agcl_vs_oracle(small_patch, mode, kernel, monkeypatch):
     """AGCL kernel vs the oracle: learned-offset mode, iter mode (per-tap warped windows), and the plain window mode
-    (no offsets: the kernel shares the taps' bilinear corners)."""
+    (no offsets: the wave kernel shares the taps' bilinear corners); both kernels (SA_AGCL_KERNEL 8 / w)."""
     from stereoalgorithms_amd.models.crestereo import AGCL
+    monkeypatch.setenv("SA_AGCL_KERNEL", kernel)
     O = ops()
     torch.manual_seed(0)
     n, c, h, w = 2, 256, 12, 20
