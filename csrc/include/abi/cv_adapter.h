@@ -11,7 +11,9 @@
 //     frame size, as the reference's TensorRT wrappers do).
 //
 // The extern "C" functions keep their names; a C++ overload of a C-linkage function is legal as long as only
-// one of them has C linkage.  Define SA_NO_OPENCV_ADAPTER to opt out.  Checked against a minimal cv::Mat mock by
+// one of them has C linkage.  This is SOURCE compatibility only: an application binary already built against the
+// reference's header calls the extern "C" symbol with a cv::Mat& where ours expects an sa::Mat&, and nothing at link
+// time catches it.  Prebuilt reference binaries must be recompiled against these headers, never linked as they are.  Define SA_NO_OPENCV_ADAPTER to opt out.  Checked against a minimal cv::Mat mock by
 // tests/test_abi_cv_adapter_cpu.py (OpenCV itself is not installed here: parity with a real cv::Mat is unpinned).
 // No include guard on purpose: each ABI header includes it after defining its SA_ABI_* marker, and the per-model
 // sections below add that model's overloads once.
