@@ -138,13 +138,14 @@ int sa_flow_head_tail_oc(const void* y, int ys, int C, const void* w16, int oc, 
 // Instance-norm apply (biased var, eps): y = act(norm(x)); if res: y = act2(resnorm(res) + y)
 typedef struct {
   const void* x; int32_t x_stride;
-  const sa_stat_t* stats;      // [N][C][2] fixed-point sums of x
+  const sa_stat_t* stats;      // [N][C][2] fixed-point sums of x (stat_slots copies of it, summed here)
   const void* res; int32_t res_stride;
   const sa_stat_t* res_stats;  // NULL -> residual used raw
   void* out; int32_t out_stride;
   int32_t N, HW, C;
   int32_t act, act2;
   float eps, alpha;
+  int32_t stat_slots;          // copies of [N][C][2] the conv epilogues accumulated into (0 / 1: one, reduced)
 } SaNormArgs;
 int sa_instnorm_apply(const SaNormArgs* a, hipStream_t stream);
 // stats[0][i] = sum_r stats[r][i], stats[r>0][i] = 0 for i < count (idempotent)

@@ -49,36 +49,52 @@ __device__ __forceinline__ void st8(f16* p, const float* v) {
   *reinterpret_cast<half8*>(p) = h;
 }
 
-// Per-channel normalisation of one 8-channel group, computed once per thread from the fixed-point
-// sums (mean, rstd), then applied to many pixels of the same image: the statistics cost no longer
-// scales with the tensor size (the per-element version read 128 B of stats per 16 B of data).
-__device__ __forceinline__ void norm8(const sa_stat_t* st, int n, int C, int c, long HW, float eps, float* mean,
-                                      float* rstd) {
+// Per-(image, channel) mean and rstd of the block's image into LDS once per block: the fixed-point sums of the
+// stat_slots copies are added in integer (bitwise the sum sa_stats_reduce would leave in copy 0), so no separate
+// fold launch precedes the apply (round 4: one 1-2 workgroup launch + edge per instance norm on the critical chain).
+// lds: [mean C][rstd C][rmean C][rrstd C] floats.
+__device__ __forceinline__ void norm_lds(const sa_stat_t* st, int slots, int N, int C, int n, long HW, float eps,
+                                         float* mean, float* rstd) {
   const double inv = 1.0 / ((double)HW * SA_STAT_SCALE);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const sa_stat_t* s = st + ((long)n * C + c + j) * 2;
-    const double m = (double)s[0] * inv;
-    const double var = (double)s[1] * inv - m * m;
-    mean[j] = (float)m;
-    rstd[j] = rsqrtf((float)(var > 0.0 ? var : 0.0) + eps);
+  const long slot = (long)N * C * 2;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const sa_stat_t* s = st + ((long)n * C + c) * 2;
+    long long s0 = 0, s1 = 0;
+    for (int r = 0; r < slots; ++r) {
+      s0 += s[r * slot];
+      s1 += s[r * slot + 1];
+    }
+    const double m = (double)s0 * inv;
+    const double var = (double)s1 * inv - m * m;
+    mean[c] = (float)m;
+    rstd[c] = rsqrtf((float)(var > 0.0 ? var : 0.0) + eps);
   }
 }
 
 // grid: (pixel chunks, N); a block's threads tile (pixels x channel groups) of one image, each thread
 // keeps one channel group and walks pixels
 __global__ __launch_bounds__(256) void instnorm_apply_kernel(const SaNormArgs a, int pix_per_block) {
+  extern __shared__ float nlds[];
   const int C8 = a.C >> 3;
   const int n = blockIdx.y;
   const int tid = threadIdx.x;
+  const int slots = a.stat_slots > 1 ? a.stat_slots : 1;
+  const bool rs = a.res && a.res_stats;
+  norm_lds(a.stats, slots, a.N, a.C, n, a.HW, a.eps, nlds, nlds + a.C);
+  if (rs) norm_lds(a.res_stats, slots, a.N, a.C, n, a.HW, a.eps, nlds + 2 * a.C, nlds + 3 * a.C);
+  __syncthreads();
   const int c8 = tid % C8;
   const int lanes_per_c = 256 / C8;  // threads sharing a channel group
   if (tid >= lanes_per_c * C8) return;
   const int c = c8 * 8;
   float mean[8], rstd[8], rmean[8], rrstd[8];
-  norm8(a.stats, n, a.C, c, a.HW, a.eps, mean, rstd);
-  const bool rs = a.res && a.res_stats;
-  if (rs) norm8(a.res_stats, n, a.C, c, a.HW, a.eps, rmean, rrstd);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    mean[j] = nlds[c + j];
+    rstd[j] = nlds[a.C + c + j];
+    rmean[j] = rs ? nlds[2 * a.C + c + j] : 0.f;
+    rrstd[j] = rs ? nlds[3 * a.C + c + j] : 1.f;
+  }
   const long p0 = (long)blockIdx.x * pix_per_block;
   const long p1 = p0 + pix_per_block < a.HW ? p0 + pix_per_block : a.HW;
   // 4 pixels per step, every load issued before the first store (out may alias x: the compiler would
@@ -323,7 +339,8 @@ extern "C" int sa_instnorm_apply(const SaNormArgs* a, hipStream_t stream) {
   const int ppb = lanes_per_c * 8;
   const long chunks = (a->HW + ppb - 1) / ppb;
   if (chunks > 2147483647L || a->N > 65535) return -3;
-  hipLaunchKernelGGL(instnorm_apply_kernel, dim3((unsigned)chunks, a->N), dim3(256), 0, stream, *a, ppb);
+  const size_t lds = (size_t)a->C * 4 * sizeof(float);
+  hipLaunchKernelGGL(instnorm_apply_kernel, dim3((unsigned)chunks, a->N), dim3(256), lds, stream, *a, ppb);
   return (int)hipGetLastError();
 }
 

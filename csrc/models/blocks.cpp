@@ -11,14 +11,9 @@ Norm parse_norm(const std::string& s) {
 
 void instnorm(hipStream_t s, const Tensor& x, const sa_stat_t* stats, const Tensor& out, int act,
               const Tensor* res, const sa_stat_t* res_stats, int act2) {
-  // fold the conv epilogues' statistic copies (idempotent: copies r > 0 are cleared)
-  int rc = sa_stats_reduce(const_cast<sa_stat_t*>(stats), kStatSlots, (long)x.n * x.c * 2, s);
-  SA_REQUIRE(rc == 0, "stats reduce failed");
-  if (res_stats) {
-    rc = sa_stats_reduce(const_cast<sa_stat_t*>(res_stats), kStatSlots, (long)x.n * x.c * 2, s);
-    SA_REQUIRE(rc == 0, "stats reduce failed");
-  }
+  // the apply kernel folds the conv epilogues' kStatSlots statistic copies itself (per block, into LDS)
   SaNormArgs a{};
+  a.stat_slots = kStatSlots;
   a.x = x.ptr;
   a.x_stride = x.stride;
   a.stats = stats;
@@ -34,7 +29,7 @@ void instnorm(hipStream_t s, const Tensor& x, const sa_stat_t* stats, const Tens
   a.act2 = act2;
   a.eps = 1e-5f;
   a.alpha = 0.01f;
-  rc = sa_instnorm_apply(&a, s);
+  const int rc = sa_instnorm_apply(&a, s);
   SA_REQUIRE(rc == 0, "instnorm failed");
   SA_LAUNCH_CHECK(s);
 }

@@ -96,6 +96,7 @@ class SaNormArgs(C.Structure):
         ("N", C.c_int32), ("HW", C.c_int32), ("C", C.c_int32),
         ("act", C.c_int32), ("act2", C.c_int32),
         ("eps", C.c_float), ("alpha", C.c_float),
+        ("stat_slots", C.c_int32),
     ]
 
 

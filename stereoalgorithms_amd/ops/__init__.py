@@ -213,7 +213,8 @@ def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1
     return out
 
 
-def instnorm_apply(x, stats, act="none", res=None, res_stats=None, act2="none", eps=1e-5, out=None):
+def instnorm_apply(x, stats, act="none", res=None, res_stats=None, act2="none", eps=1e-5, out=None, slots=1):
+    """slots > 1: stats (and res_stats) hold that many [N][C][2] copies, summed by the kernel."""
     n, h, w, c = x.shape
     out = torch.empty_like(x) if out is None else out
     a = N.SaNormArgs()
@@ -227,6 +228,7 @@ def instnorm_apply(x, stats, act="none", res=None, res_stats=None, act2="none", 
     a.N, a.HW, a.C = n, h * w, c
     a.act, a.act2 = N.ACT[act], N.ACT[act2]
     a.eps, a.alpha = eps, 0.01
+    a.stat_slots = slots
     N.check(N.dev().sa_instnorm_apply(C.byref(a), _stream()), "sa_instnorm_apply")
     return out
 

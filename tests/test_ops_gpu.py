@@ -715,11 +715,19 @@ def test_conv2d_flow_acc_and_stats():
         st1 = torch.zeros(n, 64, 2, dtype=torch.int64, device=DEV)
         O.conv2d(nhwc(x).half(), wp2, kp2, 64, 3, 3, stats=st1, tile_cfg=cfg)
         st16.zero_()
-        O.conv2d(nhwc(x).half(), wp2, kp2, 64, 3, 3, stats=st16, stats_slots=16, tile_cfg=cfg)
+        y16 = O.conv2d(nhwc(x).half(), wp2, kp2, 64, 3, 3, stats=st16, stats_slots=16, tile_cfg=cfg)
+        # the apply kernel folds the 16 copies itself (the engine's path): bitwise the apply of the reduced sums,
+        # with and without a normalised residual
+        r16 = st16.clone()
+        a_slots = O.instnorm_apply(y16, st16, act="relu", slots=16)
+        ar_slots = O.instnorm_apply(y16, st16, act="relu", res=y16, res_stats=r16, act2="relu", slots=16)
         O.stats_reduce(st16, 16)
         O.stats_reduce(st16, 16)  # idempotent
         torch.cuda.synchronize()
         assert torch.equal(st16[0], st1) and st16[1:].abs().sum().item() == 0
+        assert torch.equal(a_slots, O.instnorm_apply(y16, st16[0], act="relu"))
+        assert torch.equal(ar_slots, O.instnorm_apply(y16, st16[0], act="relu", res=y16, res_stats=st16[0],
+                                                      act2="relu"))
 
 
 def test_pool_interp():
