@@ -123,6 +123,8 @@ int sa_conv1x1_point(const void* x, int xs, int cin, const void* w, int kpad, co
 // split-K footprint of the calling thread's last successful sa_conv2d launch: slab floats and tile
 // counters it used (0, 0 when it did not split)
 void sa_conv2d_last_split(long* ws_floats, long* tiles);
+// LDS bytes per workgroup of tile config cfg (-1: not a tile config the tuner compares by footprint)
+int sa_conv2d_tile_lds(int cfg);
 // Flow-head conv2 (3x3 C -> 1, the RAFT flow head) in one launch: MFMA tap projections of a halo-tiled region
 // (planes in LDS) + the 9-tap stencil, accumulated into the flow:
 // flow[n][y][x] += bias[0] + sum_{ky,kx} sum_c y[n][y+ky-1][x+kx-1][c] * w16[ky*3+kx][c] (zero padding);

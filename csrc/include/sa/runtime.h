@@ -152,6 +152,17 @@ struct ScopedSplitK {
   ~ScopedSplitK();
 };
 
+// Convs enqueued while a ScopedSideBranch(true) is alive belong to a branch that runs beside the frame's critical
+// chain in the frame graph (set identically in the eager tuning pass and in the capture).  Their plan key carries
+// the mark, and the tuner picks among the tactics within SA_TUNE_LDS_TOL (default 0.08) of the fastest the one with
+// the smallest LDS footprint, so the branch's workgroups co-reside with the chain's instead of taking whole CUs.
+struct ScopedSideBranch {
+  bool prev;
+  explicit ScopedSideBranch(bool on);
+  ~ScopedSideBranch();
+};
+bool side_branch();
+
 // ------------------------------------------------------------------ conv tactic selection
 // The MI355X analogue of TensorRT's tactic selection at engine build (common/ONNX2TRT.cpp:111):
 // during the engine's eager tuning pass every distinct conv shape is timed over the tile / split-K

@@ -1926,6 +1926,34 @@ extern "C" void sa_conv2d_last_split(long* ws_floats, long* tiles) {
   *tiles = g_split_tiles;
 }
 
+// LDS bytes per workgroup of a tile config (the BK = 64 form of the register-staged tiles); -1 for the
+// special-purpose kernels (stem / direct / point) whose footprint the tuner does not compare
+extern "C" int sa_conv2d_tile_lds(int cfg) {
+  switch (cfg) {
+    case 0: return ConvCfg<128, 128, 2, 2, kFastK64>::SMEM;
+    case 1: return ConvCfg<128, 64, 2, 2, kFastK64>::SMEM;
+    case 2: return ConvCfg<256, 16, 4, 1, kFastK64>::SMEM;
+    case 3: return ConvCfg<64, 64, 2, 2, kFastK64>::SMEM;
+    case 4: return ConvCfg<256, 128, 4, 2, kGlds3>::SMEM;
+    case 5: return ConvCfg<128, 64, 2, 2, kGlds3>::SMEM;
+    case 7: return ConvCfg<128, 128, 2, 4, kGlds3>::SMEM;
+    case 8: return ConvCfg<256, 64, 4, 2, kGlds3>::SMEM;
+    case 10: return ConvCfg<256, 256, 2, 4, kWide>::SMEM;
+    case 11: return ConvCfg<512, 128, 4, 2, kWide>::SMEM;
+    case 14: return ConvCfg<128, 64, 2, 2, kGldsDeep>::SMEM;
+    case 15: return ConvCfg<128, 128, 2, 4, kGldsDeep>::SMEM;
+    case 16: return ConvCfg<64, 64, 2, 2, kGldsDeep>::SMEM;
+    case 17: return ConvCfg<256, 64, 4, 2, kGldsDeep>::SMEM;
+    case 18: return ConvCfg<256, 256, 2, 4, kPing>::SMEM;
+    case 19: return ConvCfg<256, 128, 2, 4, kPing>::SMEM;
+    case 26: return ConvCfg<256, 128, 4, 2, kHalo>::SMEM;
+    case 27: return ConvCfg<256, 128, 4, 2, kHalo16>::SMEM;
+    case 28: return ConvCfg<256, 128, 4, 2, kHaloP>::SMEM;
+    case 29: return ConvCfg<256, 128, 4, 2, kHaloP16>::SMEM;
+    default: return -1;
+  }
+}
+
 extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
   if (a->Kpad % 32 != 0 || a->Cin % 8 != 0 || a->nsrc < 1 || a->nsrc > 4) return -2;
   const int cfg = pick_cfg(a);
