@@ -186,6 +186,7 @@ def _declare_dev(lib):
         "sa_conv_plan_save": (_i, [C.c_char_p, C.c_char_p]),
         "sa_conv_plan_load": (_i, [C.c_char_p]),
         "sa_conv_plan_entries": (C.c_long, []),
+        "sa_conv2d_tile_lds": (_i, [_i]),
         "sa_engine_stage_times": (_i, [_p, C.POINTER(C.c_float), C.POINTER(C.c_char_p), _i]),
         "sa_algorithm_create": (_p, [C.c_char_p, _i, C.c_char_p, C.c_char_p]),
         "sa_algorithm_run": (_i, [_p, _p, _p, _i, _i, _p, _p, _i]),

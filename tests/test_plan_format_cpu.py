@@ -58,3 +58,17 @@ def test_loader_drops_unknown_tactics(tmp_path):
     assert lib.sa_conv_plan_load(str(p).encode()) == 1  # retired tactic 9 dropped, tactic 3 kept
     _, entries = read_plan(p)
     assert len(entries) == 2  # the reader itself is format-only
+
+
+def test_tile_lds_footprints():
+    """The per-tile-config LDS footprints the tuner's side-branch tie-break compares (SA_TUNE_LDS_TOL): every
+    one-workgroup-per-CU DMA-ring / halo tile needs more than half the CU's 160 KB, the small register-staged and
+    4-wave ring tiles leave room for other workgroups, the special-purpose kernels are not compared (-1)."""
+    lib = N.dev()
+    lds = {c: lib.sa_conv2d_tile_lds(c) for c in (0, 1, 3, 4, 5, 7, 14, 16, 26, 28, 22, 23, 24, 25, 99)}
+    for c in (4, 26, 28):
+        assert 81920 < lds[c] <= 163840, (c, lds[c])
+    for c in (3, 5):
+        assert 0 < lds[c] <= 81920, (c, lds[c])
+    assert lds[3] < lds[0] and lds[5] < lds[4] and lds[16] <= 163840
+    assert all(lds[c] == -1 for c in (22, 23, 24, 25, 99))
