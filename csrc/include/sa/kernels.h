@@ -30,9 +30,14 @@ enum SaEpi {
   SA_EPI_FLOW_ACC = 3,  // fp32 out[m*out_stride + c] += acc*scale + bias for c < min(Cout, out_stride)
   SA_EPI_STORE_F32 = 4,  // y = act(acc*scale + bias) -> fp32
   // 5: retired (projection epilogue; the flow-head conv2 is sa_flow_head_tail now)
-  SA_EPI_GRU_ZRQ = 6     // Cout = 3 Hd stacked [convz | convr | convq restricted to the x inputs]: z -> aux,
+  SA_EPI_GRU_ZRQ = 6,    // Cout = 3 Hd stacked [convz | convr | convq restricted to the x inputs]: z -> aux,
                          // r*h -> rh as SA_EPI_GRU_ZR, and the x half of q's pre-activation (acc + bias + cq)
                          // -> out (fp16); the following SA_EPI_GRU_Q conv over r*h alone adds it back (res)
+  SA_EPI_TAPPROJ = 7     // flow-head conv1 with the next 3x3 -> oc conv's tap projections fused: y = fp16(act(acc +
+                         // bias)) is never stored; out (fp32) [m][n-tile][taps] gets, per 128-channel n-tile, the
+                         // partial sums over its channels of y * tapw[t] (tapw fp16 [taps][Cout], taps = 9 oc <= 18);
+                         // sa_tapproj_stencil adds both partials' 3x3 neighbourhoods into the flow.  128-wide n-tiles
+                         // only (other tile configs return -5)
 };
 
 typedef struct {
@@ -92,9 +97,16 @@ typedef struct {
   // real input channels when the single source is zero-padded beyond them (0 = all channels real); lets
   // the 7x7 stem kernel (tile_cfg 22) stage only the real channels
   int32_t cin_real;
+  // SA_EPI_TAPPROJ: the projection weights fp16 [taps][Cout] and their count
+  const void* tapw;
+  int32_t taps;
 } SaConvArgs;
 
 int sa_conv2d(const SaConvArgs* a, hipStream_t stream);
+// flow [N][H][W][oc] fp32 += bias[o] + sum over the 3x3 neighbourhood (zero padding) of the two n-tile partials of
+// tap (ky*3+kx)*oc + o in P [N][H][W][2][taps] (an SA_EPI_TAPPROJ conv's output)
+int sa_tapproj_stencil(const float* P, int taps, int oc, const float* bias, float* flow, int N, int H, int W,
+                       hipStream_t stream);
 // 7x7 / pad 3 / stride 1 or 2 stem conv, <= 4 real input channels (pixel stride xs, 8-B aligned) -> 64
 // channels, weights packed [>=64][kpad] with K ordered (kh, kw, ci < cpad); act none / relu / leaky; optional
 // slotted IN statistics.  Also reachable through sa_conv2d with tile_cfg = 22.

@@ -1483,6 +1483,31 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
           h8[j] = (1.f - z8[j]) * h8[j] + z8[j] * q;
         }
         store8(hp, h8);
+      } else if (p.epi == SA_EPI_TAPPROJ) {
+        // the next conv's tap projections of y = fp16(act(v)) (what a stored y would hold): per tap, this lane's 8
+        // channels by fp16 dot products, then the sum over the CPR lanes of the row (one 128-channel n-tile)
+        typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+        half8 h;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) h[j] = (f16)act_apply(v[j], p.act, p.alpha);
+        const f16* wt = reinterpret_cast<const f16*>(p.tapw) + co;
+        float mine = 0.f, mine2 = 0.f;  // lane cc keeps the totals of taps cc and cc + CPR
+#pragma unroll
+        for (int t = 0; t < 18; ++t) {
+          if (t >= p.taps) break;
+          const half8 w8 = *reinterpret_cast<const half8*>(wt + (size_t)t * p.Cout);
+          float sacc = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; j += 2)
+            sacc = __builtin_amdgcn_fdot2(half2v{h[j], h[j + 1]}, half2v{w8[j], w8[j + 1]}, sacc, false);
+#pragma unroll
+          for (int o = 1; o < CPR; o <<= 1) sacc += __shfl_xor(sacc, o);
+          if (cc == t) mine = sacc;
+          if (cc + CPR == t) mine2 = sacc;
+        }
+        float* pp = reinterpret_cast<float*>(p.out) + (size_t)m * p.out_stride + (n0 / BN) * p.taps;
+        if (cc < p.taps) pp[cc] = mine;
+        if (cc + CPR < p.taps) pp[cc + CPR] = mine2;
       } else if (p.epi == SA_EPI_FLOW_ACC) {
         if (co == 0) {  // flow state += delta (RAFT: x only, stride 1; CREStereo: x and y)
           float* fp = reinterpret_cast<float*>(p.out) + (size_t)m * p.out_stride;
@@ -1902,6 +1927,7 @@ bool glds3_eligible(const SaConvArgs* a) {
 
 int pick_cfg(const SaConvArgs* a) {
   if (a->tile_cfg >= 0) return a->tile_cfg;
+  if (a->epi == SA_EPI_TAPPROJ) return 4;  // 128-wide n-tiles
   const int M = a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
   if (a->Cout > 64 && glds3_eligible(a) && (a->splitk <= 1 || a->ws)) {
     // measured on MI355X (tools/conv_bench.py): 256x128 / 8 waves wins once its grid covers the
@@ -1957,6 +1983,14 @@ extern "C" int sa_conv2d_tile_lds(int cfg) {
 extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
   if (a->Kpad % 32 != 0 || a->Cin % 8 != 0 || a->nsrc < 1 || a->nsrc > 4) return -2;
   const int cfg = pick_cfg(a);
+  if (a->epi == SA_EPI_TAPPROJ) {
+    // partial sums per 128-channel n-tile: the tile configs with BN = 128 only
+    const bool bn128 = cfg == 0 || cfg == 4 || cfg == 7 || cfg == 11 || cfg == 15 || cfg == 19 || (cfg >= 26 && cfg <= 29);
+    if (!bn128) return -5;
+    if (!a->tapw || a->taps < 1 || a->taps > 18 || a->stats || a->up || a->gate || a->Cout % 128 ||
+        a->out_stride < (a->Cout / 128) * a->taps)
+      return -2;
+  }
   switch (cfg) {
     case 0: return launch_cfg<128, 128, 2, 2>(a, stream);
     case 1: return launch_cfg<128, 64, 2, 2>(a, stream);
@@ -2122,7 +2156,41 @@ __global__ __launch_bounds__(256) void flow_head_tail_kernel(const f16* __restri
     flow[(((size_t)n * H + gy) * W + gx) * OC + c] += s;
   }
 }
+__global__ __launch_bounds__(256) void tapproj_stencil_kernel(const float* __restrict__ P, int taps, int oc,
+                                                              const float* __restrict__ bias, float* __restrict__ flow,
+                                                              int N, int H, int W) {
+  const long total = (long)N * H * W * oc;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int o = (int)(i % oc);
+    const long px = i / oc;
+    const int x = (int)(px % W);
+    const long r = px / W;
+    const int y = (int)(r % H);
+    const long n = r / H;
+    float s = bias ? bias[o] : 0.f;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int yy = y + ky - 1, xx = x + kx - 1;
+        if (yy < 0 || yy >= H || xx < 0 || xx >= W) continue;
+        const float* q = P + ((n * H + yy) * W + xx) * 2 * taps + (ky * 3 + kx) * oc + o;
+        s += q[0] + q[taps];
+      }
+    flow[px * oc + o] += s;
+  }
+}
 }  // namespace
+
+extern "C" int sa_tapproj_stencil(const float* P, int taps, int oc, const float* bias, float* flow, int N, int H,
+                                  int W, hipStream_t stream) {
+  if (!P || !flow || (oc != 1 && oc != 2) || taps != 9 * oc || N < 1 || H < 1 || W < 1) return -2;
+  const long total = (long)N * H * W * oc;
+  long g = (total + 255) / 256;
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL(tapproj_stencil_kernel, dim3((unsigned)g), dim3(256), 0, stream, P, taps, oc, bias, flow, N, H, W);
+  return (int)hipGetLastError();
+}
 
 extern "C" int sa_flow_head_tail_oc(const void* y, int ys, int C, const void* w16, int oc, const float* bias,
                                     float* flow, int N, int H, int W, hipStream_t stream) {

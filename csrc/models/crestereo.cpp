@@ -154,6 +154,10 @@ class CreStereo : public StereoEngine {
   Level lv_[3];  // 0: 1/4, 1: 1/8, 2: 1/16
   void* fh2_w16_ = nullptr;
   float* fh2_b_ = nullptr;
+  // SA_CRE_FH_PROJ=1: flow-head conv1 leaves conv2's tap projections (SA_EPI_TAPPROJ) in the level's fh buffer
+  // instead of its 256 channels, and a stencil adds them into the flow (iterations without the mask head).  Off by
+  // default: same-process A/B iter10 6.44 -> 6.88 ms (the flow head is on the chain here)
+  bool fh_proj_ = std::getenv("SA_CRE_FH_PROJ") && std::getenv("SA_CRE_FH_PROJ")[0] == '1';
   float *flowup4_ = nullptr, *flowup2_ = nullptr, *pe_ = nullptr;
 };
 
@@ -354,6 +358,18 @@ void CreStereo::update(hipStream_t s, Level& L, const Tensor& f1, const Tensor& 
     qa.hbuf = L.net.ptr;
     qa.h_stride = L.net.stride;
     q_[d].launch(s, qa);
+  }
+  if (!want_mask && fh_proj_) {
+    // [2 n-tiles][18 taps] fp32 partial projections per pixel, in the (otherwise unused) fh buffer
+    const Tensor pt{L.fh.ptr, B, L.h, L.w, 36, 36, DT::F32};
+    SaConvArgs pa = fh1_.args({L.net}, pt);
+    pa.epi = SA_EPI_TAPPROJ;
+    pa.act = SA_ACT_RELU;
+    pa.tapw = fh2_w16_;
+    pa.taps = 18;
+    fh1_.launch(s, pa);
+    check(sa_tapproj_stencil((const float*)L.fh.ptr, 18, 2, fh2_b_, L.flow, B, L.h, L.w, s), "flow-head tap stencil");
+    return;
   }
   if (want_mask) fh1mask_.run(s, {L.net}, L.fh, SA_ACT_RELU);
   else fh1_.run(s, {L.net}, L.fh.slice_c(0, 256), SA_ACT_RELU);

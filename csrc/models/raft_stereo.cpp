@@ -118,6 +118,13 @@ class RaftStereo : public StereoEngine {
   // profiles/flow_head_tail_r02.txt)
   float* fh2_b_ = nullptr;
   void* fh2_w16_ = nullptr;
+  // SA_RAFT_FH_PROJ: flow-head conv1 stores conv2's tap projections (SA_EPI_TAPPROJ) instead of its 256-channel
+  // output, and a stencil adds them into the flow (all but the last iteration, whose conv1 also feeds the mask
+  // head).  Default: the realtime preset only, where the flow head runs beside the chain (same-process A/B: RT b1
+  // 1.986 -> 1.865 ms; SF b1 8.26 -> 8.85, b8 43.8 -> 45.4: the epilogue's per-tap lane reductions cost more than
+  // the 256-channel store they save when conv1 is on the critical path)
+  int fh_proj_env_ = std::getenv("SA_RAFT_FH_PROJ") ? std::atoi(std::getenv("SA_RAFT_FH_PROJ")) : -1;
+  float* fhP_ = nullptr;  // [B][h0][w0][2 n-tiles][9] fp32
   // fused lookup + convc1 + convf1 (sa_raft_motion_head): fp32 [k][64] weights and biases
   float *mh_wc_ = nullptr, *mh_bc_ = nullptr, *mh_wf_ = nullptr, *mh_bf_ = nullptr;
   void* me_w1_ = nullptr;  // fused motion encoder stage-1 weights (fp16 [128][96]) and bias [128]
@@ -349,6 +356,7 @@ void RaftStereo::build(WeightSource& src) {
   corflo_ = make_tensor(a, Bn, h0, w0, 128);
   motion_ = make_tensor(a, Bn, h0, w0, 128);
   fh_ = make_tensor(a, Bn, h0, w0, 512);
+  fhP_ = (float*)a.alloc((size_t)Bn * h0 * w0 * 18 * 4);
   mask_ = make_tensor(a, Bn, h0, w0, round_up(f * f * 9, 8));
   for (int i = 0; i + 1 < rc_.n_gru; ++i) {
     pool_[i] = make_tensor(a, Bn, lh_[i + 1], lw_[i + 1], hd);
@@ -553,6 +561,20 @@ void RaftStereo::forward(hipStream_t s) {
   // flow head: conv1 (+ the mask head's conv on the last iteration), then conv2's taps + stencil into the flow
   // (x only) in one launch; mask head 1x1 on the last iteration
   auto head = [&](hipStream_t st, bool last) {
+    const bool fh_proj = fh_proj_env_ >= 0 ? fh_proj_env_ != 0 : (rc_.n_gru == 2 && rc_.slow_fast);
+    if (!last && fh_proj) {
+      // conv1's output never reaches memory: its epilogue leaves conv2's x-output tap projections per 128-channel
+      // n-tile ([2][9] floats per pixel instead of 256 fp16), the stencil sums their 3x3 neighbourhoods into the flow
+      const Tensor pt{fhP_, Bn, h0, w0, 18, 18, DT::F32};
+      SaConvArgs pa = fh1_.args({net_[0]}, pt);
+      pa.epi = SA_EPI_TAPPROJ;
+      pa.act = SA_ACT_RELU;
+      pa.tapw = fh2_w16_;
+      pa.taps = 9;
+      fh1_.launch(st, pa);
+      check(sa_tapproj_stencil(fhP_, 9, 1, fh2_b_, flow_, Bn, h0, w0, st), "flow-head tap stencil");
+      return;
+    }
     if (last) fh1mask_.run(st, {net_[0]}, fh_, SA_ACT_RELU);
     else fh1_.run(st, {net_[0]}, fh_.slice_c(0, 256), SA_ACT_RELU);
     check(sa_flow_head_tail(fh_.ptr, fh_.stride, 256, fh2_w16_, fh2_b_, flow_, Bn, h0, w0, st), "flow-head tail");

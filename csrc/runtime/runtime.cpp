@@ -801,7 +801,7 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
     const char* e = std::getenv("SA_TUNE_VERIFY");
     return !(e && e[0] == '0');
   }();
-  const bool out_f32 = t.epi == SA_EPI_STORE_F32 || t.epi == SA_EPI_FLOW_ACC;
+  const bool out_f32 = t.epi == SA_EPI_STORE_F32 || t.epi == SA_EPI_FLOW_ACC || t.epi == SA_EPI_TAPPROJ;
   char* ref = nullptr;
   unsigned* res = nullptr;
   if (verify) {

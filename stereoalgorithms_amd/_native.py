@@ -83,6 +83,7 @@ class SaConvArgs(C.Structure):
         ("KD", C.c_int32), ("Di", C.c_int32), ("Do", C.c_int32), ("sd", C.c_int32), ("pd", C.c_int32),
         ("up", C.c_int32), ("cout_real", C.c_int32), ("gate", C.c_void_p), ("gate_stride", C.c_int32),
         ("stats_slots", C.c_int32), ("cin_real", C.c_int32),
+        ("tapw", C.c_void_p), ("taps", C.c_int32),
     ]
 
 
@@ -119,7 +120,7 @@ class SaEwArgs(C.Structure):
 
 
 ACT = {"none": 0, "relu": 1, "leaky": 2, "tanh": 3, "sigmoid": 4, "relu6": 5}
-EPI = {"store": 0, "gru_zr": 1, "gru_q": 2, "flow_acc": 3, "store_f32": 4, "gru_zrq": 6}
+EPI = {"store": 0, "gru_zr": 1, "gru_q": 2, "flow_acc": 3, "store_f32": 4, "gru_zrq": 6, "tapproj": 7}
 PRE = {"raw": 0, "unit": 1, "imagenet": 2, "signed": 3}
 
 _i = C.c_int
@@ -187,6 +188,7 @@ def _declare_dev(lib):
         "sa_conv_plan_load": (_i, [C.c_char_p]),
         "sa_conv_plan_entries": (C.c_long, []),
         "sa_conv2d_tile_lds": (_i, [_i]),
+        "sa_tapproj_stencil": (_i, [_p, _i, _i, _p, _p, _i, _i, _i, _p]),
         "sa_engine_stage_times": (_i, [_p, C.POINTER(C.c_float), C.POINTER(C.c_char_p), _i]),
         "sa_algorithm_create": (_p, [C.c_char_p, _i, C.c_char_p, C.c_char_p]),
         "sa_algorithm_run": (_i, [_p, _p, _p, _i, _i, _p, _p, _i]),

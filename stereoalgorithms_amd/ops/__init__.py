@@ -141,7 +141,7 @@ def pack_conv_weight(w: torch.Tensor, segs: Sequence[tuple[int, int]] | None = N
 def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1, act="none",
            act2="none", res=None, out=None, epi="store", scale=1.0, alpha=0.01, stats=None,
            ctx=None, aux=None, hbuf=None, rh=None, tile_cfg=-1, splitk=1, workspace=None, up=0, cout_real=0,
-           gate=None, stats_slots=1, cin_real=0):
+           gate=None, stats_slots=1, cin_real=0, tapw=None, taps=0):
     """NHWC fp16 implicit-GEMM conv.  ``splitk``: 1 = off, 0 = auto, >1 = forced; needs
     ``workspace`` = (fp32 slab tensor, int32 counter tensor zero-initialised).  ``up`` = 2: transposed
     conv, the 4 parity classes (cout = 4 * cout_real) are scattered to a 2x output.  ``gate``: fp16
@@ -203,6 +203,8 @@ def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1
         assert stats.dtype == torch.int64  # fixed point, value * 2^24
         a.stats = stats.data_ptr()
         a.stats_slots = stats_slots
+    if tapw is not None:  # epi "tapproj": fp16 [taps][cout] projection weights; out fp32 [n,h,w,(cout//128)*taps]
+        a.tapw, a.taps = tapw.data_ptr(), taps
     a.tile_cfg = tile_cfg
     a.splitk = splitk
     if workspace is not None:
@@ -211,6 +213,14 @@ def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1
         a.ws, a.counters, a.ws_floats, a.n_counters = ws.data_ptr(), cnt.data_ptr(), ws.numel(), cnt.numel()
     N.check(N.dev().sa_conv2d(C.byref(a), _stream()), "sa_conv2d")
     return out
+
+
+def tapproj_stencil(P, taps, oc, bias, flow):
+    """flow [n,h,w,oc] fp32 += bias + 3x3 neighbourhood sums of the two n-tile partials in P [n,h,w,2*taps]."""
+    n, h, w, _ = flow.shape
+    N.check(N.dev().sa_tapproj_stencil(P.data_ptr(), taps, oc, bias.data_ptr() if bias is not None else None,
+                                       flow.data_ptr(), n, h, w, _stream()), "sa_tapproj_stencil")
+    return flow
 
 
 def instnorm_apply(x, stats, act="none", res=None, res_stats=None, act2="none", eps=1e-5, out=None, slots=1):

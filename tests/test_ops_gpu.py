@@ -685,6 +685,41 @@ def test_conv2d_halo_gru_and_stats(cfg):
     assert torch.allclose(tot[..., 1], (o * o).sum((2, 3)), rtol=1e-4, atol=2e-3)
 
 
+@pytest.mark.parametrize("cfg", [-1, 4, 7, 26, 28])
+@pytest.mark.parametrize("oc", [1, 2])
+def test_flow_head_tap_projection(cfg, oc):
+    """Flow head with conv2's tap projections fused into conv1's epilogue (SA_EPI_TAPPROJ: conv1's 256 channels are
+    never stored) + the 3x3 stencil, against F.conv2d(relu(conv1)) -> conv2 in fp32 on the fp16-rounded hidden
+    features; BN = 64 tile configs are refused."""
+    O = ops()
+    torch.manual_seed(31)
+    n, h, w = 2, 30, 44
+    x = torch.randn(n, 128, h, w, device=DEV)
+    w1 = torch.randn(256, 128, 3, 3, device=DEV) / math.sqrt(128 * 9)
+    b1 = torch.randn(256, device=DEV) * 0.1
+    w2 = torch.randn(oc, 256, 3, 3, device=DEV) / math.sqrt(256 * 9)
+    b2 = torch.randn(oc, device=DEV) * 0.1
+    hid = F.relu(F.conv2d(x.half().float(), w1.half().float(), b1, padding=1)).half().float()
+    flow0 = torch.randn(n, h, w, oc, device=DEV)
+    ref = flow0 + F.conv2d(hid, w2.half().float(), b2, padding=1).permute(0, 2, 3, 1)
+    wp, kpad, _ = O.pack_conv_weight(w1)
+    taps = 9 * oc
+    tapw = torch.zeros(taps, 256, device=DEV, dtype=torch.float16)
+    for t in range(9):
+        for o in range(oc):
+            tapw[t * oc + o] = w2[o, :, t // 3, t % 3].half()
+    P = torch.full((n, h, w, 2 * taps), float("nan"), device=DEV)
+    O.conv2d(nhwc(x).half(), wp, kpad, 256, 3, 3, bias=b1.contiguous(), act="relu", out=P, epi="tapproj",
+             tapw=tapw, taps=taps, tile_cfg=cfg)
+    flow = flow0.clone()
+    O.tapproj_stencil(P, taps, oc, b2.contiguous(), flow)
+    torch.cuda.synchronize()
+    assert rel_err(flow - flow0, ref - flow0) < 3e-3
+    with pytest.raises(RuntimeError):
+        O.conv2d(nhwc(x).half(), wp, kpad, 256, 3, 3, bias=b1.contiguous(), act="relu", out=P, epi="tapproj",
+                 tapw=tapw, taps=taps, tile_cfg=5)
+
+
 def test_conv2d_flow_acc_and_stats():
     O = ops()
     torch.manual_seed(4)
