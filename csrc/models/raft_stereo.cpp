@@ -366,11 +366,12 @@ void RaftStereo::build(WeightSource& src) {
 }
 
 void RaftStereo::gru(hipStream_t s, int i, const std::vector<Tensor>& x) const {
-  // the coarse levels of the mode-2 pipeline run beside the finest level's chain (side2): at batch <= 2 their
-  // small-grid convs are tuned for co-residency (decided by the configuration alone, so the eager tuning pass and
-  // the capture agree).  Same-process A/B: b1 8.438 -> 7.991 ms; at b8 (large grids) it cost 1.6 %, so not there.
-  const int pm = pipeline_mode_ >= 0 ? pipeline_mode_ : 2;
-  ScopedSideBranch sb(par_ && i >= 1 && B() <= 2 && rc_.n_gru == 3 && !rc_.slow_fast && pm == 2 && m2_main_);
+  // the coarse levels of the default schedule (mode-2 pipeline) run beside the finest level's chain (side2): at
+  // batch <= 2 their small-grid convs are tuned for co-residency.  Decided by the preset and batch alone -- not by
+  // the schedule knobs -- so the eager tuning pass and the capture agree and every schedule runs the same tactics
+  // (tests/test_raft_modes_gpu.py: bitwise-equal schedules).  Same-process A/B: b1 8.438 -> 7.991 ms; at b8 (large
+  // grids) it cost 1.6 %, so not there.
+  ScopedSideBranch sb(i >= 1 && B() <= 2 && rc_.n_gru == 3 && !rc_.slow_fast);
   std::vector<Tensor> srcs = {net_[i]};
   srcs.insert(srcs.end(), x.begin(), x.end());
   if (gru_split_) {
