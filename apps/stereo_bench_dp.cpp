@@ -15,14 +15,30 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <fstream>
+#include <iterator>
+#include <memory>
 #include <random>
 #include <string>
 #include <vector>
 
 #include "sa/dist.h"
 #include "sa/engine.h"
+#include "sa/runtime.h"
 
 namespace {
+std::string read_file(const std::string& path) {
+  if (path.empty()) return std::string();
+  std::ifstream f(path, std::ios::binary);
+  return std::string((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+}
+
+uint32_t fnv32(const std::string& s) {
+  uint32_t h = 2166136261u;
+  for (unsigned char c : s) h = (h ^ c) * 16777619u;
+  return h;
+}
+
 struct Args {
   std::string model = "raftstereo-sceneflow";
   int batch = 8, steps = 10, warmup = 3, nproc = 0, height = 480, width = 640;
@@ -39,7 +55,34 @@ int run_rank(const Args& a) {
     cfg.width = a.width;
     cfg.batch = a.batch;
     cfg.device = dev;
-    auto eng = sa::StereoEngine::create(cfg);
+    // Every rank runs rank 0's tactic plan: rank 0 builds (tuning each conv shape, saving its plan), broadcasts the
+    // plan file's bytes over RCCL, and the other ranks merge them into their tactic table before building, so no
+    // shape is timed twice and no rank picks a different kernel on noisy timings (the job's step time is the slowest
+    // rank's).  A 32-bit hash of every rank's resulting plan file is compared (min == max over ranks).
+    hipStream_t bs = nullptr;
+    HIP_CHECK(hipStreamCreateWithFlags(&bs, hipStreamNonBlocking));
+    std::unique_ptr<sa::StereoEngine> eng;
+    std::string plan;
+    if (env.rank == 0) {
+      eng = sa::StereoEngine::create(cfg);
+      plan = read_file(eng->plan_path());
+    }
+    comm.broadcast_bytes(plan, 0, bs);
+    if (env.rank != 0) {
+      if (!plan.empty()) {
+        const std::string tmp = "/tmp/sa_plan_rank" + std::to_string(env.rank) + "_" + std::to_string(getpid());
+        {
+          std::ofstream f(tmp, std::ios::binary);
+          f.write(plan.data(), (std::streamsize)plan.size());
+        }
+        sa::conv_plan_load(tmp);
+        std::remove(tmp.c_str());
+      }
+      eng = sa::StereoEngine::create(cfg);
+    }
+    const double ph = (double)fnv32(read_file(eng->plan_path()));
+    const bool plans_same = comm.allreduce_max(ph, bs) == -comm.allreduce_max(-ph, bs);
+    HIP_CHECK(hipStreamDestroy(bs));
     const size_t img = (size_t)a.batch * a.height * a.width * 3;
     std::vector<uint8_t> hl(img), hr(img);
     std::mt19937 rng(1234 + env.rank);
@@ -74,10 +117,10 @@ int run_rank(const Args& a) {
           "{\"metric\": \"%s %dx%d throughput (frames/s, whole job)\", \"value\": %.3f, \"unit\": \"frames/s\", "
           "\"n_gpus\": %d, \"steps\": %d, \"warmup\": %d, \"ms_per_step\": %.3f, \"higher_is_better\": true, "
           "\"scaling\": \"weak\", \"dtype\": \"fp16\", \"data\": \"synthetic\", \"runner\": \"native-rccl\", "
-          "\"finite\": %s, \"config\": {\"model\": \"%s\", \"global_batch\": %d, \"per_gpu_batch\": %d, "
+          "\"finite\": %s, \"plans_identical_across_ranks\": %s, \"tuned_shapes_rank0\": %ld, \"config\": {\"model\": \"%s\", \"global_batch\": %d, \"per_gpu_batch\": %d, "
           "\"parallelism\": \"dp%d\"}}\n",
           a.model.c_str(), a.height, a.width, fps, env.world, a.steps, a.warmup, dt / a.steps * 1e3,
-          finite ? "true" : "false", a.model.c_str(), env.world * a.batch, a.batch, env.world);
+          finite ? "true" : "false", plans_same ? "true" : "false", eng->tuned_shapes(), a.model.c_str(), env.world * a.batch, a.batch, env.world);
       std::fflush(stdout);
     }
     HIP_CHECK(hipFree(dl));

@@ -219,17 +219,22 @@ def main(argv=None) -> int:
                                 timeout=timedelta(seconds=int(os.environ.get("SA_DIST_TIMEOUT", "600"))), **kw)
         assert dist.get_world_size() == world and dist.get_rank() == rank
 
-    from stereoalgorithms_amd.parallel.dp import DataParallelStereo, H2DPrefetcher
+    from stereoalgorithms_amd.parallel.dp import DataParallelStereo, H2DPrefetcher, build_engine_shared_plan
     from stereoalgorithms_amd.utils.synthetic import batch_pairs
 
     B, H, W = args.per_gpu_batch, args.height, args.width
     Q = np.array([[1, 0, 0, -W / 2], [0, 1, 0, -H / 2], [0, 0, 0, 500.0], [0, 0, 1 / 60.0, 0]], np.float32)
+    plan_digests = None
     if cpu:
         eng = OracleEngine(args.model, H, W, B, args.iters, seed=0)
         eng.set_Q(Q)
     else:
         from stereoalgorithms_amd.models.engine import NativeStereoEngine
-        eng = NativeStereoEngine(args.model, None, H, W, batch=B, iters=args.iters, device=dev.index, seed=0)
+        # every rank runs rank 0's tactic plan (rank 0 tunes, the others build from its broadcast plan bytes), so
+        # no rank's noisy timing picks a slower kernel that would set the job's step time
+        eng, plan_digests = build_engine_shared_plan(
+            lambda: NativeStereoEngine(args.model, None, H, W, batch=B, iters=args.iters, device=dev.index, seed=0),
+            world if (world > 1 or force_gather) else 1, rank)
         eng.set_Q(Q)
     # every rank reprojects its frames' point clouds in the frame graph and keeps them (the reference produces a
     # cloud per frame inside its timed region, RAFTStereo/src/TRTRAFTStereo.cpp:140-144)
@@ -284,7 +289,8 @@ def main(argv=None) -> int:
     sync()
     dt = time.perf_counter() - t0
     gather_ms = None
-    ranks = [{"rank": rank, "device": str(dev), "host": socket.gethostname()}]
+    ranks = [{"rank": rank, "device": str(dev), "host": socket.gethostname(),
+              "plan_tactics": None if plan_digests is None else plan_digests[min(rank, len(plan_digests) - 1)]}]
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -409,7 +415,8 @@ def main(argv=None) -> int:
                              "device_bytes": dev_b1,
                              "host_split_ms_last_frame": host_split,
                              "weights": "scale_init (parity-tested graph)" if wpath else "seeded default init",
-                             "plan_loaded": e1.plan_status["loaded"], "plan_saved": e1.plan_status["saved"],
+                             "plan_loaded": e1.plan_status["loaded"], "plan_state": e1.plan_status["state"],
+                             "plan_saved": e1.plan_status["saved"], "plan_tactics": e1.plan_status["tactics"],
                              "device_stages_ms": {k: round(v, 3) for k, v in e1.stage_times()}}
             e1.close()
     if eng is not None:
@@ -447,6 +454,7 @@ def main(argv=None) -> int:
             "allgather_bytes_per_rank": B * H * W * 4,
             "point_clouds": f"per rank [{B},{H},{W},6] fp32 XYZRGB, reprojected in the frame graph, kept local",
             "plan": None if cpu else plan_b8,
+            "plans_identical_across_ranks": None if plan_digests is None else len(set(plan_digests)) == 1,
             "device_bytes": dev_bytes_b8,
             "latency_b1": extra,
         }

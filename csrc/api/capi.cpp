@@ -94,9 +94,13 @@ void sa_engine_host_buffers(void* e, void** left, void** right, float** disp, fl
   static_cast<sa::StereoEngine*>(e)->host_buffers((uint8_t**)left, (uint8_t**)right, disp, cloud);
 }
 int sa_engine_host_times(void* e, float* out, int max) {
-  const float* t = static_cast<sa::StereoEngine*>(e)->host_times();
+  // the device-side split (h2d / graph / d2h) exists only for engines created with SA_HOST_TIMES=1; without it
+  // only the 4 host-clock entries are returned, so unmeasured device times are never reported as 0
+  auto* eng = static_cast<sa::StereoEngine*>(e);
+  const float* t = eng->host_times();
+  const int avail = eng->host_times_device() ? 7 : 4;
   int n = 0;
-  for (; n < max && n < 7; ++n) out[n] = t[n];
+  for (; n < max && n < avail; ++n) out[n] = t[n];
   return n;
 }
 void* sa_engine_copy_stream(void* e) { return static_cast<sa::StereoEngine*>(e)->copy_stream(); }
@@ -139,6 +143,9 @@ int sa_conv_plan_save(const char* file, const char* keys) {
   return sa::conv_plan_save(file, k);
 }
 int sa_conv_plan_load(const char* file) { return sa::conv_plan_load(file); }
+void sa_conv_plan_cache_append(const char* key, int cfg, int splitk, float us) {
+  sa::conv_plan_cache_append(key, cfg, splitk, us);
+}
 long sa_conv_plan_entries(void) { return (long)sa::conv_plan_entries(); }
 
 void* sa_engine_stream(void* e) { return (void*)static_cast<sa::StereoEngine*>(e)->export_stream(); }

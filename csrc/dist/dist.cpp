@@ -203,6 +203,27 @@ double Communicator::allreduce_max(double v, hipStream_t s) {
   return v;
 }
 
+void Communicator::broadcast_bytes(std::string& data, int root, hipStream_t s) {
+  double len = env_.rank == root ? (double)data.size() : 0.0;
+  HIP_CHECK(hipMemcpyAsync(scratch_, &len, sizeof(len), hipMemcpyHostToDevice, s));
+  enqueue_ok(ncclBroadcast(scratch_, scratch_, 1, ncclDouble, root, (ncclComm_t)comm_, s), "ncclBroadcast(len)");
+  HIP_CHECK(hipMemcpyAsync(&len, scratch_, sizeof(len), hipMemcpyDeviceToHost, s));
+  wait_stream(s);
+  const size_t n = (size_t)len;
+  if (n == 0) {
+    data.clear();
+    return;
+  }
+  char* buf = nullptr;
+  HIP_CHECK(hipMalloc((void**)&buf, n));
+  if (env_.rank == root) HIP_CHECK(hipMemcpyAsync(buf, data.data(), n, hipMemcpyHostToDevice, s));
+  enqueue_ok(ncclBroadcast(buf, buf, n, ncclChar, root, (ncclComm_t)comm_, s), "ncclBroadcast(bytes)");
+  data.resize(n);
+  HIP_CHECK(hipMemcpyAsync(&data[0], buf, n, hipMemcpyDeviceToHost, s));
+  wait_stream(s);
+  HIP_CHECK(hipFree(buf));
+}
+
 void Communicator::wait_stream(hipStream_t s) {
   const auto deadline = Clock::now() + std::chrono::seconds(env_.timeout_s);
   for (;;) {

@@ -35,7 +35,8 @@ long sa_conv_tune_rejects(void);
 void sa_conv_plan_clear(void);
 void sa_conv_plan_put(const char* key, int cfg, int splitk, float us);
 int sa_conv_plan_save(const char* file, const char* keys);  // keys newline-separated; 0 or errno
-int sa_conv_plan_load(const char* file);                    // entries added, -1 absent, -2 another build / no header
+int sa_conv_plan_load(const char* file);                    // entries in the file, -1 absent, -2 another build / no header
+void sa_conv_plan_cache_append(const char* key, int cfg, int splitk, float us);  // SA_PLAN_CACHE append
 long sa_conv_plan_entries(void);
 // per-stage device times of the last frame (SA_STAGE_TIMES=1): returns the count (<= max), fills
 // ms[i] and names[i] (pointers valid for the engine's lifetime)

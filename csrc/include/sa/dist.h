@@ -51,6 +51,9 @@ class Communicator {
   void all_gather(const void* send, void* recv, size_t bytes, hipStream_t s);
   // max over ranks of a host double (blocking, bounded by the timeout)
   double allreduce_max(double v, hipStream_t s);
+  // host bytes of rank `root` -> every rank's `data` (length first, then the bytes; two ncclBroadcasts on `s`,
+  // blocking).  Used to hand rank 0's tuned tactic plan to every rank before they build their engines.
+  void broadcast_bytes(std::string& data, int root, hipStream_t s);
   void barrier(hipStream_t s);
   // Host wait for `s` with async-error polling and the deadline; throws (after abort) on failure.
   void wait_stream(hipStream_t s);

@@ -76,6 +76,7 @@ class StereoEngine {
   // ms of the last run_host: [0] whole timed region, [1] input copies, [2] enqueue, [3] device wait + output
   // copies; with SA_HOST_TIMES=1 at engine creation also the device-side [4] H2D, [5] frame graph, [6] D2H
   const float* host_times() const { return host_times_; }
+  bool host_times_device() const { return host_ev_[0] != nullptr; }  // SA_HOST_TIMES=1 split measured
 
   hipStream_t stream() const { return stream_; }
   // The engine stream handed to a caller that makes it its current stream (bench.py's data-parallel step): like

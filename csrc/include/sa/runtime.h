@@ -187,6 +187,8 @@ void conv_plan_set_arch(const std::string& gcn_arch_name);  // plan keys carry t
 const std::string& conv_plan_arch();
 // merge a plan file; returns entries added, -1 if absent, -2 if it was written by another library build
 int conv_plan_load(const std::string& file);
+// append one entry to the SA_PLAN_CACHE file (header written when the file is new, foreign or was deleted)
+void conv_plan_cache_append(const std::string& key, int cfg, int splitk, float us);
 // write the plan entries of `keys` (atomic rename); 0 or the errno of the failing step
 int conv_plan_save(const std::string& file, const std::vector<std::string>& keys);
 const std::string& conv_plan_build_id();  // hash of the loaded kernel library (plan files carry it)

@@ -438,6 +438,11 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
       wrow[j] = reinterpret_cast<const f16*>(p.weight) + (size_t)(n0 + row) * p.Kpad + lch * 8;
     }
     const void* zero_src = g_zero16;
+#ifdef SA_EXP_HALO_NODMA
+#define SA_HALO_GLDS(g, l, n, o, x) asm volatile("" ::"v"(g))
+#else
+#define SA_HALO_GLDS __builtin_amdgcn_global_load_lds
+#endif
     auto issue_a = [&](int c, int buf) {
       const int ci = c << 6;
       const f16* sp;
@@ -450,7 +455,7 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
 #pragma unroll
       for (int i = 0; i < NAH; ++i) {
         const void* g = aok[i] ? (const void*)(sp + (size_t)apix[i] * sst + alch[i]) : zero_src;
-        __builtin_amdgcn_global_load_lds(g, (lds_void_t*)(dst + (wave * NAH + i) * 1024), 16, 0, 0);
+        SA_HALO_GLDS(g, (lds_void_t*)(dst + (wave * NAH + i) * 1024), 16, 0, 0);
       }
     };
     auto issue_b = [&](int st, int buf) {
@@ -459,9 +464,24 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
       char* dst = bbuf0 + buf * BST;
 #pragma unroll
       for (int j = 0; j < NB; ++j)
-        __builtin_amdgcn_global_load_lds((const void*)(wrow[j] + koff), (lds_void_t*)(dst + (wave * NB + j) * 1024), 16,
+        SA_HALO_GLDS((const void*)(wrow[j] + koff), (lds_void_t*)(dst + (wave * NB + j) * 1024), 16,
                                          0, 0);
     };
+#ifdef SA_EXP_HALO_NOREAD
+#define SA_HALO_LD(p) (__extension__({ half8 v_; asm volatile("" : "=v"(v_)); v_; }))
+#else
+#define SA_HALO_LD(p) (*reinterpret_cast<const half8*>(p))
+#endif
+#ifdef SA_EXP_HALO_NOBAR
+#define SA_HALO_BAR() do { } while (0)
+#else
+#define SA_HALO_BAR() __builtin_amdgcn_s_barrier()
+#endif
+#ifdef SA_EXP_HALO_NOMFMA
+#define SA_HALO_MFMA(a, b, c, x, y, z) (__extension__({ asm volatile("" :: "v"(a), "v"(b)); (c); }))
+#else
+#define SA_HALO_MFMA __builtin_amdgcn_mfma_f32_16x16x32_f16
+#endif
     const int frow = lane & 15;
     // A fragment rows of this wave: output pixel (py, px) of fragment i, lane row frow
     int aq0[C::FM];
@@ -499,25 +519,25 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
     auto frag_addr_b = [&](int st, int j, int kk) { return bbuf0 + (st % 3) * BST + boff[j][kk]; };
     auto read_half = [&](int st, int kk, half8* af, half8* bf) {
 #pragma unroll
-      for (int i = 0; i < C::FM; ++i) af[i] = *reinterpret_cast<const half8*>(frag_addr_a(st, i, kk));
+      for (int i = 0; i < C::FM; ++i) af[i] = SA_HALO_LD(frag_addr_a(st, i, kk));
 #pragma unroll
-      for (int j = 0; j < C::FN; ++j) bf[j] = *reinterpret_cast<const half8*>(frag_addr_b(st, j, kk));
+      for (int j = 0; j < C::FN; ++j) bf[j] = SA_HALO_LD(frag_addr_b(st, j, kk));
     };
     auto mfma_half = [&](const half8* af, const half8* bf) {
 #pragma unroll
       for (int i = 0; i < C::FM; ++i)
 #pragma unroll
         for (int j = 0; j < C::FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = SA_HALO_MFMA(af[i], bf[j], acc[i][j], 0, 0, 0);
     };
     // the MFMAs of one k-half with the fragment reads of another interleaved one read per MFMA (as kGlds3)
     auto mfma_read = [&](const half8* am, const half8* bm, int st, int kk, half8* ar, half8* br) {
 #pragma unroll
       for (int tt = 0; tt < C::FM * C::FN; ++tt) {
         const int i = tt / C::FN, j = tt - (tt / C::FN) * C::FN;
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(am[i], bm[j], acc[i][j], 0, 0, 0);
-        if (tt < C::FM) ar[tt] = *reinterpret_cast<const half8*>(frag_addr_a(st, tt, kk));
-        else if (tt < C::FM + C::FN) br[tt - C::FM] = *reinterpret_cast<const half8*>(frag_addr_b(st, tt - C::FM, kk));
+        acc[i][j] = SA_HALO_MFMA(am[i], bm[j], acc[i][j], 0, 0, 0);
+        if (tt < C::FM) ar[tt] = SA_HALO_LD(frag_addr_a(st, tt, kk));
+        else if (tt < C::FM + C::FN) br[tt - C::FM] = SA_HALO_LD(frag_addr_b(st, tt - C::FM, kk));
       }
       static_assert(C::FM + C::FN <= C::FM * C::FN, "one read per MFMA slot");
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -548,7 +568,7 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
     else if (after0 >= 2 * NB) wait_vmcnt<2 * NB>();
     else if (after0 >= NB) wait_vmcnt<NB>();
     else wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
+    SA_HALO_BAR();
     asm volatile("" ::: "memory");
     half8 a0[C::FM], b0[C::FN], a1[C::FM], b1[C::FN];
     read_half(s0, 0, a0, b0);
@@ -561,7 +581,7 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
         else if (prev >= NB) wait_vmcnt<NB>();
         else if (prev >= NAH) wait_vmcnt<NAH>();
         else wait_vmcnt<0>();
-        __builtin_amdgcn_s_barrier();
+        SA_HALO_BAR();
         asm volatile("" ::: "memory");
         mfma_read(a1, b1, st + 1, 0, a0, b0);
         const int c = st / 9, t = st - c * 9;
@@ -1987,8 +2007,10 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
     // partial sums per 128-channel n-tile: the tile configs with BN = 128 only
     const bool bn128 = cfg == 0 || cfg == 4 || cfg == 7 || cfg == 11 || cfg == 15 || cfg == 19 || (cfg >= 26 && cfg <= 29);
     if (!bn128) return -5;
-    if (!a->tapw || a->taps < 1 || a->taps > 18 || a->stats || a->up || a->gate || a->Cout % 128 ||
-        a->out_stride < (a->Cout / 128) * a->taps)
+    // exactly two 128-channel n-tile partials per pixel at stride 2 * taps: sa_tapproj_stencil sums q[0] + q[taps]
+    // (Cout 128 read unwritten partials, Cout 384 dropped the third)
+    if (!a->tapw || a->taps < 1 || a->taps > 18 || a->stats || a->up || a->gate || a->Cout != 256 ||
+        a->out_stride != 2 * a->taps)
       return -2;
   }
   switch (cfg) {

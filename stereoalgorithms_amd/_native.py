@@ -186,6 +186,7 @@ def _declare_dev(lib):
         "sa_conv_plan_put": (None, [C.c_char_p, _i, _i, _f]),
         "sa_conv_plan_save": (_i, [C.c_char_p, C.c_char_p]),
         "sa_conv_plan_load": (_i, [C.c_char_p]),
+        "sa_conv_plan_cache_append": (None, [C.c_char_p, _i, _i, _f]),
         "sa_conv_plan_entries": (C.c_long, []),
         "sa_conv2d_tile_lds": (_i, [_i]),
         "sa_tapproj_stencil": (_i, [_p, _i, _i, _p, _p, _i, _i, _i, _p]),

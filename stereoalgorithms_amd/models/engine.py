@@ -7,6 +7,7 @@ torch.distributed (RCCL) collectives in the data-parallel path (``parallel.dp``)
 from __future__ import annotations
 
 import ctypes as C
+import sys
 
 import numpy as np
 import torch
@@ -18,6 +19,26 @@ MODEL_PRESETS = (
     "crestereo-iter2", "crestereo-iter5", "crestereo-iter10",
     "hitnet-d400", "hitnet-xl", "fastacvnet-plus",
 )
+
+
+class _NativeHandle:
+    """Owner of the native engine handle.  The engine holds one reference and every host_buffers() view holds
+    another, so the native engine (whose pinned staging those views alias) is destroyed when the LAST of them goes:
+    close() with views outstanding defers the free instead of leaving the views dangling."""
+
+    def __init__(self, lib, h):
+        self.lib, self.h = lib, h
+
+    def destroy(self):
+        if self.h:
+            self.lib.sa_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.destroy()
+        except Exception:
+            pass
 
 
 class NativeStereoEngine:
@@ -32,6 +53,7 @@ class NativeStereoEngine:
         if not h:
             raise RuntimeError(f"engine creation failed: {lib.sa_last_error().decode()}")
         self._h = h
+        self._owner = _NativeHandle(lib, h)
         self.model = model
         self.has_q = False
 
@@ -43,9 +65,13 @@ class NativeStereoEngine:
         return self._h
 
     def close(self):
+        """Release the engine.  The native engine is destroyed now unless host_buffers() views are still alive, in
+        which case it goes with the last of them (the engine object itself is unusable either way)."""
         if getattr(self, "_h", None):
-            self._lib.sa_engine_destroy(self._h)
             self._h = None
+            owner, self._owner = self._owner, None
+            if sys.getrefcount(owner) <= 2:  # only this frame's reference: no views outstanding
+                owner.destroy()
 
     def __del__(self):  # pragma: no cover - best effort
         try:
@@ -95,12 +121,16 @@ class NativeStereoEngine:
 
     @property
     def plan_status(self) -> dict:
-        """Tuned-plan cache at build: path, entries loaded (-1 absent, -2 written by another library build, -3 not
-        consulted), save result (0 ok, errno of a failed write, -1 not attempted) and the library build id."""
+        """Tuned-plan cache at build: path, entries the file held (-1 absent, -2 written by another library build, -3
+        not consulted), ``state`` (utils.plan.plan_state: absent / foreign-build / empty / loaded / not-consulted),
+        save result (0 ok, errno of a failed write, -1 not attempted), the library build id and ``tactics``, the
+        digest of the plan's tactic choices (utils.plan.tactic_digest: equal digests = identical kernels)."""
+        from stereoalgorithms_amd.utils.plan import plan_state, tactic_digest
         ld, sv = C.c_int(0), C.c_int(0)
         self._lib.sa_engine_plan_status(self._live, C.byref(ld), C.byref(sv))
-        return {"path": self.plan_path, "loaded": ld.value, "saved": sv.value, "tuned_shapes": self.tuned_shapes,
-                "build": self._lib.sa_plan_build_id().decode()}
+        return {"path": self.plan_path, "loaded": ld.value, "state": plan_state(ld.value), "saved": sv.value,
+                "tuned_shapes": self.tuned_shapes, "build": self._lib.sa_plan_build_id().decode(),
+                "tactics": tactic_digest(self.plan_path)}
 
     def nonzero_splitk_counters(self) -> int:
         """Diagnostic: split-K tile counters left non-zero (0 after every correctly ordered frame)."""
@@ -157,7 +187,9 @@ class NativeStereoEngine:
 
         def view(p, shape, ctype, dtype):
             n = int(np.prod(shape))
-            return np.ctypeslib.as_array((ctype * n).from_address(p.value)).view(dtype).reshape(shape)
+            arr = (ctype * n).from_address(p.value)
+            arr._sa_owner = self._owner  # the numpy view's base keeps the native engine alive (see close)
+            return np.ctypeslib.as_array(arr).view(dtype).reshape(shape)
         return {"left": view(ptrs[0], (b, h, w, 3), C.c_uint8, np.uint8),
                 "right": view(ptrs[1], (b, h, w, 3), C.c_uint8, np.uint8),
                 "disp": view(ptrs[2], (b, h, w), C.c_float, np.float32),

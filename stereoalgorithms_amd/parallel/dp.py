@@ -254,3 +254,67 @@ class H2DPrefetcher:
         """Just-in-time form: copy this step's inputs and hand them out."""
         self.prefetch(host_tensors)
         return self.next()
+
+
+def _native_plan_load(path: str) -> int:
+    """Merge a plan file into this process's tactic table (libstereo_amd.so, no device needed)."""
+    from stereoalgorithms_amd import _native as N
+    return int(N.dev().sa_conv_plan_load(str(path).encode()))
+
+
+def build_engine_shared_plan(make_engine, world: int, rank: int, load_plan=None):
+    """Build one engine per rank so that EVERY rank launches the tactics rank 0 tuned (ranks that
+    tune independently pick different kernels on noisy timings, and the job's step time is the slowest rank's).
+
+    Rank 0 builds first -- timing each conv shape and saving its plan file -- while the other ranks wait in the
+    broadcast of that file's bytes; each then merges the bytes into its own process tactic table (``load_plan``,
+    default the native ``sa_conv_plan_load``) and builds, finding every shape already planned (no timing, no
+    divergence), and saves the same entries under its own plan path.  Works across nodes (bytes travel over the
+    process group, not a shared file system).
+
+    Returns ``(engine, digests)``: ``digests[r]`` is rank r's ``utils.plan.tactic_digest`` of its plan file after the
+    build (all equal when the plans agree; callers assert or report it)."""
+    import os
+    import tempfile
+    from stereoalgorithms_amd.utils.plan import tactic_digest
+
+    def digest_of(eng):
+        return tactic_digest(getattr(eng, "plan_path", "") or "")
+
+    if world <= 1:
+        eng = make_engine()
+        return eng, [digest_of(eng)]
+    box = [None]
+    if rank == 0:
+        eng = make_engine()
+        path = getattr(eng, "plan_path", "") or ""
+        with open(path, "rb") if path and os.path.exists(path) else _empty() as f:
+            box = [f.read()]
+    dist.broadcast_object_list(box, src=0)
+    if rank != 0:
+        data = box[0]
+        if data:
+            fd, tmp = tempfile.mkstemp(suffix=".plan")
+            try:
+                with os.fdopen(fd, "wb") as f:
+                    f.write(data)
+                (load_plan or _native_plan_load)(tmp)
+            finally:
+                os.unlink(tmp)
+        eng = make_engine()
+    digests = [None] * world
+    dist.all_gather_object(digests, digest_of(eng))
+    return eng, digests
+
+
+class _empty:
+    """Context manager standing in for an absent plan file (read() -> b'')."""
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+    def read(self):
+        return b""

@@ -32,3 +32,30 @@ def read_plan(path) -> tuple[str | None, list[PlanEntry]]:
             key, cfg, sk, us = line.rsplit(" ", 3)
             entries.append(PlanEntry(key, int(cfg), int(sk), float(us)))
     return build, entries
+
+
+def tactic_digest(path) -> str | None:
+    """16-hex digest of a plan's tactic CHOICES: the sorted (key, cfg, splitk) triples plus the build id (timings
+    excluded).  Two processes -- or two ranks of a DP job -- with equal digests launch identical kernels for every
+    conv shape.  None when the file does not exist."""
+    import hashlib
+    import os
+    if not path or not os.path.exists(path):
+        return None
+    build, entries = read_plan(path)
+    h = hashlib.sha256((build or "").encode())
+    for e in sorted(entries, key=lambda e: e.key):
+        h.update(f"\n{e.key} {e.cfg} {e.splitk}".encode())
+    return h.hexdigest()[:16]
+
+
+PLAN_STATES = {-3: "not-consulted", -2: "foreign-build", -1: "absent"}
+
+
+def plan_state(loaded: int) -> str:
+    """The engine's plan-file outcome at build (sa_engine_plan_status 'loaded'): 'absent' (no file, every shape
+    tuned), 'foreign-build' (written by another library build, ignored), 'empty' (file found, no entries),
+    'loaded' (file found with entries), 'not-consulted' (tuning disabled)."""
+    if loaded in PLAN_STATES:
+        return PLAN_STATES[loaded]
+    return "empty" if loaded == 0 else "loaded"

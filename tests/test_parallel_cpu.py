@@ -181,3 +181,84 @@ def test_dp_point_clouds_per_rank_gloo():
     for p in procs:
         p.join(timeout=60)
     assert all(res[r] for r in range(world)), res
+
+
+class _TunedEngine:
+    """Stand-in for an engine build's tactic selection: shapes missing from the process's plan table are 'timed'
+    with rank-dependent noise (seeded by rank), i.e. independent tuning picks different tactics on every rank; the
+    chosen plan is saved to this rank's own plan path (as the native engine saves <stem>_b8_..._gfx950.plan)."""
+    table: dict = {}
+    SHAPES = [f"gfx950|{n},120,160,384|k3x3|shape{i}" for i, n in enumerate((1, 8, 8, 1, 8, 2))]
+
+    def __init__(self, plan_dir, rank):
+        import random
+        rng = random.Random(1000 + 17 * rank)
+        self.tuned_shapes = 0
+        for k in self.SHAPES:
+            if k not in self.table:
+                self.table[k] = (rng.choice([4, 10, 26, 28]), rng.choice([0, 1]), round(rng.uniform(20, 300), 2))
+                self.tuned_shapes += 1
+        d = os.path.join(plan_dir, f"rank{rank}")
+        os.makedirs(d, exist_ok=True)
+        self.plan_path = os.path.join(d, "raftstereo-sceneflow_seed0_b8_480x640_it-1_gfx950.plan")
+        with open(self.plan_path, "w") as f:
+            f.write("# sa-plan build=00000000feedbeef\n")
+            for k in self.SHAPES:
+                cfg, sk, us = self.table[k]
+                f.write(f"{k} {cfg} {sk} {us}\n")
+
+
+def _fake_plan_load(path):
+    from stereoalgorithms_amd.utils.plan import read_plan
+    _, entries = read_plan(path)
+    for e in entries:
+        _TunedEngine.table[e.key] = (e.cfg, e.splitk, e.us)
+    return len(entries)
+
+
+def _worker_plan(rank, world, port, plan_dir, shared, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        if shared:
+            eng, digests = dp.build_engine_shared_plan(lambda: _TunedEngine(plan_dir, rank), world, rank,
+                                                       load_plan=_fake_plan_load)
+        else:
+            from stereoalgorithms_amd.utils.plan import tactic_digest
+            eng = _TunedEngine(plan_dir, rank)
+            digests = [None] * world
+            dist.all_gather_object(digests, tactic_digest(eng.plan_path))
+        with open(eng.plan_path, "rb") as f:
+            data = f.read()
+        q.put((rank, (digests, eng.tuned_shapes, data)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_plan_job(world, tmp_path, shared):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_plan, args=(r, world, port, str(tmp_path), shared, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    return res
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_ranks_share_rank0_plan_gloo(world, tmp_path):
+    """rank 0 tunes and every other rank builds from rank 0's plan bytes (broadcast over the
+    process group), so all ranks' plan files are byte-identical, their tactic digests agree, and no rank but 0
+    times a shape.  Negative control: independent tuning (rank-seeded timing noise) gives different plans."""
+    res = _run_plan_job(world, tmp_path / "shared", shared=True)
+    digests0 = res[0][0]
+    assert len(set(digests0)) == 1 and digests0[0] is not None, digests0
+    assert all(res[r][0] == digests0 for r in range(world))
+    assert res[0][1] == len(_TunedEngine.SHAPES)
+    assert all(res[r][1] == 0 for r in range(1, world)), {r: res[r][1] for r in res}
+    assert all(res[r][2] == res[0][2] for r in range(world))
+    indep = _run_plan_job(world, tmp_path / "indep", shared=False)
+    assert len(set(indep[0][0])) > 1, "control: independently tuned ranks should disagree"

@@ -72,3 +72,49 @@ def test_tile_lds_footprints():
         assert 0 < lds[c] <= 81920, (c, lds[c])
     assert lds[3] < lds[0] and lds[5] < lds[4] and lds[16] <= 163840
     assert all(lds[c] == -1 for c in (22, 23, 24, 25, 99))
+
+
+def test_plan_cache_append_switches_files(tmp_path, monkeypatch):
+    """the SA_PLAN_CACHE appender verified the header once per PROCESS, so after switching to a
+    second cache file (one per test case) entries were appended without a header and every later load rejected the
+    file (-2).  The check is now keyed by path and repeated when the file was deleted."""
+    lib = _lib()
+    a, b = tmp_path / "a.plan", tmp_path / "b.plan"
+    monkeypatch.setenv("SA_PLAN_CACHE", str(a))
+    lib.sa_conv_plan_cache_append(KEYS[0].encode(), 26, 1, 41.5)
+    monkeypatch.setenv("SA_PLAN_CACHE", str(b))
+    lib.sa_conv_plan_cache_append(KEYS[1].encode(), 3, 0, 7.25)
+    lib.sa_conv_plan_cache_append(KEYS[0].encode(), 28, 1, 40.0)
+    build = lib.sa_plan_build_id().decode()
+    for f, n in ((a, 1), (b, 2)):
+        hdr, entries = read_plan(f)
+        assert hdr == build and len(entries) == n, (f, hdr, entries)
+        lib.sa_conv_plan_clear()
+        assert lib.sa_conv_plan_load(str(f).encode()) == n
+    # back to the first file after it was deleted: the header is written again
+    a.unlink()
+    monkeypatch.setenv("SA_PLAN_CACHE", str(a))
+    lib.sa_conv_plan_cache_append(KEYS[1].encode(), 3, 1, 6.0)
+    assert read_plan(a)[0] == build and lib.sa_conv_plan_load(str(a).encode()) == 1
+
+
+def test_plan_load_counts_file_entries_not_new_ones(tmp_path):
+    """loading a plan whose entries the process already holds (the second engine of the same
+    shapes) reports the file's entry count, so 'loaded 0' only ever means an empty file."""
+    lib = _lib()
+    lib.sa_conv_plan_put(KEYS[0].encode(), 26, 1, 41.5)
+    lib.sa_conv_plan_put(KEYS[1].encode(), 3, 0, 7.25)
+    p = tmp_path / "x.plan"
+    assert lib.sa_conv_plan_save(str(p).encode(), "\n".join(KEYS).encode()) == 0
+    assert lib.sa_conv_plan_load(str(p).encode()) == 2  # nothing new, still 2
+    empty = tmp_path / "empty.plan"
+    empty.write_text(f"# sa-plan build={lib.sa_plan_build_id().decode()}\n")
+    assert lib.sa_conv_plan_load(str(empty).encode()) == 0
+    from stereoalgorithms_amd.utils.plan import plan_state, tactic_digest
+    assert [plan_state(v) for v in (-3, -2, -1, 0, 5)] == ["not-consulted", "foreign-build", "absent", "empty", "loaded"]
+    d1 = tactic_digest(p)
+    q = tmp_path / "y.plan"  # same choices, other timings: same digest; another choice: different digest
+    q.write_text(p.read_text().replace("41.5", "39"))
+    assert tactic_digest(q) == d1
+    q.write_text(p.read_text().replace(" 26 1 ", " 28 1 "))
+    assert tactic_digest(q) != d1 and tactic_digest(tmp_path / "none.plan") is None
