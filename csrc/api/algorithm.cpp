@@ -33,6 +33,11 @@ bool resolve_model_spec(const std::string& spec, const std::string& default_pres
     err = "ONNX/TensorRT model files are not supported: pass a .safetensors weights file or a preset name "
           "(e.g. \"raftstereo-realtime\")";
     return false;
+  } else if (ends_with(spec, ".pth") || ends_with(spec, ".ckpt") || ends_with(spec, ".pt") || ends_with(spec, ".tar")) {
+    err = "PyTorch checkpoints are not loaded natively (unpickling executes code): convert once with "
+          "\"python -m stereoalgorithms_amd.utils.import_ckpt " + spec + " <out>.safetensors\" and pass the "
+          ".safetensors file";
+    return false;
   } else if (!spec.empty()) {
     preset = spec;
   } else {

@@ -17,6 +17,7 @@
 #include <hip/hip_fp16.h>
 
 #include <cstdlib>
+#include <type_traits>
 
 #include "sa/kernels.h"
 
@@ -93,19 +94,41 @@ enum : int {
                  // ~6 VALU per fragment address (3.7 VALU per MFMA on the b8 GRU conv, PMC) and 2-way conflicts
                  // on odd tap shifts (SQ_LDS_BANK_CONFLICT above the LDS instruction count)
   kHaloP16 = 12,  // kHaloP with 16 x 16 output patches
+  kHaloW = 13,    // wide halo tile for the batch-8 GRU / flow-head convs: a 16 x 32 output patch (512 pixels) x 128
+                  // channels, 8 waves of 128 x 64 (v_mfma_f32_16x16x32_f16, 8 x 4 fragments: 0.375 LDS reads per
+                  // MFMA instead of 0.5), K in 32-channel chunks (step = chunk, tap; K = 32 per step), the input
+                  // patch 18 x 34 x 32 stored planar (4 planes of 8 channels, as kHaloP) in two 40 KB buffers and a
+                  // 6-deep ring of 8 KB weight stages (64-B rows, XOR-swizzled on the DMA source).  The weights --
+                  // most of the L2 -> LDS traffic of a 3x3 tile -- are shared by twice the pixels of kHaloP's
+                  // 256-pixel tile: 12.3 KB of DMA per 256x128x64 of MFMA work instead of 20.8
+  kHaloW12 = 14,  // kHaloW with 12 x 32 output patches (384 pixels, 8 waves of 96 x 64): 120-row feature maps tile
+                  // exactly (10 patch rows), no idle MFMA rows in the bottom patch
+  kHaloQ = 15,    // kHaloW's tile and LDS images with a PING-PONG schedule (cdna_hip_programming.md §5 "256² 8-phase
+                  // template", T3-T5): waves 0-3 (one per SIMD) and 4-7 run one barrier apart, each step is two
+                  // clusters of FM/2 x FN MFMAs, and every barrier interval one group issues its MFMA cluster while
+                  // the other reads its next cluster's fragments and issues DMA.  kHaloW runs both waves of a SIMD in
+                  // phase, so per step the pipe idles through the barrier, the DMA issue and the LDS drain of both
+                  // (ablation: the MFMA-free kernel took 75 % of the full kernel's time)
+  kHaloQ12 = 16,  // kHaloQ with 12 x 32 output patches
 };
 __host__ __device__ constexpr bool is_glds(int mode) { return mode == kGlds3 || mode == kGldsDeep; }
 __host__ __device__ constexpr bool is_halop(int mode) { return mode == kHaloP || mode == kHaloP16; }
+__host__ __device__ constexpr bool is_haloq(int mode) { return mode == kHaloQ || mode == kHaloQ12; }
+// kHaloW geometry (32-channel chunks, 16 x 32 / 12 x 32 patches, 6-deep 64-B-row weight ring): kHaloW and kHaloQ
+__host__ __device__ constexpr bool is_halow(int mode) {
+  return mode == kHaloW || mode == kHaloW12 || is_haloq(mode);
+}
 __host__ __device__ constexpr bool is_halo(int mode) {
-  return mode == kHalo || mode == kHalo16 || is_halop(mode);
+  return mode == kHalo || mode == kHalo16 || is_halop(mode) || is_halow(mode);
 }
 
 template <int BM, int BN, int WM, int WN, int MODE = kRegK32>
 struct ConvCfg {
   static constexpr bool WIDE = MODE == kWide;
   static constexpr bool PING = MODE == kPing;
-  static constexpr bool BANDED = WIDE || PING;  // C tile staged through LDS in row bands
-  static constexpr int BK = (MODE == kRegK32 || WIDE || PING) ? 32 : 64;
+  static constexpr bool HALOW = is_halow(MODE);
+  static constexpr bool BANDED = WIDE || PING || HALOW;  // C tile staged through LDS in row bands
+  static constexpr int BK = (MODE == kRegK32 || WIDE || PING || HALOW) ? 32 : 64;
   static constexpr int KCH = BK / 8;  // 16-byte chunks per row per stage
   static constexpr int TM = BM / WM, TN = BN / WN;
   // 16x16 fragment repeats (kWide keeps its own 32x32 accumulators: a 1x1 placeholder here)
@@ -121,7 +144,7 @@ struct ConvCfg {
   // the same)
   static constexpr int PING_NS = 147456 / (A_BYTES + B_BYTES) < 6 ? 147456 / (A_BYTES + B_BYTES) : 6;
   static constexpr bool HALO = is_halo(MODE);
-  static constexpr int NSTAGE = MODE == kGlds3 || HALO ? 3 : MODE == kGldsDeep ? DEEP_NS : PING ? PING_NS : (WIDE ? 4 : 2);
+  static constexpr int NSTAGE = is_haloq(MODE) ? 9 : HALOW ? 6 : MODE == kGlds3 || HALO ? 3 : MODE == kGldsDeep ? DEEP_NS : PING ? PING_NS : (WIDE ? 4 : 2);
   // kHalo: output patch TH x TW, input patch (TH+2) x (TW+2) pixels of 128 B (one 64-channel chunk) in 1-KB DMA
   // pieces of 8 pixels, HALO_NA pieces per wave; two patch buffers + a 3-deep ring of weight stages
   static constexpr int TW = (MODE == kHalo16 || MODE == kHaloP16) ? 16 : 32;
@@ -130,20 +153,25 @@ struct ConvCfg {
   // slots fill HALO_RPP / 8 DMA instructions of 64 lanes
   static constexpr bool HALOP = is_halop(MODE);
   static constexpr int HALO_RPP = (HALO_PIX + 15) / 16 * 16;
+  // kHaloW: 4 planes of 8 channels (a 32-channel chunk)
+  static constexpr int HALO_PLANES = HALOW ? 4 : 8;
+  static constexpr int HALO_CH = HALOW ? 32 : 64;  // channels per K chunk (a split launch cuts K at chunk boundaries)
   static constexpr int HALO_NA = !HALO ? 1
-                                 : HALOP ? (HALO_RPP / 8 + NW - 1) / NW
-                                         : ((HALO_PIX + 7) / 8 + NW - 1) / NW;
+                                 : (HALOP || HALOW) ? (HALO_RPP * HALO_PLANES / 64 + NW - 1) / NW
+                                                    : ((HALO_PIX + 7) / 8 + NW - 1) / NW;
   static constexpr int A_PATCH = HALO_NA * NW * 1024;
   static constexpr int STAGE_BYTES = HALO ? 2 * A_PATCH + NSTAGE * B_BYTES : NSTAGE * (A_BYTES + B_BYTES);
   // fp32 C tile, unpadded rows; columns XOR-swizzled in 16-float blocks (cswz) so the MFMA
   // write-out (4 row groups x 16 lanes) hits 64 distinct banks; aliases the stage buffers.
   // kWide stages it in bands of CROWS rows (128 KB of fp32 per band)
   static constexpr int CST = BN;
-  static constexpr int CROWS = BANDED ? (32768 / BN < BM ? 32768 / BN : BM) : BM;
+  // kHaloW: bands of whole wave rows (TM), 2 per band (128 KB at 16 x 32)
+  static constexpr int CROWS = HALOW ? 2 * TM : BANDED ? (32768 / BN < BM ? 32768 / BN : BM) : BM;
   static constexpr int C_BYTES = CROWS * CST * 4;
   static constexpr int SMEM = STAGE_BYTES > C_BYTES ? STAGE_BYTES : C_BYTES;
   static_assert(WM * WN == 4 || (WM * WN == 8 && (is_glds(MODE) || WIDE || PING || HALO)), "4 waves (8 for kGlds3; 4 or 8 for kWide) per workgroup");
-  static_assert(!HALO || (BM % TW == 0 && TM % 16 == 0 && TW % 16 == 0 && BK == 64), "halo tiles: 16-pixel fragments inside one output row");
+  static_assert(!HALO || (BM % TW == 0 && TM % 16 == 0 && TW % 16 == 0 && BK == (HALOW ? 32 : 64)), "halo tiles: 16-pixel fragments inside one output row");
+  static_assert(!HALOW || (WM == 4 && WN == 2 && TM % TW == 0), "kHaloW: 4 x 2 waves, whole patch rows per wave");
   static_assert(!PING || (WM == 2 && WN == 4 && BM == 256), "kPing: 2 x 4 waves, one 128-row half of the tile per wave group");
   static_assert(!is_glds(MODE) || NSTAGE >= 3, "DMA rings keep at least one stage in flight across the barrier");
   static_assert(TM % 16 == 0 && TN % 16 == 0, "wave tile must be 16-aligned");
@@ -169,6 +197,38 @@ __device__ __forceinline__ int swz64(int row, int c) { return row * 128 + ((c ^ 
 __device__ __attribute__((aligned(16))) const unsigned char g_zero16[64] = {0};
 
 typedef __attribute__((address_space(3))) void lds_void_t;
+
+// compile-time loop: f(std::integral_constant<int, I>{}) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// Ablation switches of the halo main loops (tools/exp_build.sh -DSA_EXP_HALO_...; timing experiments only, results
+// are wrong): no LDS DMA, no fragment reads, no barriers, no MFMAs
+#ifdef SA_EXP_HALO_NODMA
+#define SA_HALO_GLDS(g, l, n, o, x) asm volatile("" ::"v"(g))
+#else
+#define SA_HALO_GLDS __builtin_amdgcn_global_load_lds
+#endif
+#ifdef SA_EXP_HALO_NOREAD
+#define SA_HALO_LD(p) (__extension__({ half8 v_; asm volatile("" : "=v"(v_)); v_; }))
+#else
+#define SA_HALO_LD(p) (*reinterpret_cast<const half8*>(p))
+#endif
+#ifdef SA_EXP_HALO_NOBAR
+#define SA_HALO_BAR() do { } while (0)
+#else
+#define SA_HALO_BAR() __builtin_amdgcn_s_barrier()
+#endif
+#ifdef SA_EXP_HALO_NOMFMA
+#define SA_HALO_MFMA(a, b, c, x, y, z) (__extension__({ asm volatile("" :: "v"(a), "v"(b)); (c); }))
+#else
+#define SA_HALO_MFMA __builtin_amdgcn_mfma_f32_16x16x32_f16
+#endif
 
 #define SA_STR2(x) #x
 #define SA_STR(x) SA_STR2(x)
@@ -371,6 +431,331 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
       if (kt + 1 < nk) store_tile(cur ^ 1);
       __syncthreads();
     }
+  } else if constexpr (is_haloq(MODE)) {
+    // ---------------- kHaloQ: kHaloW's LDS images, ping-pong schedule ----------------
+    // Group g = wave >> 2 (waves 0-3 / 4-7: one wave of each group per SIMD).  Barrier interval n: group 0 is in the
+    // LOAD segment of step n / 2 (n even) or runs that step's MFMAs (n odd); group 1 the same one interval later (its
+    // extra barrier before the loop, and group 0's after it, keep the barrier counts equal), so on every SIMD one
+    // wave's FM x FN MFMA cluster (512 cycles at 16 x 32) runs beside the partner's LOAD segment.  Per step:
+    //   LOAD: DMA issue (patch(c + 1) at tap 1, then W(s + L)), all FM + FN fragment reads of the step, vmcnt wait
+    //         for W(s + 1); s_barrier
+    //   MFMA: lgkmcnt(0) (own reads), setprio 1, FM x FN MFMAs, setprio 0; s_barrier
+    // The loop runs per 32-channel chunk with its 9 taps unrolled and a 9-slot weight ring (slot = tap), so every
+    // LDS offset is an immediate and every vmcnt count a constant: past the K range the DMA issues continue as
+    // dummies (an in-range source into a slot / patch buffer no later step reads), keeping the counts static.
+    // (A first version with runtime step arithmetic ran ~150 SALU/VALU per wave and step: its MFMA-free ablation
+    // took 290 us of the 329 us zr8 conv; two 16-MFMA clusters per step were 15-20 % slower than one of 32.)
+    // RAW: W(s + 1) is waited for by EVERY wave in its LOAD(s), before the barrier that precedes group 0's LOAD(s + 1)
+    // (for group 0 one barrier early).  Patch(c + 1) is issued 8 steps before its first read and waited for from
+    // tap L on.  WAR: W(s + L) refills the slot of W(s + L - 9), read >= 3 steps back and consumed by an MFMA
+    // segment of every wave since; patch(c + 1) (tap 1 of chunk c) refills chunk c - 1's buffer, last read in step
+    // 9c - 1, likewise consumed since.
+    constexpr int TW = C::TW, PW = TW + 2, RP = C::HALO_PIX;
+    constexpr int NAH = C::HALO_NA, NS = C::NSTAGE, L = 6;
+    static_assert(NS == 9 && L <= NS - 3, "kHaloQ: one weight slot per tap, the refilled slot read >= 3 steps back");
+    constexpr int NB = BN * 4 / NT;
+    static_assert(NB * NT == BN * 4 && NB >= 1, "whole-wave weight DMA pieces");
+    constexpr int APB = C::A_PATCH, BST = BN * 64;
+    constexpr int RPP = C::HALO_RPP, APL = RPP * 16;
+    static_assert(2 * APB + NS * BST <= C::SMEM, "kHaloQ buffers fit");
+    static_assert(NAH * C::NW * 64 >= 4 * RPP && RPP % 16 == 0, "kHaloQ: the DMA instructions cover all 4 planes");
+    char* const abuf0 = smem;
+    char* const bbuf0 = smem + 2 * APB;
+    const int Cin = p.Cin;
+    const int grp = wave >> 2;
+    const int cb = kt0 / 9, ce = (kt0 + nk) / 9;
+    const int nch = Cin >> 5;  // chunks of the whole K (dummy DMA sources stay below it)
+    // patch DMA: piece (wave, i) fills LDS slots (wave * NAH + i) * 64 + lane = plane * RPP + pixel; apix[i] is the
+    // source pixel (-1: padding / outside the patch -> zeros), the plane is recomputed at issue time
+    int apix[NAH];
+#pragma unroll
+    for (int i = 0; i < NAH; ++i) {
+      const int slot = (wave * NAH + i) * 64 + lane;
+      const int pl = slot / RPP, q = slot - pl * RPP;
+      const int qy = q / PW, qx = q - qy * PW;
+      const int iy = halo_oy0 - 1 + qy, ix = halo_ox0 - 1 + qx;
+      const bool ok = pl < 4 && q < RP && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+      apix[i] = ok ? (halo_img * p.H + iy) * p.W + ix : -1;
+    }
+    const int sb1 = p.src[0].channels;
+    const int sb2 = sb1 + (p.nsrc > 1 ? p.src[1].channels : 0);
+    const int sb3 = sb2 + (p.nsrc > 2 ? p.src[2].channels : 0);
+    const f16* sp0 = reinterpret_cast<const f16*>(p.src[0].ptr);
+    const f16* sp1 = reinterpret_cast<const f16*>(p.src[p.nsrc > 1 ? 1 : 0].ptr);
+    const f16* sp2 = reinterpret_cast<const f16*>(p.src[p.nsrc > 2 ? 2 : 0].ptr);
+    const f16* sp3 = reinterpret_cast<const f16*>(p.src[p.nsrc > 3 ? 3 : 0].ptr);
+    const int ss0 = p.src[0].stride, ss1 = p.src[p.nsrc > 1 ? 1 : 0].stride;
+    const int ss2 = p.src[p.nsrc > 2 ? 2 : 0].stride, ss3 = p.src[p.nsrc > 3 ? 3 : 0].stride;
+    const f16* wrow[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int row = (wave * NB + j) * 16 + (lane >> 2);
+      const int g = (0 - (row >> 2)) & 3;
+      wrow[j] = reinterpret_cast<const f16*>(p.weight) + (size_t)(n0 + row) * p.Kpad + (((lane & 3) ^ g) << 3);
+    }
+    const char* const zero_src = reinterpret_cast<const char*>(g_zero16);
+    // patch of chunk c (clamped into the K range: a dummy past it) into buffer buf
+    auto issue_a = [&](int c, int buf) {
+      const int ci = (c < nch ? c : nch - 1) << 5;
+      const f16* sp;
+      int sst;
+      if (ci < sb1) { sp = sp0 + ci; sst = ss0; }
+      else if (ci < sb2) { sp = sp1 + (ci - sb1); sst = ss1; }
+      else if (ci < sb3) { sp = sp2 + (ci - sb2); sst = ss2; }
+      else { sp = sp3 + (ci - sb3); sst = ss3; }
+      char* dst = abuf0 + buf * APB;
+#pragma unroll
+      for (int i = 0; i < NAH; ++i) {
+        const int pl = ((wave * NAH + i) * 64 + lane) / RPP;
+        const f16* src = sp + (size_t)(apix[i] < 0 ? 0 : apix[i]) * sst + (pl << 3);
+        const void* g = apix[i] >= 0 ? (const void*)src : (const void*)zero_src;
+        SA_HALO_GLDS(g, (lds_void_t*)(dst + (wave * NAH + i) * 1024), 16, 0, 0);
+      }
+    };
+    // weights of (chunk c, tap t) into slot t (c clamped into the K range: a dummy past it)
+    auto issue_b = [&](int c, int t) {
+      const int koff = t * Cin + ((c < nch ? c : nch - 1) << 5);
+      char* dst = bbuf0 + t * BST;
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        SA_HALO_GLDS((const void*)(wrow[j] + koff), (lds_void_t*)(dst + (wave * NB + j) * 1024), 16, 0, 0);
+    };
+    const int frow = lane & 15;
+    const int abase = (lane >> 4) * APL + ((wm * (C::TM / TW)) * PW + frow) * 16;
+    const int bbase = (wn * C::TN + frow) * 64 + (((lane >> 4) ^ ((0 - (frow >> 2)) & 3)) << 4);
+    char* const bptr = bbuf0 + bbase;
+    // prologue: patch(cb) and W(s0 .. s0 + L - 1), all landed before the first barrier
+    issue_a(cb, cb & 1);
+#pragma unroll
+    for (int k = 0; k < L; ++k) issue_b(cb + k / 9, k % 9);
+    wait_vmcnt<0>();
+    SA_HALO_BAR();
+    if (grp == 1) SA_HALO_BAR();
+    asm volatile("" ::: "memory");
+    half8 a[C::FM], b[C::FN];
+    for (int c = cb; c < ce; ++c) {
+      char* const aptr = abuf0 + (c & 1) * APB + abase;
+      static_for<0, 9>([&](auto T) {
+        constexpr int t = decltype(T)::value;
+        constexpr int ty = t / 3, tx = t % 3;
+        // ---- step (c, t): LOAD -- DMA issue, every fragment of the step, wait for W(s + 1) ----
+        if constexpr (t == 1) issue_a(c + 1, (c + 1) & 1);
+        issue_b(c + (t + L) / 9, (t + L) % 9);
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) b[j] = SA_HALO_LD(bptr + t * BST + j * 1024);
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+          a[i] = SA_HALO_LD(aptr + (((i * 16) / TW + ty) * PW + (i * 16) % TW + tx) * 16);
+        // pieces issued after W(s + 1): W(s + 2 .. s + L) and, at taps 1 .. L - 1, this chunk's patch
+        if constexpr (t >= 1 && t < L) wait_vmcnt<(L - 1) * NB + NAH>();
+        else wait_vmcnt<(L - 1) * NB>();
+        SA_HALO_BAR();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- step (c, t): MFMA ----
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int j = 0; j < C::FN; ++j) acc[i][j] = SA_HALO_MFMA(a[i], b[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        SA_HALO_BAR();
+      });
+    }
+    if (grp == 0) SA_HALO_BAR();
+    wait_vmcnt<0>();  // the trailing dummy DMAs land before the epilogue reuses LDS
+    __syncthreads();
+  } else if constexpr (C::HALOW) {
+    // ---------------- kHaloW: 3x3 halo patch (32-channel chunks) + 6-deep weight ring, 128 x 64 wave tiles ------
+    // Step s = (chunk c = s / 9 of 32 channels, tap t = s % 9), K = 32 per step (one v_mfma_f32_16x16x32_f16 per
+    // fragment pair).  LDS: patch buffers [2][A_PATCH] (planar: plane pl = 8 channels at pl * APL, pixel q of the
+    // (TH+2) x (TW+2) patch at q * 16 B), then the weight ring [NS][BN rows][64 B] whose 16-B slot kb of row n holds
+    // channels 8 (kb ^ g(n)), g(n) = -(n >> 2) & 3 (applied to the DMA SOURCE address, the image stays lane-linear),
+    // so every ds_read_b128 lane group of a B fragment hits 16 distinct bank slots.
+    // Schedule of step s (one raw barrier per step):
+    //   B_s: lgkmcnt(0) (this wave's reads of step s into Fc are done), vmcnt(<= pieces issued after W(s+1)),
+    //        s_barrier -- W(s+1) and the patch of s+1's chunk have landed for every wave, and every wave finished
+    //        reading step s - 1's weight slot and, at a chunk boundary, the previous chunk's patch buffer
+    //   issue: patch(c + 2) into buffer c & 1 when t == 8; W(s + NS - 1) into slot (s - 1) % NS
+    //   MFMAs of step s (Fc) with the fragment reads of step s + 1 (Fn) interleaved, one read per MFMA
+    constexpr int TW = C::TW, TH = BM / TW, PW = TW + 2, RP = C::HALO_PIX;
+    constexpr int NAH = C::HALO_NA, NS = C::NSTAGE;
+    constexpr int NB = BN * 4 / NT;  // 1-KB weight pieces per wave per step (16 rows of 64 B each)
+    static_assert(NB * NT == BN * 4 && NB >= 1, "whole-wave weight DMA pieces");
+    constexpr int APB = C::A_PATCH, BST = BN * 64;
+    constexpr int RPP = C::HALO_RPP, APL = RPP * 16;
+    static_assert(2 * APB + NS * BST <= C::SMEM, "kHaloW buffers fit");
+    static_assert(NAH * C::NW * 64 >= 4 * RPP && RPP % 16 == 0, "kHaloW: the DMA instructions cover all 4 planes");
+    static_assert(C::FM * C::FN >= C::FM + C::FN, "one fragment read per MFMA slot");
+    char* const abuf0 = smem;
+    char* const bbuf0 = smem + 2 * APB;
+    const int Cin = p.Cin;
+    const int cb = kt0 / 9, ce = (kt0 + nk) / 9;
+    const int s0 = kt0, s1 = kt0 + nk;
+    // patch DMA: instruction (wave, i) fills LDS slots (wave * NAH + i) * 64 + lane = plane * RPP + pixel; apix[i]
+    // is the source pixel (-1: padding / outside the patch, loads zeros), the plane is recomputed at issue time
+    int apix[NAH];
+#pragma unroll
+    for (int i = 0; i < NAH; ++i) {
+      const int slot = (wave * NAH + i) * 64 + lane;
+      const int pl = slot / RPP, q = slot - pl * RPP;
+      const int qy = q / PW, qx = q - qy * PW;
+      const int iy = halo_oy0 - 1 + qy, ix = halo_ox0 - 1 + qx;
+      const bool ok = pl < 4 && q < RP && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+      apix[i] = ok ? (halo_img * p.H + iy) * p.W + ix : -1;
+    }
+    const int sb1 = p.src[0].channels;
+    const int sb2 = sb1 + (p.nsrc > 1 ? p.src[1].channels : 0);
+    const int sb3 = sb2 + (p.nsrc > 2 ? p.src[2].channels : 0);
+    const f16* sp0 = reinterpret_cast<const f16*>(p.src[0].ptr);
+    const f16* sp1 = reinterpret_cast<const f16*>(p.src[p.nsrc > 1 ? 1 : 0].ptr);
+    const f16* sp2 = reinterpret_cast<const f16*>(p.src[p.nsrc > 2 ? 2 : 0].ptr);
+    const f16* sp3 = reinterpret_cast<const f16*>(p.src[p.nsrc > 3 ? 3 : 0].ptr);
+    const int ss0 = p.src[0].stride, ss1 = p.src[p.nsrc > 1 ? 1 : 0].stride;
+    const int ss2 = p.src[p.nsrc > 2 ? 2 : 0].stride, ss3 = p.src[p.nsrc > 3 ? 3 : 0].stride;
+    // weight DMA: piece j of this wave = rows (wave * NB + j) * 16 + (lane >> 2), slot lane & 3 <- channels
+    // 8 ((lane & 3) ^ g(row))
+    const f16* wrow[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int row = (wave * NB + j) * 16 + (lane >> 2);
+      const int g = (0 - (row >> 2)) & 3;
+      wrow[j] = reinterpret_cast<const f16*>(p.weight) + (size_t)(n0 + row) * p.Kpad + (((lane & 3) ^ g) << 3);
+    }
+    const void* zero_src = g_zero16;
+    auto issue_a = [&](int c, int buf) {
+      const int ci = c << 5;
+      const f16* sp;
+      int sst;
+      if (ci < sb1) { sp = sp0 + ci; sst = ss0; }
+      else if (ci < sb2) { sp = sp1 + (ci - sb1); sst = ss1; }
+      else if (ci < sb3) { sp = sp2 + (ci - sb2); sst = ss2; }
+      else { sp = sp3 + (ci - sb3); sst = ss3; }
+      char* dst = abuf0 + buf * APB;
+#pragma unroll
+      for (int i = 0; i < NAH; ++i) {
+        const int pl = ((wave * NAH + i) * 64 + lane) / RPP;
+        const void* g = apix[i] >= 0 ? (const void*)(sp + (size_t)apix[i] * sst + (pl << 3)) : zero_src;
+        __builtin_amdgcn_global_load_lds(g, (lds_void_t*)(dst + (wave * NAH + i) * 1024), 16, 0, 0);
+      }
+    };
+    auto issue_b = [&](int st) {
+      const int c = st / 9, t = st - c * 9;
+      const int koff = t * Cin + (c << 5);
+      char* dst = bbuf0 + (st % NS) * BST;
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        __builtin_amdgcn_global_load_lds((const void*)(wrow[j] + koff), (lds_void_t*)(dst + (wave * NB + j) * 1024), 16,
+                                         0, 0);
+    };
+    const int frow = lane & 15;
+    // fragment i of this wave: output pixels (wm * TM + i * 16 + frow) -> patch row wm * TM / TW + (i * 16) / TW,
+    // column (i * 16) % TW + frow; the lane reads plane lane >> 4.  Everything but the lane base is an immediate.
+    const int abase = (lane >> 4) * APL + ((wm * (C::TM / TW)) * PW + frow) * 16;
+    const int bbase = (wn * C::TN + frow) * 64 + (((lane >> 4) ^ ((0 - (frow >> 2)) & 3)) << 4);
+    auto addr_a = [&](int st, int i) {
+      const int c = st / 9, t = st - c * 9;
+      const int ty = t / 3, tx = t - ty * 3;
+      return abuf0 + (c & 1) * APB + abase + (((i * 16) / TW + ty) * PW + (i * 16) % TW + tx) * 16;
+    };
+    auto addr_b = [&](int st, int j) { return bbuf0 + (st % NS) * BST + bbase + j * 16 * 64; };
+    // MFMAs of one step, fragment-row-major, with the next step's fragment reads interleaved: the B fragments of
+    // the next step go to the other B set (bn), and A fragment i of the next step REPLACES a[i] right after its
+    // last MFMA (i, FN - 1) -- one A set instead of two keeps the 128 accumulators + fragments within 256 VGPRs
+    // The reads are unconditional: after the last step they re-read in-bounds LDS nobody uses (a runtime condition
+    // per read makes hipcc branch around every ds_read inside the MFMA stream)
+    // sched_group_barrier pins the interleave: M R M R M R M R | R | (M M M M R) x (FM - 1) -- every read issued
+    // right behind the MFMA that frees its register, so it has the rest of the step to land
+    auto mfma_step = [&](half8* a, const half8* b, int stn, half8* bn) {
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) {
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+          if (i == 0) bn[j] = *reinterpret_cast<const half8*>(addr_b(stn, j));
+        }
+        a[i] = *reinterpret_cast<const half8*>(addr_a(stn, i));
+      }
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+      for (int i = 1; i < C::FM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, C::FN, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    };
+    // issue times (x4 so the order inside an iteration is total): a steady-state patch at 4 st, W(k) at
+    // 4 (k - NS + 1) + 2 (the prologue's weights before its patch at 4 (s0 - 1) + 3)
+    int patch_time = -(1 << 30);
+    issue_a(cb, cb & 1);
+#pragma unroll
+    for (int k = 0; k < NS - 1; ++k)
+      if (s0 + k < s1) issue_b(s0 + k);
+    if (ce - cb > 1) {
+      issue_a(cb + 1, (cb + 1) & 1);
+      patch_time = 4 * (s0 - 1) + 3;
+    }
+    // pieces issued after W(st) at the barrier of step st - 1 (or the prologue for st = s0)
+    auto allowed_after = [&](int st) {
+      const int w_issued_end = (st - 1) + NS - 1 < s1 ? (st - 1) + NS - 1 : s1;  // W(s0 .. w_issued_end - 1) issued
+      int nw = w_issued_end - (st + 1);
+      if (nw < 0) nw = 0;
+      const int wtime = 4 * (st - NS + 1) + 2;
+      return nw * NB + (patch_time > wtime ? NAH : 0);
+    };
+    auto wait_le = [&](int n) {
+      if (n >= 3 * NB + NAH) wait_vmcnt<3 * NB + NAH>();
+      else if (n >= 2 * NB + NAH) wait_vmcnt<2 * NB + NAH>();
+      else if (n >= NB + NAH) wait_vmcnt<NB + NAH>();
+      else if (n >= NAH) wait_vmcnt<NAH>();
+      else if (n >= 4 * NB) wait_vmcnt<4 * NB>();
+      else if (n >= 3 * NB) wait_vmcnt<3 * NB>();
+      else if (n >= 2 * NB) wait_vmcnt<2 * NB>();
+      else if (n >= NB) wait_vmcnt<NB>();
+      else wait_vmcnt<0>();
+    };
+    static_assert(NS - 2 <= 4, "wait_le covers up to 4 weight stages after the one waited for");
+    // prologue wait: W(s0) and patch(cb) (issued first) landed; after W(s0): W(s0+1 .. s0+NS-2), patch(cb+1)
+    {
+      int nw = (s0 + NS - 1 < s1 ? s0 + NS - 1 : s1) - (s0 + 1);
+      if (nw < 0) nw = 0;
+      wait_le(nw * NB + (ce - cb > 1 ? NAH : 0));
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    half8 a[C::FM], b0[C::FN], b1[C::FN];
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) b0[j] = *reinterpret_cast<const half8*>(addr_b(s0, j));
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i) a[i] = *reinterpret_cast<const half8*>(addr_a(s0, i));
+    auto step = [&](int st, const half8* bm, half8* br) {
+      const bool more = st + 1 < s1;
+      if (more) {
+        const int c = st / 9, t = st - c * 9;
+        // WAR on the patch buffer refilled below: its last reads (step st's A fragments, issued during step st - 1)
+        // must have returned on this wave before the barrier.  The weight slot refilled below was read two steps
+        // back, by fragments step st - 1's MFMAs already consumed.
+        if (t == 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        wait_le(allowed_after(st + 1));
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (t == 8 && c + 2 < ce) {
+          issue_a(c + 2, c & 1);
+          patch_time = 4 * st;
+        }
+        if (st + NS - 1 < s1) issue_b(st + NS - 1);
+      }
+      mfma_step(a, bm, st + 1, br);
+    };
+    for (int st = s0; st < s1; st += 2) {
+      step(st, b0, b1);
+      if (st + 1 < s1) step(st + 1, b1, b0);
+    }
+    __syncthreads();  // all fragment reads done before the epilogue reuses LDS
   } else if constexpr (C::HALO) {
     // ---------------- 3x3 halo patch + weight ring via global->LDS DMA, channel-chunk-major K ----------------
     // Step s = (chunk c = s / 9, tap t = s % 9) over the whole K (never split).  LDS: patch buffers [2][A_PATCH]
@@ -438,11 +823,7 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
       wrow[j] = reinterpret_cast<const f16*>(p.weight) + (size_t)(n0 + row) * p.Kpad + lch * 8;
     }
     const void* zero_src = g_zero16;
-#ifdef SA_EXP_HALO_NODMA
-#define SA_HALO_GLDS(g, l, n, o, x) asm volatile("" ::"v"(g))
-#else
-#define SA_HALO_GLDS __builtin_amdgcn_global_load_lds
-#endif
+
     auto issue_a = [&](int c, int buf) {
       const int ci = c << 6;
       const f16* sp;
@@ -467,21 +848,7 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
         SA_HALO_GLDS((const void*)(wrow[j] + koff), (lds_void_t*)(dst + (wave * NB + j) * 1024), 16,
                                          0, 0);
     };
-#ifdef SA_EXP_HALO_NOREAD
-#define SA_HALO_LD(p) (__extension__({ half8 v_; asm volatile("" : "=v"(v_)); v_; }))
-#else
-#define SA_HALO_LD(p) (*reinterpret_cast<const half8*>(p))
-#endif
-#ifdef SA_EXP_HALO_NOBAR
-#define SA_HALO_BAR() do { } while (0)
-#else
-#define SA_HALO_BAR() __builtin_amdgcn_s_barrier()
-#endif
-#ifdef SA_EXP_HALO_NOMFMA
-#define SA_HALO_MFMA(a, b, c, x, y, z) (__extension__({ asm volatile("" :: "v"(a), "v"(b)); (c); }))
-#else
-#define SA_HALO_MFMA __builtin_amdgcn_mfma_f32_16x16x32_f16
-#endif
+
     const int frow = lane & 15;
     // A fragment rows of this wave: output pixel (py, px) of fragment i, lane row frow
     int aq0[C::FM];
@@ -1318,7 +1685,9 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
   constexpr int RPI = NT / CPR;  // rows per pass
   const int cc = tid % CPR;
   const int co = n0 + cc * 8;
-  const bool do_stats = p.stats != nullptr;
+  // kHaloW carries 128 accumulators per lane into the epilogue: it is never launched with statistics (launch_halo),
+  // so the 32 statistics registers are compiled out there
+  const bool do_stats = !C::HALOW && p.stats != nullptr;
   // Instance-norm statistics: per-thread partial sums for the (at most) two images a BM-row tile
   // can straddle, reduced across the block in LDS, then ONE double atomic per (block, image,
   // channel).  Per-thread atomics to the same N*C addresses serialise at the memory side
@@ -1542,7 +1911,7 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
 #pragma unroll
     for (int band = 0; band < BM / C::CROWS; ++band) {
       const int b0 = band * C::CROWS;
-      if (wm * 128 >= b0 && wm * 128 < b0 + C::CROWS) {
+      if (wm * C::TM >= b0 && wm * C::TM < b0 + C::CROWS) {
         if constexpr (C::WIDE) {
 #pragma unroll
           for (int i = 0; i < WFM; ++i)
@@ -1706,7 +2075,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(const SaConvAr
       constexpr int TH = BM / C::TW;
       const int gy = (p.Cout + BN - 1) / BN;
       const int T = p.N * ((p.Ho + TH - 1) / TH) * ((p.Wo + C::TW - 1) / C::TW) * gy;
-      const int S = p.splitk, nchunk = p.Cin >> 6;
+      const int S = p.splitk, nchunk = p.Cin / C::HALO_CH;
       const int nb = gridDim.x;
       const int full = (S * T - nb) / (S - 1);
       const int bid = blockIdx.x;
@@ -1855,11 +2224,13 @@ int launch_glds3(const SaConvArgs* a, hipStream_t stream, bool forced) {
 // sources are multiples of 64 channels, K unpadded.  Returns 1 when the shape does not qualify.
 template <int MODE>
 int launch_halo(const SaConvArgs* a, hipStream_t stream) {
-  constexpr int BM = 256, BN = 128;
+  constexpr int BM = (MODE == kHaloW || MODE == kHaloQ) ? 512 : (MODE == kHaloW12 || MODE == kHaloQ12) ? 384 : 256;
+  constexpr int BN = 128;
   bool ok = a->KD <= 0 && a->KH == 3 && a->KW == 3 && a->sh == 1 && a->sw == 1 && a->ph == 1 && a->pw == 1 &&
             a->dh == 1 && a->dw == 1 && a->up == 0 && a->Cin % 64 == 0 && a->Kpad == 9 * a->Cin &&
             a->Ho == a->H && a->Wo == a->W && a->splitk >= 0 && a->splitk <= 1;
   for (int i = 0; i < a->nsrc; ++i) ok = ok && a->src[i].channels % 64 == 0;
+  if (is_halow(MODE) && a->stats) ok = false;  // epilogue compiled without instance-norm statistics
   if (!ok) return 1;
   using C = ConvCfg<BM, BN, 4, 2, MODE>;
   const int th = BM / C::TW;
@@ -1871,7 +2242,7 @@ int launch_halo(const SaConvArgs* a, hipStream_t stream) {
   const long T = tiles * gy;
   const int cus = device_cus();
   const long rem = T % cus;
-  const int nchunk = a->Cin / 64;
+  const int nchunk = a->Cin / C::HALO_CH;
   int S = 1;
   if (a->splitk == 0 && a->ws && a->counters && !a->stats && rem > 0 && 2 * rem <= cus) {
     S = (int)(cus / rem);
@@ -1996,6 +2367,10 @@ extern "C" int sa_conv2d_tile_lds(int cfg) {
     case 27: return ConvCfg<256, 128, 4, 2, kHalo16>::SMEM;
     case 28: return ConvCfg<256, 128, 4, 2, kHaloP>::SMEM;
     case 29: return ConvCfg<256, 128, 4, 2, kHaloP16>::SMEM;
+    case 30: return ConvCfg<512, 128, 4, 2, kHaloW>::SMEM;
+    case 31: return ConvCfg<384, 128, 4, 2, kHaloW12>::SMEM;
+    case 32: return ConvCfg<512, 128, 4, 2, kHaloQ>::SMEM;
+    case 33: return ConvCfg<384, 128, 4, 2, kHaloQ12>::SMEM;
     default: return -1;
   }
 }
@@ -2005,7 +2380,7 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
   const int cfg = pick_cfg(a);
   if (a->epi == SA_EPI_TAPPROJ) {
     // partial sums per 128-channel n-tile: the tile configs with BN = 128 only
-    const bool bn128 = cfg == 0 || cfg == 4 || cfg == 7 || cfg == 11 || cfg == 15 || cfg == 19 || (cfg >= 26 && cfg <= 29);
+    const bool bn128 = cfg == 0 || cfg == 4 || cfg == 7 || cfg == 11 || cfg == 15 || cfg == 19 || (cfg >= 26 && cfg <= 33);
     if (!bn128) return -5;
     // exactly two 128-channel n-tile partials per pixel at stride 2 * taps: sa_tapproj_stencil sums q[0] + q[taps]
     // (Cout 128 read unwritten partials, Cout 384 dropped the third)
@@ -2096,13 +2471,17 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
       const int r = cfg == 10 ? launch_wide<256, 256, 2, 4>(a, stream) : launch_wide<512, 128, 4, 2>(a, stream);
       return r == 1 ? -5 : r;
     }
-    case 26: case 27: case 28: case 29: {
+    case 26: case 27: case 28: case 29: case 30: case 31: case 32: case 33: {
       // halo-reuse 3x3 tiles: 8 x 32 (26) / 16 x 16 (27) output patches x 128 channels; 28 / 29 the same with the
-      // planar patch image (kHaloP)
+      // planar patch image (kHaloP); 30 / 31 the wide 16 x 32 / 12 x 32 patches in 32-channel chunks (kHaloW)
       const int r = cfg == 26 ? launch_halo<kHalo>(a, stream)
                   : cfg == 27 ? launch_halo<kHalo16>(a, stream)
                   : cfg == 28 ? launch_halo<kHaloP>(a, stream)
-                              : launch_halo<kHaloP16>(a, stream);
+                  : cfg == 29 ? launch_halo<kHaloP16>(a, stream)
+                  : cfg == 30 ? launch_halo<kHaloW>(a, stream)
+                  : cfg == 31 ? launch_halo<kHaloW12>(a, stream)
+                  : cfg == 32 ? launch_halo<kHaloQ>(a, stream)
+                              : launch_halo<kHaloQ12>(a, stream);
       return r == 1 ? -5 : r;
     }
     case 18: case 19: {

@@ -755,6 +755,8 @@ constexpr Tactic kTactics[] = {
     {27, true, false, 0, 0, 0, 0, "3x3 halo patch 16x16"},
     {28, true, false, 0, 0, 0, 0, "3x3 halo patch 8x32, planar image"},
     {29, true, false, 0, 0, 0, 0, "3x3 halo patch 16x16, planar image"},
+    {32, true, false, 0, 0, 512, 128, "3x3 halo patch 16x32, 32-channel chunks, ping-pong wave groups"},
+    {33, true, false, 0, 0, 384, 128, "3x3 halo patch 12x32, 32-channel chunks, ping-pong wave groups"},
 };
 
 bool known_tactic(int cfg) {
@@ -862,7 +864,7 @@ PlanEntry tune_conv(const SaConvArgs& a, hipStream_t s) {
       // halo tiles' tail split (splitk 0) is a candidate unless SA_TUNE_HALO_SPLIT=0 (read per shape: in-process A/B
       // knob).  Same-process A/B, round 4: RAFT-SF b8 43.54 -> 43.33 ms/step, b1 8.58 -> 8.47, CREStereo iter10
       // 6.37 -> 6.30 (profiles/round4_notes.md)
-      if (sk == 0 && cfg >= 26 && cfg <= 29) {
+      if (sk == 0 && cfg >= 26 && cfg <= 33) {
         const char* hs = std::getenv("SA_TUNE_HALO_SPLIT");
         if (hs && hs[0] == '0') continue;
       }
