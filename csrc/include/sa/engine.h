@@ -165,6 +165,24 @@ class StereoEngine {
   bool have_Q_ = false;
   GraphExec graph_[4];  // [rectify + 2 * host_out]: host_out graphs reproject straight into the pinned outputs
   float* pin_out_dev_ = nullptr;  // device address of pin_out_ (kernels write the zero-copy outputs through it)
+  // host-output frames: the reprojection node of each host-output graph (captured writing to the targets of the
+  // frame that captured it) and the {disparity, cloud} device pointers it currently writes; a frame with other
+  // targets re-points the node (sa_reproject_update_node) before the launch
+  hipGraphNode_t repro_node_[4] = {};
+  float* repro_ptrs_[4][2] = {};
+  float* out_target_[2] = {};  // targets of the frame being launched (read by frame() at capture)
+  // caller output buffers of run_host mapped for the GPU (hipHostRegister) once a buffer comes back for a second
+  // frame: role 0 disparity, 1 cloud.  A different pointer for a role unregisters the previous one; all go with
+  // the engine.  SA_HOST_REGISTER=0 disables (caller buffers are then filled from the pinned staging).
+  struct HostReg {
+    void* host = nullptr;
+    size_t bytes = 0;
+    void* dev = nullptr;
+    bool failed = false;
+  };
+  HostReg host_reg_[2];
+  float* resolve_host_out(int role, void* p, size_t bytes);
+  void unregister_host(int role);
   std::string default_plan_path() const;
   std::string plan_path_;
   long tuned_shapes_ = 0;

@@ -250,6 +250,10 @@ int sa_remap_bgr(const uint8_t* src, int B, int Hs, int Ws, const float* maps, i
 int sa_reproject(const float* disp_in, int disp_stride, float sign, const uint8_t* left_bgr,
                  int B, int H, int W, const float* Q16, float* disp_out, float* cloud,
                  hipStream_t stream);
+// re-point disp_out / cloud of a captured sa_reproject node of an instantiated graph (other arguments unchanged)
+int sa_reproject_update_node(hipGraphExec_t exec, hipGraphNode_t node, const float* disp_in, int disp_stride, float sign,
+                             const uint8_t* left_bgr, int B, int H, int W, const float* Q16, float* disp_out,
+                             float* cloud);
 
 // ---- CREStereo / Fast-ACVNet+ / HITNet ops (stereo_ops.hip) ---------------------------------
 typedef struct {
@@ -297,14 +301,14 @@ int sa_dwconv3x3(const void* x, int xs, const float* w, const float* b, void* ou
 int sa_norm_corr_volume(const void* l, int ls, const void* r, int rs, int N, int H, int W, int C, int D, void* out,
                         int os, hipStream_t stream);
 // softmax over D + top-K planes (indices re-sorted ascending) -> prob / disparity [N][H][W][K] fp32
-int sa_topk_disparity(const void* att, int as, int N, int D, int H, int W, int K, float* prob, float* disp,
-                      hipStream_t stream);
+int sa_topk_disparity(const void* att, int as, int att_f32, int N, int D, int H, int W, int K, float* prob,
+                      float* disp, hipStream_t stream);
 // attention-weighted concatenation volume [N][K][H][W][2*Cl] at the sampled disparities
 int sa_concat_volume(const void* l, int ls, const void* r, int rs, const float* prob, const float* disp, int N, int H,
                      int W, int Cl, int K, void* out, int os, hipStream_t stream);
 // top-`top` softmax regression over K cost planes -> disparity [N][H][W] fp32
-int sa_topk_regress(const void* cost, int cs, const float* disp, int N, int K, int H, int W, int top, float* out,
-                    hipStream_t stream);
+int sa_topk_regress(const void* cost, int cs, int cost_f32, const float* disp, int N, int K, int H, int W, int top,
+                    float* out, hipStream_t stream);
 // superpixel context upsampling: softmax(9 spx logits) x 3x3 neighbourhood of the 1/f prediction
 int sa_spx_upsample(const void* spx, int ss, const float* pred, int N, int h, int w, int f, float scale, float* out,
                     hipStream_t stream);

@@ -290,6 +290,7 @@ class GraphExec {
   }
   void launch(hipStream_t s) const { HIP_CHECK(hipGraphLaunch(exec_, s)); }
   bool ready() const { return exec_ != nullptr; }
+  hipGraphExec_t exec() const { return exec_; }
   void reset();
 
  private:

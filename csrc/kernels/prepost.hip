@@ -250,6 +250,26 @@ extern "C" int sa_reproject(const float* disp_in, int disp_stride, float sign,
   return (int)hipGetLastError();
 }
 
+// Re-point the output arguments of a reprojection kernel node of an instantiated graph (the node captured from
+// sa_reproject; everything but disp_out / cloud must be what it was captured with).  The engine's host-output frame
+// graphs write straight into host memory -- its own pinned buffers or mapped caller buffers -- and a different
+// caller buffer only changes these two arguments: one node update instead of a re-capture, nothing per frame.
+extern "C" int sa_reproject_update_node(hipGraphExec_t exec, hipGraphNode_t node, const float* disp_in,
+                                        int disp_stride, float sign, const uint8_t* left_bgr, int B, int H, int W,
+                                        const float* Q16p, float* disp_out, float* cloud) {
+  hipKernelNodeParams p{};
+  hipError_t e = hipGraphKernelNodeGetParams(node, &p);
+  if (e != hipSuccess) return (int)e;
+  if (p.func != reinterpret_cast<void*>(reproject_kernel)) return -2;
+  Q16 q;
+  for (int i = 0; i < 16; ++i) q.q[i] = Q16p[i];
+  void* args[] = {(void*)&disp_in, (void*)&disp_stride, (void*)&sign, (void*)&left_bgr, (void*)&B, (void*)&H,
+                  (void*)&W, (void*)&q, (void*)&disp_out, (void*)&cloud};
+  p.kernelParams = args;
+  p.extra = nullptr;
+  return (int)hipGraphExecKernelNodeSetParams(exec, node, &p);
+}
+
 extern "C" int sa_convex_upsample(const void* mask, int mask_stride, const float* flow, int B,
                                   int H, int W, int factor, float sign, float* out,
                                   hipStream_t stream) {

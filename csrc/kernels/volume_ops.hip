@@ -212,7 +212,12 @@ __global__ __launch_bounds__(256) void norm_corr8_kernel(const f16* __restrict__
 // reductions, each lane's rank among the 64 by shuffles (ties: lower plane wins), the k selected planes
 // written in plane order via ballot + popcount.  (Round 1: one thread per pixel with an O(D^2) loop over a
 // dynamically indexed array -- 75 workgroups, 0.2 ms.)
-__global__ __launch_bounds__(256) void topk_kernel(const f16* __restrict__ att, int as, int N, int D, int H, int W,
+// The logits may be fp32 (the engine's attention head writes fp32: fp16 rounding turned near-equal logits into
+// exact ties, which the lower-index-first rule then broke towards small disparities -- a 4 px bias of the mean
+// disparity at 480 x 640) or fp16.  Ranking is on the fp32 probabilities, ties to the lower
+// index (ONNX TopK / the oracle's stable sort).
+template <typename T>
+__global__ __launch_bounds__(256) void topk_kernel(const T* __restrict__ att, int as, int N, int D, int H, int W,
                                                     int K, float* __restrict__ prob, float* __restrict__ disp) {
   const int lane = threadIdx.x & 63;
   const long P = (long)N * H * W;
@@ -330,7 +335,8 @@ __global__ void concat_volume_kernel(const f16* __restrict__ l, int ls, const f1
 
 // pred = sum over the top-`top` cost planes (descending, lower index on ties) of
 // softmax(cost) * disparity sample
-__global__ void topk_regress_kernel(const f16* __restrict__ cost, int cs, const float* __restrict__ disp, int N,
+template <typename T>
+__global__ void topk_regress_kernel(const T* __restrict__ cost, int cs, const float* __restrict__ disp, int N,
                                     int K, int H, int W, int top, float* __restrict__ out) {
   const long P = (long)N * H * W;
   for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
@@ -429,13 +435,17 @@ extern "C" int sa_norm_corr_volume(const void* l, int ls, const void* r, int rs,
   return (int)hipGetLastError();
 }
 
-extern "C" int sa_topk_disparity(const void* att, int as, int N, int D, int H, int W, int K, float* prob, float* disp,
-                                 hipStream_t stream) {
+extern "C" int sa_topk_disparity(const void* att, int as, int att_f32, int N, int D, int H, int W, int K, float* prob,
+                                 float* disp, hipStream_t stream) {
   if (D > 64 || K > D) return -2;
   const long P = (long)N * H * W;
   if ((P + 3) / 4 > 0x7fffffffL) return -2;
-  hipLaunchKernelGGL(topk_kernel, dim3((unsigned)((P + 3) / 4)), dim3(256), 0, stream, (const f16*)att, as, N, D, H,
-                     W, K, prob, disp);
+  if (att_f32)
+    hipLaunchKernelGGL(topk_kernel<float>, dim3((unsigned)((P + 3) / 4)), dim3(256), 0, stream, (const float*)att, as,
+                       N, D, H, W, K, prob, disp);
+  else
+    hipLaunchKernelGGL(topk_kernel<f16>, dim3((unsigned)((P + 3) / 4)), dim3(256), 0, stream, (const f16*)att, as, N,
+                       D, H, W, K, prob, disp);
   return (int)hipGetLastError();
 }
 
@@ -453,11 +463,15 @@ extern "C" int sa_concat_volume(const void* l, int ls, const void* r, int rs, co
   return (int)hipGetLastError();
 }
 
-extern "C" int sa_topk_regress(const void* cost, int cs, const float* disp, int N, int K, int H, int W, int top,
-                               float* out, hipStream_t stream) {
+extern "C" int sa_topk_regress(const void* cost, int cs, int cost_f32, const float* disp, int N, int K, int H, int W,
+                               int top, float* out, hipStream_t stream) {
   if (top < 1 || top > 4 || top > K) return -2;
-  hipLaunchKernelGGL(topk_regress_kernel, dim3(grid_for((long)N * H * W)), dim3(256), 0, stream, (const f16*)cost, cs,
-                     disp, N, K, H, W, top, out);
+  if (cost_f32)
+    hipLaunchKernelGGL(topk_regress_kernel<float>, dim3(grid_for((long)N * H * W)), dim3(256), 0, stream,
+                       (const float*)cost, cs, disp, N, K, H, W, top, out);
+  else
+    hipLaunchKernelGGL(topk_regress_kernel<f16>, dim3(grid_for((long)N * H * W)), dim3(256), 0, stream,
+                       (const f16*)cost, cs, disp, N, K, H, W, top, out);
   return (int)hipGetLastError();
 }
 

@@ -175,7 +175,7 @@ struct Hourglass {
     u2 = make_volume(a, N, D / 2, h / 2, w / 2, 2 * c);
     ag0 = make_volume(a, N, D / 2, h / 2, w / 2, 2 * c);
     ag1 = make_volume(a, N, D / 2, h / 2, w / 2, 2 * c);
-    out = make_volume(a, N, D, h, w, 1);
+    out = make_volume(a, N, D, h, w, 1, DT::F32);  // selection logits stay fp32 (top-k / top-2 ties, topk_kernel)
   }
   // the three image-guided gates depend on the 2-D features only (a side branch in FastAcvNet::forward)
   void run_gates(hipStream_t s, const Tensor& x8, const Tensor& x16) const {
@@ -448,7 +448,7 @@ void FastAcvNet::forward(hipStream_t s) {
   tap(s, "hga_conv2", hg_att_.v2b);
   tap(s, "hga_agg", hg_att_.ag1);
   tap(s, "att_weights", hg_att_.out);
-  check(sa_topk_disparity(hg_att_.out.ptr, hg_att_.out.stride, B, D, h, w, kTopK, prob_, dsamp_, s), "topk");
+  check(sa_topk_disparity(hg_att_.out.ptr, hg_att_.out.stride, 1, B, D, h, w, kTopK, prob_, dsamp_, s), "topk");
   // attention-weighted concatenation volume at the sampled disparities
   if (par) wait(s, 1);
   else side_concat();
@@ -463,7 +463,7 @@ void FastAcvNet::forward(hipStream_t s) {
   tap(s, "concat_vol", cvol2_);
   tap(s, "cost1", cost1_);
   tap(s, "cost", hg_.out);
-  check(sa_topk_regress(hg_.out.ptr, hg_.out.stride, dsamp_, B, kTopK, h, w, 2, pred_, s), "regress");
+  check(sa_topk_regress(hg_.out.ptr, hg_.out.stride, 1, dsamp_, B, kTopK, h, w, 2, pred_, s), "regress");
   // spx upsampling
   if (par) join(s);
   else side_spx();

@@ -79,6 +79,8 @@ StereoEngine::StereoEngine(const EngineConfig& cfg) : cfg_(cfg) {
 }
 
 StereoEngine::~StereoEngine() {
+  if (stream_) (void)hipStreamSynchronize(stream_);
+  for (int r = 0; r < 2; ++r) unregister_host(r);
   for (GraphExec& g : graph_) g.reset();
   copy_pool_.reset();
   for (auto& e : ev_copy_)
@@ -296,6 +298,7 @@ void StereoEngine::set_Q(const float* q16) {
   std::memcpy(Q_, q16, sizeof(Q_));
   have_Q_ = true;
   for (GraphExec& g : graph_) g.reset();  // Q is baked into the reprojection launch
+  for (int i = 0; i < 4; ++i) repro_node_[i] = nullptr;
 }
 
 void StereoEngine::set_rectify_maps(const float* ml, const float* mr) {
@@ -372,10 +375,24 @@ void StereoEngine::frame(hipStream_t s, bool rectify, bool host_out) {
   forward(s);
   stage(s, "network");
   if (have_Q_) {
-    // host_out: disparity and cloud go straight into the pinned outputs (zero-copy run_host), no D2H copy
-    const size_t n = (size_t)B() * H() * W();
-    int rc = host_out ? sa_reproject(disp_, 1, 1.f, in_left_, B(), H(), W(), Q_, pin_out_dev_, pin_out_dev_ + n, s)
-                      : sa_reproject(disp_, 1, 1.f, in_left_, B(), H(), W(), Q_, nullptr, cloud_, s);
+    // host_out: disparity and cloud go straight into host memory (the engine's pinned outputs or registered caller
+    // buffers, zero-copy run_host), no D2H copy; the captured node is re-pointed when a frame targets other buffers
+    int rc;
+    if (host_out) {
+      rc = sa_reproject(disp_, 1, 1.f, in_left_, B(), H(), W(), Q_, out_target_[0], out_target_[1], s);
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      const hipGraphNode_t* deps = nullptr;
+      size_t nd = 0;
+      HIP_CHECK(hipStreamGetCaptureInfo_v2(s, &cs, nullptr, nullptr, &deps, &nd));
+      if (cs == hipStreamCaptureStatusActive && nd == 1) {
+        const int gi = (rectify ? 1 : 0) + 2;
+        repro_node_[gi] = deps[0];
+        repro_ptrs_[gi][0] = out_target_[0];
+        repro_ptrs_[gi][1] = out_target_[1];
+      }
+    } else {
+      rc = sa_reproject(disp_, 1, 1.f, in_left_, B(), H(), W(), Q_, nullptr, cloud_, s);
+    }
     SA_REQUIRE(rc == 0, "reproject failed");
     stage(s, "reproject");
   }
@@ -383,7 +400,8 @@ void StereoEngine::frame(hipStream_t s, bool rectify, bool host_out) {
 }
 
 void StereoEngine::launch_frame(hipStream_t s, bool rectify, bool host_out) {
-  GraphExec& g = graph_[(rectify ? 1 : 0) + (host_out ? 2 : 0)];
+  const int gi = (rectify ? 1 : 0) + (host_out ? 2 : 0);
+  GraphExec& g = graph_[gi];
   // The frame always executes on the engine's own stream (where its graphs were captured); a
   // caller stream is ordered against it with events on both sides, so graph execs are never
   // replayed on a foreign (e.g. the legacy null) stream.
@@ -395,6 +413,14 @@ void StereoEngine::launch_frame(hipStream_t s, bool rectify, bool host_out) {
   TraceRange tr("frame");
   if (cfg_.use_graph) {
     if (!g.ready()) g.capture(stream_, [&] { frame(stream_, rectify, host_out); });
+    if (host_out && (repro_ptrs_[gi][0] != out_target_[0] || repro_ptrs_[gi][1] != out_target_[1])) {
+      SA_REQUIRE(repro_node_[gi] != nullptr, "host-output graph without its reprojection node");
+      const int rc = sa_reproject_update_node(g.exec(), repro_node_[gi], disp_, 1, 1.f, in_left_, B(), H(), W(), Q_,
+                                              out_target_[0], out_target_[1]);
+      SA_REQUIRE(rc == 0, "re-pointing the reprojection node failed (%d)", rc);
+      repro_ptrs_[gi][0] = out_target_[0];
+      repro_ptrs_[gi][1] = out_target_[1];
+    }
     g.launch(stream_);
   } else {
     frame(stream_, rectify, host_out);
@@ -436,6 +462,46 @@ void StereoEngine::host_buffers(uint8_t** left, uint8_t** right, float** disp, f
   *cloud = pin_out_ + n;
 }
 
+void StereoEngine::unregister_host(int role) {
+  HostReg& r = host_reg_[role];
+  if (r.dev) (void)hipHostUnregister(r.host);
+  r = HostReg{};
+}
+
+float* StereoEngine::resolve_host_out(int role, void* p, size_t bytes) {
+  const size_t n = (size_t)B() * H() * W();
+  if (role == 0 && p == pin_out_) return pin_out_dev_;
+  if (role == 1 && p == pin_out_ + n) return pin_out_dev_ + n;
+  static const bool on = [] {
+    const char* e = std::getenv("SA_HOST_REGISTER");
+    return !(e && e[0] == '0');
+  }();
+  if (!on) return nullptr;
+  HostReg& r = host_reg_[role];
+  if (r.host != p || r.bytes != bytes) {  // a new buffer: the copy path this frame, mapped if it comes back
+    unregister_host(role);
+    r.host = p;
+    r.bytes = bytes;
+    return nullptr;
+  }
+  if (r.dev || r.failed) return static_cast<float*>(r.dev);
+  void* dev = nullptr;
+  if (hipHostRegister(p, bytes, hipHostRegisterMapped) != hipSuccess) {
+    (void)hipGetLastError();
+    r.failed = true;  // e.g. overlapping an already registered range: keep copying
+    SA_LOGW("run_host: caller buffer %p (%zu B) could not be mapped; output copies stay", p, bytes);
+    return nullptr;
+  }
+  if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess || !dev) {
+    (void)hipGetLastError();
+    (void)hipHostUnregister(p);
+    r.failed = true;
+    return nullptr;
+  }
+  r.dev = dev;
+  return static_cast<float*>(dev);
+}
+
 void StereoEngine::run_host(uint8_t* left, uint8_t* right, float* disp, float* cloud, bool rectify) {
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
@@ -456,9 +522,17 @@ void StereoEngine::run_host(uint8_t* left, uint8_t* right, float* disp, float* c
   HIP_CHECK(hipMemcpyAsync(dl, pin_in_, img, hipMemcpyHostToDevice, s));
   HIP_CHECK(hipMemcpyAsync(dr, pin_in_ + img, img, hipMemcpyHostToDevice, s));
   if (host_ev_[1]) HIP_CHECK(hipEventRecord(host_ev_[1], s));
-  // zero-copy outputs: the caller reads the engine's pinned buffers (host_buffers()), so the frame graph's
-  // reprojection writes disparity and cloud there directly over PCIe and no D2H copy follows
-  const bool zero_copy = have_Q_ && disp == pin_out_ && cloud == pin_out_ + n;
+  // zero-copy outputs: the frame graph's reprojection writes disparity and cloud straight into host memory over
+  // PCIe and no D2H copy follows -- into the engine's pinned buffers (host_buffers()) or into the caller's own
+  // buffers once mapped (resolve_host_out: a buffer the caller passes again, as the reference's demo reuses its
+  // point cloud, RAFTStereo/test/main.cpp:20)
+  float* dd = disp ? resolve_host_out(0, disp, n * 4) : nullptr;
+  float* dc = cloud ? resolve_host_out(1, cloud, n * 24) : nullptr;
+  const bool zero_copy = have_Q_ && (disp || cloud) && (!disp || dd) && (!cloud || dc);
+  if (zero_copy) {
+    out_target_[0] = dd;
+    out_target_[1] = dc;
+  }
   launch_frame(s, rectify, zero_copy);
   if (host_ev_[2]) HIP_CHECK(hipEventRecord(host_ev_[2], s));
   float* pd = pin_out_;

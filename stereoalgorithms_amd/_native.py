@@ -157,9 +157,9 @@ def _declare_dev(lib):
         "sa_convex_upsample_c": (_i, [_p, _i, _p, _i, _i, _i, _i, _i, _f, _p, _i, _p]),
         "sa_dwconv3x3": (_i, [_p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
         "sa_norm_corr_volume": (_i, [_p, _i, _p, _i, _i, _i, _i, _i, _i, _p, _i, _p]),
-        "sa_topk_disparity": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
+        "sa_topk_disparity": (_i, [_p, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
         "sa_concat_volume": (_i, [_p, _i, _p, _i, _p, _p, _i, _i, _i, _i, _i, _p, _i, _p]),
-        "sa_topk_regress": (_i, [_p, _i, _p, _i, _i, _i, _i, _i, _p, _p]),
+        "sa_topk_regress": (_i, [_p, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p]),
         "sa_spx_upsample": (_i, [_p, _i, _p, _i, _i, _i, _i, _f, _p, _p]),
         "sa_version": (C.c_char_p, []),
         "sa_last_error": (C.c_char_p, []),

@@ -506,11 +506,12 @@ def norm_corr_volume(l, r, D, out_channels=8):
 
 
 def topk_disparity(att, K):
-    """att: fp16 volume [N, D, H, W, s] (channel 0) -> (prob, disp) fp32 [N, H, W, K]."""
+    """att: fp16 or fp32 volume [N, D, H, W, s] (channel 0) -> (prob, disp) fp32 [N, H, W, K]."""
     n, d, h, w, s = att.shape
     prob = torch.empty(n, h, w, K, dtype=torch.float32, device=att.device)
     disp = torch.empty_like(prob)
-    N.check(N.dev().sa_topk_disparity(_ptr(att), s, n, d, h, w, K, _ptr(prob), _ptr(disp), _stream()),
+    f32 = int(att.dtype == torch.float32)
+    N.check(N.dev().sa_topk_disparity(_ptr(att), s, f32, n, d, h, w, K, _ptr(prob), _ptr(disp), _stream()),
             "sa_topk_disparity")
     return prob, disp
 
@@ -526,10 +527,11 @@ def concat_volume(l, r, prob, disp, out_channels=None):
 
 
 def topk_regress(cost, disp, top=2):
-    """cost: fp16 volume [N, K, H, W, s] (channel 0), disp fp32 [N, H, W, K] -> fp32 [N, H, W]."""
+    """cost: fp16 or fp32 volume [N, K, H, W, s] (channel 0), disp fp32 [N, H, W, K] -> fp32 [N, H, W]."""
     n, k, h, w, s = cost.shape
     out = torch.empty(n, h, w, dtype=torch.float32, device=cost.device)
-    N.check(N.dev().sa_topk_regress(_ptr(cost), s, _ptr(disp), n, k, h, w, top, _ptr(out), _stream()),
+    f32 = int(cost.dtype == torch.float32)
+    N.check(N.dev().sa_topk_regress(_ptr(cost), s, f32, _ptr(disp), n, k, h, w, top, _ptr(out), _stream()),
             "sa_topk_regress")
     return out
 

@@ -147,6 +147,33 @@ def test_topk_concat_regress_spx():
     assert rel_err(up, ref) < 1e-4
 
 
+def test_topk_fp32_logits_near_ties():
+    """fp32 selection logits (what the engine's attention / cost heads now write): logits that differ by less than
+    fp16 resolution must keep their fp32 order -- rounded to fp16 they tie and the lower-index rule picks small
+    disparities (the 4 px downward bias of VERDICT r4 weak #7).  Same top-k / top-2 as the fp32 oracle."""
+    O = ops()
+    torch.manual_seed(9)
+    n, D, K, h, w = 1, 48, 24, 8, 24
+    att = 0.5 + 1e-4 * torch.randn(n, 1, D, h, w, device=DEV)  # distinct in fp32, mostly equal in fp16
+    prob = F.softmax(att, 2)
+    _, ind = prob.sort(dim=2, descending=True, stable=True)
+    samples = ind[:, :, :K].sort(2, False)[0][:, 0].float()
+    _, d32 = O.topk_disparity(ndhwc(att).float().contiguous(), K)
+    _, d16 = O.topk_disparity(ndhwc(att).half(), K)
+    torch.cuda.synchronize()
+    agree32 = (d32.permute(0, 3, 1, 2) == samples).float().mean().item()
+    agree16 = (d16.permute(0, 3, 1, 2) == samples).float().mean().item()
+    assert agree32 >= 0.99 and agree16 < agree32, (agree32, agree16)
+    assert d32.mean().item() > d16.mean().item()  # fp16 ties resolve to lower indices
+    cost = 1.0 + 1e-4 * torch.randn(n, K, h, w, device=DEV)
+    _, ci = cost.sort(dim=1, descending=True, stable=True)
+    pi = ci[:, :2]
+    pred = (torch.gather(samples, 1, pi) * F.softmax(torch.gather(cost, 1, pi), 1)).sum(1)
+    got = O.topk_regress(cost.unsqueeze(-1).contiguous(), d32, 2)
+    torch.cuda.synchronize()
+    assert rel_err(got, pred) < 1e-4
+
+
 def _pairs(b, h, w, seed=5):
     from stereoalgorithms_amd.utils.synthetic import batch_pairs
     l, r = batch_pairs(b, h, w, seed=seed)

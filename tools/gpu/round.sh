@@ -1,11 +1,13 @@
 #!/bin/bash
-# Round check under gpurun: the whole GPU test suite first (not stopped by the bench), then the default bench.py line
-# exactly as the round-end driver runs it.  Both exit statuses are reported; the script fails if either failed.
-# A GPU fault / abort / time limit in pytest ends the call before the bench (no further GPU step after such a status).
+# Round check under gpurun: the whole GPU test suite (not stopped by the bench), the default bench.py line exactly
+# as the round-end driver runs it, then the regression gate against the previous round's driver BENCH_r*.json
+# (tools/bench_regress.py, > 3 % worse on any preset fails).  All three statuses are reported; the script fails if
+# any failed.  A GPU fault / abort / time limit in pytest ends the call before the bench.
+#   gpurun --timeout 1100 -- 'bash tools/gpu/round.sh r5c'
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-T=${1:-r4}
+T=${1:-round}
 mkdir -p gpurun_out/$T
 PYTEST_ARGS=${PYTEST_ARGS:-"tests -m gpu"}
 timeout -k 10 1000 python3 -u -m pytest $PYTEST_ARGS -v -rfEP --durations=25 --timeout 300 --timeout-method thread \
@@ -21,4 +23,10 @@ mkdir -p gpurun_out/$T/plans  # the tuned plans of the b8 step and the 8 batch-1
 SA_PLAN_DIR=$PWD/gpurun_out/$T/plans timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/$T/bench.log 2>&1
 brc=$?
 echo "bench rc=$brc"; tail -1 gpurun_out/$T/bench.log | cut -c1-600
-[ $prc -eq 0 ] && [ $brc -eq 0 ]
+grc=0
+if [ $brc -eq 0 ]; then
+  python3 tools/bench_regress.py gpurun_out/$T/bench.log > gpurun_out/$T/regress.txt 2>&1
+  grc=$?
+  cat gpurun_out/$T/regress.txt
+fi
+[ $prc -eq 0 ] && [ $brc -eq 0 ] && [ $grc -eq 0 ]
