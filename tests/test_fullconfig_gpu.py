@@ -143,3 +143,10 @@ def test_fastacvnet_end_to_end(tmp_path, monkeypatch):
     print(f"mean disparity: engine {disp.mean().item():.3f} oracle-fp16 {ref16.mean().item():.3f} "
           f"oracle-fp32 {ref.mean().item():.3f}")
     assert dm <= 1.5 * d16 + 0.05 * ref.abs().mean().item()
+    # Round 5: the attention / cost logits are fp32 in the engine.  Stored in fp16 they tied, and the lower-index rule
+    # biased the mean disparity by ~4 px (42.35 vs 46.29 in round 4, the fp16-autocast oracle still shows it); now the
+    # engine tracks the fp32 oracle's mean.  What remains is the top-2 choice among near-equal random-init cost logits
+    # flipping under fp16 activation storage inside the hourglass -- the fp32 oracle with fp16-rounded activations and
+    # fp32 logits flips as often (tests/test_fast_acvnet_cpu.py::test_fp16_storage_flips_come_from_near_ties).
+    assert dm <= 0.6, dm
+    assert within >= 0.4, within
