@@ -267,6 +267,10 @@ typedef struct {
   void* out; int32_t out_stride; int32_t out_channels;  // fp16, 36 used, rest zero-filled
 } SaAgclArgs;
 int sa_agcl_corr(const SaAgclArgs* a, hipStream_t stream);
+// iter-mode AGCL + the motion encoder's convc1 (1x1, 36 -> cout = 256, + bias, relu) in one launch (a->out unused):
+// w16 [256][64] fp16 (columns >= 36 zero), bias fp32 [256], out fp16 NHWC with pixel stride out_stride
+int sa_agcl_conv1x1(const SaAgclArgs* a, const void* w16, const float* bias, int cout, void* out, int out_stride,
+                    hipStream_t stream);
 
 // ws: fp32 workspace of sa_linear_attention_ws_floats(N, S, heads, dim) floats (per-chunk partial KV / Ksum)
 long sa_linear_attention_ws_floats(int N, int S, int heads, int dim);

@@ -15,6 +15,7 @@
 // Upstream ops: SURVEY.md §2.6 (grid_sample / local group correlation / linear attention rows).
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
 #include <cstdlib>
 #include <hip/hip_fp16.h>
 
@@ -279,6 +280,301 @@ __global__ __launch_bounds__(256) void agclw_kernel(const SaAgclArgs a) {
     reinterpret_cast<f16*>(a.out)[pix * a.out_stride + (lane >> 4) * ntap + (lane & 15)] = (f16)(res * (1.f / 64.f));
 }
 
+// Iter mode, tiled (the CREStereo refinement hot path: agcl8 above spends 43 us per 1/4-scale b1 iteration because
+// every one of the 9 taps recomputes the flow lookup and the 4 bilinear corners of its neighbour, i.e. each warped
+// right pixel is rebuilt 9 times).  Here one workgroup owns a TH x TW output tile and one 64-channel group
+// (blockIdx.y): phase 1 warps the tile plus its window halo once into LDS in fp32 (halo positions clamped to the
+// image = the replicate padding of the warped map; zero outside the right image, non-finite samples give zero),
+// phase 2 takes the 9 window dot products per output pixel from LDS.  8 lanes per pixel own 8 channels each; the
+// 16-B chunk j of LDS pixel p is stored at chunk j ^ (p & 1), so the 16-lane groups of a ds_read_b128 (4 pixels of
+// alternating parity) hit 16 distinct 16-B bank slots.  The 9 per-lane partial sums are reduce-scattered across the 8
+// lanes (7 + 3 shuffles instead of 27): lane c8 ends with tap c8, lane 0 also with tap 8.
+// RX, RY: window half-widths (1x9: 4, 0; 3x3: 1, 1).
+template <int RX, int RY>
+__global__ __launch_bounds__(256) void agcl_iter_tile_kernel(const SaAgclArgs a) {
+  constexpr int TW = 32, TH = 4, HWX = TW + 2 * RX, HP = HWX * (TH + 2 * RY);
+  constexpr int PX = 2 * RX + 1;
+  static_assert(PX * (2 * RY + 1) == 9, "9-tap window");
+  __shared__ float4 warped[HP][16];
+  const int tid = threadIdx.x, c8 = tid & 7, slot = tid >> 3;
+  const int g = blockIdx.y;
+  const int tiles_x = (a.W + TW - 1) / TW, tiles_y = (a.H + TH - 1) / TH;
+  const int bt = blockIdx.x;
+  const int tx = bt % tiles_x, ty = (bt / tiles_x) % tiles_y, n = bt / (tiles_x * tiles_y);
+  const int x0 = tx * TW - RX, y0 = ty * TH - RY;
+  const long img = (long)n * a.H * a.W;
+  const f16* f2 = reinterpret_cast<const f16*>(a.f2) + img * a.f2_stride + g * 64 + c8 * 8;
+  // Everything is issued before anything is consumed (the kernel is latency-bound: one flow load -> four dependent
+  // corner loads per pixel, a few pixels per lane): the flows of all this lane's halo pixels and the left chunks of
+  // its phase-2 pixels first, then the corners four pixels (16 loads) at a time.
+  constexpr int NPI = (HP + 31) / 32, NQ = TH * TW / 32;
+  float2 fl[NPI];
+  int hw_[NPI];
+#pragma unroll
+  for (int i = 0; i < NPI; ++i) {
+    const int p = slot + 32 * i < HP ? slot + 32 * i : HP - 1;
+    int hh = y0 + p / HWX, ww = x0 + p % HWX;
+    hh = hh < 0 ? 0 : (hh >= a.H ? a.H - 1 : hh);
+    ww = ww < 0 ? 0 : (ww >= a.W ? a.W - 1 : ww);
+    hw_[i] = (hh << 16) | ww;
+    fl[i] = *reinterpret_cast<const float2*>(a.flow + (img + (long)hh * a.W + ww) * 2);
+  }
+  half8 lf[NQ];
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const int q = slot + 32 * i;
+    const int h = ty * TH + q / TW, w = tx * TW + q % TW;
+    if (h < a.H && w < a.W)
+      lf[i] = *reinterpret_cast<const half8*>(reinterpret_cast<const f16*>(a.f1) + (img + (long)h * a.W + w) * a.f1_stride +
+                                              g * 64 + c8 * 8);
+    else
+      lf[i] = half8{};
+  }
+#pragma unroll
+  for (int i0 = 0; i0 < NPI; i0 += 4) {
+    constexpr int CH = 4;
+    half8 rv[CH][4];
+    float wv[CH][4];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      if (i0 + j >= NPI) break;
+      const int i = i0 + j;
+      const float sx = (float)(hw_[i] & 0xffff) + fl[i].x, sy = (float)(hw_[i] >> 16) + fl[i].y;
+      const bool fin = isfinite(sx) && isfinite(sy);
+      const float xf = fin ? floorf(sx) : 0.f, yf = fin ? floorf(sy) : 0.f;
+      const int xi = (int)xf, yi = (int)yf;
+      const float ax = sx - xf, ay = sy - yf;
+      const float wts[4] = {(1.f - ax) * (1.f - ay), ax * (1.f - ay), (1.f - ax) * ay, ax * ay};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int xx = xi + (t & 1), yy = yi + (t >> 1);
+        const bool ok = fin && xx >= 0 && xx < a.W && yy >= 0 && yy < a.H && wts[t] != 0.f;
+        wv[j][t] = ok ? wts[t] : 0.f;
+        if (ok) rv[j][t] = *reinterpret_cast<const half8*>(f2 + ((long)yy * a.W + xx) * a.f2_stride);
+        else rv[j][t] = half8{};
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      if (i0 + j >= NPI) break;
+      const int p = slot + 32 * (i0 + j);
+      float acc[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        acc[e] = wv[j][0] * (float)rv[j][0][e] + wv[j][1] * (float)rv[j][1][e] + wv[j][2] * (float)rv[j][2][e] +
+                 wv[j][3] * (float)rv[j][3][e];
+      if (p < HP) {
+        const int s = p & 1;
+        warped[p][(2 * c8) ^ s] = float4{acc[0], acc[1], acc[2], acc[3]};
+        warped[p][(2 * c8 + 1) ^ s] = float4{acc[4], acc[5], acc[6], acc[7]};
+      }
+    }
+  }
+  __syncthreads();
+  const bool b2 = c8 & 4, b1 = c8 & 2, b0 = c8 & 1;
+#pragma unroll
+  for (int iq = 0; iq < NQ; ++iq) {
+    const int q = slot + 32 * iq;
+    const int oy = q / TW, ox = q % TW;
+    const int h = ty * TH + oy, w = tx * TW + ox;
+    if (h >= a.H || w >= a.W) continue;  // uniform over the pixel's 8 lanes (the shuffles stay inside them)
+    const long pix = img + (long)h * a.W + w;
+    const half8 l8 = lf[iq];
+    float l[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) l[j] = (float)l8[j];
+    float r[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int dx = k % PX - RX, dy = k / PX - RY;
+      const int p = (oy + RY + dy) * HWX + ox + RX + dx;
+      const int s = p & 1;
+      const float4 u = warped[p][(2 * c8) ^ s], v = warped[p][(2 * c8 + 1) ^ s];
+      r[k] = l[0] * u.x + l[1] * u.y + l[2] * u.z + l[3] * u.w + l[4] * v.x + l[5] * v.y + l[6] * v.z + l[7] * v.w;
+    }
+    // reduce-scatter taps 0..7 over the 8 lanes: after the xor-4 / xor-2 / xor-1 steps lane c8 holds tap c8
+    float r4[4], r2[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r4[i] = (b2 ? r[i + 4] : r[i]) + __shfl_xor(b2 ? r[i] : r[i + 4], 4);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) r2[i] = (b1 ? r4[i + 2] : r4[i]) + __shfl_xor(b1 ? r4[i] : r4[i + 2], 2);
+    const float mine = (b0 ? r2[1] : r2[0]) + __shfl_xor(b0 ? r2[0] : r2[1], 1);
+    float t8 = r[8];
+    t8 += __shfl_xor(t8, 4);
+    t8 += __shfl_xor(t8, 2);
+    t8 += __shfl_xor(t8, 1);
+    f16* o = reinterpret_cast<f16*>(a.out) + pix * a.out_stride + g * 9;
+    o[c8] = (f16)(mine * (1.f / 64.f));
+    if (c8 == 0) o[8] = (f16)(t8 * (1.f / 64.f));
+  }
+}
+
+// Iter-mode AGCL fused with the motion encoder's convc1 (1x1, 36 -> 256, bias, relu): the CREStereo 1/4-scale
+// chain ran AGCL (15-25 us) then a K = 36 GEMM whose tile prologue / epilogue cost 15-30 us for 0.4 GFLOP.  One
+// workgroup (8 waves) owns a 2 x 32 pixel tile and all four channel groups:
+//   phase 1  warps the tile + window halo once for all 256 channels into LDS as fp16 (32 lanes per pixel, lane cc
+//            owns 16-B chunk cc; the halo replicate padding / zero outside / non-finite rules of the kernel above);
+//   phase 2  lane (g, c8) of a pixel's 32 takes the 9 window dot products of group g over its 8 channels
+//            (fp16 pairs, fp32 sums), reduce-scatters them over the group's 8 lanes and writes the fp16-rounded
+//            correlation (the value the unfused path stores) into an LDS [64 px][36 + pad] A tile;
+//   GEMM     [64 x 64] x [64 x 256] with v_mfma_f32_16x16x32_f16 (wave w: columns 32w..32w+31, weights as B
+//            fragments straight from global memory), bias + relu, staged through LDS for 16-B stores.
+// w16: [256][64] fp16 (k >= 36 zero), bias fp32 [256].
+template <int RX, int RY>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void agcl_iter_c1_kernel(const SaAgclArgs a, const f16* __restrict__ w16,
+                                                           const float* __restrict__ bias, f16* __restrict__ out,
+                                                           int out_stride) {
+  constexpr int TW = 32, TH = 2, HWX = TW + 2 * RX, HP = HWX * (TH + 2 * RY), NPX = TH * TW;
+  constexpr int PX = 2 * RX + 1;
+  static_assert(PX * (2 * RY + 1) == 9, "9-tap window");
+  constexpr int CRS = 72, OS = 256 + 8;
+  constexpr int WP_BYTES = HP * 512, OST_BYTES = NPX * OS * 2;
+  __shared__ __attribute__((aligned(16))) char smem[WP_BYTES > OST_BYTES ? WP_BYTES : OST_BYTES];
+  __shared__ __attribute__((aligned(16))) f16 cr[NPX * CRS];
+  __shared__ float2 spos[HP];
+  half8* wp = reinterpret_cast<half8*>(smem);  // [HP][32] 16-B chunks
+  typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+  typedef float floatx4 __attribute__((ext_vector_type(4)));
+  const int tid = threadIdx.x, cc = tid & 31, ps = tid >> 5, c8 = tid & 7, g = (tid >> 3) & 3;
+  const int tiles_x = (a.W + TW - 1) / TW, tiles_y = (a.H + TH - 1) / TH;
+  const int bt = blockIdx.x;
+  const int tx = bt % tiles_x, ty = (bt / tiles_x) % tiles_y, n = bt / (tiles_x * tiles_y);
+  const int x0 = tx * TW - RX, y0 = ty * TH - RY;
+  const long img = (long)n * a.H * a.W;
+  const f16* f2 = reinterpret_cast<const f16*>(a.f2) + img * a.f2_stride + cc * 8;
+  constexpr int NPI = (HP + 15) / 16, NQ = NPX / 16;
+  // the halo's sample positions go through LDS (one flow load per halo pixel instead of one per lane and pixel)
+  for (int p = tid; p < HP; p += 512) {
+    int hh = y0 + p / HWX, ww = x0 + p % HWX;
+    hh = hh < 0 ? 0 : (hh >= a.H ? a.H - 1 : hh);
+    ww = ww < 0 ? 0 : (ww >= a.W ? a.W - 1 : ww);
+    const float2 f = *reinterpret_cast<const float2*>(a.flow + (img + (long)hh * a.W + ww) * 2);
+    spos[p] = float2{(float)ww + f.x, (float)hh + f.y};
+  }
+  half8 lf[NQ];
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const int q = ps + 16 * i;
+    const int h = ty * TH + q / TW, w = tx * TW + q % TW;
+    if (h < a.H && w < a.W)
+      lf[i] = *reinterpret_cast<const half8*>(reinterpret_cast<const f16*>(a.f1) + (img + (long)h * a.W + w) * a.f1_stride +
+                                              cc * 8);
+    else
+      lf[i] = half8{};
+  }
+  for (int e = tid; e < NPX * (CRS - 36); e += 512) cr[(e / (CRS - 36)) * CRS + 36 + e % (CRS - 36)] = (f16)0.f;
+  __syncthreads();
+#pragma unroll
+  for (int i0 = 0; i0 < NPI; i0 += 4) {
+    constexpr int CH = 4;
+    half8 rv[CH][4];
+    float wv[CH][4];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      if (i0 + j >= NPI) break;
+      const int i = i0 + j;
+      const float2 sp = spos[ps + 16 * i < HP ? ps + 16 * i : HP - 1];
+      const float sx = sp.x, sy = sp.y;
+      const bool fin = isfinite(sx) && isfinite(sy);
+      const float xf = fin ? floorf(sx) : 0.f, yf = fin ? floorf(sy) : 0.f;
+      const int xi = (int)xf, yi = (int)yf;
+      const float ax = sx - xf, ay = sy - yf;
+      const float wts[4] = {(1.f - ax) * (1.f - ay), ax * (1.f - ay), (1.f - ax) * ay, ax * ay};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int xx = xi + (t & 1), yy = yi + (t >> 1);
+        const bool ok = fin && xx >= 0 && xx < a.W && yy >= 0 && yy < a.H && wts[t] != 0.f;
+        wv[j][t] = ok ? wts[t] : 0.f;
+        if (ok) rv[j][t] = *reinterpret_cast<const half8*>(f2 + ((long)yy * a.W + xx) * a.f2_stride);
+        else rv[j][t] = half8{};
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      if (i0 + j >= NPI) break;
+      const int p = ps + 16 * (i0 + j);
+      half8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        o[e] = (f16)(wv[j][0] * (float)rv[j][0][e] + wv[j][1] * (float)rv[j][1][e] + wv[j][2] * (float)rv[j][2][e] +
+                     wv[j][3] * (float)rv[j][3][e]);
+      if (p < HP) wp[p * 32 + cc] = o;
+    }
+  }
+  __syncthreads();
+  const bool b2 = c8 & 4, b1 = c8 & 2, b0 = c8 & 1;
+#pragma unroll
+  for (int iq = 0; iq < NQ; ++iq) {
+    const int q = ps + 16 * iq;
+    const int oy = q / TW, ox = q % TW;
+    const half8 l8 = lf[iq];
+    float r[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int dx = k % PX - RX, dy = k / PX - RY;
+      const half8 v = wp[((oy + RY + dy) * HWX + ox + RX + dx) * 32 + cc];
+      float acc = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; e += 2)
+        acc = __builtin_amdgcn_fdot2(half2v{l8[e], l8[e + 1]}, half2v{v[e], v[e + 1]}, acc, false);
+      r[k] = acc;
+    }
+    float r4[4], r2[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r4[i] = (b2 ? r[i + 4] : r[i]) + __shfl_xor(b2 ? r[i] : r[i + 4], 4);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) r2[i] = (b1 ? r4[i + 2] : r4[i]) + __shfl_xor(b1 ? r4[i] : r4[i + 2], 2);
+    const float mine = (b0 ? r2[1] : r2[0]) + __shfl_xor(b0 ? r2[0] : r2[1], 1);
+    float t8 = r[8];
+    t8 += __shfl_xor(t8, 4);
+    t8 += __shfl_xor(t8, 2);
+    t8 += __shfl_xor(t8, 1);
+    cr[q * CRS + g * 9 + c8] = (f16)(mine * (1.f / 64.f));
+    if (c8 == 0) cr[q * CRS + g * 9 + 8] = (f16)(t8 * (1.f / 64.f));
+  }
+  __syncthreads();
+  const int lane = tid & 63, wv = tid >> 6, r16 = lane & 15, kofs = (lane >> 4) * 8;
+  half8 bfr[2][2];
+  float bj[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int nn = wv * 32 + 16 * j + r16;
+    bj[j] = bias[nn];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) bfr[j][ks] = *reinterpret_cast<const half8*>(w16 + nn * 64 + ks * 32 + kofs);
+  }
+  floatx4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const half8 av = *reinterpret_cast<const half8*>(cr + (16 * i + r16) * CRS + ks * 32 + kofs);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bfr[j][ks], acc[i][j], 0, 0, 0);
+    }
+  f16* ost = reinterpret_cast<f16*>(smem);  // phase 2's reads of wp all happened before the barrier above
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        ost[(16 * i + (lane >> 4) * 4 + rr) * OS + wv * 32 + 16 * j + r16] = (f16)fmaxf(acc[i][j][rr] + bj[j], 0.f);
+  __syncthreads();
+#pragma unroll
+  for (int c = tid; c < NPX * 32; c += 512) {
+    const int row = c >> 5, ch = (c & 31) * 8;
+    const int h = ty * TH + row / TW, w = tx * TW + row % TW;
+    if (h < a.H && w < a.W)
+      *reinterpret_cast<half8*>(out + (img + (long)h * a.W + w) * out_stride + ch) =
+          *reinterpret_cast<const half8*>(ost + row * OS + ch);
+  }
+}
+
 __global__ void zero_tail_kernel(f16* out, int stride, long P, int c0, int c1) {
   const int n = c1 - c0;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < P * n; i += (long)gridDim.x * blockDim.x)
@@ -340,11 +636,38 @@ __global__ __launch_bounds__(256) void linear_attn_out_kernel(const f16* __restr
   const int t = blockIdx.x, h = blockIdx.y, n = blockIdx.z, tid = threadIdx.x;
   const int l0 = t * LA_CHUNK, hoff = h * D;
   const float* src = ws + ((size_t)n * heads + h) * nch * (D * D + D);
-  for (int e = tid; e < D * D + D; e += 256) {
-    float a = 0.f;
-    for (int c = 0; c < nch; ++c) a += src[(size_t)c * (D * D + D) + e];
-    if (e < D * D) kv[e / D][e % D] = a;
-    else ksum[e - D * D] = a;
+  // sum of the chunk partials, every load of a chunk issued before the adds (a serial c-loop left one L2 round
+  // trip per chunk exposed: 28 us per call at the CREStereo 1/16 size, 19 chunks)
+  constexpr int E = D * D + D, NE = (E + 255) / 256;
+  float part[NE];
+#pragma unroll
+  for (int j = 0; j < NE; ++j) part[j] = 0.f;
+  int c = 0;
+  for (; c + 4 <= nch; c += 4) {
+    float v[4][NE];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < NE; ++j) {
+        const int e = tid + 256 * j;
+        v[u][j] = e < E ? src[(size_t)(c + u) * E + e] : 0.f;
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < NE; ++j) part[j] += v[u][j];
+  }
+  for (; c < nch; ++c)
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      const int e = tid + 256 * j;
+      part[j] += e < E ? src[(size_t)c * E + e] : 0.f;
+    }
+#pragma unroll
+  for (int j = 0; j < NE; ++j) {
+    const int e = tid + 256 * j;
+    if (e < D * D) kv[e / D][e % D] = part[j];
+    else if (e < E) ksum[e - D * D] = part[j];
   }
   for (int e = tid; e < LA_CHUNK * D; e += 256) {
     const int l = e / D, d = e % D;
@@ -471,7 +794,13 @@ extern "C" int sa_agcl_corr(const SaAgclArgs* a, hipStream_t stream) {
   const char* ak = std::getenv("SA_AGCL_KERNEL");  // per launch (captured once per graph): in-process A/B knob
   const bool wave = ak && ak[0] == 'w';
   const long P = (long)a->N * a->H * a->W;
-  if (a->C == 256 && wave && (P + 3) / 4 < (1L << 31)) {
+  const char* at = std::getenv("SA_AGCL_TILE");  // 0: iter mode falls back to the per-tap kernels (A/B knob)
+  const long tiles = (long)a->N * ((a->H + 3) / 4) * ((a->W + 31) / 32);
+  if (a->C == 256 && a->iter_mode && !wave && !(at && at[0] == '0') && tiles < (1L << 31)) {
+    const dim3 g((unsigned)tiles, 4);
+    if (a->small_patch) hipLaunchKernelGGL((agcl_iter_tile_kernel<1, 1>), g, dim3(256), 0, stream, *a);
+    else hipLaunchKernelGGL((agcl_iter_tile_kernel<4, 0>), g, dim3(256), 0, stream, *a);
+  } else if (a->C == 256 && wave && (P + 3) / 4 < (1L << 31)) {
     const dim3 g((unsigned)((P + 3) / 4));
     if (a->iter_mode || a->offset) hipLaunchKernelGGL(agclw_kernel<0>, g, dim3(256), 0, stream, *a);
     else if (a->small_patch) hipLaunchKernelGGL(agclw_kernel<3>, g, dim3(256), 0, stream, *a);
@@ -484,6 +813,23 @@ extern "C" int sa_agcl_corr(const SaAgclArgs* a, hipStream_t stream) {
     hipLaunchKernelGGL(zero_tail_kernel, dim3(grid_for(P * (a->out_channels - 36))), dim3(256), 0, stream,
                        (f16*)a->out, a->out_stride, P, 36, a->out_channels);
   }
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_agcl_conv1x1(const SaAgclArgs* a, const void* w16, const float* bias, int cout, void* out,
+                               int out_stride, hipStream_t stream) {
+  if (!a->iter_mode || a->C != 256 || cout != 256 || !w16 || !bias || !out || out_stride < 256 || out_stride % 8 ||
+      a->f1_stride % 8 || a->f2_stride % 8 || ((uintptr_t)out | (uintptr_t)w16 | (uintptr_t)a->f1 | (uintptr_t)a->f2) % 16 ||
+      (uintptr_t)a->flow % 8 || a->H >= 65536 || a->W >= 65536)
+    return -2;
+  const long tiles = (long)a->N * ((a->H + 1) / 2) * ((a->W + 31) / 32);
+  if (tiles >= (1L << 31)) return -2;
+  if (a->small_patch)
+    hipLaunchKernelGGL((agcl_iter_c1_kernel<1, 1>), dim3((unsigned)tiles), dim3(512), 0, stream, *a, (const f16*)w16,
+                       bias, (f16*)out, out_stride);
+  else
+    hipLaunchKernelGGL((agcl_iter_c1_kernel<4, 0>), dim3((unsigned)tiles), dim3(512), 0, stream, *a, (const f16*)w16,
+                       bias, (f16*)out, out_stride);
   return (int)hipGetLastError();
 }
 

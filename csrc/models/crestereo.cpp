@@ -149,10 +149,16 @@ class CreStereo : public StereoEngine {
   // On for batch <= 2 (the hoisted columns cost +11 % MACs, a throughput loss at large batch); SA_CRE_GRU_SPLIT=0/1.
   ConvLayer zrq_[2], qh_[2];
   bool par_ = !(std::getenv("SA_CRE_PARALLEL") && std::getenv("SA_CRE_PARALLEL")[0] == '0');
+  bool agcl_first_ = !(std::getenv("SA_CRE_AGCL_FIRST") && std::getenv("SA_CRE_AGCL_FIRST")[0] == '0');
   int gru_split_mode_ = std::getenv("SA_CRE_GRU_SPLIT") ? std::atoi(std::getenv("SA_CRE_GRU_SPLIT")) : -1;
   bool gru_split_ = false;
   Level lv_[3];  // 0: 1/4, 1: 1/8, 2: 1/16
   void* fh2_w16_ = nullptr;
+  // iter-mode AGCL fused with convc1 (sa_agcl_conv1x1): [256][64] fp16 weights (k >= 36 zero) + fp32 bias;
+  // SA_CRE_FUSE_C1=0 runs AGCL and convc1 as two launches
+  void* c1_w16_ = nullptr;
+  float* c1_b_ = nullptr;
+  bool fuse_c1_ = !(std::getenv("SA_CRE_FUSE_C1") && std::getenv("SA_CRE_FUSE_C1")[0] == '0');
   float* fh2_b_ = nullptr;
   // SA_CRE_FH_PROJ=1: flow-head conv1 leaves conv2's tap projections (SA_EPI_TAPPROJ) in the level's fh buffer
   // instead of its 256 channels, and a stencil adds them into the flow (iterations without the mask head).  Off by
@@ -218,6 +224,17 @@ void CreStereo::build(WeightSource& src) {
   gru_split_ = gru_split_mode_ >= 0 ? gru_split_mode_ != 0 : B <= 2;
   convc1_.build(a, ws, {u + "encoder.convc1"}, {{36, 40}}, s1);
   convc2_.build(a, ws, {u + "encoder.convc2"}, {{256, 256}}, s3);
+  {
+    const HostTensor& w1 = ws.get(u + "encoder.convc1.weight");  // [256][36][1][1]
+    const HostTensor& b1 = ws.get(u + "encoder.convc1.bias");
+    std::vector<_Float16> w16((size_t)256 * 64, (_Float16)0.f);
+    for (int o = 0; o < 256; ++o)
+      for (int c = 0; c < 36; ++c) w16[(size_t)o * 64 + c] = (_Float16)w1.data[(size_t)o * 36 + c];
+    c1_w16_ = a.alloc(w16.size() * 2);
+    HIP_CHECK(hipMemcpy(c1_w16_, w16.data(), w16.size() * 2, hipMemcpyHostToDevice));
+    c1_b_ = (float*)a.alloc(256 * 4);
+    HIP_CHECK(hipMemcpy(c1_b_, b1.data.data(), 256 * 4, hipMemcpyHostToDevice));
+  }
   convf1_.build(a, ws, {u + "encoder.convf1"}, {{2, 8}}, s3);
   convf2_.build(a, ws, {u + "encoder.convf2"}, {{128, 128}}, s3);
   mconv_.build(a, ws, {u + "encoder.conv"}, {{256, 256}}, s3);
@@ -304,10 +321,23 @@ void CreStereo::update(hipStream_t s, Level& L, const Tensor& f1, const Tensor& 
   // motion encoder -> xin[128:254].  Its flow branch (flow features -> convf1 -> convf2) and correlation branch
   // (AGCL -> convc1 -> convc2) are independent until the final conv: the flow branch runs on the side stream
   // (SA_CRE_PARALLEL=0: one stream; iter10 b1 6.45 -> 6.15 ms, profiles/round4_notes.md)
+  // The AGCL node is captured before the flow branch's first node: the graph executor keeps a node's first child on
+  // the parent's queue and moves later children to other queues, so the correlation chain (the longer branch) stays
+  // on the main queue and the join before mconv waits on the already finished flow branch instead of mconv crossing
+  // queues behind convc2 (SA_CRE_AGCL_FIRST=0: flow branch captured first, as in round 4)
   const bool par = par_ && !tuning_pass_;
   const long P = (long)B * L.h * L.w;
+  auto agcl_c1 = [&] {  // correlation -> convc1 (+ relu) into L.cor1
+    if (iter_mode && fuse_c1_) {
+      check(sa_agcl_conv1x1(&ag, c1_w16_, c1_b_, 256, L.cor1.ptr, L.cor1.stride, s), "agcl + convc1");
+      return;
+    }
+    check(sa_agcl_corr(&ag, s), "agcl");
+    convc1_.run(s, {L.corr}, L.cor1, SA_ACT_RELU);
+  };
   {
     hipStream_t fs = par ? fork(s) : s;
+    if (agcl_first_) agcl_c1();
     ScopedSplitK sk(par ? &splitk_side_ : current_splitk());
     check(sa_flow_features(L.flow, 2, P, L.flowfeat.ptr, L.flowfeat.stride, 8, L.xin.slice_c(254, 2).ptr,
                            L.xin.stride, fs),
@@ -315,8 +345,7 @@ void CreStereo::update(hipStream_t s, Level& L, const Tensor& f1, const Tensor& 
     convf1_.run(fs, {L.flowfeat}, L.flo1, SA_ACT_RELU);
     convf2_.run(fs, {L.flo1}, L.corflo.slice_c(192, 64), SA_ACT_RELU);
   }
-  check(sa_agcl_corr(&ag, s), "agcl");
-  convc1_.run(s, {L.corr}, L.cor1, SA_ACT_RELU);
+  if (!agcl_first_) agcl_c1();
   convc2_.run(s, {L.cor1}, L.corflo.slice_c(0, 192), SA_ACT_RELU);
   if (par) join(s);
   mconv_.run(s, {L.corflo}, L.xin.slice_c(128, 126), SA_ACT_RELU);

@@ -359,6 +359,28 @@ def agcl_corr(f1, f2, flow, offset=None, small_patch=False, iter_mode=False, out
     return out
 
 
+def agcl_conv1x1(f1, f2, flow, weight, bias, small_patch=False):
+    """Iter-mode AGCL fused with a 1x1 conv 36 -> 256 + bias + relu (CREStereo's convc1): f1/f2 fp16 NHWC
+    [N,H,W,256], flow fp32 [N,H,W,2], weight [256,36(,1,1)], bias [256] -> fp16 [N,H,W,256]."""
+    n, h, w, c = f1.shape
+    w2 = weight.reshape(weight.shape[0], -1)
+    assert w2.shape == (256, 36) and bias.shape == (256,)
+    w16 = torch.zeros(256, 64, dtype=torch.float16, device=f1.device)
+    w16[:, :36] = w2.to(torch.float16)
+    b32 = bias.float().contiguous()
+    out = torch.empty(n, h, w, 256, dtype=torch.float16, device=f1.device)
+    a = N.SaAgclArgs()
+    a.f1, a.f1_stride = f1.data_ptr(), _pix_stride(f1)
+    a.f2, a.f2_stride = f2.data_ptr(), _pix_stride(f2)
+    assert flow.dtype == torch.float32 and flow.is_contiguous() and flow.shape == (n, h, w, 2)
+    a.flow = flow.data_ptr()
+    a.N, a.H, a.W, a.C = n, h, w, c
+    a.small_patch, a.iter_mode = int(small_patch), 1
+    N.check(N.dev().sa_agcl_conv1x1(C.byref(a), w16.data_ptr(), b32.data_ptr(), 256, out.data_ptr(), 256, _stream()),
+            "sa_agcl_conv1x1")
+    return out
+
+
 def linear_attention(q, k, v, heads=8, eps=1e-6):
     """q: fp16 [N, L, heads*dim], k/v: [N, S, heads*dim] (last dim may be a slice) -> fp16 [N, L, heads*dim]."""
     n, l, d = q.shape

@@ -26,15 +26,17 @@ def rel_err(a, b):
 
 @pytest.mark.parametrize("small_patch", [False, True])
 @pytest.mark.parametrize("mode", ["offset", "iter", "window"])
-@pytest.mark.parametrize("kernel", ["8", "w"])
+@pytest.mark.parametrize("kernel", ["8", "w", "t"])
 def test_agcl_vs_oracle(small_patch, mode, kernel, monkeypatch):
     """AGCL kernel vs the oracle: learned-offset mode, iter mode (per-tap warped windows), and the plain window mode
-    (no offsets: the wave kernel shares the taps' bilinear corners); both kernels (SA_AGCL_KERNEL 8 / w)."""
+    (no offsets: the wave kernel shares the taps' bilinear corners); every kernel (SA_AGCL_KERNEL 8 / w; "t" = the
+    default dispatch, whose iter mode is the tiled warp-once kernel -- run on ragged 4 x 32 tiles)."""
     from stereoalgorithms_amd.models.crestereo import AGCL
     monkeypatch.setenv("SA_AGCL_KERNEL", kernel)
+    monkeypatch.setenv("SA_AGCL_TILE", "1" if kernel == "t" else "0")
     O = ops()
     torch.manual_seed(0)
-    n, c, h, w = 2, 256, 12, 20
+    n, c, h, w = (2, 256, 13, 70) if kernel == "t" else (2, 256, 12, 20)
     iter_mode = mode == "iter"
     f1 = torch.randn(n, c, h, w, device=DEV).half().float()
     f2 = torch.randn(n, c, h, w, device=DEV).half().float()
@@ -50,6 +52,31 @@ def test_agcl_vs_oracle(small_patch, mode, kernel, monkeypatch):
     torch.cuda.synchronize()
     assert out.shape == (n, h, w, 40) and out[..., 36:].abs().max().item() == 0
     assert rel_err(out[..., :36].permute(0, 3, 1, 2), ref) < 5e-3
+
+
+@pytest.mark.parametrize("small_patch", [False, True])
+@pytest.mark.parametrize("shape", [(2, 13, 70), (1, 120, 160)])
+def test_agcl_conv1x1_vs_oracle(small_patch, shape):
+    """Fused iter-mode AGCL + convc1 (1x1 36 -> 256, bias, relu) vs the oracle's corr_iter -> conv2d -> relu, on
+    ragged 2 x 32 tiles and at the 1/4-scale b1 size; the correlation is rounded to fp16 like the unfused path."""
+    from stereoalgorithms_amd.models.crestereo import AGCL
+    O = ops()
+    torch.manual_seed(3)
+    n, h, w = shape
+    c = 256
+    f1 = torch.randn(n, c, h, w, device=DEV).half().float()
+    f2 = torch.randn(n, c, h, w, device=DEV).half().float()
+    flow = torch.randn(n, 2, h, w, device=DEV) * 3
+    wt = torch.randn(256, 36, 1, 1, device=DEV) / 6
+    b = torch.randn(256, device=DEV) * 0.1
+    with torch.no_grad():
+        corr = AGCL(f1, f2).corr_iter(flow, small_patch)
+        ref = F.relu(F.conv2d(corr.half().float(), wt.half().float(), b))
+    out = O.agcl_conv1x1(nhwc(f1).half(), nhwc(f2).half(), nhwc(flow), wt, b, small_patch=small_patch)
+    torch.cuda.synchronize()
+    assert out.shape == (n, h, w, 256)
+    assert torch.isfinite(out.float()).all()
+    assert rel_err(out.permute(0, 3, 1, 2), ref) < 5e-3
 
 
 @pytest.mark.parametrize("n,L,S", [(2, 77, 90), (2, 1200, 1200), (1, 1200, 1200)])

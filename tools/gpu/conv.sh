@@ -12,7 +12,7 @@ if [ -n "$TESTS" ]; then
   timeout -k 10 300 python3 -u -m pytest $TESTS -x -v --timeout 120 --timeout-method thread > gpurun_out/$T/pytest.log 2>&1
   rc=$?; tail -3 gpurun_out/$T/pytest.log; [ $rc -eq 0 ] || exit $rc
 fi
-ARGS="--graph --iters ${ITERS:-20} --shapes ${SHAPES:-zr8,q8,fh8} --cfgs ${CFGS:--1}"
+ARGS="--graph --iters ${ITERS:-20} --shapes ${SHAPES:-zr8,q8,fh8} --cfgs=${CFGS:--1}"
 [ -n "$SPLITS" ] && ARGS="$ARGS --splits $SPLITS"
 : > gpurun_out/$T/bench.txt
 for v in ${LIBS:-default}; do
