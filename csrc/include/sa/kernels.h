@@ -271,6 +271,14 @@ int sa_agcl_corr(const SaAgclArgs* a, hipStream_t stream);
 // w16 [256][64] fp16 (columns >= 36 zero), bias fp32 [256], out fp16 NHWC with pixel stride out_stride
 int sa_agcl_conv1x1(const SaAgclArgs* a, const void* w16, const float* bias, int cout, void* out, int out_stride,
                     hipStream_t stream);
+// CREStereo motion-encoder head in one launch (iter mode): AGCL -> convc1 (as sa_agcl_conv1x1) and, when wf16 is set,
+// convf1 (7x7, 2 -> 128, pad 3, + fbias, relu) on the fp16 flow into flo, plus the fp16 flow copy into fcopy[0:2]
+typedef struct {
+  const void* w16; const float* bias; void* cor; int32_t cor_stride;      // convc1: [256][64] fp16, k >= 36 zero
+  const void* wf16; const float* fbias; void* flo; int32_t flo_stride;    // convf1: [128][128] fp16, k = c*49+ky*7+kx
+  void* fcopy; int32_t fcopy_stride;                                      // fp16 (x, y) of the flow per pixel
+} SaCreHeadArgs;
+int sa_cre_motion_head(const SaAgclArgs* a, const SaCreHeadArgs* h, hipStream_t stream);
 
 // ws: fp32 workspace of sa_linear_attention_ws_floats(N, S, heads, dim) floats (per-chunk partial KV / Ksum)
 long sa_linear_attention_ws_floats(int N, int S, int heads, int dim);

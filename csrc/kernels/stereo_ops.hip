@@ -419,17 +419,26 @@ __global__ __launch_bounds__(256) void agcl_iter_tile_kernel(const SaAgclArgs a)
 //            correlation (the value the unfused path stores) into an LDS [64 px][36 + pad] A tile;
 //   GEMM     [64 x 64] x [64 x 256] with v_mfma_f32_16x16x32_f16 (wave w: columns 32w..32w+31, weights as B
 //            fragments straight from global memory), bias + relu, staged through LDS for 16-B stores.
-// w16: [256][64] fp16 (k >= 36 zero), bias fp32 [256].
-template <int RX, int RY>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void agcl_iter_c1_kernel(const SaAgclArgs a, const f16* __restrict__ w16,
-                                                           const float* __restrict__ bias, f16* __restrict__ out,
-                                                           int out_stride) {
+// FL: the flow branch's first conv rides along -- convf1 (7x7, 2 -> 128, pad 3, bias, relu) over the fp16 flow of an
+// 8 x 38 halo tile staged in LDS, as a second [64 x 128(98 taps)] x [128 x 128] MFMA GEMM, plus the fp16 copy of the
+// flow the GRU input carries (xin[254:256]); the flow branch then needs no launch of its own before convf2.
+// w16: [256][64] fp16 (k >= 36 zero), bias fp32 [256]; wf16: [128][128] fp16, k = c * 49 + ky * 7 + kx (k >= 98 zero).
+template <int RX, int RY, bool FL>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void agcl_iter_c1_kernel(
+    const SaAgclArgs a, const SaCreHeadArgs hd) {
+  const f16* __restrict__ w16 = reinterpret_cast<const f16*>(hd.w16);
+  const float* __restrict__ bias = hd.bias;
+  f16* __restrict__ out = reinterpret_cast<f16*>(hd.cor);
+  const int out_stride = hd.cor_stride;
   constexpr int TW = 32, TH = 2, HWX = TW + 2 * RX, HP = HWX * (TH + 2 * RY), NPX = TH * TW;
   constexpr int PX = 2 * RX + 1;
   static_assert(PX * (2 * RY + 1) == 9, "9-tap window");
   constexpr int CRS = 72, OS = 256 + 8;
-  constexpr int WP_BYTES = HP * 512, OST_BYTES = NPX * OS * 2;
-  __shared__ __attribute__((aligned(16))) char smem[WP_BYTES > OST_BYTES ? WP_BYTES : OST_BYTES];
+  constexpr int AFS = 136, FHW = TW + 6, FHP = (TH + 6) * FHW;  // convf1 A-tile row stride, flow halo width / size
+  constexpr int WP_BYTES = HP * 512, OST_BYTES = NPX * OS * 2, AF_BYTES = FL ? NPX * AFS * 2 : 0;
+  constexpr int SMEM = WP_BYTES > OST_BYTES + AF_BYTES ? WP_BYTES : OST_BYTES + AF_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  __shared__ f16 fh[FL ? FHP * 2 : 2];
   __shared__ __attribute__((aligned(16))) f16 cr[NPX * CRS];
   __shared__ float2 spos[HP];
   half8* wp = reinterpret_cast<half8*>(smem);  // [HP][32] 16-B chunks
@@ -450,6 +459,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
     ww = ww < 0 ? 0 : (ww >= a.W ? a.W - 1 : ww);
     const float2 f = *reinterpret_cast<const float2*>(a.flow + (img + (long)hh * a.W + ww) * 2);
     spos[p] = float2{(float)ww + f.x, (float)hh + f.y};
+  }
+  if constexpr (FL) {
+    // zero-padded fp16 flow around the tile for convf1, and the tile's own flow into the GRU input slice
+    for (int p = tid; p < FHP; p += 512) {
+      const int hh = ty * TH - 3 + p / FHW, ww = tx * TW - 3 + p % FHW;
+      float2 f = float2{0.f, 0.f};
+      if (hh >= 0 && hh < a.H && ww >= 0 && ww < a.W)
+        f = *reinterpret_cast<const float2*>(a.flow + (img + (long)hh * a.W + ww) * 2);
+      fh[2 * p] = (f16)f.x;
+      fh[2 * p + 1] = (f16)f.y;
+      const int r = p / FHW - 3, c = p % FHW - 3;
+      if (r >= 0 && r < TH && c >= 0 && c < TW && hh < a.H && ww < a.W) {
+        f16* fc = reinterpret_cast<f16*>(hd.fcopy) + (img + (long)hh * a.W + ww) * hd.fcopy_stride;
+        fc[0] = (f16)f.x;
+        fc[1] = (f16)f.y;
+      }
+    }
   }
   half8 lf[NQ];
 #pragma unroll
@@ -533,6 +559,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
     if (c8 == 0) cr[q * CRS + g * 9 + 8] = (f16)(t8 * (1.f / 64.f));
   }
   __syncthreads();
+  f16* af = reinterpret_cast<f16*>(smem + OST_BYTES);  // convf1 A tile [64 px][AFS] (the warped image is dead now)
+  if constexpr (FL) {
+#pragma unroll
+    for (int j = 0; j < NPX * 128 / 512; ++j) {
+      const int e = tid + 512 * j, m = e >> 7, kk = e & 127;
+      f16 v = (f16)0.f;
+      if (kk < 98) {
+        const int c = kk >= 49, t = kk - 49 * c, ky = t / 7, kx = t - 7 * ky;
+        v = fh[2 * ((m / TW + ky) * FHW + m % TW + kx) + c];
+      }
+      af[m * AFS + kk] = v;
+    }
+  }
   const int lane = tid & 63, wv = tid >> 6, r16 = lane & 15, kofs = (lane >> 4) * 8;
   half8 bfr[2][2];
   float bj[2];
@@ -572,6 +611,34 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
     if (h < a.H && w < a.W)
       *reinterpret_cast<half8*>(out + (img + (long)h * a.W + w) * out_stride + ch) =
           *reinterpret_cast<const half8*>(ost + row * OS + ch);
+  }
+  if constexpr (FL) {
+    // convf1: wave w -> output columns 16w .. 16w + 15, all 64 rows, 4 k-steps over the 98 (128) taps
+    const f16* wf = reinterpret_cast<const f16*>(hd.wf16);
+    half8 bf[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) bf[ks] = *reinterpret_cast<const half8*>(wf + (16 * wv + r16) * 128 + ks * 32 + kofs);
+    const float fb = hd.fbias[16 * wv + r16];
+    floatx4 a2[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a2[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const half8 av = *reinterpret_cast<const half8*>(af + (16 * i + r16) * AFS + ks * 32 + kofs);
+        a2[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bf[ks], a2[i], 0, 0, 0);
+      }
+    f16* flo = reinterpret_cast<f16*>(hd.flo);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = 16 * i + (lane >> 4) * 4 + rr;
+        const int h = ty * TH + row / TW, w = tx * TW + row % TW;
+        if (h < a.H && w < a.W)
+          flo[(img + (long)h * a.W + w) * hd.flo_stride + 16 * wv + r16] = (f16)fmaxf(a2[i][rr] + fb, 0.f);
+      }
   }
 }
 
@@ -816,21 +883,37 @@ extern "C" int sa_agcl_corr(const SaAgclArgs* a, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-extern "C" int sa_agcl_conv1x1(const SaAgclArgs* a, const void* w16, const float* bias, int cout, void* out,
-                               int out_stride, hipStream_t stream) {
-  if (!a->iter_mode || a->C != 256 || cout != 256 || !w16 || !bias || !out || out_stride < 256 || out_stride % 8 ||
-      a->f1_stride % 8 || a->f2_stride % 8 || ((uintptr_t)out | (uintptr_t)w16 | (uintptr_t)a->f1 | (uintptr_t)a->f2) % 16 ||
-      (uintptr_t)a->flow % 8 || a->H >= 65536 || a->W >= 65536)
+extern "C" int sa_cre_motion_head(const SaAgclArgs* a, const SaCreHeadArgs* h, hipStream_t stream) {
+  const bool fl = h->wf16 != nullptr;
+  if (!a->iter_mode || a->C != 256 || !h->w16 || !h->bias || !h->cor || h->cor_stride < 256 || h->cor_stride % 8 ||
+      a->f1_stride % 8 || a->f2_stride % 8 ||
+      ((uintptr_t)h->cor | (uintptr_t)h->w16 | (uintptr_t)a->f1 | (uintptr_t)a->f2) % 16 || (uintptr_t)a->flow % 8 ||
+      a->H >= 65536 || a->W >= 65536)
+    return -2;
+  if (fl && (!h->fbias || !h->flo || h->flo_stride < 128 || !h->fcopy || h->fcopy_stride < 2 || (uintptr_t)h->wf16 % 16))
     return -2;
   const long tiles = (long)a->N * ((a->H + 1) / 2) * ((a->W + 31) / 32);
   if (tiles >= (1L << 31)) return -2;
-  if (a->small_patch)
-    hipLaunchKernelGGL((agcl_iter_c1_kernel<1, 1>), dim3((unsigned)tiles), dim3(512), 0, stream, *a, (const f16*)w16,
-                       bias, (f16*)out, out_stride);
-  else
-    hipLaunchKernelGGL((agcl_iter_c1_kernel<4, 0>), dim3((unsigned)tiles), dim3(512), 0, stream, *a, (const f16*)w16,
-                       bias, (f16*)out, out_stride);
+  const dim3 g((unsigned)tiles);
+  if (a->small_patch) {
+    if (fl) hipLaunchKernelGGL((agcl_iter_c1_kernel<1, 1, true>), g, dim3(512), 0, stream, *a, *h);
+    else hipLaunchKernelGGL((agcl_iter_c1_kernel<1, 1, false>), g, dim3(512), 0, stream, *a, *h);
+  } else {
+    if (fl) hipLaunchKernelGGL((agcl_iter_c1_kernel<4, 0, true>), g, dim3(512), 0, stream, *a, *h);
+    else hipLaunchKernelGGL((agcl_iter_c1_kernel<4, 0, false>), g, dim3(512), 0, stream, *a, *h);
+  }
   return (int)hipGetLastError();
+}
+
+extern "C" int sa_agcl_conv1x1(const SaAgclArgs* a, const void* w16, const float* bias, int cout, void* out,
+                               int out_stride, hipStream_t stream) {
+  if (cout != 256) return -2;
+  SaCreHeadArgs h{};
+  h.w16 = w16;
+  h.bias = bias;
+  h.cor = out;
+  h.cor_stride = out_stride;
+  return sa_cre_motion_head(a, &h, stream);
 }
 
 extern "C" long sa_linear_attention_ws_floats(int N, int S, int heads, int dim) {

@@ -159,6 +159,14 @@ class CreStereo : public StereoEngine {
   void* c1_w16_ = nullptr;
   float* c1_b_ = nullptr;
   bool fuse_c1_ = !(std::getenv("SA_CRE_FUSE_C1") && std::getenv("SA_CRE_FUSE_C1")[0] == '0');
+  // iter mode, one stream: sa_cre_motion_head (AGCL -> convc1 and flow -> convf1 in one launch) then convc2 and convf2
+  // as ONE 3x3 conv over [cor1 | flo1] with block-diagonal weights (c2f2_: 1.7x the MACs of the pair, but no fork /
+  // join -- each cross-queue edge of the frame graph costs ~6.5 us, tools/graph_repro/xq_latency.hip -- and no
+  // separate launches); SA_CRE_HEAD=0 keeps the forked flow branch
+  void* f1_w16_ = nullptr;
+  float* f1_b_ = nullptr;
+  ConvLayer c2f2_;
+  bool head_ = !(std::getenv("SA_CRE_HEAD") && std::getenv("SA_CRE_HEAD")[0] == '0');
   float* fh2_b_ = nullptr;
   // SA_CRE_FH_PROJ=1: flow-head conv1 leaves conv2's tap projections (SA_EPI_TAPPROJ) in the level's fh buffer
   // instead of its 256 channels, and a stencil adds them into the flow (iterations without the mask head).  Off by
@@ -234,6 +242,33 @@ void CreStereo::build(WeightSource& src) {
     HIP_CHECK(hipMemcpy(c1_w16_, w16.data(), w16.size() * 2, hipMemcpyHostToDevice));
     c1_b_ = (float*)a.alloc(256 * 4);
     HIP_CHECK(hipMemcpy(c1_b_, b1.data.data(), 256 * 4, hipMemcpyHostToDevice));
+    // convf1 [128][2][7][7] -> [128][128] fp16, k = c * 49 + ky * 7 + kx (the flattened weight order), k >= 98 zero
+    const HostTensor& wf = ws.get(u + "encoder.convf1.weight");
+    const HostTensor& bf = ws.get(u + "encoder.convf1.bias");
+    std::vector<_Float16> wf16((size_t)128 * 128, (_Float16)0.f);
+    for (int o = 0; o < 128; ++o)
+      for (int k = 0; k < 98; ++k) wf16[(size_t)o * 128 + k] = (_Float16)wf.data[(size_t)o * 98 + k];
+    f1_w16_ = a.alloc(wf16.size() * 2);
+    HIP_CHECK(hipMemcpy(f1_w16_, wf16.data(), wf16.size() * 2, hipMemcpyHostToDevice));
+    f1_b_ = (float*)a.alloc(128 * 4);
+    HIP_CHECK(hipMemcpy(f1_b_, bf.data.data(), 128 * 4, hipMemcpyHostToDevice));
+    // [convc2 (192 <- cor1 256) ; convf2 (64 <- flo1 128)] block-diagonal over the 384 input channels
+    const HostTensor& wc2 = ws.get(u + "encoder.convc2.weight");
+    const HostTensor& bc2 = ws.get(u + "encoder.convc2.bias");
+    const HostTensor& wf2 = ws.get(u + "encoder.convf2.weight");
+    const HostTensor& bf2 = ws.get(u + "encoder.convf2.bias");
+    std::vector<float> w((size_t)256 * 384 * 9, 0.f), b(256);
+    for (int o = 0; o < 192; ++o) {
+      b[o] = bc2.data[o];
+      for (int c = 0; c < 256; ++c)
+        for (int t = 0; t < 9; ++t) w[((size_t)o * 384 + c) * 9 + t] = wc2.data[((size_t)o * 256 + c) * 9 + t];
+    }
+    for (int o = 0; o < 64; ++o) {
+      b[192 + o] = bf2.data[o];
+      for (int c = 0; c < 128; ++c)
+        for (int t = 0; t < 9; ++t) w[((size_t)(192 + o) * 384 + 256 + c) * 9 + t] = wf2.data[((size_t)o * 128 + c) * 9 + t];
+    }
+    c2f2_.build_raw(a, w, b, 256, 384, {{256, 256}, {128, 128}}, s3);
   }
   convf1_.build(a, ws, {u + "encoder.convf1"}, {{2, 8}}, s3);
   convf2_.build(a, ws, {u + "encoder.convf2"}, {{128, 128}}, s3);
@@ -327,27 +362,43 @@ void CreStereo::update(hipStream_t s, Level& L, const Tensor& f1, const Tensor& 
   // queues behind convc2 (SA_CRE_AGCL_FIRST=0: flow branch captured first, as in round 4)
   const bool par = par_ && !tuning_pass_;
   const long P = (long)B * L.h * L.w;
-  auto agcl_c1 = [&] {  // correlation -> convc1 (+ relu) into L.cor1
-    if (iter_mode && fuse_c1_) {
-      check(sa_agcl_conv1x1(&ag, c1_w16_, c1_b_, 256, L.cor1.ptr, L.cor1.stride, s), "agcl + convc1");
-      return;
+  if (iter_mode && head_) {
+    SaCreHeadArgs hd{};
+    hd.w16 = c1_w16_;
+    hd.bias = c1_b_;
+    hd.cor = L.cor1.ptr;
+    hd.cor_stride = L.cor1.stride;
+    hd.wf16 = f1_w16_;
+    hd.fbias = f1_b_;
+    hd.flo = L.flo1.ptr;
+    hd.flo_stride = L.flo1.stride;
+    hd.fcopy = L.xin.slice_c(254, 2).ptr;
+    hd.fcopy_stride = L.xin.stride;
+    check(sa_cre_motion_head(&ag, &hd, s), "motion-encoder head");
+    c2f2_.run(s, {L.cor1, L.flo1}, L.corflo, SA_ACT_RELU);
+  } else {
+    auto agcl_c1 = [&] {  // correlation -> convc1 (+ relu) into L.cor1
+      if (iter_mode && fuse_c1_) {
+        check(sa_agcl_conv1x1(&ag, c1_w16_, c1_b_, 256, L.cor1.ptr, L.cor1.stride, s), "agcl + convc1");
+        return;
+      }
+      check(sa_agcl_corr(&ag, s), "agcl");
+      convc1_.run(s, {L.corr}, L.cor1, SA_ACT_RELU);
+    };
+    {
+      hipStream_t fs = par ? fork(s) : s;
+      if (agcl_first_) agcl_c1();
+      ScopedSplitK sk(par ? &splitk_side_ : current_splitk());
+      check(sa_flow_features(L.flow, 2, P, L.flowfeat.ptr, L.flowfeat.stride, 8, L.xin.slice_c(254, 2).ptr,
+                             L.xin.stride, fs),
+            "flow features");
+      convf1_.run(fs, {L.flowfeat}, L.flo1, SA_ACT_RELU);
+      convf2_.run(fs, {L.flo1}, L.corflo.slice_c(192, 64), SA_ACT_RELU);
     }
-    check(sa_agcl_corr(&ag, s), "agcl");
-    convc1_.run(s, {L.corr}, L.cor1, SA_ACT_RELU);
-  };
-  {
-    hipStream_t fs = par ? fork(s) : s;
-    if (agcl_first_) agcl_c1();
-    ScopedSplitK sk(par ? &splitk_side_ : current_splitk());
-    check(sa_flow_features(L.flow, 2, P, L.flowfeat.ptr, L.flowfeat.stride, 8, L.xin.slice_c(254, 2).ptr,
-                           L.xin.stride, fs),
-          "flow features");
-    convf1_.run(fs, {L.flowfeat}, L.flo1, SA_ACT_RELU);
-    convf2_.run(fs, {L.flo1}, L.corflo.slice_c(192, 64), SA_ACT_RELU);
+    if (!agcl_first_) agcl_c1();
+    convc2_.run(s, {L.cor1}, L.corflo.slice_c(0, 192), SA_ACT_RELU);
+    if (par) join(s);
   }
-  if (!agcl_first_) agcl_c1();
-  convc2_.run(s, {L.cor1}, L.corflo.slice_c(0, 192), SA_ACT_RELU);
-  if (par) join(s);
   mconv_.run(s, {L.corflo}, L.xin.slice_c(128, 126), SA_ACT_RELU);
   // SepConvGRU: horizontal then vertical; z/r and q gates fused into the conv epilogues
   for (int d = 0; d < 2 && gru_split_; ++d) {

@@ -158,6 +158,7 @@ def build(jobs: int | None = None, verbose: bool = False) -> dict:
     gdir = ROOT / "tools" / "graph_repro"
     for src, out, extra in (("graph_capture_repro.hip", "graph_capture_repro", []),
                             ("overlap_repro.hip", "overlap_repro", []),
+                            ("xq_latency.hip", "xq_latency", []),
                             ("other_kernel.hip", "other_kernel.hsaco", ["--genco"])):
         s, o = gdir / src, BINDIR / out
         if not o.exists() or o.stat().st_mtime < s.stat().st_mtime:

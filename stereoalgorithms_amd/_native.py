@@ -111,6 +111,14 @@ class SaAgclArgs(C.Structure):
     ]
 
 
+class SaCreHeadArgs(C.Structure):
+    _fields_ = [
+        ("w16", C.c_void_p), ("bias", C.c_void_p), ("cor", C.c_void_p), ("cor_stride", C.c_int32),
+        ("wf16", C.c_void_p), ("fbias", C.c_void_p), ("flo", C.c_void_p), ("flo_stride", C.c_int32),
+        ("fcopy", C.c_void_p), ("fcopy_stride", C.c_int32),
+    ]
+
+
 class SaEwArgs(C.Structure):
     _fields_ = [
         ("x", C.c_void_p), ("x_stride", C.c_int32), ("add", C.c_void_p), ("add_stride", C.c_int32),
@@ -149,6 +157,7 @@ def _declare_dev(lib):
         "sa_reproject": (_i, [_p, _i, _f, _p, _i, _i, _i, _p, _p, _p, _p]),
         "sa_agcl_corr": (_i, [C.POINTER(SaAgclArgs), _p]),
         "sa_agcl_conv1x1": (_i, [C.POINTER(SaAgclArgs), _p, _p, _i, _p, _i, _p]),
+        "sa_cre_motion_head": (_i, [C.POINTER(SaAgclArgs), C.POINTER(SaCreHeadArgs), _p]),
         "sa_linear_attention": (_i, [_p, _i, _p, _i, _p, _i, _p, _i, _i, _i, _i, _i, _i, _f, _p, _p]),
         "sa_linear_attention_ws_floats": (C.c_long, [_i, _i, _i, _i]),
         "sa_layernorm": (_i, [_p, _i, _p, _p, _p, _i, _p, _i, C.c_long, _i, _f, _p]),

@@ -381,6 +381,34 @@ def agcl_conv1x1(f1, f2, flow, weight, bias, small_patch=False):
     return out
 
 
+def cre_motion_head(f1, f2, flow, wc, bc, wf, bf, small_patch=False):
+    """CREStereo motion-encoder head in one launch (iter mode): relu(convc1(AGCL)) -> [N,H,W,256], relu(convf1(flow))
+    -> [N,H,W,128] (7x7, pad 3) and the fp16 flow copy -> [N,H,W,2].  wc [256,36(,1,1)], wf [128,2,7,7]."""
+    n, h, w, c = f1.shape
+    dev = f1.device
+    wc16 = torch.zeros(256, 64, dtype=torch.float16, device=dev)
+    wc16[:, :36] = wc.reshape(256, 36).to(torch.float16)
+    wf16 = torch.zeros(128, 128, dtype=torch.float16, device=dev)
+    wf16[:, :98] = wf.reshape(128, 98).to(torch.float16)  # k = c * 49 + ky * 7 + kx
+    bc32, bf32 = bc.float().contiguous(), bf.float().contiguous()
+    cor = torch.empty(n, h, w, 256, dtype=torch.float16, device=dev)
+    flo = torch.empty(n, h, w, 128, dtype=torch.float16, device=dev)
+    fcopy = torch.empty(n, h, w, 2, dtype=torch.float16, device=dev)
+    a = N.SaAgclArgs()
+    a.f1, a.f1_stride = f1.data_ptr(), _pix_stride(f1)
+    a.f2, a.f2_stride = f2.data_ptr(), _pix_stride(f2)
+    assert flow.dtype == torch.float32 and flow.is_contiguous() and flow.shape == (n, h, w, 2)
+    a.flow = flow.data_ptr()
+    a.N, a.H, a.W, a.C = n, h, w, c
+    a.small_patch, a.iter_mode = int(small_patch), 1
+    hd = N.SaCreHeadArgs()
+    hd.w16, hd.bias, hd.cor, hd.cor_stride = wc16.data_ptr(), bc32.data_ptr(), cor.data_ptr(), 256
+    hd.wf16, hd.fbias, hd.flo, hd.flo_stride = wf16.data_ptr(), bf32.data_ptr(), flo.data_ptr(), 128
+    hd.fcopy, hd.fcopy_stride = fcopy.data_ptr(), 2
+    N.check(N.dev().sa_cre_motion_head(C.byref(a), C.byref(hd), _stream()), "sa_cre_motion_head")
+    return cor, flo, fcopy
+
+
 def linear_attention(q, k, v, heads=8, eps=1e-6):
     """q: fp16 [N, L, heads*dim], k/v: [N, S, heads*dim] (last dim may be a slice) -> fp16 [N, L, heads*dim]."""
     n, l, d = q.shape

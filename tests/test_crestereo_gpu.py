@@ -79,6 +79,34 @@ def test_agcl_conv1x1_vs_oracle(small_patch, shape):
     assert rel_err(out.permute(0, 3, 1, 2), ref) < 5e-3
 
 
+@pytest.mark.parametrize("small_patch", [False, True])
+@pytest.mark.parametrize("shape", [(2, 13, 70), (1, 120, 160)])
+def test_cre_motion_head_vs_oracle(small_patch, shape):
+    """One-launch motion-encoder head: relu(convc1(AGCL iter)) as above, relu(convf1(flow)) (7x7, pad 3, on the
+    fp16-rounded flow like the unfused path's flow features) and the fp16 flow copy."""
+    from stereoalgorithms_amd.models.crestereo import AGCL
+    O = ops()
+    torch.manual_seed(4)
+    n, h, w = shape
+    f1 = torch.randn(n, 256, h, w, device=DEV).half().float()
+    f2 = torch.randn(n, 256, h, w, device=DEV).half().float()
+    flow = torch.randn(n, 2, h, w, device=DEV) * 3
+    wc = torch.randn(256, 36, 1, 1, device=DEV) / 6
+    bc = torch.randn(256, device=DEV) * 0.1
+    wf = torch.randn(128, 2, 7, 7, device=DEV) / 10
+    bf = torch.randn(128, device=DEV) * 0.1
+    with torch.no_grad():
+        corr = AGCL(f1, f2).corr_iter(flow, small_patch)
+        ref_c = F.relu(F.conv2d(corr.half().float(), wc.half().float(), bc))
+        ref_f = F.relu(F.conv2d(flow.half().float(), wf.half().float(), bf, padding=3))
+    cor, flo, fcopy = O.cre_motion_head(nhwc(f1).half(), nhwc(f2).half(), nhwc(flow), wc, bc, wf, bf,
+                                        small_patch=small_patch)
+    torch.cuda.synchronize()
+    assert rel_err(cor.permute(0, 3, 1, 2), ref_c) < 5e-3
+    assert rel_err(flo.permute(0, 3, 1, 2), ref_f) < 2e-3
+    assert torch.equal(fcopy, nhwc(flow).half())
+
+
 @pytest.mark.parametrize("n,L,S", [(2, 77, 90), (2, 1200, 1200), (1, 1200, 1200)])
 def test_linear_attention_layer_pieces(n, L, S):
     """Chunked linear attention (partial KV / Ksum per 64 tokens, ordered reduction) vs the oracle, at the
