@@ -145,6 +145,7 @@ class RaftStereo : public StereoEngine {
   // 176.2 FPS, and with the RCCL all-gather forced at world size 1 (SA_DP_GATHER_WORLD1=1) 174.2 -> 177.2 FPS
   // (profiles/pipeline_b8_r02.txt), so mode 2 is now the default at every batch.
   // SA_RAFT_PIPELINE=0/1/2 forces a mode (1: G32 one iteration ahead; 2: G32 and G16 ahead, see forward()).
+  int cnet_first_mode_ = std::getenv("SA_RAFT_CNET_FIRST") ? std::atoi(std::getenv("SA_RAFT_CNET_FIRST")) : -1;
   int pipeline_mode_ = std::getenv("SA_RAFT_PIPELINE") ? std::atoi(std::getenv("SA_RAFT_PIPELINE")) : -1;
   float* pyr_ = nullptr;
   float* flow_ = nullptr;
@@ -448,8 +449,18 @@ void RaftStereo::forward(hipStream_t s) {
           "corr pyramid");
   };
   if (rc_.shared) cnet_.run(s, sp_, img_);  // shared trunk on both images
-  feature_branch(par ? fork(s) : s);
-  if (!rc_.shared) cnet_.run(s, sp_, img_.slice_n(0, Bn));
+  // SA_RAFT_CNET_FIRST=1: capture the context trunk's first node before the feature branch's (the graph executor keeps
+  // a node's first child on the parent's queue), so the two trunks' queue assignment swaps.  Default: on for the
+  // realtime preset only (same-process A/B b1: realtime 1.884 -> 1.864 ms, sceneflow 8.50 -> 8.63 ms)
+  const bool cnet_first = cnet_first_mode_ >= 0 ? cnet_first_mode_ != 0 : rc_.slow_fast;
+  if (cnet_first && par && !rc_.shared) {
+    hipStream_t fs = fork(s);
+    cnet_.run(s, sp_, img_.slice_n(0, Bn));
+    feature_branch(fs);
+  } else {
+    feature_branch(par ? fork(s) : s);
+    if (!rc_.shared) cnet_.run(s, sp_, img_.slice_n(0, Bn));
+  }
   Tensor x = cnet_.out().slice_n(0, Bn);
   Tensor lvl_in[3];
   lvl_in[0] = x;
