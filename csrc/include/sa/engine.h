@@ -146,8 +146,9 @@ class StereoEngine {
   void stage(hipStream_t s, const char* name);
 
   // the captured body; host_out: the reprojection writes the disparity and the cloud straight into pin_out_
-  void frame(hipStream_t s, bool rectify, bool host_out = false);
-  void launch_frame(hipStream_t s, bool rectify, bool host_out = false);
+  // host_in: the frame's first node copies the inputs from mapped host memory (in_src_) into the device buffers
+  void frame(hipStream_t s, bool rectify, bool host_out = false, bool host_in = false);
+  void launch_frame(hipStream_t s, bool rectify, bool host_out = false, bool host_in = false);
 
   EngineConfig cfg_;
   DeviceArena arena_;
@@ -163,14 +164,19 @@ class StereoEngine {
   float* rect_maps_ = nullptr;  // [2][H][W][2]
   float Q_[16];
   bool have_Q_ = false;
-  GraphExec graph_[4];  // [rectify + 2 * host_out]: host_out graphs reproject straight into the pinned outputs
+  GraphExec graph_[8];  // [rectify + 2 * host_out + 4 * host_in]: host_out graphs reproject straight into host memory
   float* pin_out_dev_ = nullptr;  // device address of pin_out_ (kernels write the zero-copy outputs through it)
   // host-output frames: the reprojection node of each host-output graph (captured writing to the targets of the
   // frame that captured it) and the {disparity, cloud} device pointers it currently writes; a frame with other
   // targets re-points the node (sa_reproject_update_node) before the launch
-  hipGraphNode_t repro_node_[4] = {};
-  float* repro_ptrs_[4][2] = {};
+  hipGraphNode_t repro_node_[8] = {};
+  float* repro_ptrs_[8][2] = {};
   float* out_target_[2] = {};  // targets of the frame being launched (read by frame() at capture)
+  // host-input frames: the input-copy node of each host_in graph and the {left, right} sources it reads
+  hipGraphNode_t in_node_[8] = {};
+  const uint8_t* in_ptrs_[8][2] = {};
+  const uint8_t* in_src_[2] = {};  // device addresses of the mapped inputs of the frame being launched
+  uint8_t* pin_in_dev_ = nullptr;
   // caller output buffers of run_host mapped for the GPU (hipHostRegister) once a buffer comes back for a second
   // frame: role 0 disparity, 1 cloud.  A different pointer for a role unregisters the previous one; all go with
   // the engine.  SA_HOST_REGISTER=0 disables (caller buffers are then filled from the pinned staging).
@@ -180,8 +186,9 @@ class StereoEngine {
     void* dev = nullptr;
     bool failed = false;
   };
-  HostReg host_reg_[2];
+  HostReg host_reg_[4];  // roles 0 disparity, 1 cloud, 2 left input, 3 right input
   float* resolve_host_out(int role, void* p, size_t bytes);
+  void* resolve_host_reg(int role, void* p, size_t bytes);
   void unregister_host(int role);
   std::string default_plan_path() const;
   std::string plan_path_;

@@ -255,6 +255,12 @@ int sa_reproject_update_node(hipGraphExec_t exec, hipGraphNode_t node, const flo
                              const uint8_t* left_bgr, int B, int H, int W, const float* Q16, float* disp_out,
                              float* cloud);
 
+// both frame images from mapped host memory (a, b: device addresses of registered / pinned host arrays) into device
+// buffers; bytes % 16 == 0, 16-B aligned.  _update_node re-points a captured node's sources.
+int sa_copy_frames(const void* a, const void* b, void* da, void* db, long bytes, hipStream_t stream);
+int sa_copy_frames_update_node(hipGraphExec_t exec, hipGraphNode_t node, const void* a, const void* b, void* da,
+                               void* db, long bytes);
+
 // ---- CREStereo / Fast-ACVNet+ / HITNet ops (stereo_ops.hip) ---------------------------------
 typedef struct {
   const void* f1; int32_t f1_stride;      // left features fp16 NHWC, C channels (4 groups)

@@ -270,6 +270,57 @@ extern "C" int sa_reproject_update_node(hipGraphExec_t exec, hipGraphNode_t node
   return (int)hipGraphExecKernelNodeSetParams(exec, node, &p);
 }
 
+// Frame inputs straight from mapped host memory (run_host's zero-copy input path): one launch copies both images of
+// the frame from the caller's registered arrays or the engine's pinned staging into device memory -- PCIe reads
+// issued by the CUs, replacing two host-enqueued DMA copies ahead of the graph.  16 B per lane; bytes % 16 == 0.
+__global__ __launch_bounds__(256) void copy_frames_kernel(const uint4* __restrict__ a, const uint4* __restrict__ b,
+                                                          uint4* __restrict__ da, uint4* __restrict__ db, long n16) {
+  const uint4* src = blockIdx.y ? b : a;
+  uint4* dst = blockIdx.y ? db : da;
+  constexpr int U = 4;
+  for (long i = ((long)blockIdx.x * 256 + threadIdx.x) * U; i < n16; i += (long)gridDim.x * 256 * U) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i + u < n16) v[u] = src[i + u];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i + u < n16) dst[i + u] = v[u];
+  }
+}
+
+static dim3 copy_frames_grid(long n16) {
+  long g = (n16 + 1023) / 1024;
+  if (g > 1024) g = 1024;
+  if (g < 1) g = 1;
+  return dim3((unsigned)g, 2);
+}
+
+extern "C" int sa_copy_frames(const void* a, const void* b, void* da, void* db, long bytes, hipStream_t stream) {
+  if (bytes <= 0 || bytes % 16 || ((uintptr_t)a | (uintptr_t)b | (uintptr_t)da | (uintptr_t)db) % 16) return -2;
+  const long n16 = bytes / 16;
+  hipLaunchKernelGGL(copy_frames_kernel, copy_frames_grid(n16), dim3(256), 0, stream, (const uint4*)a, (const uint4*)b,
+                     (uint4*)da, (uint4*)db, n16);
+  return (int)hipGetLastError();
+}
+
+// re-point the sources of a captured sa_copy_frames node (destinations / size unchanged)
+extern "C" int sa_copy_frames_update_node(hipGraphExec_t exec, hipGraphNode_t node, const void* a, const void* b,
+                                          void* da, void* db, long bytes) {
+  if (bytes <= 0 || bytes % 16 || ((uintptr_t)a | (uintptr_t)b) % 16) return -2;
+  hipKernelNodeParams p{};
+  hipError_t e = hipGraphKernelNodeGetParams(node, &p);
+  if (e != hipSuccess) return (int)e;
+  if (p.func != reinterpret_cast<void*>(copy_frames_kernel)) return -2;
+  const long n16 = bytes / 16;
+  const uint4 *sa = (const uint4*)a, *sb = (const uint4*)b;
+  uint4 *sda = (uint4*)da, *sdb = (uint4*)db;
+  void* args[] = {(void*)&sa, (void*)&sb, (void*)&sda, (void*)&sdb, (void*)&n16};
+  p.kernelParams = args;
+  p.extra = nullptr;
+  return (int)hipGraphExecKernelNodeSetParams(exec, node, &p);
+}
+
 extern "C" int sa_convex_upsample(const void* mask, int mask_stride, const float* flow, int B,
                                   int H, int W, int factor, float sign, float* out,
                                   hipStream_t stream) {

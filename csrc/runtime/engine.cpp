@@ -80,7 +80,7 @@ StereoEngine::StereoEngine(const EngineConfig& cfg) : cfg_(cfg) {
 
 StereoEngine::~StereoEngine() {
   if (stream_) (void)hipStreamSynchronize(stream_);
-  for (int r = 0; r < 2; ++r) unregister_host(r);
+  for (int r = 0; r < 4; ++r) unregister_host(r);
   for (GraphExec& g : graph_) g.reset();
   copy_pool_.reset();
   for (auto& e : ev_copy_)
@@ -168,6 +168,7 @@ void StereoEngine::init() {
   HIP_CHECK(hipHostMalloc((void**)&pin_in_, 2 * img, hipHostMallocDefault));
   HIP_CHECK(hipHostMalloc((void**)&pin_out_, (size_t)B() * H() * W() * 7 * 4 + 2 * img, hipHostMallocDefault));
   HIP_CHECK(hipHostGetDevicePointer((void**)&pin_out_dev_, pin_out_, 0));
+  HIP_CHECK(hipHostGetDevicePointer((void**)&pin_in_dev_, pin_in_, 0));
   for (auto& e : ev_copy_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   if (const char* ht = std::getenv("SA_HOST_TIMES"))
     if (ht[0] == '1')
@@ -298,7 +299,7 @@ void StereoEngine::set_Q(const float* q16) {
   std::memcpy(Q_, q16, sizeof(Q_));
   have_Q_ = true;
   for (GraphExec& g : graph_) g.reset();  // Q is baked into the reprojection launch
-  for (int i = 0; i < 4; ++i) repro_node_[i] = nullptr;
+  for (int i = 0; i < 8; ++i) repro_node_[i] = in_node_[i] = nullptr;
 }
 
 void StereoEngine::set_rectify_maps(const float* ml, const float* mr) {
@@ -359,10 +360,32 @@ std::vector<std::pair<std::string, float>> StereoEngine::stage_times() const {
   return out;
 }
 
-void StereoEngine::frame(hipStream_t s, bool rectify, bool host_out) {
+void StereoEngine::frame(hipStream_t s, bool rectify, bool host_out, bool host_in) {
   ScopedSplitK sk(&splitk_);
   nstage_ = 0;
   stage(s, "start");
+  const int gi = (rectify ? 1 : 0) + (host_out ? 2 : 0) + (host_in ? 4 : 0);
+  auto captured_node = [&](hipGraphNode_t* node) {  // the node just captured on s (when capturing)
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    const hipGraphNode_t* deps = nullptr;
+    size_t nd = 0;
+    HIP_CHECK(hipStreamGetCaptureInfo_v2(s, &cs, nullptr, nullptr, &deps, &nd));
+    if (cs == hipStreamCaptureStatusActive && nd == 1) {
+      *node = deps[0];
+      return true;
+    }
+    return false;
+  };
+  if (host_in) {
+    const size_t img = (size_t)B() * H() * W() * 3;
+    const int rc = sa_copy_frames(in_src_[0], in_src_[1], rectify ? raw_left_ : in_left_, rectify ? raw_right_ : in_right_,
+                                  (long)img, s);
+    SA_REQUIRE(rc == 0, "input copy failed (%d)", rc);
+    if (captured_node(&in_node_[gi])) {
+      in_ptrs_[gi][0] = in_src_[0];
+      in_ptrs_[gi][1] = in_src_[1];
+    }
+  }
   if (rectify) {
     SA_REQUIRE(rect_maps_ != nullptr, "rectification requested but no maps set");
     // left images use map 0, right images map 1 (maps laid out [2][H][W][2])
@@ -380,13 +403,7 @@ void StereoEngine::frame(hipStream_t s, bool rectify, bool host_out) {
     int rc;
     if (host_out) {
       rc = sa_reproject(disp_, 1, 1.f, in_left_, B(), H(), W(), Q_, out_target_[0], out_target_[1], s);
-      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-      const hipGraphNode_t* deps = nullptr;
-      size_t nd = 0;
-      HIP_CHECK(hipStreamGetCaptureInfo_v2(s, &cs, nullptr, nullptr, &deps, &nd));
-      if (cs == hipStreamCaptureStatusActive && nd == 1) {
-        const int gi = (rectify ? 1 : 0) + 2;
-        repro_node_[gi] = deps[0];
+      if (rc == 0 && captured_node(&repro_node_[gi])) {
         repro_ptrs_[gi][0] = out_target_[0];
         repro_ptrs_[gi][1] = out_target_[1];
       }
@@ -399,8 +416,8 @@ void StereoEngine::frame(hipStream_t s, bool rectify, bool host_out) {
   SA_LAUNCH_CHECK(s);
 }
 
-void StereoEngine::launch_frame(hipStream_t s, bool rectify, bool host_out) {
-  const int gi = (rectify ? 1 : 0) + (host_out ? 2 : 0);
+void StereoEngine::launch_frame(hipStream_t s, bool rectify, bool host_out, bool host_in) {
+  const int gi = (rectify ? 1 : 0) + (host_out ? 2 : 0) + (host_in ? 4 : 0);
   GraphExec& g = graph_[gi];
   // The frame always executes on the engine's own stream (where its graphs were captured); a
   // caller stream is ordered against it with events on both sides, so graph execs are never
@@ -412,7 +429,16 @@ void StereoEngine::launch_frame(hipStream_t s, bool rectify, bool host_out) {
   }
   TraceRange tr("frame");
   if (cfg_.use_graph) {
-    if (!g.ready()) g.capture(stream_, [&] { frame(stream_, rectify, host_out); });
+    if (!g.ready()) g.capture(stream_, [&] { frame(stream_, rectify, host_out, host_in); });
+    if (host_in && (in_ptrs_[gi][0] != in_src_[0] || in_ptrs_[gi][1] != in_src_[1])) {
+      SA_REQUIRE(in_node_[gi] != nullptr, "host-input graph without its input-copy node");
+      const size_t img = (size_t)B() * H() * W() * 3;
+      const int rc = sa_copy_frames_update_node(g.exec(), in_node_[gi], in_src_[0], in_src_[1],
+                                                rectify ? raw_left_ : in_left_, rectify ? raw_right_ : in_right_, (long)img);
+      SA_REQUIRE(rc == 0, "re-pointing the input-copy node failed (%d)", rc);
+      in_ptrs_[gi][0] = in_src_[0];
+      in_ptrs_[gi][1] = in_src_[1];
+    }
     if (host_out && (repro_ptrs_[gi][0] != out_target_[0] || repro_ptrs_[gi][1] != out_target_[1])) {
       SA_REQUIRE(repro_node_[gi] != nullptr, "host-output graph without its reprojection node");
       const int rc = sa_reproject_update_node(g.exec(), repro_node_[gi], disp_, 1, 1.f, in_left_, B(), H(), W(), Q_,
@@ -423,7 +449,7 @@ void StereoEngine::launch_frame(hipStream_t s, bool rectify, bool host_out) {
     }
     g.launch(stream_);
   } else {
-    frame(stream_, rectify, host_out);
+    frame(stream_, rectify, host_out, host_in);
   }
   static const bool sync_frame = [] {
     const char* v = std::getenv("SA_SYNC_FRAME");
@@ -472,6 +498,12 @@ float* StereoEngine::resolve_host_out(int role, void* p, size_t bytes) {
   const size_t n = (size_t)B() * H() * W();
   if (role == 0 && p == pin_out_) return pin_out_dev_;
   if (role == 1 && p == pin_out_ + n) return pin_out_dev_ + n;
+  return static_cast<float*>(resolve_host_reg(role, p, bytes));
+}
+
+// Device address of a caller host buffer for role `role`: mapped (hipHostRegister) once the same (pointer, size)
+// comes back for a second frame, nullptr before that, after a failed registration, or with SA_HOST_REGISTER=0.
+void* StereoEngine::resolve_host_reg(int role, void* p, size_t bytes) {
   static const bool on = [] {
     const char* e = std::getenv("SA_HOST_REGISTER");
     return !(e && e[0] == '0');
@@ -484,12 +516,12 @@ float* StereoEngine::resolve_host_out(int role, void* p, size_t bytes) {
     r.bytes = bytes;
     return nullptr;
   }
-  if (r.dev || r.failed) return static_cast<float*>(r.dev);
+  if (r.dev || r.failed) return r.dev;
   void* dev = nullptr;
   if (hipHostRegister(p, bytes, hipHostRegisterMapped) != hipSuccess) {
     (void)hipGetLastError();
     r.failed = true;  // e.g. overlapping an already registered range: keep copying
-    SA_LOGW("run_host: caller buffer %p (%zu B) could not be mapped; output copies stay", p, bytes);
+    SA_LOGW("run_host: caller buffer %p (%zu B) could not be mapped; copies stay", p, bytes);
     return nullptr;
   }
   if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess || !dev) {
@@ -499,7 +531,7 @@ float* StereoEngine::resolve_host_out(int role, void* p, size_t bytes) {
     return nullptr;
   }
   r.dev = dev;
-  return static_cast<float*>(dev);
+  return dev;
 }
 
 void StereoEngine::run_host(uint8_t* left, uint8_t* right, float* disp, float* cloud, bool rectify) {
@@ -511,16 +543,45 @@ void StereoEngine::run_host(uint8_t* left, uint8_t* right, float* disp, float* c
   const size_t n = (size_t)B() * H() * W();
   // Buffers handed out by host_buffers() are the pinned staging itself: a caller that fills / reads them in place
   // skips the pageable <-> pinned copies (the D2H lands in the caller's array directly).
+  // Zero-copy inputs (SA_HOST_IN=0: DMA copies from the pinned staging instead): the frame graph's first node reads
+  // the images over PCIe from the engine's pinned staging (host_buffers()) or from the caller's arrays once mapped
+  // (a caller passing the same input arrays again, like a camera's frame buffers); otherwise the caller's arrays
+  // are staged into the pinned buffers first.
+  static const bool host_in_on = [] {
+    const char* e = std::getenv("SA_HOST_IN");
+    return !(e && e[0] == '0');
+  }();
+  const bool host_in = host_in_on && cfg_.use_graph && img % 16 == 0;
+  const uint8_t* src[2] = {nullptr, nullptr};
   std::vector<HostCopyPool::Task> in;
-  if (left != pin_in_) in.push_back({pin_in_, left, img, nullptr});
-  if (right != pin_in_ + img) in.push_back({pin_in_ + img, right, img, nullptr});
+  for (int i = 0; i < 2; ++i) {
+    uint8_t* user = i ? right : left;
+    uint8_t* pin = pin_in_ + i * img;
+    if (user == pin) {
+      src[i] = pin_in_dev_ + i * img;
+      continue;
+    }
+    const uint8_t* dev =
+        host_in && ((uintptr_t)user & 15) == 0 ? static_cast<const uint8_t*>(resolve_host_reg(2 + i, user, img)) : nullptr;
+    if (dev) {
+      src[i] = dev;
+    } else {
+      in.push_back({pin, user, img, nullptr});
+      src[i] = pin_in_dev_ + i * img;
+    }
+  }
   copy_pool_->run(in);
   const auto t1 = clk::now();
   if (host_ev_[0]) HIP_CHECK(hipEventRecord(host_ev_[0], s));
-  uint8_t* dl = rectify ? raw_left_ : in_left_;
-  uint8_t* dr = rectify ? raw_right_ : in_right_;
-  HIP_CHECK(hipMemcpyAsync(dl, pin_in_, img, hipMemcpyHostToDevice, s));
-  HIP_CHECK(hipMemcpyAsync(dr, pin_in_ + img, img, hipMemcpyHostToDevice, s));
+  if (host_in) {
+    in_src_[0] = src[0];
+    in_src_[1] = src[1];
+  } else {
+    uint8_t* dl = rectify ? raw_left_ : in_left_;
+    uint8_t* dr = rectify ? raw_right_ : in_right_;
+    HIP_CHECK(hipMemcpyAsync(dl, pin_in_, img, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(dr, pin_in_ + img, img, hipMemcpyHostToDevice, s));
+  }
   if (host_ev_[1]) HIP_CHECK(hipEventRecord(host_ev_[1], s));
   // zero-copy outputs: the frame graph's reprojection writes disparity and cloud straight into host memory over
   // PCIe and no D2H copy follows -- into the engine's pinned buffers (host_buffers()) or into the caller's own
@@ -533,7 +594,7 @@ void StereoEngine::run_host(uint8_t* left, uint8_t* right, float* disp, float* c
     out_target_[0] = dd;
     out_target_[1] = dc;
   }
-  launch_frame(s, rectify, zero_copy);
+  launch_frame(s, rectify, zero_copy, host_in);
   if (host_ev_[2]) HIP_CHECK(hipEventRecord(host_ev_[2], s));
   float* pd = pin_out_;
   float* pc = pin_out_ + n;

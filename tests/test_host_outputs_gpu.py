@@ -47,3 +47,40 @@ def test_caller_buffers_reuse_and_swap():
         e.run_host(l, r, cloud=False, out=d3)
         assert np.array_equal(d3, ref_d)
     e.close()
+
+
+def test_caller_inputs_zero_copy_and_fresh_arrays():
+    """Zero-copy INPUTS (the frame graph's first node reads the caller's mapped arrays over PCIe): the same arrays
+    refilled every frame (a camera's frame buffers) and fresh arrays every frame (a freed array's address comes back
+    with other pages: the mapping must follow them) give, frame by frame, the pinned-I/O path's bytes for that
+    frame's images -- outputs included."""
+    from stereoalgorithms_amd.models.engine import NativeStereoEngine
+    e = NativeStereoEngine("raftstereo-realtime", None, 480, 640, batch=1, device=0)
+    e.set_Q(Q)
+    pairs = [batch_pairs(1, 480, 640, seed=s) for s in (3, 4)]
+    hb = e.host_buffers()
+    refs = []
+    for l, r in pairs:
+        hb["left"][...] = l
+        hb["right"][...] = r
+        e.run_host(hb["left"], hb["right"], cloud=True, out=hb["disp"], cloud_out=hb["cloud"])
+        refs.append((hb["disp"].copy(), hb["cloud"].copy()))
+    hb = None
+    assert not np.array_equal(refs[0][0], refs[1][0])
+    L, R = np.empty_like(pairs[0][0]), np.empty_like(pairs[0][1])
+    d, c = np.empty((1, 480, 640), np.float32), np.empty((1, 480, 640, 6), np.float32)
+    for k in range(5):  # mapped from the second frame on, new content every frame
+        i = k % 2
+        L[...] = pairs[i][0]
+        R[...] = pairs[i][1]
+        e.run_host(L, R, cloud=True, out=d, cloud_out=c)
+        assert np.array_equal(d, refs[i][0]) and np.array_equal(c, refs[i][1], equal_nan=True), k
+    del L, R, d, c
+    for k in range(6):
+        i = k % 2
+        L, R = pairs[i][0].copy(), pairs[i][1].copy()
+        d, c = np.empty((1, 480, 640), np.float32), np.empty((1, 480, 640, 6), np.float32)
+        e.run_host(L, R, cloud=True, out=d, cloud_out=c)
+        assert np.array_equal(d, refs[i][0]) and np.array_equal(c, refs[i][1], equal_nan=True), k
+        del L, R, d, c
+    e.close()
