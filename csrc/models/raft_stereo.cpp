@@ -372,7 +372,11 @@ void RaftStereo::gru(hipStream_t s, int i, const std::vector<Tensor>& x) const {
   // the schedule knobs -- so the eager tuning pass and the capture agree and every schedule runs the same tactics
   // (tests/test_raft_modes_gpu.py: bitwise-equal schedules).  Same-process A/B: b1 8.438 -> 7.991 ms; at b8 (large
   // grids) it cost 1.6 %, so not there.
-  ScopedSideBranch sb(i >= 1 && B() <= 2 && rc_.n_gru == 3 && !rc_.slow_fast);
+  // Round 5: the finest level's GRU convs too (they share the chip with the coarse levels' chain, which is the
+  // longer path of the b1 iteration cycle): same-process A/B b1 8.208 -> 8.078 ms.  SA_RAFT_SIDE_MASK: bit i marks
+  // level i, bit 3 the flow head (default 15; 6 = round 4's coarse levels only; 4 / 0: b1 8.51 / 8.62 ms).
+  const int side_mask = std::getenv("SA_RAFT_SIDE_MASK") ? std::atoi(std::getenv("SA_RAFT_SIDE_MASK")) : 15;
+  ScopedSideBranch sb(((side_mask >> i) & 1) && B() <= 2 && rc_.n_gru == 3 && !rc_.slow_fast);
   std::vector<Tensor> srcs = {net_[i]};
   srcs.insert(srcs.end(), x.begin(), x.end());
   if (gru_split_) {
@@ -573,6 +577,9 @@ void RaftStereo::forward(hipStream_t s) {
   // flow head: conv1 (+ the mask head's conv on the last iteration), then conv2's taps + stencil into the flow
   // (x only) in one launch; mask head 1x1 on the last iteration
   auto head = [&](hipStream_t st, bool last) {
+    // SA_RAFT_SIDE_MASK bit 3: the flow head's conv1 tuned for co-residency as well (b1 7.960 -> 7.924 ms)
+    const int side_mask = std::getenv("SA_RAFT_SIDE_MASK") ? std::atoi(std::getenv("SA_RAFT_SIDE_MASK")) : 15;
+    ScopedSideBranch sb(((side_mask >> 3) & 1) && Bn <= 2 && rc_.n_gru == 3 && !rc_.slow_fast);
     const bool fh_proj = fh_proj_env_ >= 0 ? fh_proj_env_ != 0 : (rc_.n_gru == 2 && rc_.slow_fast);
     if (!last && fh_proj) {
       // conv1's output never reaches memory: its epilogue leaves conv2's x-output tap projections per 128-channel
