@@ -173,3 +173,39 @@ def test_pmc_summary_busy_fraction(tmp_path):
     assert "SQ_VALU_MFMA_BUSY_CYCLES         2e+08" in out
     # 2e8 / (4e6 / 8 * 1024) = 0.390625
     assert "held clock, busy / (GRBM_GUI_ACTIVE / 8 x 1024): 0.391" in out
+
+
+def test_bench_regress_gate(tmp_path):
+    """tools/bench_regress.py: a > tol slower preset (or lower throughput) fails the gate, faster ones pass; the
+    baseline may be a driver BENCH_rNN.json (bench line inside run.stdout_tail) or a plain bench log."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+
+    def line(fps, sf_ms, sf_net):
+        return json.dumps({"metric": "m", "value": fps, "latency_b1": {
+            "raftstereo-sceneflow": {"latency_ms_mean": sf_ms,
+                                     "device_stages_ms": {"encoders+corr": 1.0, "gru_iterations": sf_net - 1.0,
+                                                          "reproject": 0.16}}}})
+
+    base = tmp_path / "BENCH_r01.json"
+    base.write_text(json.dumps({"parsed": {}, "run": {"stdout_tail": "noise\n" + line(100.0, 8.0, 7.0) + "\n"}}))
+
+    def gate(text):
+        f = tmp_path / "fresh.log"
+        f.write_text("warmup...\n" + text + "\n")
+        r = subprocess.run([sys.executable, str(root / "tools" / "bench_regress.py"), str(f), "--baseline", str(base)],
+                           capture_output=True, text=True)
+        return r.returncode, r.stdout
+
+    rc, out = gate(line(101.0, 7.9, 6.9))
+    assert rc == 0 and "0 regression(s)" in out
+    rc, out = gate(line(95.0, 7.9, 6.9))  # throughput -5 %
+    assert rc == 1 and "REGRESSION" in out
+    rc, out = gate(line(100.0, 8.4, 7.0))  # latency +5 %
+    assert rc == 1 and "raftstereo-sceneflow latency" in out
+    rc, out = gate(line(100.0, 8.1, 7.1))  # +1.25 % / +1.4 %: within the 3 % tolerance
+    assert rc == 0
