@@ -285,6 +285,9 @@ typedef struct {
   void* fcopy; int32_t fcopy_stride;                                      // fp16 (x, y) of the flow per pixel
 } SaCreHeadArgs;
 int sa_cre_motion_head(const SaAgclArgs* a, const SaCreHeadArgs* h, hipStream_t stream);
+// the same head from a correlation already in a->out (a->out_stride, 36 channels; offset mode: sa_agcl_corr first);
+// convf1 / fcopy required
+int sa_cre_motion_head_pre(const SaAgclArgs* a, const SaCreHeadArgs* h, hipStream_t stream);
 
 // ws: fp32 workspace of sa_linear_attention_ws_floats(N, S, heads, dim) floats (per-chunk partial KV / Ksum)
 long sa_linear_attention_ws_floats(int N, int S, int heads, int dim);

@@ -423,7 +423,9 @@ __global__ __launch_bounds__(256) void agcl_iter_tile_kernel(const SaAgclArgs a)
 // 8 x 38 halo tile staged in LDS, as a second [64 x 128(98 taps)] x [128 x 128] MFMA GEMM, plus the fp16 copy of the
 // flow the GRU input carries (xin[254:256]); the flow branch then needs no launch of its own before convf2.
 // w16: [256][64] fp16 (k >= 36 zero), bias fp32 [256]; wf16: [128][128] fp16, k = c * 49 + ky * 7 + kx (k >= 98 zero).
-template <int RX, int RY, bool FL>
+// PRE: the correlation was computed by sa_agcl_corr (offset mode, the coarse levels) and is read from a.out
+// (a.out_stride per pixel, 36 channels) instead of phases 1 / 2.
+template <int RX, int RY, bool FL, bool PRE = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void agcl_iter_c1_kernel(
     const SaAgclArgs a, const SaCreHeadArgs hd) {
   const f16* __restrict__ w16 = reinterpret_cast<const f16*>(hd.w16);
@@ -435,12 +437,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
   static_assert(PX * (2 * RY + 1) == 9, "9-tap window");
   constexpr int CRS = 72, OS = 256 + 8;
   constexpr int AFS = 136, FHW = TW + 6, FHP = (TH + 6) * FHW;  // convf1 A-tile row stride, flow halo width / size
-  constexpr int WP_BYTES = HP * 512, OST_BYTES = NPX * OS * 2, AF_BYTES = FL ? NPX * AFS * 2 : 0;
+  constexpr int WP_BYTES = PRE ? 0 : HP * 512, OST_BYTES = NPX * OS * 2, AF_BYTES = FL ? NPX * AFS * 2 : 0;
   constexpr int SMEM = WP_BYTES > OST_BYTES + AF_BYTES ? WP_BYTES : OST_BYTES + AF_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   __shared__ f16 fh[FL ? FHP * 2 : 2];
   __shared__ __attribute__((aligned(16))) f16 cr[NPX * CRS];
-  __shared__ float2 spos[HP];
+  __shared__ float2 spos[PRE ? 1 : HP];
   half8* wp = reinterpret_cast<half8*>(smem);  // [HP][32] 16-B chunks
   typedef _Float16 half2v __attribute__((ext_vector_type(2)));
   typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -453,7 +455,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
   const f16* f2 = reinterpret_cast<const f16*>(a.f2) + img * a.f2_stride + cc * 8;
   constexpr int NPI = (HP + 15) / 16, NQ = NPX / 16;
   // the halo's sample positions go through LDS (one flow load per halo pixel instead of one per lane and pixel)
-  for (int p = tid; p < HP; p += 512) {
+  for (int p = tid; p < (PRE ? 0 : HP); p += 512) {
     int hh = y0 + p / HWX, ww = x0 + p % HWX;
     hh = hh < 0 ? 0 : (hh >= a.H ? a.H - 1 : hh);
     ww = ww < 0 ? 0 : (ww >= a.W ? a.W - 1 : ww);
@@ -480,6 +482,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
   half8 lf[NQ];
 #pragma unroll
   for (int i = 0; i < NQ; ++i) {
+    if constexpr (PRE) break;
     const int q = ps + 16 * i;
     const int h = ty * TH + q / TW, w = tx * TW + q % TW;
     if (h < a.H && w < a.W)
@@ -489,9 +492,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
       lf[i] = half8{};
   }
   for (int e = tid; e < NPX * (CRS - 36); e += 512) cr[(e / (CRS - 36)) * CRS + 36 + e % (CRS - 36)] = (f16)0.f;
+  if constexpr (PRE) {
+    for (int e = tid; e < NPX * 36; e += 512) {
+      const int m = e / 36, kk = e - 36 * m;
+      const int h = ty * TH + m / TW, w = tx * TW + m % TW;
+      cr[m * CRS + kk] = h < a.H && w < a.W
+                             ? reinterpret_cast<const f16*>(a.out)[(img + (long)h * a.W + w) * a.out_stride + kk]
+                             : (f16)0.f;
+    }
+  }
   __syncthreads();
 #pragma unroll
-  for (int i0 = 0; i0 < NPI; i0 += 4) {
+  for (int i0 = 0; i0 < (PRE ? 0 : NPI); i0 += 4) {
     constexpr int CH = 4;
     half8 rv[CH][4];
     float wv[CH][4];
@@ -531,6 +543,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
   const bool b2 = c8 & 4, b1 = c8 & 2, b0 = c8 & 1;
 #pragma unroll
   for (int iq = 0; iq < NQ; ++iq) {
+    if constexpr (PRE) break;
     const int q = ps + 16 * iq;
     const int oy = q / TW, ox = q % TW;
     const half8 l8 = lf[iq];
@@ -902,6 +915,17 @@ extern "C" int sa_cre_motion_head(const SaAgclArgs* a, const SaCreHeadArgs* h, h
     if (fl) hipLaunchKernelGGL((agcl_iter_c1_kernel<4, 0, true>), g, dim3(512), 0, stream, *a, *h);
     else hipLaunchKernelGGL((agcl_iter_c1_kernel<4, 0, false>), g, dim3(512), 0, stream, *a, *h);
   }
+  return (int)hipGetLastError();
+}
+
+extern "C" int sa_cre_motion_head_pre(const SaAgclArgs* a, const SaCreHeadArgs* h, hipStream_t stream) {
+  if (!a->out || a->out_stride < 36 || !h->w16 || !h->bias || !h->cor || h->cor_stride < 256 || h->cor_stride % 8 ||
+      ((uintptr_t)h->cor | (uintptr_t)h->w16) % 16 || (uintptr_t)a->flow % 8 || !h->wf16 || !h->fbias || !h->flo ||
+      h->flo_stride < 128 || !h->fcopy || h->fcopy_stride < 2 || (uintptr_t)h->wf16 % 16)
+    return -2;
+  const long tiles = (long)a->N * ((a->H + 1) / 2) * ((a->W + 31) / 32);
+  if (tiles >= (1L << 31)) return -2;
+  hipLaunchKernelGGL((agcl_iter_c1_kernel<4, 0, true, true>), dim3((unsigned)tiles), dim3(512), 0, stream, *a, *h);
   return (int)hipGetLastError();
 }
 

@@ -156,18 +156,21 @@ void Trunk::build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std::s
   plan.commit(a);
 }
 
+void Trunk::run_step(hipStream_t s, const StatsPool& sp, const Tensor& img, int k) const {
+  if (k == 0) {
+    if (norm == Norm::Instance) {
+      conv1.run(s, {img}, c1y, SA_ACT_NONE, nullptr, SA_ACT_NONE, sp.resolve(c1st));
+      instnorm(s, c1y, sp.resolve(c1st), c1a, SA_ACT_RELU);
+    } else {
+      conv1.run(s, {img}, c1a, SA_ACT_RELU);
+    }
+    return;
+  }
+  layers[k - 1].run(s, sp, k == 1 ? c1a : layers[k - 2].out);
+}
+
 void Trunk::run(hipStream_t s, const StatsPool& sp, const Tensor& img) const {
-  if (norm == Norm::Instance) {
-    conv1.run(s, {img}, c1y, SA_ACT_NONE, nullptr, SA_ACT_NONE, sp.resolve(c1st));
-    instnorm(s, c1y, sp.resolve(c1st), c1a, SA_ACT_RELU);
-  } else {
-    conv1.run(s, {img}, c1a, SA_ACT_RELU);
-  }
-  const Tensor* x = &c1a;
-  for (const auto& rb : layers) {
-    rb.run(s, sp, *x);
-    x = &rb.out;
-  }
+  for (int k = 0; k < steps(); ++k) run_step(s, sp, img, k);
 }
 
 }  // namespace sa

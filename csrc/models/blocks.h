@@ -67,6 +67,9 @@ struct Trunk {
   void build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std::string& prefix, Norm norm, int N, int H,
              int W, int conv1_stride, const int strides[3]);
   void run(hipStream_t s, const StatsPool& sp, const Tensor& img) const;
+  // the trunk in steps (0: conv1 [+ norm], k >= 1: residual layer k - 1), for interleaving two trunks' launches
+  int steps() const { return 1 + (int)layers.size(); }
+  void run_step(hipStream_t s, const StatsPool& sp, const Tensor& img, int k) const;
   const Tensor& out() const { return layers.back().out; }
 };
 

@@ -159,14 +159,16 @@ class CreStereo : public StereoEngine {
   void* c1_w16_ = nullptr;
   float* c1_b_ = nullptr;
   bool fuse_c1_ = !(std::getenv("SA_CRE_FUSE_C1") && std::getenv("SA_CRE_FUSE_C1")[0] == '0');
-  // iter mode, one stream: sa_cre_motion_head (AGCL -> convc1 and flow -> convf1 in one launch) then convc2 and convf2
+  // one stream: sa_cre_motion_head (iter mode: AGCL -> convc1 and flow -> convf1 in one launch; offset mode: the same
+  // head after sa_agcl_corr) then convc2 and convf2
   // as ONE 3x3 conv over [cor1 | flo1] with block-diagonal weights (c2f2_: 1.7x the MACs of the pair, but no fork /
   // join -- each cross-queue edge of the frame graph costs ~6.5 us, tools/graph_repro/xq_latency.hip -- and no
   // separate launches); SA_CRE_HEAD=0 keeps the forked flow branch
   void* f1_w16_ = nullptr;
   float* f1_b_ = nullptr;
   ConvLayer c2f2_;
-  bool head_ = !(std::getenv("SA_CRE_HEAD") && std::getenv("SA_CRE_HEAD")[0] == '0');
+  // SA_CRE_HEAD: 0 off, 1 iter mode (1/4 level) only, 2 (default) every level
+  int head_mode_ = std::getenv("SA_CRE_HEAD") ? std::atoi(std::getenv("SA_CRE_HEAD")) : 2;
   float* fh2_b_ = nullptr;
   // SA_CRE_FH_PROJ=1: flow-head conv1 leaves conv2's tap projections (SA_EPI_TAPPROJ) in the level's fh buffer
   // instead of its 256 channels, and a stencil adds them into the flow (iterations without the mask head).  Off by
@@ -362,7 +364,7 @@ void CreStereo::update(hipStream_t s, Level& L, const Tensor& f1, const Tensor& 
   // queues behind convc2 (SA_CRE_AGCL_FIRST=0: flow branch captured first, as in round 4)
   const bool par = par_ && !tuning_pass_;
   const long P = (long)B * L.h * L.w;
-  if (iter_mode && head_) {
+  if (head_mode_ >= 2 || (head_mode_ == 1 && iter_mode)) {
     SaCreHeadArgs hd{};
     hd.w16 = c1_w16_;
     hd.bias = c1_b_;
@@ -374,7 +376,12 @@ void CreStereo::update(hipStream_t s, Level& L, const Tensor& f1, const Tensor& 
     hd.flo_stride = L.flo1.stride;
     hd.fcopy = L.xin.slice_c(254, 2).ptr;
     hd.fcopy_stride = L.xin.stride;
-    check(sa_cre_motion_head(&ag, &hd, s), "motion-encoder head");
+    if (iter_mode) {
+      check(sa_cre_motion_head(&ag, &hd, s), "motion-encoder head");
+    } else {  // offset mode (coarse levels): the correlation first, the head from it
+      check(sa_agcl_corr(&ag, s), "agcl");
+      check(sa_cre_motion_head_pre(&ag, &hd, s), "motion-encoder head");
+    }
     c2f2_.run(s, {L.cor1, L.flo1}, L.corflo, SA_ACT_RELU);
   } else {
     auto agcl_c1 = [&] {  // correlation -> convc1 (+ relu) into L.cor1

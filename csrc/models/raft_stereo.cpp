@@ -75,6 +75,9 @@ class RaftStereo : public StereoEngine {
   RaftCfg rc_;
   StatsPool sp_;
   Tensor img_;  // [2B][H][W][8] preprocessed
+  Tensor imgc_;  // [B][H][W][8] the context trunk's own copy of the left images (SA_RAFT_EARLY_FORK)
+  // same-process A/B: b1 8.299 -> 8.218 ms, b8 40.74 -> 40.69 ms; SA_RAFT_EARLY_FORK=0 forks after the preprocessing
+  bool early_fork_ = !(std::getenv("SA_RAFT_EARLY_FORK") && std::getenv("SA_RAFT_EARLY_FORK")[0] == '0');
   Trunk fnet_, cnet_;
   ConvLayer fconv2_;          // fnet.conv2 (1x1 128->256) (non-shared)
   ResBlock shared_rb_;        // conv2.0 (shared backbone)
@@ -157,6 +160,7 @@ void RaftStereo::build(WeightSource& src) {
   const int Bn = B();
   const int hd = rc_.hidden;
   img_ = make_tensor(a, 2 * Bn, H(), W(), 8);
+  if (early_fork_) imgc_ = make_tensor(a, Bn, H(), W(), 8);
 
   // ---------------- encoders ----------------
   // conv1 stride 1 + (n_downsample > 2); layer strides 1, 1 + (n_downsample > 1), 1 + (n_downsample > 0)
@@ -431,10 +435,17 @@ static void check(int rc, const char* what) { SA_REQUIRE(rc == 0, "%s failed (rc
 void RaftStereo::forward(hipStream_t s) {
   const int Bn = B();
   const int hd = rc_.hidden;
-  sp_.zero(s);
+  const bool par0 = par_ && !tuning_pass_;
+  // SA_RAFT_EARLY_FORK=1: the two encoder branches fork before the preprocessing (each preprocesses what it reads),
+  // so neither waits on a node of the other's queue
+  const bool early = early_fork_ && par0 && !rc_.shared;
+  hipStream_t fs_early = early ? fork(s) : nullptr;
+  hipStream_t sf = early ? fs_early : s;
+  sp_.zero(sf);
   // preprocess: left images -> img[0:B], right -> img[B:2B], 2*(x/255)-1, RGB, 8-ch padded
-  check(sa_preprocess(in_left_, Bn, H(), W(), SA_PRE_SIGNED, img_.ptr, 8, 0, 8, s), "preprocess");
-  check(sa_preprocess(in_right_, Bn, H(), W(), SA_PRE_SIGNED, img_.slice_n(Bn, Bn).ptr, 8, 0, 8, s), "preprocess");
+  check(sa_preprocess(in_left_, Bn, H(), W(), SA_PRE_SIGNED, img_.ptr, 8, 0, 8, sf), "preprocess");
+  check(sa_preprocess(in_right_, Bn, H(), W(), SA_PRE_SIGNED, img_.slice_n(Bn, Bn).ptr, 8, 0, 8, sf), "preprocess");
+  if (early) check(sa_preprocess(in_left_, Bn, H(), W(), SA_PRE_SIGNED, imgc_.ptr, 8, 0, 8, s), "preprocess");
 
   // encoders.  The feature branch (fnet -> fmap -> correlation pyramid) and the context branch
   // (cnet -> levels -> heads) are independent after the shared trunk: parallel graph branches.
@@ -461,6 +472,22 @@ void RaftStereo::forward(hipStream_t s) {
     hipStream_t fs = fork(s);
     cnet_.run(s, sp_, img_.slice_n(0, Bn));
     feature_branch(fs);
+  } else if (early) {
+    // the two trunks' launches interleaved layer by layer in capture order: the graph's host-side enqueue follows
+    // it, and a branch captured whole after the other one started ~0.8 ms late (timeline_r5_sf)
+    const int n = std::max(fnet_.steps(), cnet_.steps());
+    for (int k = 0; k < n; ++k) {
+      if (k < fnet_.steps()) {
+        ScopedSplitK sk2(&splitk_side_);
+        fnet_.run_step(fs_early, sp_, img_, k);
+      }
+      if (k < cnet_.steps()) cnet_.run_step(s, sp_, imgc_, k);
+    }
+    ScopedSplitK sk2(&splitk_side_);
+    fconv2_.run(fs_early, {fnet_.out()}, fmap_);
+    check(sa_corr1d_pyramid(fmap_.ptr, fmap_.slice_n(Bn, Bn).ptr, 256, Bn, h0, w0, w0, 256, rc_.levels, pyr_,
+                            fs_early),
+          "corr pyramid");
   } else {
     feature_branch(par ? fork(s) : s);
     if (!rc_.shared) cnet_.run(s, sp_, img_.slice_n(0, Bn));

@@ -158,6 +158,7 @@ def _declare_dev(lib):
         "sa_agcl_corr": (_i, [C.POINTER(SaAgclArgs), _p]),
         "sa_agcl_conv1x1": (_i, [C.POINTER(SaAgclArgs), _p, _p, _i, _p, _i, _p]),
         "sa_cre_motion_head": (_i, [C.POINTER(SaAgclArgs), C.POINTER(SaCreHeadArgs), _p]),
+        "sa_cre_motion_head_pre": (_i, [C.POINTER(SaAgclArgs), C.POINTER(SaCreHeadArgs), _p]),
         "sa_linear_attention": (_i, [_p, _i, _p, _i, _p, _i, _p, _i, _i, _i, _i, _i, _i, _f, _p, _p]),
         "sa_linear_attention_ws_floats": (C.c_long, [_i, _i, _i, _i]),
         "sa_layernorm": (_i, [_p, _i, _p, _p, _p, _i, _p, _i, C.c_long, _i, _f, _p]),

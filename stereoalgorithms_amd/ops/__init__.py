@@ -381,6 +381,33 @@ def agcl_conv1x1(f1, f2, flow, weight, bias, small_patch=False):
     return out
 
 
+def cre_motion_head_pre(corr, flow, wc, bc, wf, bf):
+    """cre_motion_head from a correlation already computed (offset mode: agcl_corr first): corr fp16 [N,H,W,>=36]
+    (pixel stride = its last dim), flow fp32 [N,H,W,2] -> (cor [N,H,W,256], flo [N,H,W,128], fcopy [N,H,W,2])."""
+    n, h, w, cc = corr.shape
+    dev = corr.device
+    wc16 = torch.zeros(256, 64, dtype=torch.float16, device=dev)
+    wc16[:, :36] = wc.reshape(256, 36).to(torch.float16)
+    wf16 = torch.zeros(128, 128, dtype=torch.float16, device=dev)
+    wf16[:, :98] = wf.reshape(128, 98).to(torch.float16)
+    bc32, bf32 = bc.float().contiguous(), bf.float().contiguous()
+    cor = torch.empty(n, h, w, 256, dtype=torch.float16, device=dev)
+    flo = torch.empty(n, h, w, 128, dtype=torch.float16, device=dev)
+    fcopy = torch.empty(n, h, w, 2, dtype=torch.float16, device=dev)
+    assert corr.dtype == torch.float16 and corr.is_contiguous() and cc >= 36
+    assert flow.dtype == torch.float32 and flow.is_contiguous() and flow.shape == (n, h, w, 2)
+    a = N.SaAgclArgs()
+    a.flow = flow.data_ptr()
+    a.N, a.H, a.W, a.C = n, h, w, 256
+    a.out, a.out_stride, a.out_channels = corr.data_ptr(), cc, 36
+    hd = N.SaCreHeadArgs()
+    hd.w16, hd.bias, hd.cor, hd.cor_stride = wc16.data_ptr(), bc32.data_ptr(), cor.data_ptr(), 256
+    hd.wf16, hd.fbias, hd.flo, hd.flo_stride = wf16.data_ptr(), bf32.data_ptr(), flo.data_ptr(), 128
+    hd.fcopy, hd.fcopy_stride = fcopy.data_ptr(), 2
+    N.check(N.dev().sa_cre_motion_head_pre(C.byref(a), C.byref(hd), _stream()), "sa_cre_motion_head_pre")
+    return cor, flo, fcopy
+
+
 def cre_motion_head(f1, f2, flow, wc, bc, wf, bf, small_patch=False):
     """CREStereo motion-encoder head in one launch (iter mode): relu(convc1(AGCL)) -> [N,H,W,256], relu(convf1(flow))
     -> [N,H,W,128] (7x7, pad 3) and the fp16 flow copy -> [N,H,W,2].  wc [256,36(,1,1)], wf [128,2,7,7]."""

@@ -107,6 +107,38 @@ def test_cre_motion_head_vs_oracle(small_patch, shape):
     assert torch.equal(fcopy, nhwc(flow).half())
 
 
+@pytest.mark.parametrize("shape", [(2, 13, 70), (1, 30, 40), (1, 60, 80)])
+def test_cre_motion_head_pre_vs_oracle(shape):
+    """The coarse levels' head: AGCL in offset mode (learned offsets) by agcl_corr, then convc1 + convf1 + flow copy
+    from that correlation in one launch, vs the oracle."""
+    from stereoalgorithms_amd.models.crestereo import AGCL
+    O = ops()
+    torch.manual_seed(5)
+    n, h, w = shape
+    f1 = torch.randn(n, 256, h, w, device=DEV).half().float()
+    f2 = torch.randn(n, 256, h, w, device=DEV).half().float()
+    flow = torch.randn(n, 2, h, w, device=DEV) * 3
+    offset = (torch.rand(n, 18, h, w, device=DEV) * 2 - 1).half().float()
+    wc = torch.randn(256, 36, 1, 1, device=DEV) / 6
+    bc = torch.randn(256, device=DEV) * 0.1
+    wf = torch.randn(128, 2, 7, 7, device=DEV) / 10
+    bf = torch.randn(128, device=DEV) * 0.1
+    corr = O.agcl_corr(nhwc(f1).half(), nhwc(f2).half(), nhwc(flow), nhwc(offset).half(), small_patch=False,
+                       iter_mode=False)
+    cor, flo, fcopy = O.cre_motion_head_pre(corr, nhwc(flow), wc, bc, wf, bf)
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        ref_corr = AGCL(f1, f2).corr_offset(flow, offset, False)
+        ref_c = F.relu(F.conv2d(ref_corr.half().float(), wc.half().float(), bc))
+        ref_f = F.relu(F.conv2d(flow.half().float(), wf.half().float(), bf, padding=3))
+        # the arithmetic of the head alone, on the kernel's own fp16 correlation
+        own_c = F.relu(F.conv2d(corr[..., :36].permute(0, 3, 1, 2).float(), wc.half().float(), bc))
+    assert rel_err(cor.permute(0, 3, 1, 2), own_c) < 2e-3
+    assert rel_err(cor.permute(0, 3, 1, 2), ref_c) < 5e-3
+    assert rel_err(flo.permute(0, 3, 1, 2), ref_f) < 2e-3
+    assert torch.equal(fcopy, nhwc(flow).half())
+
+
 @pytest.mark.parametrize("n,L,S", [(2, 77, 90), (2, 1200, 1200), (1, 1200, 1200)])
 def test_linear_attention_layer_pieces(n, L, S):
     """Chunked linear attention (partial KV / Ksum per 64 tokens, ordered reduction) vs the oracle, at the

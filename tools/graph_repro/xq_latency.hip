@@ -9,6 +9,8 @@
 //   forkjoin A (s0) -> B (s1) -> C (s0)                           (fork edge A->B and join edge B->C)
 //   ready    A (s0) -> {B short on s1, D long on s0} -> C (s0)   (join on a side branch that finished long ago)
 //   fanout   A (s0) -> {B (s1), D (s0)} both short -> C (s0)     (join where both branches end together)
+//   busy     A (s0) -> {B short on s1, 20 chip-filling kernels on s0} -> C (s0): does the side queue's B start
+//            promptly while the other queue keeps the chip full?  (A->B is the number to read)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -38,8 +40,8 @@ __global__ void spin_kernel(unsigned long long* stamps, int slot, unsigned ticks
   }
 }
 
-static void launch(hipStream_t s, unsigned long long* st, int slot, unsigned us) {
-  hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, s, st, slot, us * 100u);
+static void launch(hipStream_t s, unsigned long long* st, int slot, unsigned us, int blocks = 1, int threads = 64) {
+  hipLaunchKernelGGL(spin_kernel, dim3(blocks), dim3(threads), 0, s, st, slot, us * 100u);
 }
 
 struct Case {
@@ -59,8 +61,8 @@ int main(int argc, char** argv) {
   CHECK(hipEventCreateWithFlags(&ej, hipEventDisableTiming));
   unsigned long long* st;
   CHECK(hipMalloc(&st, 64 * sizeof(unsigned long long)));
-  const char* names[] = {"serial", "forkjoin", "ready", "fanout"};
-  for (int c = 0; c < 4; ++c) {
+  const char* names[] = {"serial", "forkjoin", "ready", "fanout", "busy"};
+  for (int c = 0; c < 5; ++c) {
     hipGraph_t g;
     CHECK(hipStreamBeginCapture(s0, hipStreamCaptureModeThreadLocal));
     launch(s0, st, 0, 20);  // A
@@ -70,8 +72,11 @@ int main(int argc, char** argv) {
     } else {
       CHECK(hipEventRecord(ef, s0));
       CHECK(hipStreamWaitEvent(s1, ef, 0));
-      launch(s1, st, 1, c == 2 ? 5 : 20);  // B on the side stream
-      if (c >= 2) launch(s0, st, 3, c == 2 ? 60 : 20);  // D on the main stream
+      launch(s1, st, 1, c == 2 || c == 4 ? 5 : 20);  // B on the side stream
+      if (c == 4)
+        for (int k = 0; k < 20; ++k) launch(s0, st, 3, 20, 2048, 256);  // chip-filling kernels, D = the last one
+      else if (c >= 2)
+        launch(s0, st, 3, c == 2 ? 60 : 20);  // D on the main stream
       CHECK(hipEventRecord(ej, s1));
       CHECK(hipStreamWaitEvent(s0, ej, 0));
       launch(s0, st, 2, 20);  // C
