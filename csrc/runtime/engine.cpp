@@ -385,6 +385,7 @@ void StereoEngine::frame(hipStream_t s, bool rectify, bool host_out, bool host_i
       in_ptrs_[gi][0] = in_src_[0];
       in_ptrs_[gi][1] = in_src_[1];
     }
+    stage(s, "input");  // the PCIe read of the frame: its own stage, not the network's
   }
   if (rectify) {
     SA_REQUIRE(rect_maps_ != nullptr, "rectification requested but no maps set");
