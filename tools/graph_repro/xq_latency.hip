@@ -108,6 +108,47 @@ int main(int argc, char** argv) {
     CHECK(hipGraphExecDestroy(ge));
     CHECK(hipGraphDestroy(g));
   }
+  // two graphs, one per stream, linked by an external event: graph A on s0 = A -> record(ev) -> D (60 us);
+  // graph B on s1 = wait(ev) -> B.  A->B is the cross-graph edge (explicit queue placement instead of the executor's)
+  {
+    hipEvent_t ex;
+    CHECK(hipEventCreateWithFlags(&ex, hipEventDisableTiming));
+    hipGraph_t ga, gb;
+    CHECK(hipStreamBeginCapture(s0, hipStreamCaptureModeThreadLocal));
+    launch(s0, st, 0, 20);
+    CHECK(hipEventRecordWithFlags(ex, s0, hipEventRecordExternal));
+    launch(s0, st, 3, 60);
+    CHECK(hipStreamEndCapture(s0, &ga));
+    CHECK(hipStreamBeginCapture(s1, hipStreamCaptureModeThreadLocal));
+    CHECK(hipStreamWaitEvent(s1, ex, hipEventWaitExternal));
+    launch(s1, st, 1, 5);
+    CHECK(hipStreamEndCapture(s1, &gb));
+    hipGraphExec_t ea, eb;
+    CHECK(hipGraphInstantiate(&ea, ga, nullptr, nullptr, 0));
+    CHECK(hipGraphInstantiate(&eb, gb, nullptr, nullptr, 0));
+    std::vector<double> ab, span;
+    for (int r = 0; r < reps + 3; ++r) {
+      CHECK(hipMemset(st, 0, 64 * sizeof(unsigned long long)));
+      CHECK(hipDeviceSynchronize());
+      CHECK(hipGraphLaunch(ea, s0));
+      CHECK(hipGraphLaunch(eb, s1));
+      CHECK(hipDeviceSynchronize());
+      unsigned long long h[8];
+      CHECK(hipMemcpy(h, st, sizeof(h), hipMemcpyDeviceToHost));
+      if (r < 3) continue;
+      ab.push_back(((double)h[2] - (double)h[1]) / 100.0);
+      span.push_back(((double)h[7] - (double)h[0]) / 100.0);
+    }
+    std::sort(ab.begin(), ab.end());
+    std::sort(span.begin(), span.end());
+    std::printf("%-9s A->B %6.2f us  (two graphs, external event)  span(A..D) %7.2f us\n", "xgraph", ab[ab.size() / 2],
+                span[span.size() / 2]);
+    CHECK(hipGraphExecDestroy(ea));
+    CHECK(hipGraphExecDestroy(eb));
+    CHECK(hipGraphDestroy(ga));
+    CHECK(hipGraphDestroy(gb));
+    CHECK(hipEventDestroy(ex));
+  }
   CHECK(hipFree(st));
   return 0;
 }
