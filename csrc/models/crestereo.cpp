@@ -149,6 +149,7 @@ class CreStereo : public StereoEngine {
   // On for batch <= 2 (the hoisted columns cost +11 % MACs, a throughput loss at large batch); SA_CRE_GRU_SPLIT=0/1.
   ConvLayer zrq_[2], qh_[2];
   bool par_ = !(std::getenv("SA_CRE_PARALLEL") && std::getenv("SA_CRE_PARALLEL")[0] == '0');
+  bool prep_side_ = !(std::getenv("SA_CRE_PREP_SIDE") && std::getenv("SA_CRE_PREP_SIDE")[0] == '0');
   bool agcl_first_ = !(std::getenv("SA_CRE_AGCL_FIRST") && std::getenv("SA_CRE_AGCL_FIRST")[0] == '0');
   int gru_split_mode_ = std::getenv("SA_CRE_GRU_SPLIT") ? std::atoi(std::getenv("SA_CRE_GRU_SPLIT")) : -1;
   bool gru_split_ = false;
@@ -477,8 +478,15 @@ void CreStereo::forward(hipStream_t s) {
   const int h4 = L4.h, w4 = L4.w;
   check(sa_avgpool_k(fmap_.ptr, 256, fmap8_.ptr, 256, 2 * B, h4, w4, 256, 2, s), "pool8");
   check(sa_avgpool_k(fmap_.ptr, 256, fmap16_.ptr, 256, 2 * B, h4, w4, 256, 4, s), "pool16");
-  offc8_.run(s, {fmap8_.slice_n(0, B)}, off8_, SA_ACT_TANH);
-  offc16_.run(s, {fmap16_.slice_n(0, B)}, off16_, SA_ACT_TANH);
+  // The offset convs and the GRU-state preparation (tanh / relu / pooling) only feed the update iterations: they
+  // run on the side stream beside the 1/16 attention chain (~0.3 ms of small dependent launches) and join before
+  // the first 1/16 update (SA_CRE_PREP_SIDE=0: in line)
+  const bool prep_side = par_ && !tuning_pass_ && prep_side_;
+  hipStream_t ps = prep_side ? fork(s) : s;
+  {
+  ScopedSplitK psk(prep_side ? &splitk_side_ : current_splitk());  // this block only: the main stream keeps its own
+  offc8_.run(ps, {fmap8_.slice_n(0, B)}, off8_, SA_ACT_TANH);
+  offc16_.run(ps, {fmap16_.slice_n(0, B)}, off16_, SA_ACT_TANH);
   // net = tanh(fmap1[:128]), inp = relu(fmap1[128:]) at 1/4, pooled to 1/8 and 1/16
   {
     SaEwArgs e{};
@@ -490,17 +498,18 @@ void CreStereo::forward(hipStream_t s) {
     e.C = 128;
     e.act = SA_ACT_TANH;
     e.scale = 1.f;
-    check(sa_ew(&e, s), "tanh");
+    check(sa_ew(&e, ps), "tanh");
     e.x = fmap_.slice_c(128, 128).ptr;
     e.out = L4.xin.ptr;
     e.out_stride = L4.xin.stride;
     e.act = SA_ACT_RELU;
-    check(sa_ew(&e, s), "relu");
+    check(sa_ew(&e, ps), "relu");
   }
   for (int l = 1; l < 3; ++l) {
     const int k = l == 1 ? 2 : 4;
-    check(sa_avgpool_k(L4.net.ptr, L4.net.stride, lv_[l].net.ptr, lv_[l].net.stride, B, h4, w4, 128, k, s), "pool");
-    check(sa_avgpool_k(L4.xin.ptr, L4.xin.stride, lv_[l].xin.ptr, lv_[l].xin.stride, B, h4, w4, 128, k, s), "pool");
+    check(sa_avgpool_k(L4.net.ptr, L4.net.stride, lv_[l].net.ptr, lv_[l].net.stride, B, h4, w4, 128, k, ps), "pool");
+    check(sa_avgpool_k(L4.xin.ptr, L4.xin.stride, lv_[l].xin.ptr, lv_[l].xin.stride, B, h4, w4, 128, k, ps), "pool");
+  }
   }
   // 1/16 tokens: pooled features + position encoding -> self attention (both images batched) ->
   // cross attention (left attends to right, then right to the updated left)
@@ -525,6 +534,7 @@ void CreStereo::forward(hipStream_t s) {
   const Tensor c16l{cross1_.ptr, B, L16.h, L16.w, 256, 256, DT::F16};
   const Tensor c16r{cross2_.ptr, B, L16.h, L16.w, 256, 256, DT::F16};
 
+  if (prep_side) join(s);
   // RUM 1/16
   device_zero(L16.flow, (size_t)B * L16.h * L16.w * 2 * 4, s);
   const int n_coarse = iters_ / 2;
