@@ -108,6 +108,37 @@ int main(int argc, char** argv) {
     CHECK(hipGraphExecDestroy(ge));
     CHECK(hipGraphDestroy(g));
   }
+  // independent roots: s1's single kernel B forked before anything ran on s0, s0 then runs 20 x 40 us kernels
+  // (case "roots_fill": chip-filling ones).  B's start relative to the first s0 kernel's start is the number.
+  for (int fill = 0; fill < 2; ++fill) {
+    hipGraph_t g;
+    CHECK(hipStreamBeginCapture(s0, hipStreamCaptureModeThreadLocal));
+    CHECK(hipEventRecord(ef, s0));
+    CHECK(hipStreamWaitEvent(s1, ef, 0));
+    for (int k = 0; k < 20; ++k) launch(s0, st, k == 0 ? 0 : 3, 40, fill ? 2048 : 1, fill ? 256 : 64);
+    launch(s1, st, 1, 5);
+    CHECK(hipEventRecord(ej, s1));
+    CHECK(hipStreamWaitEvent(s0, ej, 0));
+    launch(s0, st, 2, 5);
+    CHECK(hipStreamEndCapture(s0, &g));
+    hipGraphExec_t ge;
+    CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    std::vector<double> b0;
+    for (int r = 0; r < reps + 3; ++r) {
+      CHECK(hipMemset(st, 0, 64 * sizeof(unsigned long long)));
+      CHECK(hipGraphLaunch(ge, s0));
+      CHECK(hipStreamSynchronize(s0));
+      unsigned long long h[8];
+      CHECK(hipMemcpy(h, st, sizeof(h), hipMemcpyDeviceToHost));
+      if (r < 3) continue;
+      b0.push_back(((double)h[2] - (double)h[0]) / 100.0);  // B start - first s0 kernel start
+    }
+    std::sort(b0.begin(), b0.end());
+    std::printf("%-9s B starts %7.2f us after the first s0 kernel (s0 chain 20 x 40 us)\n", fill ? "roots_fil" : "roots",
+                b0[b0.size() / 2]);
+    CHECK(hipGraphExecDestroy(ge));
+    CHECK(hipGraphDestroy(g));
+  }
   // two graphs, one per stream, linked by an external event: graph A on s0 = A -> record(ev) -> D (60 us);
   // graph B on s1 = wait(ev) -> B.  A->B is the cross-graph edge (explicit queue placement instead of the executor's)
   {
