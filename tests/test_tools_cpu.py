@@ -209,3 +209,25 @@ def test_bench_regress_gate(tmp_path):
     assert rc == 1 and "raftstereo-sceneflow latency" in out
     rc, out = gate(line(100.0, 8.1, 7.1))  # +1.25 % / +1.4 %: within the 3 % tolerance
     assert rc == 0
+
+
+def test_timeline_cross_queue_links(tmp_path):
+    """tools/timeline.py splits the critical chain's links by hardware queue (rocprofv3 Queue_Id): a chain that
+    hops queues twice per frame reports those hops and their gaps apart from the same-queue links."""
+    hdr = "Kernel_Name,Start_Timestamp,End_Timestamp,Grid_Size_X,Workgroup_Size_X,Queue_Id\n"
+    rows = []
+    for f in range(3):
+        t = f * 1_000_000
+        rows += [("preprocess_kernel", t, t + 1000, 2), ("a_kernel", t + 2000, t + 5000, 2),
+                 ("b_kernel", t + 15000, t + 20000, 4),   # 10 us cross-queue gap
+                 ("c_kernel", t + 21000, t + 25000, 4),   # 1 us same-queue gap
+                 ("d_kernel", t + 37000, t + 40000, 2)]   # 12 us cross-queue gap
+    csv = tmp_path / "q_kernel_trace.csv"
+    csv.write_text(hdr + "".join(f"{n},{s},{e},256,256,{q}\n" for n, s, e, q in rows))
+    r = subprocess.run([sys.executable, str(ROOT / "tools" / "timeline.py"), str(csv), "--chain", "5"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    m = re.search(r"links: (\d+) same-queue \(([\d.]+) us of gaps\), (\d+) cross-queue \(([\d.]+) us", r.stdout)
+    assert m, r.stdout
+    assert (int(m.group(1)), int(m.group(3))) == (2, 2), r.stdout
+    assert abs(float(m.group(2)) - 2.0) < 1e-6 and abs(float(m.group(4)) - 22.0) < 1e-6, r.stdout

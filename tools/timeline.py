@@ -36,7 +36,8 @@ def load(d):
             wy = int(r.get("Workgroup_Size_Y", 1) or 1)
             wz = int(r.get("Workgroup_Size_Z", 1) or 1)
             wgs = max(1, (gx // max(wx, 1)) * (gy // max(wy, 1)) * (gz // max(wz, 1)))
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), wgs))
+            q = int(r.get("Queue_Id", -1) or -1)
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), wgs, q))
     rows.sort()
     return rows
 
@@ -97,15 +98,15 @@ def main():
     fr = rows[lo:hi]
     # drop the tail of foreign kernels after the frame's last kernel (next frame's host copies etc.)
     t0 = fr[0][0]
-    t1 = max(e for _, e, _, _ in fr)
-    busy, gaps = union([(s, e) for s, e, _, _ in fr])
+    t1 = max(r[1] for r in fr)
+    busy, gaps = union([(r[0], r[1]) for r in fr])
     span = t1 - t0
     print(f"frame {a.frame}: {len(fr)} kernels, span {span / 1e3:.1f} us, busy {busy / 1e3:.1f} us "
           f"({100 * busy / span:.1f} %), idle {(span - busy) / 1e3:.1f} us in {len(gaps)} gaps "
           f"(>5us: {sum(1 for g in gaps if g > 5000)}, sum {sum(g for g in gaps if g > 5000) / 1e3:.1f} us)")
     if a.list:
-        for s, e, n, w in fr[:a.list]:
-            print(f"  +{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f} us  wg {w:6d}  {n}")
+        for s, e, n, w, q in fr[:a.list]:
+            print(f"  +{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f} us  wg {w:6d}  q{q}  {n}")
 
     if a.iter_marker:
         its = [i for i, r in enumerate(fr) if a.iter_marker in r[2]]
@@ -114,8 +115,8 @@ def main():
         for k, (i, j) in enumerate(zip(its, its[1:] + [len(fr)])):
             seg = fr[i:j]
             s0 = seg[0][0]
-            s1 = fr[j][0] if j < len(fr) else max(e for _, e, _, _ in seg)
-            b, g = union([(s, min(e, s1)) for s, e, _, _ in seg])
+            s1 = fr[j][0] if j < len(fr) else max(r[1] for r in seg)
+            b, g = union([(r[0], min(r[1], s1)) for r in seg])
             spans.append(s1 - s0)
             if k < 3 or k >= len(its) - 2 or k == len(its) // 2:
                 print(f"  it {k:2d}: span {(s1 - s0) / 1e3:7.1f} us  busy {b / 1e3:7.1f}  idle {(s1 - s0 - b) / 1e3:6.1f} "
@@ -148,9 +149,15 @@ def main():
     tot_gap = sum(max(0, fr[j][0] - fr[i][1]) for i, j in zip(chain, chain[1:]))
     print(f"\ncritical chain: {len(chain)} kernels, {tot_k / 1e3:.1f} us in kernels + {tot_gap / 1e3:.1f} us of "
           f"launch gaps = {(tot_k + tot_gap) / 1e3:.1f} us (frame span {span / 1e3:.1f})")
+    # links by hardware queue: a link between kernels of different queues is a graph edge the executor turned into
+    # a barrier packet (rocprofv3 Queue_Id; -1 when the trace has none)
+    same = [max(0, fr[j][0] - fr[i][1]) for i, j in zip(chain, chain[1:]) if fr[i][4] == fr[j][4]]
+    cross = [max(0, fr[j][0] - fr[i][1]) for i, j in zip(chain, chain[1:]) if fr[i][4] != fr[j][4]]
+    print(f"  links: {len(same)} same-queue ({sum(same) / 1e3:.1f} us of gaps), {len(cross)} cross-queue "
+          f"({sum(cross) / 1e3:.1f} us of gaps, {sum(cross) / max(1, len(cross)) / 1e3:.1f} us each)")
     per = defaultdict(lambda: [0, 0, 0])
     for i, j in zip([None] + chain[:-1], chain):
-        s, e, n, w = fr[j]
+        s, e, n, w, _ = fr[j]
         g = 0 if i is None else max(0, s - fr[i][1])
         per[n][0] += 1
         per[n][1] += e - s
@@ -160,9 +167,9 @@ def main():
         print(f"  {n:60s} {c:4d} {k / 1e3:9.1f} {g / 1e3:8.1f}")
     print(f"\n  last {a.chain} links:")
     for i, j in list(zip([None] + chain[:-1], chain))[-a.chain:]:
-        s, e, n, w = fr[j]
+        s, e, n, w, q = fr[j]
         g = 0 if i is None else s - fr[i][1]
-        print(f"  +{(s - t0) / 1e3:9.1f}  gap {g / 1e3:6.1f}  dur {(e - s) / 1e3:7.1f}  wg {w:6d}  {n}")
+        print(f"  +{(s - t0) / 1e3:9.1f}  gap {g / 1e3:6.1f}  dur {(e - s) / 1e3:7.1f}  wg {w:6d}  q{q:<2d} {n}")
     return 0
 
 
