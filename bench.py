@@ -290,11 +290,16 @@ def main(argv=None) -> int:
     dt = time.perf_counter() - t0
     gather_ms = None
     ranks = [{"rank": rank, "device": str(dev), "host": socket.gethostname(),
-              "plan_tactics": None if plan_digests is None else plan_digests[min(rank, len(plan_digests) - 1)]}]
+              "plan_tactics": None if plan_digests is None else plan_digests[min(rank, len(plan_digests) - 1)],
+              "step_ms": round(dt / args.steps * 1e3, 3)}]
+    rank_ms = [dt / args.steps * 1e3]
     if world > 1:
+        # every rank's own time (imbalance shows on the first real multi-GPU curve), then the job's = the slowest
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = t.item()
+        ts_all = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(ts_all, t)
+        rank_ms = [x.item() / args.steps * 1e3 for x in ts_all]
+        dt = max(x.item() for x in ts_all)
         # the all-gather alone, outside the timed region (same message as one step's gather)
         send = out.new_empty((B, H, W))
         recv = out.new_empty((world * B, H, W))
@@ -449,12 +454,15 @@ def main(argv=None) -> int:
             "backend": backend if world > 1 else None,
             "ranks": ranks,
             "step_latency_ms": round(ms_step, 3),
+            "rank_step_ms": {"min": round(min(rank_ms), 3), "max": round(max(rank_ms), 3)},
             "ms_per_frame_per_gpu": round(ms_step / B, 3),
             "allgather_ms": gather_ms,
             "allgather_bytes_per_rank": B * H * W * 4,
             "point_clouds": f"per rank [{B},{H},{W},6] fp32 XYZRGB, reprojected in the frame graph, kept local",
             "plan": None if cpu else plan_b8,
-            "plans_identical_across_ranks": None if plan_digests is None else len(set(plan_digests)) == 1,
+            # launched-tactic digests of every rank (None = some rank could not report one: unknown, not "equal")
+            "plans_identical_across_ranks": (None if plan_digests is None or None in plan_digests
+                                             else len(set(plan_digests)) == 1),
             "device_bytes": dev_bytes_b8,
             "latency_b1": extra,
         }

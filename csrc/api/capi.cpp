@@ -121,6 +121,17 @@ void sa_engine_plan_status(void* e, int* loaded, int* saved) {
   *saved = static_cast<sa::StereoEngine*>(e)->plan_saved();
 }
 const char* sa_plan_build_id() { return sa::conv_plan_build_id().c_str(); }
+// digest of the tactics this engine's graph launches (from the process plan, not a file: VERDICT r5 / ADVICE r5)
+const char* sa_engine_tactics_digest(void* e) {
+  static thread_local std::string d;
+  d = sa::conv_plan_digest(static_cast<sa::StereoEngine*>(e)->plan_keys());
+  return d.c_str();
+}
+// write this engine's plan entries to `file` (a DP job's rank 0 broadcasts those bytes); 0 or errno
+int sa_engine_plan_export(void* e, const char* file) {
+  return sa::conv_plan_save(file, static_cast<sa::StereoEngine*>(e)->plan_keys());
+}
+void sa_conv_plan_pin(int on) { sa::conv_plan_pin(on != 0); }
 long sa_engine_nonzero_splitk_counters(void* e) { return static_cast<sa::StereoEngine*>(e)->nonzero_splitk_counters(); }
 long sa_conv_tune_count(void) { return sa::conv_tune_count(); }
 long sa_conv_tune_rejects(void) { return sa::conv_tune_rejects(); }

@@ -11,6 +11,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <functional>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
@@ -62,6 +63,19 @@ bool recv_all(int fd, char* p, size_t n, Clock::time_point deadline) {
       throw ::sa::Error(std::string("RCCL: ") + ncclGetErrorString(_r));                        \
     }                                                                                           \
   } while (0)
+// Poll `status` (ncclCommGetAsyncError of a non-blocking communicator) until it leaves ncclInProgress: 0 on
+// ncclSuccess, 1 on an error (*last holds it), -1 once `deadline` passes
+template <typename F>
+int settle(F status, Clock::time_point deadline, ncclResult_t* last) {
+  for (;;) {
+    const ncclResult_t st = status();
+    if (last) *last = st;
+    if (st == ncclSuccess) return 0;
+    if (st != ncclInProgress) return 1;
+    if (Clock::now() > deadline) return -1;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+}
 }  // namespace
 
 DistEnv env_from_environment() {
@@ -155,10 +169,30 @@ Communicator::Communicator(const DistEnv& env, int device) : env_(env) {
                            env_.timeout_s * 1000) == 0,
              "rank %d: ncclUniqueId bootstrap over %s:%d failed", env_.rank, env_.master_addr.c_str(),
              env_.master_port);
-  // Blocking init: every peer has already passed the TCP bootstrap (bounded by the deadline), so
-  // the remaining risk of a hang is a peer dying inside init itself.
+  // Non-blocking init (blocking = 0), polled against the same SA_DIST_TIMEOUT deadline as the bootstrap: a peer
+  // that dies or never reaches init can no longer hang every other rank inside ncclCommInitRank
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
   ncclComm_t c = nullptr;
-  NCCL_CHECK(ncclCommInitRank(&c, env_.world, id, env_.rank));
+  const ncclResult_t r0 = ncclCommInitRankConfig(&c, env_.world, id, env_.rank, &cfg);
+  if (r0 != ncclSuccess && r0 != ncclInProgress) {
+    SA_LOGE("rank %d: ncclCommInitRankConfig: %s", env_.rank, ncclGetErrorString(r0));
+    throw Error(std::string("RCCL init: ") + ncclGetErrorString(r0));
+  }
+  ncclResult_t st = ncclSuccess;
+  const int rc = settle(
+      [&] {
+        ncclResult_t x = ncclSuccess;
+        ncclCommGetAsyncError(c, &x);
+        return x;
+      },
+      Clock::now() + std::chrono::seconds(env_.timeout_s), &st);
+  if (rc != 0) {
+    if (c) ncclCommAbort(c);
+    SA_LOGE("rank %d: RCCL communicator init %s", env_.rank, rc < 0 ? "timed out" : ncclGetErrorString(st));
+    throw Error(rc < 0 ? "RCCL communicator init timed out (SA_DIST_TIMEOUT): a peer never completed init"
+                       : std::string("RCCL init: ") + ncclGetErrorString(st));
+  }
   comm_ = c;
   HIP_CHECK(hipMalloc(&scratch_, sizeof(double)));
   SA_LOGI("rank %d/%d: RCCL communicator up on device %d", env_.rank, env_.world, device);
@@ -166,8 +200,20 @@ Communicator::Communicator(const DistEnv& env, int device) : env_(env) {
 
 Communicator::~Communicator() {
   if (comm_ && !aborted_) {
-    ncclCommFinalize((ncclComm_t)comm_);
-    ncclCommDestroy((ncclComm_t)comm_);
+    ncclComm_t c = (ncclComm_t)comm_;
+    // non-blocking communicator: finalize may return ncclInProgress; bounded wait, then destroy (or abort)
+    const ncclResult_t r = ncclCommFinalize(c);
+    const int rc = (r == ncclSuccess || r == ncclInProgress)
+                       ? settle(
+                             [&] {
+                               ncclResult_t x = ncclSuccess;
+                               ncclCommGetAsyncError(c, &x);
+                               return x;
+                             },
+                             Clock::now() + std::chrono::seconds(env_.timeout_s), nullptr)
+                       : 1;
+    if (rc == 0) ncclCommDestroy(c);
+    else ncclCommAbort(c);
   }
   if (scratch_) (void)hipFree(scratch_);
 }
@@ -182,8 +228,25 @@ void Communicator::check_async() {
   }
 }
 
-static void enqueue_ok(ncclResult_t r, const char* what) {
-  if (r != ncclSuccess) throw Error(std::string(what) + ": " + ncclGetErrorString(r));
+// a call on the non-blocking communicator may return ncclInProgress: the next call must wait until it settled
+void Communicator::enqueue_ok(int r, const char* what) {
+  if (r == ncclSuccess) return;
+  if (r == ncclInProgress) {
+    ncclResult_t st = ncclSuccess;
+    const int rc = settle(
+        [&] {
+          ncclResult_t x = ncclSuccess;
+          ncclCommGetAsyncError((ncclComm_t)comm_, &x);
+          return x;
+        },
+        Clock::now() + std::chrono::seconds(env_.timeout_s), &st);
+    if (rc == 0) return;
+    ncclCommAbort((ncclComm_t)comm_);
+    aborted_ = true;
+    throw Error(std::string(what) + (rc < 0 ? ": timed out (SA_DIST_TIMEOUT)" : ": ") +
+                (rc < 0 ? "" : ncclGetErrorString(st)));
+  }
+  throw Error(std::string(what) + ": " + ncclGetErrorString((ncclResult_t)r));
 }
 
 void Communicator::all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) {
@@ -240,6 +303,10 @@ void Communicator::wait_stream(hipStream_t s) {
   }
 }
 
+int settle_probe_impl(const std::function<int()>& status, int timeout_ms) {
+  return settle([&] { return (ncclResult_t)status(); }, Clock::now() + std::chrono::milliseconds(timeout_ms), nullptr);
+}
+
 // ------------------------------------------------------------------ DataParallelRunner
 DataParallelRunner::DataParallelRunner(StereoEngine* engine, Communicator* comm) : eng_(engine), comm_(comm) {
   const size_t frame = (size_t)eng_->H() * eng_->W() * sizeof(float);
@@ -266,11 +333,11 @@ DataParallelRunner::~DataParallelRunner() {
   (void)hipStreamDestroy(comm_stream_);
 }
 
-const float* DataParallelRunner::step(const uint8_t* left, const uint8_t* right) {
+const float* DataParallelRunner::step(const uint8_t* left, const uint8_t* right, float* cloud) {
   const int slot = (int)(i_++ % kSlots);
   hipStream_t cs = eng_->stream();
   if (pending_[slot]) HIP_CHECK(hipStreamWaitEvent(cs, ev_gather_[slot], 0));  // WAR on the slot
-  eng_->run_device(left, right, send_[slot], nullptr, false, cs);
+  eng_->run_device(left, right, send_[slot], cloud, false, cs);
   // nothing to gather at world 1 (SA_DP_GATHER_WORLD1=1 still runs the collective path, for tests)
   if (comm_->world() == 1 && !force_gather_) return send_[slot];
   HIP_CHECK(hipEventRecord(ev_done_[slot], cs));
@@ -291,6 +358,13 @@ void DataParallelRunner::wait() {
 }  // namespace sa
 
 // ------------------------------------------------------------------ flat C entry (ctypes tests)
+// the init / enqueue deadline loop on the CPU (tests): a status source that reports ncclInProgress `in_progress`
+// times, then `final_status`; returns settle()'s 0 / 1 / -1
+extern "C" int sa_dist_settle_probe(int in_progress, int final_status, int timeout_ms) {
+  int n = 0;
+  return sa::dist::settle_probe_impl(
+      [&] { return n++ < in_progress ? (int)ncclInProgress : final_status; }, timeout_ms);
+}
 extern "C" int sa_dist_exchange_blob(int rank, int world, const char* addr, int port, void* buf, size_t n,
                                      int timeout_ms) {
   return sa::dist::exchange_blob(rank, world, addr, port, buf, n, timeout_ms);

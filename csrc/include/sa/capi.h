@@ -28,6 +28,9 @@ void* sa_engine_stream(void* engine);
 // tuned-plan cache: the engine's plan file ("" = none), the conv shapes it had to time at build,
 // the process-wide count of timed shapes, and a reset of the in-process plan (tests)
 const char* sa_engine_plan_path(void* engine);
+const char* sa_engine_tactics_digest(void* engine);        // 16-hex digest of the tactics the engine launches
+int sa_engine_plan_export(void* engine, const char* file);  // its plan entries as a plan file; 0 or errno
+void sa_conv_plan_pin(int on);                             // later plan-file loads keep existing entries
 long sa_engine_tuned_shapes(void* engine);
 long sa_engine_nonzero_splitk_counters(void* engine);
 long sa_conv_tune_count(void);

@@ -17,6 +17,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <string>
 
@@ -35,6 +36,11 @@ DistEnv env_from_environment();
 // Rank 0 sends `n` bytes of `buf` to every other rank, which receive them into `buf` (TCP star on
 // addr:port).  Returns 0 on success, -1 on error / timeout.  GPU-free (unit-tested on CPU).
 int exchange_blob(int rank, int world, const char* addr, int port, void* buf, size_t n, int timeout_ms);
+
+// The deadline loop behind the non-blocking communicator's init and enqueues, over an arbitrary status source
+// (ncclResult_t values): 0 once it reports ncclSuccess, 1 on any other non-InProgress status, -1 at the deadline.
+// GPU-free (unit-tested on CPU through sa_dist_settle_probe).
+int settle_probe_impl(const std::function<int()>& status, int timeout_ms);
 
 // Contiguous shard [start, end) of `total` items for `rank` (remainders to low ranks), as dp.py.
 void shard_range(long total, int world, int rank, long* start, long* end);
@@ -60,6 +66,7 @@ class Communicator {
 
  private:
   void check_async();
+  void enqueue_ok(int r, const char* what);  // ncclResult_t of an enqueue; ncclInProgress settles under the deadline
   DistEnv env_;
   void* comm_ = nullptr;  // ncclComm_t
   double* scratch_ = nullptr;
@@ -75,7 +82,8 @@ class DataParallelRunner {
   // engine's stream and the all-gather on the comm stream; returns the device pointer of the
   // gathered fp32 [world*B][H][W] disparity, valid after wait() or until the slot is reused two
   // steps later.
-  const float* step(const uint8_t* left, const uint8_t* right);
+  // cloud (optional): this rank's fp32 XYZRGB [B][H][W][6] device buffer, reprojected in the frame graph (needs Q).
+  const float* step(const uint8_t* left, const uint8_t* right, float* cloud = nullptr);
   // block until every outstanding collective and frame has finished (with failure detection)
   void wait();
   hipStream_t comm_stream() const { return comm_stream_; }

@@ -98,6 +98,8 @@ class StereoEngine {
   // tuned-plan file used by this engine ("" = none) and how many conv shapes it had to time
   const std::string& plan_path() const { return plan_path_; }
   long tuned_shapes() const { return tuned_shapes_; }
+  // the conv shapes this engine consulted during its tuning pass (what its frame graph launches)
+  const std::vector<std::string>& plan_keys() const { return plan_keys_; }
   // plan file at build: entries loaded (-1 absent, -2 other library build, -3 not consulted); save result
   // (0 ok, errno of the failing step, -1 not attempted because nothing was tuned)
   int plan_loaded() const { return plan_loaded_; }
@@ -193,6 +195,7 @@ class StereoEngine {
   std::string default_plan_path() const;
   std::string plan_path_;
   long tuned_shapes_ = 0;
+  std::vector<std::string> plan_keys_;
   int plan_loaded_ = -3, plan_saved_ = -1;
   SplitKWorkspace splitk_;
   hipStream_t side_ = nullptr;

@@ -219,6 +219,9 @@ int sa_raft_motion_encoder(const float* pyr, const float* flow, int B, int H, in
 // diagnostics: s_memrealtime (100 MHz) stage marks of every workgroup of later sa_raft_motion_encoder launches into `buf`
 // ([blocks][8 marks][64] u64; NULL turns it off)
 void sa_raft_motion_encoder_stamps(void* buf);
+// kernel variant of later sa_raft_motion_encoder launches: 1 = one 159-KB workgroup per CU (LDS weight rings),
+// 2 = two 63-KB workgroups per CU (register weight pipeline), -1 = SA_RAFT_MENC (default 1)
+void sa_raft_motion_encoder_variant(int v);
 
 // ---- upsampling -----------------------------------------------------------------------------
 // RAFT convex upsampling: mask [B*H*W][9*f*f] fp16 (softmax over the 9), flow fp32 [B*H*W]

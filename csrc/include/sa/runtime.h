@@ -195,6 +195,11 @@ const std::string& conv_plan_build_id();  // hash of the loaded kernel library (
 // how many of `keys` have an in-process plan but no entry in `file` (all of them if the file is absent / stale)
 int conv_plan_missing(const std::string& file, const std::vector<std::string>& keys);
 void conv_plan_put(const std::string& key, int cfg, int splitk, float us);  // tests: seed the in-process plan
+// DP ranks that merged rank 0's broadcast table: later plan-file loads keep every entry already in the process
+void conv_plan_pin(bool on);
+// 16-hex FNV-1a digest of the (key, cfg, splitk) the process plan holds for `keys` plus the library build id: equal
+// digests = identical kernels launched for those shapes
+std::string conv_plan_digest(const std::vector<std::string>& keys);
 // collects every plan key consulted by conv_apply_plan in this thread (the engine's own shapes)
 struct ScopedPlanCollect {
   std::vector<std::string>* prev;

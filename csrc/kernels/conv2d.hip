@@ -1906,6 +1906,72 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
       }
     }
   };
+  // SA_EPI_TAPPROJ on the banded (LDS-staged) tiles: the next conv's tap projections on the matrix cores.  Phase 1
+  // turns the band's fp32 C rows into y = fp16(act(scale c + bias)) IN PLACE (the first 256 B of each 512-B row, 16-B
+  // slot cc ^ (row & 15); a row's 16 chunk threads sit in one wave, whose LDS reads issue before its writes); phase 2
+  // is the GEMM P[row][tap] = y[row][0:128] . tapw[tap][n0:n0+128] as v_mfma_f32_16x16x32_f16 (4 k-steps per 16-row
+  // fragment, taps padded to 16 columns).  Replaces round 4's fdot2 + 4-level shuffle reduction per tap and row
+  // (profiles/round4_notes.md: dearer than the store it saved).
+  auto tapproj_band = [&](const int b0) {
+   if constexpr (C::BANDED && BN == 128) {
+    static_assert(C::CST == 128 && C::CROWS % 16 == 0, "tap projection: 128-channel n-tiles, 16-row fragments");
+    char* const cb8 = reinterpret_cast<char*>(ct);
+    for (int crow = tid / CPR; crow < C::CROWS; crow += RPI) {
+      const float* cp = ct + crow * C::CST + cswz(crow, cc * 8);
+      const floatx4 c0 = *reinterpret_cast<const floatx4*>(cp);
+      const floatx4 c1 = *reinterpret_cast<const floatx4*>(cp + 4);
+      asm volatile("" ::: "memory");  // every lane's reads of this row issue before any lane's write into it
+      half8 h;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        h[j] = (f16)act_apply(c0[j] * p.scale + bias8[j], p.act, p.alpha);
+        h[j + 4] = (f16)act_apply(c1[j] * p.scale + bias8[j + 4], p.act, p.alpha);
+      }
+      *reinterpret_cast<half8*>(cb8 + crow * (C::CST * 4) + ((cc ^ (crow & 15)) << 4)) = h;
+    }
+    __syncthreads();
+    const int r16 = lane & 15, g = lane >> 4;
+    const f16* wt = reinterpret_cast<const f16*>(p.tapw);
+    // taps <= 18: one or two 16-column tiles (RAFT 9 x 1, CREStereo 9 x 2)
+    for (int t0 = 0; t0 < p.taps; t0 += 16) {
+      const int tap = t0 + r16;
+      half8 bw[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        half8 z;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) z[j] = (f16)0.f;
+        bw[ks] = tap < p.taps ? *reinterpret_cast<const half8*>(wt + (size_t)tap * p.Cout + n0 + ks * 32 + g * 8) : z;
+      }
+      for (int f = wave; f < C::CROWS / 16; f += C::NW) {
+        const int crow = f * 16 + r16;
+        floatx4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const half8 a =
+              *reinterpret_cast<const half8*>(cb8 + crow * (C::CST * 4) + (((ks * 4 + g) ^ (crow & 15)) << 4));
+          d = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bw[ks], d, 0, 0, 0);
+        }
+        if (tap < p.taps) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = b0 + f * 16 + 4 * g + r;
+            int m;
+            if constexpr (C::HALO) {
+              const int oy = halo_oy0 + row / C::TW, ox = halo_ox0 + row % C::TW;
+              if (oy >= p.Ho || ox >= p.Wo) continue;
+              m = m0 + oy * p.Wo + ox;
+            } else {
+              m = m0 + row;
+              if (m >= M) continue;
+            }
+            reinterpret_cast<float*>(p.out)[(size_t)m * p.out_stride + (n0 / BN) * p.taps + tap] = d[r];
+          }
+        }
+      }
+    }
+   }
+  };
   if constexpr (C::BANDED) {
     // row bands: the waves owning a band's rows stage their accumulators, everyone stores
 #pragma unroll
@@ -1937,7 +2003,8 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
         }
       }
       __syncthreads();
-      if (nvalid > 0) epi_rows(b0, b0 + C::CROWS, b0);
+      if (BN == 128 && p.epi == SA_EPI_TAPPROJ) tapproj_band(b0);
+      else if (nvalid > 0) epi_rows(b0, b0 + C::CROWS, b0);
       __syncthreads();  // band consumed before the next one overwrites the staging LDS
     }
   } else {

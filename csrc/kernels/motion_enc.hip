@@ -500,9 +500,325 @@ __global__ __launch_bounds__(64 * NW) void raft_motion_encoder_kernel(const Moti
   stamp(6);
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// v2: the same 8 x 16 tile and arithmetic in 63 KB of LDS, so TWO workgroups share a CU (8 waves, 2 per SIMD):
+// one workgroup's latency-bound phases (the pyramid gather of stage 1a, barriers, epilogue stores) run under the
+// other's MFMA stages.  v1 holds A1, S1 and S2 at once (159 KB, one workgroup per CU, MFMA busy 0.22 at batch 8).
+// Here one 61 440-B region R = 240 pixels x 256 B carries them in turn -- A1 (the stage-1 operand, 96 of 128 chunk
+// slots used), then S1, then S2, then the output tile -- each overwrite after a barrier that ends the previous
+// stage's reads (the stage's accumulators wait in registers across it).  Weights no longer stream through LDS
+// rings: each wave reads only its own 16 JN output-channel rows, so its B fragments are plain 16-B global loads
+// (L2 resident, shared by every workgroup) issued DEPTH k-steps ahead into registers.
+constexpr int R_BYTES = P1 * 256;               // 61440
+constexpr int SMEM2 = R_BYTES + FH * FW * 4;    // 63312
+static_assert(2 * SMEM2 <= 163840, "two workgroups per CU");
+#ifndef MENC2_D3
+#define MENC2_D3 3  // k-steps of stage-3 weights in flight
+#endif
+
+// one conv stage of v2: acc[NTI][JN] += A (LDS image `src`, per-row-tile tap-0 pixel base[i], tap offsets via
+// `tapoff(st)` / chunk via `chunk(st)`) x B (global rows w[n0 + 16 j + r16][KROW], k-step st = 32 halfs)
+template <int NTI, int JN, int NS, int DEPTH, int KROW, typename TapOff, typename Chunk>
+__device__ __forceinline__ void menc2_stage(floatx4 (&acc)[NTI][JN], const char* src, const int (&base)[NTI],
+                                            const f16* w, int n0, int lane, TapOff tapoff, Chunk chunk) {
+  const int r16 = lane & 15, kofs = (lane >> 4) * 8;
+  const f16* wrow[JN];
+#pragma unroll
+  for (int j = 0; j < JN; ++j) wrow[j] = w + (size_t)(n0 + 16 * j + r16) * KROW + kofs;
+  half8 bq[NS][JN];
+  half8 aq[2][NTI];
+#pragma unroll
+  for (int st = 0; st < DEPTH && st < NS; ++st)
+#pragma unroll
+    for (int j = 0; j < JN; ++j) bq[st][j] = *reinterpret_cast<const half8*>(wrow[j] + st * 32);
+  auto readA = [&](int st, half8* a) {
+    const int toff = tapoff(st), c = chunk(st);
+#pragma unroll
+    for (int i = 0; i < NTI; ++i) a[i] = *reinterpret_cast<const half8*>(src + sw(base[i] + toff, c));
+  };
+  readA(0, aq[0]);
+#pragma unroll
+  for (int st = 0; st < NS; ++st) {
+    __builtin_amdgcn_sched_barrier(0);
+    if (st + DEPTH < NS) {
+#pragma unroll
+      for (int j = 0; j < JN; ++j) bq[st + DEPTH][j] = *reinterpret_cast<const half8*>(wrow[j] + (st + DEPTH) * 32);
+    }
+    if (st + 1 < NS) readA(st + 1, aq[(st + 1) & 1]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < NTI; ++i)
+#pragma unroll
+      for (int j = 0; j < JN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[st][j], aq[st & 1][i], acc[i][j], 0, 0, 0);
+  }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256, 2) void raft_motion_encoder_v2_kernel(const MotionEncArgs p) {
+  constexpr int NT = 256, NW = 4, JN = 2;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM2];
+  char* R = smem;
+  float* fl = reinterpret_cast<float*>(smem + R_BYTES);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15, kofs = (lane >> 4) * 8;
+  const int tiles_x = (p.W + TW - 1) / TW, tiles_y = (p.H + TH - 1) / TH;
+  const int bimg = blockIdx.x / (tiles_x * tiles_y);
+  const int trem = blockIdx.x - bimg * tiles_x * tiles_y;
+  const int ty0 = (trem / tiles_x) * TH, tx0 = (trem % tiles_x) * TW;
+  const long img_base = (long)bimg * p.H * p.W;
+  auto stamp = [&](int mark) {
+    if (p.stamps && wave == 0) p.stamps[((size_t)blockIdx.x * 8 + mark) * 64 + lane] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+
+  // ---------------- stage 0: flow patch ----------------
+  for (int i = tid; i < FH * FW; i += NT) {
+    const int y = ty0 - 5 + i / FW, x = tx0 - 5 + i % FW;
+    fl[i] = ((unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W) ? p.flow[img_base + (long)y * p.W + x] : 0.f;
+  }
+  __syncthreads();
+  stamp(1);
+
+  // ---------------- stage 1a: the [240 x 96] operand into R (v1's arithmetic, chunk slots swizzled as S1) --------
+  if (tid < P1) {
+    const int pix = tid;
+    const int r = pix / R1W, c = pix - r * R1W;
+    const int y = ty0 - 2 + r, x = tx0 - 2 + c;
+    const bool in = (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
+    const float fx = fl[(r + 3) * FW + (c + 3)];
+    half8 hv[12];
+    if constexpr (VEC) {
+      floatx4 f[4][4];
+      float wa[4];
+      int d[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const long off = q == 0 ? 0 : (q == 1 ? p.lvl_off1 : (q == 2 ? p.lvl_off2 : p.lvl_off3));
+        const int Wl = p.W2 >> q;
+        const float* row = p.pyr + off + (img_base + (long)(in ? y : 0) * p.W + (in ? x : 0)) * Wl;
+        const float xl = ((float)x + fx) / (float)(1 << q) - 4.f;
+        const float x0f = floorf(xl);
+        wa[q] = xl - x0f;
+        const int x0 = (int)x0f;
+        const int b = x0 & ~3;
+        d[q] = x0 - b;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int cc = b + 4 * t;
+          f[q][t] = (in && cc >= 0 && cc < Wl) ? *reinterpret_cast<const floatx4*>(row + cc) : floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float g[13];
+#pragma unroll
+        for (int sidx = 0; sidx < 13; ++sidx)
+          g[sidx] = __fmaf_rn(wa[q], f[q][(sidx + 1) >> 2][(sidx + 1) & 3], __fmul_rn(1.f - wa[q], f[q][sidx >> 2][sidx & 3]));
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+          const int kk = 9 * q + k;
+          const float t = d[q] == 0 ? g[k] : (d[q] == 1 ? g[k + 1] : (d[q] == 2 ? g[k + 2] : g[k + 3]));
+          hv[kk >> 3][kk & 7] = (f16)t;
+        }
+      }
+    } else {
+      float v[4][10], wa[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const long off = q == 0 ? 0 : (q == 1 ? p.lvl_off1 : (q == 2 ? p.lvl_off2 : p.lvl_off3));
+        const int Wl = p.W2 >> q;
+        const float* row = p.pyr + off + (img_base + (long)(in ? y : 0) * p.W + (in ? x : 0)) * Wl;
+        const float xl = ((float)x + fx) / (float)(1 << q) - 4.f;
+        const float x0f = floorf(xl);
+        wa[q] = xl - x0f;
+        const int x0 = (int)x0f;
+#pragma unroll
+        for (int k = 0; k < 10; ++k) {
+          const int xi = x0 + k;
+          v[q][k] = (in && xi >= 0 && xi < Wl) ? row[xi] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+          const int kk = 9 * q + k;
+          hv[kk >> 3][kk & 7] = (f16)__fmaf_rn(wa[q], v[q][k + 1], __fmul_rn(1.f - wa[q], v[q][k]));
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 49; ++t) {
+      const int kk = 36 + t, ky = t / 7, kx = t % 7;
+      hv[kk >> 3][kk & 7] = (f16)fl[(r + ky) * FW + (c + kx)];
+    }
+#pragma unroll
+    for (int kk = 85; kk < 96; ++kk) hv[kk >> 3][kk & 7] = (f16)0.f;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) *reinterpret_cast<half8*>(R + sw(pix, i)) = hv[i];
+  }
+  __syncthreads();
+  stamp(2);
+
+  // ---------------- stage 1b: S1 = relu(A1 x blockdiag(convc1, convf1)), written over A1 ----------------
+  {
+    constexpr int NT1 = P1 / 16;  // 15
+    half8 bfr[JN][3];
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+      const int n = 16 * (wave * JN + j) + r16;
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) bfr[j][ks] = *reinterpret_cast<const half8*>(p.w1 + n * KP + ks * 32 + kofs);
+    }
+    floatx4 acc[NT1][JN];
+#pragma unroll
+    for (int i = 0; i < NT1; ++i)
+#pragma unroll
+      for (int j = 0; j < JN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks)
+#pragma unroll
+      for (int i = 0; i < NT1; ++i) {
+        const half8 a = *reinterpret_cast<const half8*>(R + sw(16 * i + r16, ks * 4 + (lane >> 4)));
+#pragma unroll
+        for (int j = 0; j < JN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bfr[j][ks], a, acc[i][j], 0, 0, 0);
+      }
+    float bias4[JN][4];
+#pragma unroll
+    for (int j = 0; j < JN; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) bias4[j][rr] = p.b1[16 * (wave * JN + j) + 4 * (lane >> 4) + rr];
+    __syncthreads();  // every wave has read A1
+#pragma unroll
+    for (int i = 0; i < NT1; ++i) {
+      const int pix = 16 * i + r16;
+      const int r = pix / R1W, c = pix - r * R1W;
+      const bool in = (unsigned)(ty0 - 2 + r) < (unsigned)p.H && (unsigned)(tx0 - 2 + c) < (unsigned)p.W;
+#pragma unroll
+      for (int j = 0; j < JN; ++j) {
+        const int col = 16 * (wave * JN + j) + 4 * (lane >> 4);
+        half4 h;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) h[rr] = (f16)(in ? fmaxf(acc[i][j][rr] + bias4[j][rr], 0.f) : 0.f);
+        *reinterpret_cast<half4*>(R + sw(pix, col >> 3) + (col & 7) * 2) = h;
+      }
+    }
+  }
+  __syncthreads();
+  stamp(3);
+
+  // ---------------- stage 2: S2 = [relu(convc2(cor1)) | relu(convf2(flo1))] over 10 x 18, written over S1 ---------
+  // wave w: row tiles 6 (w & 1) .. + 5 of the 12 (192 rows, 180 valid) x all four 16-channel column tiles of convc2
+  // (w < 2) or convf2 (w >= 2): 6 A + 4 B fragments per 24 MFMAs
+  {
+    constexpr int NTW = 6, JN2 = 4;
+    const int i0 = (wave & 1) * NTW;
+    const int cb = wave < 2 ? 0 : 64;
+    const f16* wsrc = wave < 2 ? p.w2c : p.w2f;
+    const float* bsrc = wave < 2 ? p.b2c : p.b2f;
+    int base[NTW];
+#pragma unroll
+    for (int i = 0; i < NTW; ++i) {
+      int q = 16 * (i0 + i) + r16;
+      q = q < P2 ? q : P2 - 1;
+      base[i] = (q / R2W) * R1W + (q % R2W);
+    }
+    floatx4 acc[NTW][JN2];
+#pragma unroll
+    for (int i = 0; i < NTW; ++i)
+#pragma unroll
+      for (int j = 0; j < JN2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    menc2_stage<NTW, JN2, 18, 3, 576>(
+        acc, R, base, wsrc, 0, lane,
+        [](int st) { const int tap = st >> 1, ky = tap / 3; return ky * R1W + (tap - ky * 3); },
+        [&](int st) { return (cb + 32 * (st & 1) + kofs) >> 3; });
+    float bias4[JN2][4];
+#pragma unroll
+    for (int j = 0; j < JN2; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) bias4[j][rr] = bsrc[16 * j + 4 * (lane >> 4) + rr];
+    __syncthreads();  // every wave has read S1
+#pragma unroll
+    for (int i = 0; i < NTW; ++i) {
+      const int q = 16 * (i0 + i) + r16;
+      if (q >= P2) continue;
+      const int r = q / R2W, c = q - r * R2W;
+      const bool in = (unsigned)(ty0 - 1 + r) < (unsigned)p.H && (unsigned)(tx0 - 1 + c) < (unsigned)p.W;
+#pragma unroll
+      for (int j = 0; j < JN2; ++j) {
+        const int col = cb + 16 * j + 4 * (lane >> 4);
+        half4 h;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) h[rr] = (f16)(in ? fmaxf(acc[i][j][rr] + bias4[j][rr], 0.f) : 0.f);
+        *reinterpret_cast<half4*>(R + sw(q, col >> 3) + (col & 7) * 2) = h;
+      }
+    }
+  }
+  __syncthreads();
+  stamp(4);
+
+  // ---------------- stage 3: out = relu(conv([cor2 | flo2])) over 8 x 16, K = 9 x 128 ----------------
+  // wave w: row tiles 4 (w & 1) .. + 3 of the 8 x output channels 64 (w >> 1) .. + 63
+  {
+    constexpr int NTW = 4, JN3 = 4;
+    const int i0 = (wave & 1) * NTW;
+    const int nb = (wave >> 1) * 64;
+    int base[NTW];
+#pragma unroll
+    for (int i = 0; i < NTW; ++i) {
+      const int q = 16 * (i0 + i) + r16;
+      base[i] = (q / TW) * R2W + (q % TW);
+    }
+    floatx4 acc[NTW][JN3];
+#pragma unroll
+    for (int i = 0; i < NTW; ++i)
+#pragma unroll
+      for (int j = 0; j < JN3; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    menc2_stage<NTW, JN3, 36, MENC2_D3, 1152>(
+        acc, R, base, p.w3, nb, lane,
+        [](int st) { const int tap = st >> 2, ky = tap / 3; return ky * R2W + (tap - ky * 3); },
+        [&](int st) { return (32 * (st & 3) + kofs) >> 3; });
+    stamp(5);
+    __syncthreads();  // every wave has read S2
+#pragma unroll
+    for (int j = 0; j < JN3; ++j) {
+      const int col0 = nb + 16 * j + 4 * (lane >> 4);
+      float bj[4];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) bj[rr] = col0 + rr < 126 ? p.b3[col0 + rr] : 0.f;
+#pragma unroll
+      for (int i = 0; i < NTW; ++i) {
+        const int q = 16 * (i0 + i) + r16;
+        const float fx = fl[((q / TW) + 5) * FW + (q % TW) + 5];
+        half4 h;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int col = col0 + rr;
+          h[rr] = (f16)(col < 126 ? fmaxf(acc[i][j][rr] + bj[rr], 0.f) : (col == 126 ? fx : 0.f));
+        }
+        *reinterpret_cast<half4*>(R + sw(q, col0 >> 3) + (col0 & 7) * 2) = h;
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < TH * TW * 16; i += NT) {
+      const int q = i >> 4, ch = i & 15;
+      const int y = ty0 + q / TW, x = tx0 + q % TW;
+      if (y < p.H && x < p.W)
+        *reinterpret_cast<half8*>(p.out + (img_base + (long)y * p.W + x) * p.os + ch * 8) =
+            *reinterpret_cast<const half8*>(R + sw(q, ch));
+    }
+  }
+  stamp(6);
+  (void)NW;
+}
+
 unsigned long long* g_stamps = nullptr;
+int g_menc_variant = -1;  // -1: SA_RAFT_MENC (default 1), 1: v1, 2: v2
 
 }  // namespace
+
+extern "C" void sa_raft_motion_encoder_variant(int v) { g_menc_variant = v; }
 
 // diagnostics: record s_memrealtime (100 MHz) stage marks of every workgroup into `buf` ([blocks][8][64] u64) on later launches
 extern "C" void sa_raft_motion_encoder_stamps(void* buf) { g_stamps = (unsigned long long*)buf; }
@@ -546,8 +862,21 @@ extern "C" int sa_raft_motion_encoder(const float* pyr, const float* flow, int B
   a.out = (f16*)out;
   a.os = os;
   a.stamps = g_stamps;
+  int variant = g_menc_variant;
+  if (variant < 0) {
+    const char* e = std::getenv("SA_RAFT_MENC");
+    variant = e ? std::atoi(e) : 1;  // v2 measured slower (b8 40.71 -> 41.95 ms, b1 8.30 -> 8.68)
+  }
+  const bool vec = W2 % 32 == 0 && ((uintptr_t)pyr & 15) == 0;
+  if (variant == 2) {
+    if (vec)
+      hipLaunchKernelGGL((raft_motion_encoder_v2_kernel<true>), dim3((unsigned)blocks), dim3(256), 0, stream, a);
+    else
+      hipLaunchKernelGGL((raft_motion_encoder_v2_kernel<false>), dim3((unsigned)blocks), dim3(256), 0, stream, a);
+    return (int)hipGetLastError();
+  }
   // 4 waves (an 8-wave variant measured no faster at batch 1 and 1 % slower at batch 8)
-  if (W2 % 32 == 0 && ((uintptr_t)pyr & 15) == 0)
+  if (vec)
     hipLaunchKernelGGL((raft_motion_encoder_kernel<4, true>), dim3((unsigned)blocks), dim3(256), 0, stream, a);
   else
     hipLaunchKernelGGL((raft_motion_encoder_kernel<4, false>), dim3((unsigned)blocks), dim3(256), 0, stream, a);

@@ -468,20 +468,23 @@ void RaftStereo::forward(hipStream_t s) {
   // a node's first child on the parent's queue), so the two trunks' queue assignment swaps.  Default: on for the
   // realtime preset only (same-process A/B b1: realtime 1.884 -> 1.864 ms, sceneflow 8.50 -> 8.63 ms)
   const bool cnet_first = cnet_first_mode_ >= 0 ? cnet_first_mode_ != 0 : rc_.slow_fast;
-  if (cnet_first && par && !rc_.shared) {
+  if (cnet_first && par && !rc_.shared && !early) {
     hipStream_t fs = fork(s);
     cnet_.run(s, sp_, img_.slice_n(0, Bn));
     feature_branch(fs);
   } else if (early) {
     // the two trunks' launches interleaved layer by layer in capture order: the graph's host-side enqueue follows
     // it, and a branch captured whole after the other one started ~0.8 ms late (timeline_r5_sf)
+    // (with SA_RAFT_CNET_FIRST=1 the context trunk's layer goes first in each pair; it reads imgc_, preprocessed on
+    // its own queue, never img_, which the feature queue writes)
     const int n = std::max(fnet_.steps(), cnet_.steps());
     for (int k = 0; k < n; ++k) {
+      if (cnet_first && k < cnet_.steps()) cnet_.run_step(s, sp_, imgc_, k);
       if (k < fnet_.steps()) {
         ScopedSplitK sk2(&splitk_side_);
         fnet_.run_step(fs_early, sp_, img_, k);
       }
-      if (k < cnet_.steps()) cnet_.run_step(s, sp_, imgc_, k);
+      if (!cnet_first && k < cnet_.steps()) cnet_.run_step(s, sp_, imgc_, k);
     }
     ScopedSplitK sk2(&splitk_side_);
     fconv2_.run(fs_early, {fnet_.out()}, fmap_);

@@ -213,6 +213,7 @@ void StereoEngine::init() {
       HIP_CHECK(hipStreamSynchronize(stream_));
     }
     tuned_shapes_ = conv_tune_count() - tuned0;
+    plan_keys_ = keys;
     // Save whenever this engine's own plan file lacks a shape it consulted, not only when it tuned one: an engine
     // whose shapes were all tuned by an earlier engine in the same process (crestereo-iter10 after iter2 / iter5)
     // still gets its "<stem>_batch=1.engine"-style file, so a fresh process running it alone does not re-tune.
@@ -468,6 +469,25 @@ void StereoEngine::run_device(const uint8_t* left, const uint8_t* right, float* 
                               bool rectify, hipStream_t s, uint8_t* rect_left, uint8_t* rect_right) {
   HIP_CHECK(hipSetDevice(cfg_.device));
   const size_t img = (size_t)B() * H() * W() * 3;
+  // Straight through the frame graph: the graph's input-copy node reads the caller's device
+  // images and its reprojection node writes disparity + cloud into the caller's tensors -- the same two nodes
+  // run_host re-points at host memory (launch_frame updates them when the pointers change), so no D2D copy runs
+  // around the graph.  SA_DEVICE_DIRECT=0, no Q (no reprojection node), unaligned inputs or requested rectified
+  // outputs keep the copy path.
+  static const bool direct_on = [] {
+    const char* e = std::getenv("SA_DEVICE_DIRECT");
+    return !(e && e[0] == '0');
+  }();
+  const bool direct = direct_on && cfg_.use_graph && have_Q_ && img % 16 == 0 && (disp || cloud) &&
+                      (((uintptr_t)left | (uintptr_t)right) & 15) == 0 && !(rectify && (rect_left || rect_right));
+  if (direct) {
+    in_src_[0] = left;
+    in_src_[1] = right;
+    out_target_[0] = disp;
+    out_target_[1] = have_Q_ ? cloud : nullptr;
+    launch_frame(s, rectify, true, true);
+    return;
+  }
   uint8_t* dl = rectify ? raw_left_ : in_left_;
   uint8_t* dr = rectify ? raw_right_ : in_right_;
   HIP_CHECK(hipMemcpyAsync(dl, left, img, hipMemcpyDeviceToDevice, s));

@@ -6,6 +6,7 @@
 #include <mutex>
 #include <unordered_map>
 #include <cstring>
+#include <cstdio>
 #include <cerrno>
 #include <dlfcn.h>
 #include <fstream>
@@ -982,6 +983,37 @@ const std::string& conv_plan_arch() { return g_arch; }
 ScopedPlanCollect::ScopedPlanCollect(std::vector<std::string>* keys) : prev(g_plan_collect) { g_plan_collect = keys; }
 ScopedPlanCollect::~ScopedPlanCollect() { g_plan_collect = prev; }
 
+namespace {
+bool g_plan_pinned = false;
+}
+void conv_plan_pin(bool on) {
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  g_plan_pinned = on;
+}
+
+std::string conv_plan_digest(const std::vector<std::string>& keys) {
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  auto& m = plan_map();
+  std::vector<std::string> rows;
+  for (const std::string& k : keys) {
+    auto it = m.find(k);
+    rows.push_back(k + ' ' + (it == m.end() ? std::string("-") : std::to_string(it->second.cfg) + ' ' +
+                                                                  std::to_string(it->second.splitk)));
+  }
+  std::sort(rows.begin(), rows.end());
+  rows.erase(std::unique(rows.begin(), rows.end()), rows.end());
+  uint64_t h = 1469598103934665603ull;  // FNV-1a 64
+  auto mix = [&](const std::string& t) {
+    for (unsigned char c : t) h = (h ^ c) * 1099511628211ull;
+    h = (h ^ '\n') * 1099511628211ull;
+  };
+  mix(build_id());
+  for (const std::string& r : rows) mix(r);
+  char buf[17];
+  std::snprintf(buf, sizeof buf, "%016llx", (unsigned long long)h);
+  return buf;
+}
+
 int conv_plan_load(const std::string& file) {
   std::lock_guard<std::mutex> lk(g_plan_mu);
   auto& m = plan_map();
@@ -991,7 +1023,9 @@ int conv_plan_load(const std::string& file) {
   std::unordered_map<std::string, PlanEntry> fresh;
   const int n = load_plan_file(fresh, file);
   if (n == -2) return -2;
-  for (auto& kv : fresh) m[kv.first] = kv.second;
+  // pinned (a DP rank holding rank 0's broadcast table): a file never overrides an entry the process already has
+  for (auto& kv : fresh)
+    if (!g_plan_pinned || !m.count(kv.first)) m[kv.first] = kv.second;
   (void)before;
   // the entries the FILE holds (a second engine of the same shapes finds them all in the process map already, and
   // reporting "0 new" there could not be told apart from an empty file: VERDICT r4 weak #9)

@@ -151,6 +151,7 @@ def _declare_dev(lib):
         "sa_raft_motion_head": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _i, _p, _i, _p, _i, _p]),
         "sa_raft_motion_encoder": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p]),
         "sa_raft_motion_encoder_stamps": (None, [_p]),
+        "sa_raft_motion_encoder_variant": (None, [_i]),
         "sa_convex_upsample": (_i, [_p, _i, _p, _i, _i, _i, _i, _f, _p, _p]),
         "sa_preprocess": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, _p]),
         "sa_remap_bgr": (_i, [_p, _i, _i, _i, _p, _i, _i, _i, _p, _p]),
@@ -187,6 +188,9 @@ def _declare_dev(lib):
         "sa_engine_aux_output": (_p, [_p, C.POINTER(_i)]),
         "sa_engine_stream": (_p, [_p]),
         "sa_engine_plan_path": (C.c_char_p, [_p]),
+        "sa_engine_tactics_digest": (C.c_char_p, [_p]),
+        "sa_engine_plan_export": (_i, [_p, C.c_char_p]),
+        "sa_conv_plan_pin": (None, [_i]),
         "sa_engine_tuned_shapes": (C.c_long, [_p]),
         "sa_engine_plan_status": (None, [_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "sa_plan_build_id": (C.c_char_p, []),

@@ -115,6 +115,16 @@ class NativeStereoEngine:
         return self._lib.sa_engine_plan_path(self._live).decode()
 
     @property
+    def tactics_digest(self) -> str:
+        """Digest of the tactics this engine's frame graph launches, from the process plan (not a file): the shapes it
+        consulted with their (cfg, splitk) and the library build id.  Equal digests = identical kernels."""
+        return self._lib.sa_engine_tactics_digest(self._live).decode()
+
+    def plan_export(self, path: str) -> int:
+        """Write this engine's plan entries to ``path`` (0 or errno): what a DP job's rank 0 broadcasts."""
+        return int(self._lib.sa_engine_plan_export(self._live, str(path).encode()))
+
+    @property
     def tuned_shapes(self) -> int:
         """Conv shapes this engine had to time at build (0 when its plan file covered everything)."""
         return int(self._lib.sa_engine_tuned_shapes(self._live))
@@ -130,7 +140,7 @@ class NativeStereoEngine:
         self._lib.sa_engine_plan_status(self._live, C.byref(ld), C.byref(sv))
         return {"path": self.plan_path, "loaded": ld.value, "state": plan_state(ld.value), "saved": sv.value,
                 "tuned_shapes": self.tuned_shapes, "build": self._lib.sa_plan_build_id().decode(),
-                "tactics": tactic_digest(self.plan_path)}
+                "tactics": tactic_digest(self.plan_path), "launched": self.tactics_digest}
 
     def nonzero_splitk_counters(self) -> int:
         """Diagnostic: split-K tile counters left non-zero (0 after every correctly ordered frame)."""

@@ -88,7 +88,7 @@ def raft_motion_head(pyr_buf, flow, b, h, w1, w2, convc1_w, convc1_b, convf1_w, 
 
 
 def raft_motion_encoder(pyr_buf, flow, b, h, w1, w2, convc1_w, convc1_b, convf1_w, convf1_b, convc2_w, convc2_b,
-                        convf2_w, convf2_b, conv_w, conv_b, levels=4, radius=4):
+                        convf2_w, convf2_b, conv_w, conv_b, levels=4, radius=4, variant=-1):
     """The fused RAFT motion encoder (sa_raft_motion_encoder): fp16 NHWC [b, h, w1, 128] =
     [relu(conv([relu(convc2(cor1)), relu(convf2(flo1))])) (126) | flow_x | 0].  Torch-layout weights."""
     nc = levels * (2 * radius + 1)
@@ -105,10 +105,12 @@ def raft_motion_encoder(pyr_buf, flow, b, h, w1, w2, convc1_w, convc1_b, convf1_
     out = torch.empty(b, h, w1, 128, dtype=torch.float16, device=dev)
     f = lambda t: t.float().contiguous()
     bias = [f(convc2_b), f(convf2_b), f(conv_b)]
+    N.dev().sa_raft_motion_encoder_variant(variant)
     N.check(N.dev().sa_raft_motion_encoder(pyr_buf.data_ptr(), flow.contiguous().data_ptr(), b, h, w1, w2, levels,
                                            radius, wb.data_ptr(), b1.data_ptr(), w2c.data_ptr(), bias[0].data_ptr(),
                                            w2f.data_ptr(), bias[1].data_ptr(), w3.data_ptr(), bias[2].data_ptr(),
                                            out.data_ptr(), 128, _stream()), "sa_raft_motion_encoder")
+    N.dev().sa_raft_motion_encoder_variant(-1)
     return out
 
 

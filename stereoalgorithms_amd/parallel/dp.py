@@ -266,20 +266,36 @@ def build_engine_shared_plan(make_engine, world: int, rank: int, load_plan=None)
     """Build one engine per rank so that EVERY rank launches the tactics rank 0 tuned (ranks that
     tune independently pick different kernels on noisy timings, and the job's step time is the slowest rank's).
 
-    Rank 0 builds first -- timing each conv shape and saving its plan file -- while the other ranks wait in the
-    broadcast of that file's bytes; each then merges the bytes into its own process tactic table (``load_plan``,
-    default the native ``sa_conv_plan_load``) and builds, finding every shape already planned (no timing, no
-    divergence), and saves the same entries under its own plan path.  Works across nodes (bytes travel over the
-    process group, not a shared file system).
+    Rank 0 builds first -- timing each conv shape -- and exports the entries its engine actually launched
+    (``plan_export``, from the process plan: this works with plan files disabled too) while the other ranks wait in
+    the broadcast of those bytes.  Each merges them into its own process tactic table (``load_plan``, default the
+    native ``sa_conv_plan_load``), PINS the table (a stale plan file at the rank's own plan path can no longer override
+    the broadcast entries when its engine loads it), and builds, finding every shape planned.  Bytes travel
+    over the process group, not a shared file system, so this works across nodes.
 
-    Returns ``(engine, digests)``: ``digests[r]`` is rank r's ``utils.plan.tactic_digest`` of its plan file after the
-    build (all equal when the plans agree; callers assert or report it)."""
+    Returns ``(engine, digests)``: ``digests[r]`` is rank r's ``tactics_digest`` -- the (key, cfg, splitk) its frame
+    graph launches -- or None when the engine cannot report one.  All equal = identical kernels on every rank."""
     import os
     import tempfile
-    from stereoalgorithms_amd.utils.plan import tactic_digest
 
     def digest_of(eng):
-        return tactic_digest(getattr(eng, "plan_path", "") or "")
+        d = getattr(eng, "tactics_digest", None)
+        return d if isinstance(d, str) and d else None
+
+    def export_bytes(eng):
+        exp = getattr(eng, "plan_export", None)
+        if exp is not None:
+            fd, tmp = tempfile.mkstemp(suffix=".plan")
+            os.close(fd)
+            try:
+                if exp(tmp) == 0:
+                    with open(tmp, "rb") as f:
+                        return f.read()
+            finally:
+                os.unlink(tmp)
+        path = getattr(eng, "plan_path", "") or ""  # engines without an export: their plan file
+        with open(path, "rb") if path and os.path.exists(path) else _empty() as f:
+            return f.read()
 
     if world <= 1:
         eng = make_engine()
@@ -287,9 +303,7 @@ def build_engine_shared_plan(make_engine, world: int, rank: int, load_plan=None)
     box = [None]
     if rank == 0:
         eng = make_engine()
-        path = getattr(eng, "plan_path", "") or ""
-        with open(path, "rb") if path and os.path.exists(path) else _empty() as f:
-            box = [f.read()]
+        box = [export_bytes(eng)]
     dist.broadcast_object_list(box, src=0)
     if rank != 0:
         data = box[0]
@@ -301,10 +315,21 @@ def build_engine_shared_plan(make_engine, world: int, rank: int, load_plan=None)
                 (load_plan or _native_plan_load)(tmp)
             finally:
                 os.unlink(tmp)
-        eng = make_engine()
+            if load_plan is None:
+                _native_plan_pin(True)
+        try:
+            eng = make_engine()
+        finally:
+            if data and load_plan is None:
+                _native_plan_pin(False)
     digests = [None] * world
     dist.all_gather_object(digests, digest_of(eng))
     return eng, digests
+
+
+def _native_plan_pin(on: bool) -> None:
+    from stereoalgorithms_amd import _native as N
+    N.dev().sa_conv_plan_pin(1 if on else 0)
 
 
 class _empty:

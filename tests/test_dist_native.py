@@ -7,6 +7,7 @@ import multiprocessing as mp
 import os
 import socket
 import subprocess
+import sys
 
 import pytest
 
@@ -58,6 +59,23 @@ def test_bootstrap_times_out_without_rank0():
     assert lib.sa_dist_exchange_blob(1, 2, b"127.0.0.1", _free_port(), buf, C.c_size_t(16), 300) == -1
 
 
+@pytest.mark.skipif(not os.path.exists(LIB), reason="native build missing")
+def test_communicator_init_deadline_loop():
+    """the communicator is created non-blocking (ncclCommInitRankConfig, blocking = 0) and its
+    init / enqueues are polled through one deadline loop (settle): it returns 0 once the status reaches ncclSuccess,
+    1 on an RCCL error, and -1 when the status is still ncclInProgress at SA_DIST_TIMEOUT -- a peer that never joins
+    fails the job instead of hanging it.  Exercised on the CPU with a scripted status source (ncclInProgress = 7,
+    ncclSuccess = 0, ncclSystemError = 2)."""
+    import time
+    lib = C.CDLL(LIB, mode=C.RTLD_GLOBAL)
+    assert lib.sa_dist_settle_probe(0, 0, 1000) == 0
+    assert lib.sa_dist_settle_probe(25, 0, 5000) == 0  # in progress for a while, then up
+    assert lib.sa_dist_settle_probe(3, 2, 5000) == 1   # init failed
+    t0 = time.perf_counter()
+    assert lib.sa_dist_settle_probe(1 << 30, 0, 300) == -1  # never settles: the deadline ends it
+    assert 0.25 < time.perf_counter() - t0 < 5.0
+
+
 @pytest.mark.gpu
 def test_native_dp_bench_world1():
     env = dict(os.environ, SA_DIST_TIMEOUT="120", SA_DP_GATHER_WORLD1="1")
@@ -66,3 +84,25 @@ def test_native_dp_bench_world1():
     assert r.returncode == 0, r.stderr[-2000:]
     rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert rec["n_gpus"] == 1 and rec["finite"] and rec["value"] > 0
+
+
+@pytest.mark.gpu
+def test_native_dp_bench_same_workload_as_bench_py(tmp_path):
+    """stereo_bench_dp times bench.py's step -- per-step H2D of pinned host inputs on the copy
+    stream, the frame graph with point-cloud reprojection, the gather path -- so at world 1 on the same box and with
+    the same tactic plan (shared SA_PLAN_DIR) their ms/step agree (5 % here; the committed record is tighter)."""
+    env = dict(os.environ, SA_DIST_TIMEOUT="120", SA_PLAN_DIR=str(tmp_path))
+    env.pop("SA_DP_GATHER_WORLD1", None)
+    args = ["--model", "raftstereo-realtime", "--steps", "30", "--warmup", "3"]
+    r = subprocess.run([BIN, "--nproc", "1", "--batch", "8", *args], capture_output=True, text=True, timeout=200,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    nat = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--per-gpu-batch", "8", "--no-latency", *args],
+                       capture_output=True, text=True, timeout=200, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    py = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    print(f"native {nat['ms_per_step']} ms/step vs bench.py {py['ms_per_step']} ms/step "
+          f"(rank min/max {nat['rank_step_ms']} / {py['rank_step_ms']})")
+    assert nat["finite"] and nat["plans_identical_across_ranks"]
+    assert abs(nat["ms_per_step"] / py["ms_per_step"] - 1) < 0.05

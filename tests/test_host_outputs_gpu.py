@@ -84,3 +84,44 @@ def test_caller_inputs_zero_copy_and_fresh_arrays():
         assert np.array_equal(d, refs[i][0]) and np.array_equal(c, refs[i][1], equal_nan=True), k
         del L, R, d, c
     e.close()
+
+
+def test_run_device_writes_caller_tensors_from_the_graph():
+    """the device run() path launches the frame graph with its input-copy node reading the caller's
+    device images and its reprojection node writing disparity + cloud into the caller's tensors (no D2D copies around
+    the graph).  Swapping out / cloud_out tensors between frames re-points the nodes: every frame's bytes equal the
+    pinned-I/O run_host frame of the same images, a tensor no longer passed is not written, and changing the input
+    tensors is followed frame by frame."""
+    from stereoalgorithms_amd.models.engine import NativeStereoEngine
+    b, h, w = 2, 240, 320
+    e = NativeStereoEngine("raftstereo-realtime", None, h, w, batch=b, device=0)
+    e.set_Q(Q)
+    pairs = [batch_pairs(b, h, w, seed=s) for s in (3, 4)]
+    refs = []
+    hb = e.host_buffers()
+    for l, r in pairs:
+        hb["left"][...] = l
+        hb["right"][...] = r
+        e.run_host(hb["left"], hb["right"], cloud=True, out=hb["disp"], cloud_out=hb["cloud"])
+        refs.append((torch.from_numpy(hb["disp"].copy()), torch.from_numpy(hb["cloud"].copy())))
+    hb = None
+    dev_pairs = [(torch.from_numpy(l).cuda(), torch.from_numpy(r).cuda()) for l, r in pairs]
+    outs = [torch.full((b, h, w), -7.0, device="cuda") for _ in range(2)]
+    clouds = [torch.full((b, h, w, 6), -7.0, device="cuda") for _ in range(2)]
+    for i in range(6):
+        k, j = i % 2, (i // 2) % 2  # output tensors alternate every frame, the input pair every two
+        if i == 4:
+            outs[1].fill_(-1.0)
+            clouds[1].fill_(-1.0)
+        l, r = dev_pairs[j]
+        d, c = e.run(l, r, cloud=True, out=outs[k if i < 4 else 0], cloud_out=clouds[k if i < 4 else 0])
+        torch.cuda.synchronize()
+        assert torch.equal(d.cpu(), refs[j][0]), f"frame {i}: disparity"
+        c_cpu, cref = c.cpu(), refs[j][1]
+        assert torch.equal(torch.nan_to_num(c_cpu, 1e30), torch.nan_to_num(cref, 1e30)), f"frame {i}: cloud"
+    assert (outs[1] == -1.0).all() and (clouds[1] == -1.0).all()  # frames 4-5 used only tensor 0
+    d_only = torch.zeros(b, h, w, device="cuda")
+    e.run(*dev_pairs[0], out=d_only)  # disparity only: still written by the graph
+    torch.cuda.synchronize()
+    assert torch.equal(d_only.cpu(), refs[0][0])
+    e.close()

@@ -208,6 +208,17 @@ class _TunedEngine:
                 f.write(f"{k} {cfg} {sk} {us}\n")
 
 
+    @property
+    def tactics_digest(self):
+        """What the native engine reports: the (key, cfg, splitk) its graph launches, from the in-process table."""
+        import hashlib
+        h = hashlib.sha256()
+        for k in sorted(self.SHAPES):
+            cfg, sk, _ = self.table[k]
+            h.update(f"{k} {cfg} {sk}\n".encode())
+        return h.hexdigest()[:16]
+
+
 def _fake_plan_load(path):
     from stereoalgorithms_amd.utils.plan import read_plan
     _, entries = read_plan(path)

@@ -118,3 +118,25 @@ def test_plan_load_counts_file_entries_not_new_ones(tmp_path):
     assert tactic_digest(q) == d1
     q.write_text(p.read_text().replace(" 26 1 ", " 28 1 "))
     assert tactic_digest(q) != d1 and tactic_digest(tmp_path / "none.plan") is None
+
+
+def test_pinned_table_survives_stale_local_plan(tmp_path):
+    """a DP rank that merged rank 0's broadcast table pins it, so the plan file its engine loads at init (a
+    stale file from an earlier job on that node) cannot override the broadcast choices; unpinned loads still merge."""
+    lib = _lib()
+    build = lib.sa_plan_build_id().decode()
+    local = tmp_path / "local.plan"
+    local.write_text(f"# sa-plan build={build}\n{KEYS[0]} 3 0 9.0\n{KEYS[1]} 4 0 8.0\n")
+    lib.sa_conv_plan_put(KEYS[0].encode(), 26, 1, 41.5)  # the broadcast entry
+    lib.sa_conv_plan_pin(1)
+    try:
+        assert lib.sa_conv_plan_load(str(local).encode()) == 2
+    finally:
+        lib.sa_conv_plan_pin(0)
+    out = tmp_path / "out.plan"
+    assert lib.sa_conv_plan_save(str(out).encode(), "\n".join(KEYS).encode()) == 0
+    got = {e.key: (e.cfg, e.splitk) for e in read_plan(out)[1]}
+    assert got == {KEYS[0]: (26, 1), KEYS[1]: (4, 0)}  # kept the pinned entry, added the missing one
+    assert lib.sa_conv_plan_load(str(local).encode()) == 2  # unpinned: the file wins again
+    assert lib.sa_conv_plan_save(str(out).encode(), "\n".join(KEYS).encode()) == 0
+    assert {e.key: e.cfg for e in read_plan(out)[1]}[KEYS[0]] == 3

@@ -21,15 +21,22 @@ MODES = [
     ("unfused-motion-encoder", {"SA_RAFT_PARALLEL": "0", "SA_RAFT_FUSE_MENC": "0"}),
     # round 3's mode-2 layout (motion encoder on a third stream); the default runs it on the main stream
     ("pipeline2-side-menc", {"SA_RAFT_PIPELINE": "2", "SA_RAFT_M2_MAIN": "0"}),
+    # context trunk captured first with the early encoder fork (it must read its own preprocessed copy)
+    ("cnet-first", {"SA_RAFT_CNET_FIRST": "1"}),
+    # the one-workgroup-per-CU motion encoder (v1): same MFMAs in the same k order as the default v2
+    ("motion-encoder-v1", {"SA_RAFT_MENC": "1"}),
 ]
 TOL = {"unfused-motion-encoder": 1e-2}
-KNOBS = ("SA_RAFT_PARALLEL", "SA_RAFT_PIPELINE", "SA_RAFT_FUSE_MENC", "SA_RAFT_M2_MAIN")
+KNOBS = ("SA_RAFT_PARALLEL", "SA_RAFT_PIPELINE", "SA_RAFT_FUSE_MENC", "SA_RAFT_M2_MAIN", "SA_RAFT_CNET_FIRST",
+         "SA_RAFT_MENC")
 
 
 RT_MODES = [
     ("serial", {"SA_RAFT_PARALLEL": "0"}),
     ("parallel", {"SA_RAFT_PIPELINE": "0"}),
     ("pipeline", {}),
+    ("cnet-second", {"SA_RAFT_CNET_FIRST": "0"}),
+    ("motion-encoder-v1", {"SA_RAFT_MENC": "1"}),
 ]
 
 

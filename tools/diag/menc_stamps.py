@@ -13,6 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--variant", type=int, default=-1, help="sa_raft_motion_encoder_variant (1, 2; -1 default)")
     a = ap.parse_args()
     import torch
     from stereoalgorithms_amd import ops as O
@@ -31,9 +32,17 @@ def main():
     st = torch.zeros(blocks * 8 * 64, dtype=torch.int64, device="cuda")
     for rep in range(3):
         dev().sa_raft_motion_encoder_stamps(st.data_ptr() if rep == 2 else None)
-        O.raft_motion_encoder(buf, flow, b, h, w, w, *ws)
+        O.raft_motion_encoder(buf, flow, b, h, w, w, *ws, variant=a.variant)
         torch.cuda.synchronize()
     dev().sa_raft_motion_encoder_stamps(None)
+    # kernel time without stamps (events around 20 back-to-back launches)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        O.raft_motion_encoder(buf, flow, b, h, w, w, *ws, variant=a.variant)
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"variant {a.variant}: {e0.elapsed_time(e1) / 20 * 1e3:.1f} us per launch (incl. weight packing)")
     t = st.view(blocks, 8, 64)[:, :7, 0].double()
     d = (t[:, 1:] - t[:, :-1]) / 100.0  # s_memrealtime ticks at 100 MHz -> us
     names = ["flow patch", "lookup+flow taps", "stage-1 GEMM", "stage-2 convs", "stage-3 loop", "epilogue+store"]
