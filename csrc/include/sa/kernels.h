@@ -216,6 +216,12 @@ int sa_raft_motion_head(const float* pyr, const float* flow, int B, int H, int W
 int sa_raft_motion_encoder(const float* pyr, const float* flow, int B, int H, int W, int W2, int levels, int radius,
                            const void* w1, const float* b1, const void* w2c, const float* b2c, const void* w2f,
                            const float* b2f, const void* w3, const float* b3, void* out, int os, hipStream_t stream);
+// the same with the previous flow head's tap projections (SA_EPI_TAPPROJ output P [B][H][W][2][9], bias: the tail
+// conv's) applied while the flow is read: flow_out (!= flow) receives flow + stencil(P) -- sa_tapproj_stencil fused
+int sa_raft_motion_encoder_proj(const float* pyr, const float* flow, int B, int H, int W, int W2, int levels,
+                                int radius, const void* w1, const float* b1, const void* w2c, const float* b2c,
+                                const void* w2f, const float* b2f, const void* w3, const float* b3, void* out, int os,
+                                const float* proj, const float* proj_bias, float* flow_out, hipStream_t stream);
 // diagnostics: s_memrealtime (100 MHz) stage marks of every workgroup of later sa_raft_motion_encoder launches into `buf`
 // ([blocks][8 marks][64] u64; NULL turns it off)
 void sa_raft_motion_encoder_stamps(void* buf);

@@ -66,7 +66,37 @@ struct MotionEncArgs {
   f16* out;  // [B][H][W][os], channels 0..127
   int os;
   unsigned long long* stamps;  // diagnostics (sa_raft_motion_encoder_stamps): [block][8 marks][64 lanes] or null
+  // fused flow-head stencil (null: off): the previous flow head's tap projections P [B][H][W][2][9] fp32
+  // (SA_EPI_TAPPROJ) are applied while the flow patch is loaded -- flow(p) = flow_in(p) + bias + sum over the 3x3
+  // taps of both n-tile partials, in sa_tapproj_stencil's order (bitwise the same flow) -- and the tile's own pixels
+  // of the updated flow are written to flow_out (a different buffer: neighbouring tiles still read flow_in)
+  const float* proj;
+  const float* proj_bias;
+  float* flow_out;
 };
+
+// stage 0 of both variants: the fp32 flow patch (image rows ty0-5 .., cols tx0-5 ..), zero outside, with the
+// previous flow head's stencil applied when p.proj is set
+__device__ __forceinline__ float menc_flow_at(const MotionEncArgs& p, long img_base, int y, int x, int ty0, int tx0) {
+  if ((unsigned)y >= (unsigned)p.H || (unsigned)x >= (unsigned)p.W) return 0.f;
+  const long px = img_base + (long)y * p.W + x;
+  float v = p.flow[px];
+  if (p.proj) {
+    float s = p.proj_bias ? p.proj_bias[0] : 0.f;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int yy = y + ky - 1, xx = x + kx - 1;
+        if (yy < 0 || yy >= p.H || xx < 0 || xx >= p.W) continue;
+        const float* q = p.proj + (img_base + (long)yy * p.W + xx) * 18 + (ky * 3 + kx);
+        s += q[0] + q[9];
+      }
+    v += s;
+    if (y >= ty0 && y < ty0 + 8 && x >= tx0 && x < tx0 + 16) p.flow_out[px] = v;
+  }
+  return v;
+}
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
@@ -150,10 +180,7 @@ __global__ __launch_bounds__(64 * NW) void raft_motion_encoder_kernel(const Moti
   stamp(0);
 
   // ---------------- stage 0: flow patch (image rows ty0-5 .., cols tx0-5 ..), zero outside ----------------
-  for (int i = tid; i < FH * FW; i += NT) {
-    const int y = ty0 - 5 + i / FW, x = tx0 - 5 + i % FW;
-    fl[i] = ((unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W) ? p.flow[img_base + (long)y * p.W + x] : 0.f;
-  }
+  for (int i = tid; i < FH * FW; i += NT) fl[i] = menc_flow_at(p, img_base, ty0 - 5 + i / FW, tx0 - 5 + i % FW, ty0, tx0);
   __syncthreads();
 
   stamp(1);
@@ -574,10 +601,7 @@ __global__ __launch_bounds__(256, 2) void raft_motion_encoder_v2_kernel(const Mo
   stamp(0);
 
   // ---------------- stage 0: flow patch ----------------
-  for (int i = tid; i < FH * FW; i += NT) {
-    const int y = ty0 - 5 + i / FW, x = tx0 - 5 + i % FW;
-    fl[i] = ((unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W) ? p.flow[img_base + (long)y * p.W + x] : 0.f;
-  }
+  for (int i = tid; i < FH * FW; i += NT) fl[i] = menc_flow_at(p, img_base, ty0 - 5 + i / FW, tx0 - 5 + i % FW, ty0, tx0);
   __syncthreads();
   stamp(1);
 
@@ -827,7 +851,17 @@ extern "C" int sa_raft_motion_encoder(const float* pyr, const float* flow, int B
                                       int radius, const void* w1, const float* b1, const void* w2c, const float* b2c,
                                       const void* w2f, const float* b2f, const void* w3, const float* b3, void* out,
                                       int os, hipStream_t stream) {
+  return sa_raft_motion_encoder_proj(pyr, flow, B, H, W, W2, levels, radius, w1, b1, w2c, b2c, w2f, b2f, w3, b3, out,
+                                     os, nullptr, nullptr, nullptr, stream);
+}
+
+extern "C" int sa_raft_motion_encoder_proj(const float* pyr, const float* flow, int B, int H, int W, int W2,
+                                           int levels, int radius, const void* w1, const float* b1, const void* w2c,
+                                           const float* b2c, const void* w2f, const float* b2f, const void* w3,
+                                           const float* b3, void* out, int os, const float* proj,
+                                           const float* proj_bias, float* flow_out, hipStream_t stream) {
   if (levels != 4 || radius != 4 || os < 128 || os % 8 || B < 1 || H < 1 || W < 1) return -2;
+  if (proj && (!flow_out || flow_out == flow)) return -2;
   if (((uintptr_t)out | (uintptr_t)w1 | (uintptr_t)w2c | (uintptr_t)w2f | (uintptr_t)w3) & 15) return -2;
   long off[4] = {0, 0, 0, 0};
   long acc = 0;
@@ -862,6 +896,9 @@ extern "C" int sa_raft_motion_encoder(const float* pyr, const float* flow, int B
   a.out = (f16*)out;
   a.os = os;
   a.stamps = g_stamps;
+  a.proj = proj;
+  a.proj_bias = proj_bias;
+  a.flow_out = flow_out;
   int variant = g_menc_variant;
   if (variant < 0) {
     const char* e = std::getenv("SA_RAFT_MENC");

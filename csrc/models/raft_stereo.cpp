@@ -62,7 +62,7 @@ class RaftStereo : public StereoEngine {
   const char* name() const override { return "RAFTStereo"; }
   const float* aux_output(int* n) const override {
     *n = B() * lh_[0] * lw_[0];
-    return flow_;
+    return flow_();
   }
 
  protected:
@@ -123,9 +123,9 @@ class RaftStereo : public StereoEngine {
   void* fh2_w16_ = nullptr;
   // SA_RAFT_FH_PROJ: flow-head conv1 stores conv2's tap projections (SA_EPI_TAPPROJ) instead of its 256-channel
   // output, and a stencil adds them into the flow (all but the last iteration, whose conv1 also feeds the mask
-  // head).  Default: the realtime preset only, where the flow head runs beside the chain (same-process A/B: RT b1
-  // 1.986 -> 1.865 ms; SF b1 8.26 -> 8.85, b8 43.8 -> 45.4: the epilogue's per-tap lane reductions cost more than
-  // the 256-channel store they save when conv1 is on the critical path)
+  // head).  Round 4 had it on for the realtime preset only (its per-tap lane reductions cost more than the store
+  // they saved on the SF chain: b1 8.26 -> 8.85, b8 43.8 -> 45.4); round 6 computes the projections with MFMAs on
+  // the LDS-staged C tile of the banded tiles and is on by default (SA_RAFT_FH_PROJ=0 turns it off)
   int fh_proj_env_ = std::getenv("SA_RAFT_FH_PROJ") ? std::atoi(std::getenv("SA_RAFT_FH_PROJ")) : -1;
   float* fhP_ = nullptr;  // [B][h0][w0][2 n-tiles][9] fp32
   // fused lookup + convc1 + convf1 (sa_raft_motion_head): fp32 [k][64] weights and biases
@@ -151,7 +151,17 @@ class RaftStereo : public StereoEngine {
   int cnet_first_mode_ = std::getenv("SA_RAFT_CNET_FIRST") ? std::atoi(std::getenv("SA_RAFT_CNET_FIRST")) : -1;
   int pipeline_mode_ = std::getenv("SA_RAFT_PIPELINE") ? std::atoi(std::getenv("SA_RAFT_PIPELINE")) : -1;
   float* pyr_ = nullptr;
-  float* flow_ = nullptr;
+  // flow state, ping-pong: flowbuf_[flow_cur_] holds the current flow; with the stencil fused into the motion
+  // encoder (SA_RAFT_FH_FUSE) a head leaves its tap projections pending and the next motion encoder writes
+  // flow + stencil into the other buffer (its neighbours still read the old one).  forward() resets the state, so
+  // every capture / eager pass walks the same buffers.
+  float* flowbuf_[2] = {nullptr, nullptr};
+  int flow_cur_ = 0;
+  bool flow_pending_ = false;
+  float* flow_() const { return flowbuf_[flow_cur_]; }
+  // SA_RAFT_FH_FUSE=0: the tap stencil as its own launch after the flow-head conv (round 6: fused into the next
+  // motion encoder's flow-patch load, one launch and one flow round trip less per iteration)
+  bool fh_fuse_ = !(std::getenv("SA_RAFT_FH_FUSE") && std::getenv("SA_RAFT_FH_FUSE")[0] == '0');
   int lh_[3], lw_[3];
 };
 
@@ -239,7 +249,8 @@ void RaftStereo::build(WeightSource& src) {
     }
     pyr_ = (float*)a.alloc(tot * 4);
   }
-  flow_ = (float*)a.alloc((size_t)Bn * lh_[0] * lw_[0] * 4);
+  flowbuf_[0] = (float*)a.alloc((size_t)Bn * lh_[0] * lw_[0] * 4);
+  flowbuf_[1] = (float*)a.alloc((size_t)Bn * lh_[0] * lw_[0] * 4);
 
   // ---------------- update block ----------------
   const int cor_planes = rc_.levels * (2 * rc_.radius + 1);
@@ -540,7 +551,9 @@ void RaftStereo::forward(hipStream_t s) {
   for (int i = par_heads ? 2 : 0; i < rc_.n_gru; ++i) heads(s, i);
   if (par_heads) wait(s, 7);
   if (par) join(s);
-  device_zero(flow_, (size_t)Bn * h0 * w0 * 4, s);
+  flow_cur_ = 0;
+  flow_pending_ = false;
+  device_zero(flow_(), (size_t)Bn * h0 * w0 * 4, s);
   stage(s, "encoders+corr");
 
   auto pool = [&](hipStream_t st, int i) {  // pool_[i] = pool2x(net[i])
@@ -576,24 +589,36 @@ void RaftStereo::forward(hipStream_t s) {
   // 1.838 ms network, tools/ab_engine.py, profiles/round4_notes.md)
   const bool menc = fuse_motion_ && fuse_menc_ && (fuse_menc_mode_ >= 0 ? fuse_menc_mode_ != 0 : true);
   auto motion = [&](hipStream_t ms) {
+    const bool pend = flow_pending_;
+    flow_pending_ = false;
+    if (pend && !menc) {  // unfused motion encoder: the pending stencil as its own launch first
+      check(sa_tapproj_stencil(fhP_, 9, 1, fh2_b_, flow_(), Bn, h0, w0, ms), "flow-head tap stencil");
+    }
     if (menc) {
       const SaConvArgs c2 = convc2_.args({cor1_}, corflo_.slice_c(0, 64));
       const SaConvArgs f2 = convf2_.args({flo1_}, corflo_.slice_c(64, 64));
       const SaConvArgs m3 = mconv_.args({corflo_}, motion_.slice_c(0, 126));
       SA_REQUIRE(c2.Kpad == 576 && f2.Kpad == 576 && m3.Kpad == 1152 && motion_.stride >= 128,
                  "fused motion encoder layout (Kpad %d/%d/%d)", c2.Kpad, f2.Kpad, m3.Kpad);
-      check(sa_raft_motion_encoder(pyr_, flow_, Bn, h0, w0, w0, rc_.levels, rc_.radius, me_w1_, me_b1_, c2.weight,
-                                   c2.bias, f2.weight, f2.bias, m3.weight, m3.bias, motion_.ptr, motion_.stride, ms),
+      float* fin = flow_();
+      float* fout = nullptr;
+      if (pend) {  // flow(t) = flow(t-1) + the previous head's stencil, written to the other buffer by this kernel
+        flow_cur_ ^= 1;
+        fout = flow_();
+      }
+      check(sa_raft_motion_encoder_proj(pyr_, fin, Bn, h0, w0, w0, rc_.levels, rc_.radius, me_w1_, me_b1_, c2.weight,
+                                        c2.bias, f2.weight, f2.bias, m3.weight, m3.bias, motion_.ptr, motion_.stride,
+                                        pend ? fhP_ : nullptr, pend ? fh2_b_ : nullptr, fout, ms),
             "motion encoder");
       return;
     }
     if (fuse_motion_) {
-      check(sa_raft_motion_head(pyr_, flow_, Bn, h0, w0, w0, rc_.levels, rc_.radius, mh_wc_, mh_bc_, mh_wf_,
+      check(sa_raft_motion_head(pyr_, flow_(), Bn, h0, w0, w0, rc_.levels, rc_.radius, mh_wc_, mh_bc_, mh_wf_,
                                 mh_bf_, cor1_.ptr, cor1_.stride, flo1_.ptr, flo1_.stride,
                                 motion_.slice_c(126, 2).ptr, motion_.stride, ms),
             "motion head");
     } else {
-      check(sa_corr1d_lookup(pyr_, flow_, Bn, h0, w0, w0, rc_.levels, rc_.radius, corr_feat_.ptr,
+      check(sa_corr1d_lookup(pyr_, flow_(), Bn, h0, w0, w0, rc_.levels, rc_.radius, corr_feat_.ptr,
                              corr_feat_.stride, corr_feat_.c, flow_feat_.ptr, flow_feat_.stride, 8,
                              motion_.slice_c(126, 2).ptr, motion_.stride, ms),
             "corr lookup");
@@ -610,7 +635,9 @@ void RaftStereo::forward(hipStream_t s) {
     // SA_RAFT_SIDE_MASK bit 3: the flow head's conv1 tuned for co-residency as well (b1 7.960 -> 7.924 ms)
     const int side_mask = std::getenv("SA_RAFT_SIDE_MASK") ? std::atoi(std::getenv("SA_RAFT_SIDE_MASK")) : 15;
     ScopedSideBranch sb(((side_mask >> 3) & 1) && Bn <= 2 && rc_.n_gru == 3 && !rc_.slow_fast);
-    const bool fh_proj = fh_proj_env_ >= 0 ? fh_proj_env_ != 0 : (rc_.n_gru == 2 && rc_.slow_fast);
+    // default on (round 6: the projection runs on the matrix cores and the stencil rides the next motion encoder;
+    // b8 timeline 941 -> 893 us per iteration with the stencil still a launch, profiles/round6_notes.md)
+    const bool fh_proj = fh_proj_env_ >= 0 ? fh_proj_env_ != 0 : true;
     if (!last && fh_proj) {
       // conv1's output never reaches memory: its epilogue leaves conv2's x-output tap projections per 128-channel
       // n-tile ([2][9] floats per pixel instead of 256 fp16), the stencil sums their 3x3 neighbourhoods into the flow
@@ -621,12 +648,14 @@ void RaftStereo::forward(hipStream_t s) {
       pa.tapw = fh2_w16_;
       pa.taps = 9;
       fh1_.launch(st, pa);
-      check(sa_tapproj_stencil(fhP_, 9, 1, fh2_b_, flow_, Bn, h0, w0, st), "flow-head tap stencil");
+      // fused: the next motion encoder applies the stencil while it loads the flow (no launch here)
+      if (fh_fuse_) flow_pending_ = true;
+      else check(sa_tapproj_stencil(fhP_, 9, 1, fh2_b_, flow_(), Bn, h0, w0, st), "flow-head tap stencil");
       return;
     }
     if (last) fh1mask_.run(st, {net_[0]}, fh_, SA_ACT_RELU);
     else fh1_.run(st, {net_[0]}, fh_.slice_c(0, 256), SA_ACT_RELU);
-    check(sa_flow_head_tail(fh_.ptr, fh_.stride, 256, fh2_w16_, fh2_b_, flow_, Bn, h0, w0, st), "flow-head tail");
+    check(sa_flow_head_tail(fh_.ptr, fh_.stride, 256, fh2_w16_, fh2_b_, flow_(), Bn, h0, w0, st), "flow-head tail");
     if (last) mask2_.run(st, {fh_.slice_c(256, 256)}, mask_);
   };
   // finest GRU + flow head
@@ -799,7 +828,8 @@ void RaftStereo::forward(hipStream_t s) {
   }
   stage(s, "gru_iterations");
   // convex upsampling; disparity = -flow_up
-  check(sa_convex_upsample(mask_.ptr, mask_.stride, flow_, Bn, h0, w0, f, -1.f, disp_, s),
+  SA_REQUIRE(!flow_pending_, "flow-head stencil left pending after the last iteration");
+  check(sa_convex_upsample(mask_.ptr, mask_.stride, flow_(), Bn, h0, w0, f, -1.f, disp_, s),
         "convex upsample");
   (void)hd;
 }

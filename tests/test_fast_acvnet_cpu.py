@@ -51,3 +51,14 @@ def test_fp16_storage_flips_come_from_near_ties():
     print(f"mean disparity shift: fp16 logits {bias16:+.3f} px, fp32 logits {bias32:+.3f} px (ref {ref.mean():.2f})")
     assert bias16 < -2.0  # fp16 logits: ties -> lower indices -> smaller disparities
     assert abs(bias32) < 0.6
+
+
+def test_conditioning_trainer_reduces_loss():
+    """utils.condition.train_synthetic (the conditioned weights of the GPU parity test): deterministic fresh pairs,
+    loss falls, the model comes back in eval mode with frozen parameters."""
+    from stereoalgorithms_amd.utils.condition import train_synthetic
+    torch.set_num_threads(max(1, min(8, torch.get_num_threads())))
+    m = FA.build("fastacvnet-plus", seed=0)
+    losses = train_synthetic(m, steps=12, h=64, w=128, batch=1)
+    assert len(losses) == 12 and losses[-1] < losses[0]
+    assert not m.training and not any(p.requires_grad for p in m.parameters())

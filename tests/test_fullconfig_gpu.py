@@ -104,7 +104,42 @@ def test_crestereo_iter10_full_config(tmp_path, monkeypatch):
 
 
 def test_fastacvnet_end_to_end(tmp_path, monkeypatch):
-    """End-to-end Fast-ACVNet+ at 480x640 vs the oracle, asserted.
+    """Per-pixel end-to-end Fast-ACVNet+ parity at 480x640 (option b): >= 98 % of the pixels
+    within 1 px of the fp32 oracle and |mean difference| <= 0.25 px.
+
+    The weights are CONDITIONED: the seeded random init plus 300 Adam steps on synthetic pairs with known disparity
+    (utils.condition.train_synthetic, on the GPU here).  A random-init network cannot be held to this: its top-24 /
+    top-2 selections sit on near-equal logits, and even the fp32 oracle with fp16 activation storage agrees with
+    itself within 1 px on ~45-55 % of the pixels when only the accumulation order changes
+    (test_fastacvnet_random_weights_precision below keeps that study).  Trained, the same fp16-storage oracle agrees
+    on 99.98 % (utils/condition.py), so what is left to measure is the engine's arithmetic."""
+    from stereoalgorithms_amd.models import fast_acvnet as FA
+    from stereoalgorithms_amd.utils.condition import imagenet_input, train_synthetic
+    m = FA.build("fastacvnet-plus", seed=0)
+    losses = train_synthetic(m, steps=300, device="cuda")
+    print(f"conditioning: smooth-L1 {losses[0]:.3f} -> {losses[-1]:.3f}")
+    assert losses[-1] < 0.25 * losses[0]
+    eng, plan = _engine(tmp_path, monkeypatch, m.cpu(), "fastacvnet-plus", 1)
+    left, right = _pairs(1)
+    disp = eng.run(left, right).clone()
+    disp2 = eng.run(left, right)
+    torch.cuda.synchronize()
+    _plan(plan)
+    assert torch.equal(disp, disp2) and torch.isfinite(disp).all()
+    m = m.cuda()
+    with torch.no_grad():
+        ref = m(imagenet_input(left), imagenet_input(right)).reshape(disp.shape)
+    assert ref.abs().mean().item() >= 5.0, "degenerate oracle output"
+    rel, within, err = _stats(disp, ref, "fastacvnet-plus (conditioned) engine vs fp32")
+    dm = abs(disp.mean().item() - ref.mean().item())
+    print(f"mean disparity: engine {disp.mean().item():.3f} oracle-fp32 {ref.mean().item():.3f}")
+    assert within >= 0.98, within
+    assert dm <= 0.25, dm
+
+
+def test_fastacvnet_random_weights_precision(tmp_path, monkeypatch):
+    """Random-init Fast-ACVNet+ at 480x640 vs the oracle: a precision-sensitivity study, not a
+    parity test (the per-pixel one is test_fastacvnet_end_to_end, on conditioned weights).
 
     The attention top-24 and the final top-2 candidate selections are discontinuous; on a random-init
     network the candidate logits are nearly tied, so the fp32 oracle itself, re-run with fp16 convs, picks

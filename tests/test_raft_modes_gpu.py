@@ -23,12 +23,16 @@ MODES = [
     ("pipeline2-side-menc", {"SA_RAFT_PIPELINE": "2", "SA_RAFT_M2_MAIN": "0"}),
     # context trunk captured first with the early encoder fork (it must read its own preprocessed copy)
     ("cnet-first", {"SA_RAFT_CNET_FIRST": "1"}),
-    # the one-workgroup-per-CU motion encoder (v1): same MFMAs in the same k order as the default v2
-    ("motion-encoder-v1", {"SA_RAFT_MENC": "1"}),
+    # the two-workgroups-per-CU motion encoder (v2): same MFMAs in the same k order as the default v1
+    ("motion-encoder-v2", {"SA_RAFT_MENC": "2"}),
+    # the flow-head tap stencil as its own launch instead of inside the next motion encoder: same arithmetic
+    ("fh-stencil-launch", {"SA_RAFT_FH_FUSE": "0"}),
+    # conv1's 256 channels stored + the tail kernel (other summation order than the tap projections)
+    ("fh-no-projection", {"SA_RAFT_FH_PROJ": "0"}),
 ]
-TOL = {"unfused-motion-encoder": 1e-2}
+TOL = {"unfused-motion-encoder": 1e-2, "fh-no-projection": 5e-2}
 KNOBS = ("SA_RAFT_PARALLEL", "SA_RAFT_PIPELINE", "SA_RAFT_FUSE_MENC", "SA_RAFT_M2_MAIN", "SA_RAFT_CNET_FIRST",
-         "SA_RAFT_MENC")
+         "SA_RAFT_MENC", "SA_RAFT_FH_FUSE", "SA_RAFT_FH_PROJ")
 
 
 RT_MODES = [
@@ -36,7 +40,8 @@ RT_MODES = [
     ("parallel", {"SA_RAFT_PIPELINE": "0"}),
     ("pipeline", {}),
     ("cnet-second", {"SA_RAFT_CNET_FIRST": "0"}),
-    ("motion-encoder-v1", {"SA_RAFT_MENC": "1"}),
+    ("motion-encoder-v2", {"SA_RAFT_MENC": "2"}),
+    ("fh-stencil-launch", {"SA_RAFT_FH_FUSE": "0"}),
 ]
 
 
