@@ -103,6 +103,12 @@ typedef struct {
 } SaConvArgs;
 
 int sa_conv2d(const SaConvArgs* a, hipStream_t stream);
+// One ConvGRU level in one launch: the z/r conv `za` (SA_EPI_GRU_ZR or SA_EPI_GRU_ZRQ), a grid-wide barrier, the q
+// conv `qa` (SA_EPI_GRU_Q), on `grid` <= 128 co-resident workgroups (64x64 deep-ring tiles, split-K slices over the
+// workspace both args carry).  `bar`: 4 zero-initialised uints owned by this level (arrivals, generation, timeout
+// flag), reusable across launches and graph replays.  Sources must be multiples of 64 channels (3x3 or 1x1, no
+// statistics).  Returns -2 on ineligible args.
+int sa_gru_level(const SaConvArgs* za, const SaConvArgs* qa, unsigned* bar, int grid, hipStream_t stream);
 // flow [N][H][W][oc] fp32 += bias[o] + sum over the 3x3 neighbourhood (zero padding) of the two n-tile partials of
 // tap (ky*3+kx)*oc + o in P [N][H][W][2][taps] (an SA_EPI_TAPPROJ conv's output)
 int sa_tapproj_stencil(const float* P, int taps, int oc, const float* bias, float* flow, int N, int H, int W,

@@ -2442,6 +2442,119 @@ extern "C" int sa_conv2d_tile_lds(int cfg) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// One ConvGRU level in ONE launch (the coarse levels' launch / join bind at batch 1).  Phase A
+// runs the z/r(/q-x) conv with its gate epilogue (SA_EPI_GRU_ZR or _ZRQ: z, r*h, and with ZRQ the x half of q's
+// pre-activation), a grid-wide barrier, then phase B the q conv with its state-update epilogue (SA_EPI_GRU_Q, h
+// updated in place; q's 3x3 taps read r*h of neighbouring tiles, hence the barrier).  Each phase's (tile, K-slice)
+// items are dealt round-robin to the G workgroups and run by conv_tile exactly as conv_igemm_kernel's split-K
+// grid runs them (last-arriving slice sums the slabs in fixed order and runs the epilogue).
+//
+// Grid barrier: a generation counter in `bar` ([0] arrivals, [1] generation, [2] timeout flag).  Every workgroup
+// reads the generation BEFORE it arrives, so the last arriver's bump is always seen as a change; agent-scope
+// release fence before arriving and acquire fence after leaving (the split-K protocol of conv_tile, valid across
+// XCDs).  The arrivals counter returns to 0, so graph replays need no reset.  G <= 128 workgroups of <= 80 KB LDS:
+// they are co-resident on 256 CUs even beside another queue's kernels (those never wait on this one, so their CUs
+// free up); the spin still gives up after ~2^24 polls and raises bar[2] instead of hanging the GPU.
+namespace {
+__device__ __forceinline__ void gru_grid_sync(unsigned* bar, unsigned nwg) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned gen = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == nwg - 1) {
+      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_store(bar + 1, gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      unsigned spins = 0;
+      while (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 24)) {
+          __hip_atomic_store(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+template <int BM, int BN, int WM, int WN, int MODE>
+__device__ __forceinline__ void gru_level_phase(const SaConvArgs& p, char* smem, int S) {
+  using C = ConvCfg<BM, BN, WM, WN, MODE>;
+  const int M = p.N * p.Ho * p.Wo;
+  const int gy = (p.Cout + BN - 1) / BN;
+  const int T = ((M + BM - 1) / BM) * gy;
+  const int nk_all = p.Kpad / C::BK;
+  for (int it = blockIdx.x; it < T * S; it += gridDim.x) {
+    const int tile = it / S, z = it - tile * S;
+    const int kt0 = (int)((long)z * nk_all / S);
+    const int nk = (int)((long)(z + 1) * nk_all / S) - kt0;
+    conv_tile<BM, BN, WM, WN, MODE>(p, smem, tile / gy, tile % gy, kt0, nk, S, z, tile * S, tile, 0, 0);
+    __syncthreads();  // the next item's prologue reuses the LDS this item's epilogue read
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int MODE>
+__global__ __launch_bounds__(64 * WM * WN) void gru_level_kernel(const SaConvArgs za, const SaConvArgs qa,
+                                                                  unsigned* bar, int Sa, int Sb) {
+  using C = ConvCfg<BM, BN, WM, WN, MODE>;
+  __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
+  gru_level_phase<BM, BN, WM, WN, MODE>(za, smem, Sa);
+  gru_grid_sync(bar, gridDim.x);
+  gru_level_phase<BM, BN, WM, WN, MODE>(qa, smem, Sb);
+}
+
+// split of one phase: about `grid` items, K slices of at least 16 k-steps, slabs / counters within the workspace
+int gru_level_split(const SaConvArgs* a, int grid, int BM, int BN, int BK) {
+  const int M = a->N * a->Ho * a->Wo;
+  const long T = (long)((M + BM - 1) / BM) * ((a->Cout + BN - 1) / BN);
+  const int nk = a->Kpad / BK;
+  int S = (int)((grid + T - 1) / T);
+  if (S > 8) S = 8;
+  while (S > 1 && (nk / S < 16 || (long)S * T * BM * BN > a->ws_floats || T > a->n_counters)) --S;
+  return S < 1 ? 1 : S;
+}
+}  // namespace
+
+template <int MODE>
+int launch_gru_level(const SaConvArgs* za, const SaConvArgs* qa, unsigned* bar, int grid, hipStream_t stream) {
+  constexpr int BM = 64, BN = 64;
+  using C = ConvCfg<BM, BN, 2, 2, MODE>;
+  for (const SaConvArgs* a : {za, qa}) {
+    if (a->Kpad % 32 != 0 || a->nsrc < 1 || a->nsrc > 4 || !glds3_eligible(a) || a->stats || a->up || a->gate ||
+        a->KD > 0 || !a->ws || !a->counters)
+      return -2;
+  }
+  if (!(za->epi == SA_EPI_GRU_ZR || za->epi == SA_EPI_GRU_ZRQ) || qa->epi != SA_EPI_GRU_Q) return -2;
+  const int Sa = gru_level_split(za, grid, BM, BN, C::BK), Sb = gru_level_split(qa, grid, BM, BN, C::BK);
+  // workspace high-water mark of the two phases (sa_conv2d_last_split: the engine right-sizes its workspaces)
+  auto tiles = [&](const SaConvArgs* a) { return (long)((a->N * a->Ho * a->Wo + BM - 1) / BM) * ((a->Cout + BN - 1) / BN); };
+  const long fa = Sa > 1 ? Sa * tiles(za) : 0, fb = Sb > 1 ? Sb * tiles(qa) : 0;
+  g_split_floats = (fa > fb ? fa : fb) * BM * BN;
+  g_split_tiles = (Sa > 1 || Sb > 1) ? (tiles(za) > tiles(qa) ? tiles(za) : tiles(qa)) : 0;
+  hipLaunchKernelGGL((gru_level_kernel<BM, BN, 2, 2, MODE>), dim3((unsigned)grid), dim3(C::NT), 0, stream, *za, *qa,
+                     bar, Sa, Sb);
+  return (int)hipGetLastError();
+}
+
+// tiles: 64x64 over 4 waves, register-staged (kFastK64, 32 KB of LDS: co-resides with the other queue's kernels) by
+// default, or the 8-deep DMA ring (kGldsDeep, 128 KB) with SA_GRU_LEVEL_CFG=6
+extern "C" int sa_gru_level(const SaConvArgs* za, const SaConvArgs* qa, unsigned* bar, int grid, hipStream_t stream) {
+  if (!za || !qa || !bar || grid < 1 || grid > 128) return -2;
+  static const int cfg = [] {
+    const char* e = std::getenv("SA_GRU_LEVEL_CFG");
+    return e ? std::atoi(e) : 3;
+  }();
+  return cfg == 6 ? launch_gru_level<kGldsDeep>(za, qa, bar, grid, stream)
+                  : launch_gru_level<kFastK64>(za, qa, bar, grid, stream);
+}
+
 extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
   if (a->Kpad % 32 != 0 || a->Cin % 8 != 0 || a->nsrc < 1 || a->nsrc > 4) return -2;
   const int cfg = pick_cfg(a);

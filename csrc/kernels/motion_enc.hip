@@ -75,27 +75,52 @@ struct MotionEncArgs {
   float* flow_out;
 };
 
-// stage 0 of both variants: the fp32 flow patch (image rows ty0-5 .., cols tx0-5 ..), zero outside, with the
-// previous flow head's stencil applied when p.proj is set
-__device__ __forceinline__ float menc_flow_at(const MotionEncArgs& p, long img_base, int y, int x, int ty0, int tx0) {
-  if ((unsigned)y >= (unsigned)p.H || (unsigned)x >= (unsigned)p.W) return 0.f;
-  const long px = img_base + (long)y * p.W + x;
-  float v = p.flow[px];
+// stage 0 of both variants: the fp32 flow patch (image rows ty0-5 .., cols tx0-5 ..), zero outside.  With p.proj
+// the previous flow head's stencil is applied on the way: the projections of the 20 x 28 pixels the patch's 3x3
+// stencils touch are first copied into LDS scratch `pl` (8-B loads, each image row's 28 x 18 floats contiguous; 40 KB
+// of an area the later stages have not written yet), then each patch pixel sums its nine taps there, in
+// sa_tapproj_stencil's order (bitwise the same flow)
+constexpr int PLH = FH + 2, PLW = FW + 2;  // 20 x 28 projection pixels
+constexpr int PL_BYTES = PLH * PLW * 18 * 4;  // 40320
+__device__ __forceinline__ void menc_flow_patch(const MotionEncArgs& p, long img_base, int ty0, int tx0, float* fl,
+                                                float* pl, int tid, int nt) {
   if (p.proj) {
-    float s = p.proj_bias ? p.proj_bias[0] : 0.f;
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int yy = y + ky - 1, xx = x + kx - 1;
-        if (yy < 0 || yy >= p.H || xx < 0 || xx >= p.W) continue;
-        const float* q = p.proj + (img_base + (long)yy * p.W + xx) * 18 + (ky * 3 + kx);
-        s += q[0] + q[9];
-      }
-    v += s;
-    if (y >= ty0 && y < ty0 + 8 && x >= tx0 && x < tx0 + 16) p.flow_out[px] = v;
+    // row r of the scratch = image row ty0 - 6 + r, columns tx0 - 6 .. tx0 + 21 (9 float2 per pixel)
+    for (int i = tid; i < PLH * PLW * 9; i += nt) {
+      const int r = i / (PLW * 9), rem = i - r * (PLW * 9);
+      const int c = rem / 9, k = rem - c * 9;
+      const int y = ty0 - 6 + r, x = tx0 - 6 + c;
+      float2 v = make_float2(0.f, 0.f);
+      if ((unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W)
+        v = reinterpret_cast<const float2*>(p.proj + (img_base + (long)y * p.W + x) * 18)[k];
+      reinterpret_cast<float2*>(pl)[i] = v;
+    }
+    __syncthreads();
   }
-  return v;
+  for (int i = tid; i < FH * FW; i += nt) {
+    const int r = i / FW, c = i - r * FW;
+    const int y = ty0 - 5 + r, x = tx0 - 5 + c;
+    float v = 0.f;
+    if ((unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W) {
+      const long px = img_base + (long)y * p.W + x;
+      v = p.flow[px];
+      if (p.proj) {
+        float s = p.proj_bias ? p.proj_bias[0] : 0.f;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            const int yy = y + ky - 1, xx = x + kx - 1;
+            if (yy < 0 || yy >= p.H || xx < 0 || xx >= p.W) continue;
+            const float* q = pl + ((r + ky) * PLW + (c + kx)) * 18 + (ky * 3 + kx);
+            s += q[0] + q[9];
+          }
+        v += s;
+        if (y >= ty0 && y < ty0 + 8 && x >= tx0 && x < tx0 + 16) p.flow_out[px] = v;
+      }
+    }
+    fl[i] = v;
+  }
 }
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -180,7 +205,8 @@ __global__ __launch_bounds__(64 * NW) void raft_motion_encoder_kernel(const Moti
   stamp(0);
 
   // ---------------- stage 0: flow patch (image rows ty0-5 .., cols tx0-5 ..), zero outside ----------------
-  for (int i = tid; i < FH * FW; i += NT) fl[i] = menc_flow_at(p, img_base, ty0 - 5 + i / FW, tx0 - 5 + i % FW, ty0, tx0);
+  static_assert(PL_BYTES <= P2 * 256, "projection scratch fits the S2 area");
+  menc_flow_patch(p, img_base, ty0, tx0, fl, reinterpret_cast<float*>(s2), tid, NT);
   __syncthreads();
 
   stamp(1);
@@ -601,7 +627,8 @@ __global__ __launch_bounds__(256, 2) void raft_motion_encoder_v2_kernel(const Mo
   stamp(0);
 
   // ---------------- stage 0: flow patch ----------------
-  for (int i = tid; i < FH * FW; i += NT) fl[i] = menc_flow_at(p, img_base, ty0 - 5 + i / FW, tx0 - 5 + i % FW, ty0, tx0);
+  static_assert(PL_BYTES <= R_BYTES, "projection scratch fits R");
+  menc_flow_patch(p, img_base, ty0, tx0, fl, reinterpret_cast<float*>(R), tid, NT);
   __syncthreads();
   stamp(1);
 

@@ -128,6 +128,10 @@ class RaftStereo : public StereoEngine {
   // the LDS-staged C tile of the banded tiles and is on by default (SA_RAFT_FH_PROJ=0 turns it off)
   int fh_proj_env_ = std::getenv("SA_RAFT_FH_PROJ") ? std::atoi(std::getenv("SA_RAFT_FH_PROJ")) : -1;
   float* fhP_ = nullptr;  // [B][h0][w0][2 n-tiles][9] fp32
+  // SA_RAFT_FUSED_LEVEL (bit i = GRU level i): the level's z/r(+q-x) conv, a grid barrier and its q conv in ONE
+  // launch (sa_gru_level) at batch <= 2 with the GRU split; lvl_bar_ holds each level's barrier words
+  int fused_level_mask_ = std::getenv("SA_RAFT_FUSED_LEVEL") ? std::atoi(std::getenv("SA_RAFT_FUSED_LEVEL")) : 0;
+  unsigned* lvl_bar_ = nullptr;
   // fused lookup + convc1 + convf1 (sa_raft_motion_head): fp32 [k][64] weights and biases
   float *mh_wc_ = nullptr, *mh_bc_ = nullptr, *mh_wf_ = nullptr, *mh_bf_ = nullptr;
   void* me_w1_ = nullptr;  // fused motion encoder stage-1 weights (fp16 [128][96]) and bias [128]
@@ -251,6 +255,8 @@ void RaftStereo::build(WeightSource& src) {
   }
   flowbuf_[0] = (float*)a.alloc((size_t)Bn * lh_[0] * lw_[0] * 4);
   flowbuf_[1] = (float*)a.alloc((size_t)Bn * lh_[0] * lw_[0] * 4);
+  lvl_bar_ = (unsigned*)a.alloc(3 * 4 * sizeof(unsigned));
+  HIP_CHECK(hipMemset(lvl_bar_, 0, 3 * 4 * sizeof(unsigned)));
 
   // ---------------- update block ----------------
   const int cor_planes = rc_.levels * (2 * rc_.radius + 1);
@@ -405,7 +411,6 @@ void RaftStereo::gru(hipStream_t s, int i, const std::vector<Tensor>& x) const {
     za.h_stride = net_[i].stride;
     za.rh = rh_[i].ptr;
     za.rh_stride = rh_[i].stride;
-    gzrq_[i].launch(s, za);
     SaConvArgs qa = gqh_[i].args({rh_[i]}, net_[i]);
     qa.epi = SA_EPI_GRU_Q;
     qa.ctx = nullptr;  // cq and convq's bias are in qx
@@ -415,6 +420,23 @@ void RaftStereo::gru(hipStream_t s, int i, const std::vector<Tensor>& x) const {
     qa.aux_stride = z_[i].stride;
     qa.hbuf = net_[i].ptr;
     qa.h_stride = net_[i].stride;
+    if (((fused_level_mask_ >> i) & 1) && B() <= 2 && za.ws && qa.ws) {
+      // one launch: z/r/q-x conv, grid barrier, q conv (sa_gru_level); untuned fixed tiles, so nothing is planned
+      static const int grid = std::getenv("SA_GRU_LEVEL_GRID") ? std::atoi(std::getenv("SA_GRU_LEVEL_GRID")) : 64;
+      const int rc = sa_gru_level(&za, &qa, lvl_bar_ + 4 * i, grid, s);
+      if (rc == 0) {
+        SA_LAUNCH_CHECK(s);
+        if (const SplitKWorkspace* sk = current_splitk()) {
+          long fl = 0, tiles = 0;
+          sa_conv2d_last_split(&fl, &tiles);
+          sk->max_floats = std::max<int64_t>(sk->max_floats, fl);
+          sk->max_counters = std::max<int32_t>(sk->max_counters, (int32_t)tiles);
+        }
+        return;
+      }
+      SA_LOGW("fused GRU level %d not eligible (rc %d): two launches", i, rc);
+    }
+    gzrq_[i].launch(s, za);
     gqh_[i].launch(s, qa);
     return;
   }

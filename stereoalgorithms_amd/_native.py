@@ -139,6 +139,7 @@ _f = C.c_float
 def _declare_dev(lib):
     sig = {
         "sa_conv2d": (_i, [C.POINTER(SaConvArgs), _p]),
+        "sa_gru_level": (_i, [C.POINTER(SaConvArgs), C.POINTER(SaConvArgs), _p, _i, _p]),
         "sa_flow_head_tail": (_i, [_p, _i, _i, _p, _p, _p, _i, _i, _i, _p]),
         "sa_flow_head_tail_oc": (_i, [_p, _i, _i, _p, _i, _p, _p, _i, _i, _i, _p]),
         "sa_instnorm_apply": (_i, [C.POINTER(SaNormArgs), _p]),

@@ -143,7 +143,7 @@ def pack_conv_weight(w: torch.Tensor, segs: Sequence[tuple[int, int]] | None = N
 def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1, act="none",
            act2="none", res=None, out=None, epi="store", scale=1.0, alpha=0.01, stats=None,
            ctx=None, aux=None, hbuf=None, rh=None, tile_cfg=-1, splitk=1, workspace=None, up=0, cout_real=0,
-           gate=None, stats_slots=1, cin_real=0, tapw=None, taps=0):
+           gate=None, stats_slots=1, cin_real=0, tapw=None, taps=0, launch=True):
     """NHWC fp16 implicit-GEMM conv.  ``splitk``: 1 = off, 0 = auto, >1 = forced; needs
     ``workspace`` = (fp32 slab tensor, int32 counter tensor zero-initialised).  ``up`` = 2: transposed
     conv, the 4 parity classes (cout = 4 * cout_real) are scattered to a 2x output.  ``gate``: fp16
@@ -213,8 +213,18 @@ def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1
         ws, cnt = workspace
         assert ws.dtype == torch.float32 and cnt.dtype == torch.int32
         a.ws, a.counters, a.ws_floats, a.n_counters = ws.data_ptr(), cnt.data_ptr(), ws.numel(), cnt.numel()
+    if not launch:  # the filled SaConvArgs (e.g. for gru_level), nothing enqueued
+        return a
     N.check(N.dev().sa_conv2d(C.byref(a), _stream()), "sa_conv2d")
     return out
+
+
+def gru_level(za, qa, bar, grid=128):
+    """One ConvGRU level in one launch (sa_gru_level): ``za`` / ``qa`` are conv2d(..., launch=False) args of the
+    z/r(/q-x) conv (epi gru_zr / gru_zrq) and the q conv (epi gru_q), both with a split-K workspace; ``bar`` an int32
+    tensor of 4 zeros owned by this level (grid barrier words, [2] = timeout flag)."""
+    assert bar.dtype == torch.int32 and bar.numel() >= 4 and bar.is_cuda
+    N.check(N.dev().sa_gru_level(C.byref(za), C.byref(qa), bar.data_ptr(), int(grid), _stream()), "sa_gru_level")
 
 
 def tapproj_stencil(P, taps, oc, bias, flow):

@@ -573,6 +573,52 @@ def test_conv2d_gru_zrq_split(cfg, splitk):
     assert rel_err(nchw(net_h), ref) < 4e-3
 
 
+@pytest.mark.parametrize("n,h,w,xs,grid", [(1, 30, 40, (256,), 128), (2, 60, 80, (128, 128), 64),
+                                           (1, 13, 21, (128,), 7)])
+def test_gru_level_one_launch(n, h, w, xs, grid):
+    """sa_gru_level: the ZRQ conv, a grid-wide barrier and the q conv in ONE launch on `grid`
+    workgroups (split-K slices dealt round-robin) == the fp32 ConvGRU; replays reuse the barrier words (generation
+    counter) and give identical bits; the timeout flag stays clear."""
+    O = ops()
+    torch.manual_seed(6)
+    hd = 128
+    net = torch.randn(n, hd, h, w, device=DEV).tanh()
+    x = torch.randn(n, sum(xs), h, w, device=DEV)
+    cz, cr, cq = (torch.randn(n, hd, h, w, device=DEV) * 0.5 for _ in range(3))
+    cin = hd + sum(xs)
+    wz, wr, wq = (torch.randn(hd, cin, 3, 3, device=DEV) / math.sqrt(cin * 9) for _ in range(3))
+    bz, br, bq = (torch.randn(hd, device=DEV) * 0.1 for _ in range(3))
+    hx = torch.cat([net, x], 1).half().float()
+    z = torch.sigmoid(F.conv2d(hx, wz.half().float(), bz, padding=1) + cz.half().float())
+    r = torch.sigmoid(F.conv2d(hx, wr.half().float(), br, padding=1) + cr.half().float())
+    rh = (r * net.half().float()).half().float()
+    q = torch.tanh(F.conv2d(torch.cat([rh, x.half().float()], 1), wq.half().float(), bq, padding=1) + cq.half().float())
+    ref = (1 - z) * net.half().float() + z * q
+    ctx = nhwc(torch.cat([cz, cr, cq], 1)).half()
+    xh = [nhwc(t).half() for t in torch.split(x, list(xs), 1)]
+    wqx = wq.clone()
+    wqx[:, :hd] = 0
+    wzrq, kpad, _ = O.pack_conv_weight(torch.cat([wz, wr, wqx], 0))
+    wqh, kph, _ = O.pack_conv_weight(wq[:, :hd].contiguous())
+    bar = torch.zeros(4, dtype=torch.int32, device=DEV)
+    ws = O.splitk_workspace(1 << 22, 4096)
+    outs = []
+    for _ in range(3):
+        net_h = nhwc(net).half()
+        zb = torch.empty(n, h, w, hd, device=DEV, dtype=torch.float16)
+        rhb, qx = torch.empty_like(zb), torch.empty_like(zb)
+        za = O.conv2d([net_h, *xh], wzrq, kpad, 3 * hd, 3, 3, bias=torch.cat([bz, br, bq]).contiguous(), out=qx,
+                      epi="gru_zrq", ctx=ctx, aux=zb, hbuf=net_h, rh=rhb, splitk=0, workspace=ws, launch=False)
+        qa = O.conv2d([rhb], wqh, kph, hd, 3, 3, out=net_h, epi="gru_q", res=qx, aux=zb, hbuf=net_h, splitk=0,
+                      workspace=ws, launch=False)
+        O.gru_level(za, qa, bar, grid)
+        torch.cuda.synchronize()
+        outs.append(net_h.clone())
+    assert rel_err(nchw(outs[0]), ref) < 4e-3
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert bar[0].item() == 0 and bar[1].item() == 3 and bar[2].item() == 0
+
+
 @pytest.mark.parametrize("cfg", [26, 27, 28, 29, 30, 31, 32, 33])
 @pytest.mark.parametrize("srcs,cout,hw,n", [
     ((128, 256), 256, (120, 160), 1),   # RAFT 1/4 z/r (two sources, 2 n-tiles), patches tile the image exactly
