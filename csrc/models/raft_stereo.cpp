@@ -129,7 +129,10 @@ class RaftStereo : public StereoEngine {
   int fh_proj_env_ = std::getenv("SA_RAFT_FH_PROJ") ? std::atoi(std::getenv("SA_RAFT_FH_PROJ")) : -1;
   float* fhP_ = nullptr;  // [B][h0][w0][2 n-tiles][9] fp32
   // SA_RAFT_FUSED_LEVEL (bit i = GRU level i): the level's z/r(+q-x) conv, a grid barrier and its q conv in ONE
-  // launch (sa_gru_level) at batch <= 2 with the GRU split; lvl_bar_ holds each level's barrier words
+  // launch (sa_gru_level) at batch <= 2 with the GRU split; lvl_bar_ holds each level's barrier words.  Measured at
+  // batch 1 (same-process A/B, profiles/round6_notes.md): coarsest level fused 8.49 -> 9.27 ms (128 workgroups of
+  // 128-KB deep-ring tiles), 8.55 -> 10.18 / 8.65 -> 10.38 ms (64 / 128 workgroups of 32-KB register-staged tiles),
+  // both coarse levels 11.54 ms: off by default (0)
   int fused_level_mask_ = std::getenv("SA_RAFT_FUSED_LEVEL") ? std::atoi(std::getenv("SA_RAFT_FUSED_LEVEL")) : 0;
   unsigned* lvl_bar_ = nullptr;
   // fused lookup + convc1 + convf1 (sa_raft_motion_head): fp32 [k][64] weights and biases
@@ -163,9 +166,11 @@ class RaftStereo : public StereoEngine {
   int flow_cur_ = 0;
   bool flow_pending_ = false;
   float* flow_() const { return flowbuf_[flow_cur_]; }
-  // SA_RAFT_FH_FUSE=0: the tap stencil as its own launch after the flow-head conv (round 6: fused into the next
-  // motion encoder's flow-patch load, one launch and one flow round trip less per iteration)
-  bool fh_fuse_ = !(std::getenv("SA_RAFT_FH_FUSE") && std::getenv("SA_RAFT_FH_FUSE")[0] == '0');
+  // SA_RAFT_FH_FUSE=1: the tap stencil applied inside the next motion encoder's flow-patch load instead of as its
+  // own launch after the flow-head conv (one launch and one flow round trip less per iteration).  Measured slower at
+  // batch 8 (bench-shaped A/B 39.92 -> 40.13 ms scattered loads, 40.79 -> 41.83 ms LDS-staged): the motion encoder's
+  // one-workgroup-per-CU prologue is on the chain and the separate stencil overlaps the coarse levels.  Off by default.
+  bool fh_fuse_ = std::getenv("SA_RAFT_FH_FUSE") && std::getenv("SA_RAFT_FH_FUSE")[0] == '1';
   int lh_[3], lw_[3];
 };
 
@@ -657,9 +662,10 @@ void RaftStereo::forward(hipStream_t s) {
     // SA_RAFT_SIDE_MASK bit 3: the flow head's conv1 tuned for co-residency as well (b1 7.960 -> 7.924 ms)
     const int side_mask = std::getenv("SA_RAFT_SIDE_MASK") ? std::atoi(std::getenv("SA_RAFT_SIDE_MASK")) : 15;
     ScopedSideBranch sb(((side_mask >> 3) & 1) && Bn <= 2 && rc_.n_gru == 3 && !rc_.slow_fast);
-    // default on (round 6: the projection runs on the matrix cores and the stencil rides the next motion encoder;
-    // b8 timeline 941 -> 893 us per iteration with the stencil still a launch, profiles/round6_notes.md)
-    const bool fh_proj = fh_proj_env_ >= 0 ? fh_proj_env_ != 0 : true;
+    // default: the realtime preset (flow head beside the chain) and batch > 2 (round 6: the projection runs on the
+    // matrix cores; b8 timeline 941 -> 893 us per iteration, bench-shaped A/B 41.65 -> 41.37 ms); sceneflow at batch 1
+    // measured 8.419 (off) vs 8.473 ms (on), so off there (profiles/round6_notes.md)
+    const bool fh_proj = fh_proj_env_ >= 0 ? fh_proj_env_ != 0 : ((rc_.n_gru == 2 && rc_.slow_fast) || Bn > 2);
     if (!last && fh_proj) {
       // conv1's output never reaches memory: its epilogue leaves conv2's x-output tap projections per 128-channel
       // n-tile ([2][9] floats per pixel instead of 256 fp16), the stencil sums their 3x3 neighbourhoods into the flow

@@ -25,14 +25,17 @@ MODES = [
     ("cnet-first", {"SA_RAFT_CNET_FIRST": "1"}),
     # the two-workgroups-per-CU motion encoder (v2): same MFMAs in the same k order as the default v1
     ("motion-encoder-v2", {"SA_RAFT_MENC": "2"}),
-    # the flow-head tap stencil as its own launch instead of inside the next motion encoder: same arithmetic
-    ("fh-stencil-launch", {"SA_RAFT_FH_FUSE": "0"}),
-    # conv1's 256 channels stored + the tail kernel (other summation order than the tap projections)
-    ("fh-no-projection", {"SA_RAFT_FH_PROJ": "0"}),
+    # conv1's tap projections + their stencil as its own launch (the default at batch > 2) and inside the next
+    # motion encoder: same arithmetic as each other, other summation order than conv1 stored + the tail kernel
+    ("fh-projection", {"SA_RAFT_FH_PROJ": "1"}),
+    ("fh-projection-fused-stencil", {"SA_RAFT_FH_PROJ": "1", "SA_RAFT_FH_FUSE": "1"}),
+    # the fused coarse GRU level (z/r + grid barrier + q in one launch): other tiles, other summation order
+    ("fused-gru-level", {"SA_RAFT_FUSED_LEVEL": "4"}),
 ]
-TOL = {"unfused-motion-encoder": 1e-2, "fh-no-projection": 5e-2}
+TOL = {"unfused-motion-encoder": 1e-2, "fh-projection": 5e-2, "fh-projection-fused-stencil": 5e-2,
+       "fused-gru-level": 5e-2}
 KNOBS = ("SA_RAFT_PARALLEL", "SA_RAFT_PIPELINE", "SA_RAFT_FUSE_MENC", "SA_RAFT_M2_MAIN", "SA_RAFT_CNET_FIRST",
-         "SA_RAFT_MENC", "SA_RAFT_FH_FUSE", "SA_RAFT_FH_PROJ")
+         "SA_RAFT_MENC", "SA_RAFT_FH_FUSE", "SA_RAFT_FH_PROJ", "SA_RAFT_FUSED_LEVEL")
 
 
 RT_MODES = [
@@ -41,7 +44,7 @@ RT_MODES = [
     ("pipeline", {}),
     ("cnet-second", {"SA_RAFT_CNET_FIRST": "0"}),
     ("motion-encoder-v2", {"SA_RAFT_MENC": "2"}),
-    ("fh-stencil-launch", {"SA_RAFT_FH_FUSE": "0"}),
+    ("fh-fused-stencil", {"SA_RAFT_FH_FUSE": "1"}),
 ]
 
 
