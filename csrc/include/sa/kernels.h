@@ -103,6 +103,11 @@ typedef struct {
 } SaConvArgs;
 
 int sa_conv2d(const SaConvArgs* a, hipStream_t stream);
+// direct 3x3x3 / stride 1 / pad 1 conv over NDHWC fp16 volumes with Cin in {8, 16, 32}, Cout <= 32 (tile_cfg 34):
+// y = act(acc * scale + bias) [* gate[n][h][w][c]] -> fp16
+int sa_conv3d_small(const void* x, int xs, int Cin, const void* w, int Kpad, const float* bias, void* out, int os,
+                    int N, int D, int H, int W, int Cout, int act, float alpha, float scale, const void* gate, int gs,
+                    hipStream_t stream);
 // One ConvGRU level in one launch: the z/r conv `za` (SA_EPI_GRU_ZR or SA_EPI_GRU_ZRQ), a grid-wide barrier, the q
 // conv `qa` (SA_EPI_GRU_Q), on `grid` <= 128 co-resident workgroups (64x64 deep-ring tiles, split-K slices over the
 // workspace both args carry).  `bar`: 4 zero-initialised uints owned by this level (arrivals, generation, timeout

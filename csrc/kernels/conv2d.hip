@@ -2602,6 +2602,21 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
                                    a->out_stride, a->N, a->H, a->W, a->act, a->alpha, a->stats, a->stats_slots,
                                    a->res, a->res_stride, a->act2, stream);
     }
+    case 34: {
+      // direct 3x3x3 conv for small channel counts (conv3d_small.hip): one 8 / 16 / 32-channel source, <= 32 outputs,
+      // stride 1, pad 1, store epilogue with optional gate
+      const int sd = a->sd > 0 ? a->sd : 1;
+      const bool ok = a->KD == 3 && a->KH == 3 && a->KW == 3 && sd == 1 && a->sh == 1 && a->sw == 1 && a->pd == 1 &&
+                      a->ph == 1 && a->pw == 1 && a->dh == 1 && a->dw == 1 && a->nsrc == 1 &&
+                      a->src[0].channels == a->Cin && (a->Cin == 8 || a->Cin == 16 || a->Cin == 32) &&
+                      a->Cout <= 32 && a->up == 0 && !a->res && !a->stats && a->epi == SA_EPI_STORE &&
+                      a->Do == a->Di && a->Ho == a->H && a->Wo == a->W;
+      if (!ok) return -5;
+      note_split(1, 0, 0);
+      return sa_conv3d_small(a->src[0].ptr, a->src[0].stride, a->Cin, a->weight, a->Kpad, a->bias, a->out,
+                             a->out_stride, a->N, a->Di, a->H, a->W, a->Cout, a->act, a->alpha, a->scale, a->gate,
+                             a->gate_stride, stream);
+    }
     case 25: {
       // strided 1x1 conv (conv_point.hip): 64 -> 96 / 96 -> 128, weights in registers, no LDS
       const bool ok = a->nsrc == 1 && a->src[0].channels == a->Cin && a->KH == 1 && a->KW == 1 && a->ph == 0 &&

@@ -758,6 +758,7 @@ constexpr Tactic kTactics[] = {
     {29, true, false, 0, 0, 0, 0, "3x3 halo patch 16x16, planar image"},
     {32, true, false, 0, 0, 512, 128, "3x3 halo patch 16x32, 32-channel chunks, ping-pong wave groups"},
     {33, true, false, 0, 0, 384, 128, "3x3 halo patch 12x32, 32-channel chunks, ping-pong wave groups"},
+    {34, false, false, 0, 0, 0, 0, "direct 3x3x3, 8-32 channels, 2x4x32 voxel blocks"},
 };
 
 bool known_tactic(int cfg) {
@@ -767,6 +768,16 @@ bool known_tactic(int cfg) {
 }
 
 bool tactic_applies(const Tactic& t, const SaConvArgs& a, long M) {
+  // SA_TUNE_SKIP: comma-separated tactic ids never timed (read per shape: an in-process A/B knob, e.g. "34")
+  if (const char* sk = std::getenv("SA_TUNE_SKIP")) {
+    for (const char* q = sk; *q;) {
+      char* end = nullptr;
+      const long v = std::strtol(q, &end, 10);
+      if (end == q) break;
+      if (v == t.cfg) return false;
+      q = *end ? end + 1 : end;
+    }
+  }
   // SA_TUNE_MIN_TILES: the grid size below which the wide tiles are not timed (default 256 = one per CU)
   const char* mt = std::getenv("SA_TUNE_MIN_TILES");  // read per shape (tuning is rare): in-process A/B knob
   const long min_tiles = mt ? std::atol(mt) : 256L;

@@ -542,7 +542,7 @@ def deconv_as_conv_weight(wt: torch.Tensor) -> torch.Tensor:
 
 
 def conv3d(x, wpacked, kpad, cout, k=3, stride=1, pad=None, bias=None, act="none", alpha=0.01, gate=None,
-           up=0, cout_real=0, out=None):
+           up=0, cout_real=0, out=None, tile_cfg=-1):
     """NDHWC fp16 volume [N, D, H, W, C] conv (implicit GEMM over (kd, kh, kw, ci)).  ``gate``: fp16
     [N, H, W, >=cout] multiplied after the activation (broadcast over depth).  ``up`` = 3 scatters the
     8 parity classes of a transposed conv (cout = 8 * cout_real)."""
@@ -568,7 +568,7 @@ def conv3d(x, wpacked, kpad, cout, k=3, stride=1, pad=None, bias=None, act="none
     a.Cout, a.Kpad = cout, kpad
     a.out, a.out_stride = out.data_ptr(), out.shape[-1]
     a.epi, a.act, a.alpha, a.scale = N.EPI["store"], N.ACT[act], alpha, 1.0
-    a.tile_cfg, a.splitk = -1, 1
+    a.tile_cfg, a.splitk = tile_cfg, 1
     a.up, a.cout_real = up, cout_real
     if gate is not None:
         a.gate, a.gate_stride = gate.data_ptr(), _pix_stride(gate)

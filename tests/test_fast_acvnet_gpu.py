@@ -58,6 +58,32 @@ def test_conv3d_gated(cin, cout, stride):
     assert rel_err(out.permute(0, 4, 1, 2, 3), ref) < 3e-3
 
 
+@pytest.mark.parametrize("cin_real,cin,cout", [(1, 8, 8), (16, 16, 16), (16, 16, 32), (32, 32, 16), (32, 32, 32),
+                                              (8, 8, 16)])
+@pytest.mark.parametrize("gated", [False, True])
+def test_conv3d_small_direct(cin_real, cin, cout, gated):
+    """Tactic 34 (conv3d_small.hip): the direct 3x3x3 conv for 8-32 channels (Fast-ACVNet+'s
+    correlation stem has 1 real input channel in an 8-channel volume) == F.conv3d + bias + leaky ReLU (+ the
+    depth-broadcast gate), on volumes whose D / H / W overhang the 2 x 4 x 32 voxel blocks."""
+    O = ops()
+    torch.manual_seed(3)
+    n, d, h, w = 2, 7, 10, 37
+    x = torch.randn(n, cin_real, d, h, w, device=DEV).half().float()
+    wt = torch.randn(cout, cin_real, 3, 3, 3, device=DEV) / (cin_real * 27) ** 0.5
+    b = torch.randn(cout, device=DEV) * 0.1
+    ref = F.leaky_relu(F.conv3d(x, wt, b, 1, 1), 0.01)
+    gate = torch.rand(n, cout, h, w, device=DEV).half().float() if gated else None
+    if gated:
+        ref = ref * gate.unsqueeze(2)
+    xv = torch.zeros(n, d, h, w, cin, device=DEV, dtype=torch.float16)
+    xv[..., :cin_real] = ndhwc(x).half()
+    wp, kpad, _ = O.pack_conv3d_weight(wt, cin_pad=cin)
+    out = O.conv3d(xv, wp, kpad, cout, 3, 1, bias=b.float(), act="leaky", tile_cfg=34,
+                   gate=nhwc(gate).half() if gated else None)
+    torch.cuda.synchronize()
+    assert rel_err(out.permute(0, 4, 1, 2, 3), ref) < 3e-3
+
+
 @pytest.mark.parametrize("is3d", [False, True])
 def test_transposed_conv_parity_scatter(is3d):
     O = ops()

@@ -14,7 +14,7 @@ if [ -n "$TESTS" ]; then
 fi
 if [ -n "$KNOB" ]; then
   timeout -k 10 400 python3 -u tools/ab_engine.py --knob $KNOB --values ${VALUES:-0,1} --model ${MODEL:-raftstereo-sceneflow} \
-      --batch ${BATCH:-1} --rounds ${ROUNDS:-6} > gpurun_out/$T/ab.log 2>&1 || { echo "ab rc=$?"; tail -5 gpurun_out/$T/ab.log; exit 1; }
+      --batch ${BATCH:-1} --rounds ${ROUNDS:-6} ${CLEAR:+--clear-plan} > gpurun_out/$T/ab.log 2>&1 || { echo "ab rc=$?"; tail -5 gpurun_out/$T/ab.log; exit 1; }
   tail -${TAILN:-4} gpurun_out/$T/ab.log
 fi
 exit ${prc:-0}
