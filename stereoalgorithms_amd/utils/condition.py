@@ -4,10 +4,11 @@ A random-init Fast-ACVNet+ is numerically chaotic: its top-24 / top-2 selections
 fp32 oracle re-run with fp16 activation storage -- or merely with fp64 instead of fp32 accumulation under the same
 fp16 storage -- agrees with itself within 1 px on only ~45-55 % of the pixels (measured at 240x320; no per-pixel
 parity test of ANY fp16 engine can pass against it).  A few hundred Adam steps on pairs with known disparity
-(``utils.synthetic.stereo_pair``) give the cost volumes real margins: after 300 steps at 128x256 the same fp16-storage
-oracle agrees with the fp32 oracle on 99.98 % of the pixels (mean |diff| 0.005 px), and the prediction tracks the
-ground truth (mean |err| ~2 px at 240x320).  The network keeps its architecture, and its activations stay inside the
-fp16 range (a learning rate of 2e-3 overflowed them; 1e-3 does not).
+(``utils.synthetic.stereo_pair``) give the cost volumes real margins: after 300 steps (128x256, lr 1e-3, or the default
+96x192, lr 5e-4) the same fp16-storage oracle agrees with the fp32 oracle on 99.94-99.98 % of the pixels (mean |diff|
+0.004-0.005 px), and the prediction tracks the ground truth (mean |err| 2-3.3 px at 240x320).  The network keeps its
+architecture; its activations must stay inside the fp16 range (lr 2e-3 overflowed them), which
+``fp16_storage_agreement`` checks before any engine is compared against the oracle.
 
 The reference ships no checkpoint (/root/reference/README_en.md:267-272 points to a download), so trained upstream
 weights stay unpinned; this is the stand-in for "a trained network" that per-pixel parity needs.
@@ -34,8 +35,8 @@ def imagenet_input(bgr_u8: np.ndarray | torch.Tensor, device=None) -> torch.Tens
     return (x - mean) / std
 
 
-def train_synthetic(model: torch.nn.Module, steps: int = 300, h: int = 128, w: int = 256, batch: int = 2,
-                    lr: float = 1e-3, seed: int = 1000, device="cpu", log_every: int = 0) -> list[float]:
+def train_synthetic(model: torch.nn.Module, steps: int = 300, h: int = 96, w: int = 192, batch: int = 2,
+                    lr: float = 5e-4, seed: int = 1000, device="cpu", log_every: int = 0) -> list[float]:
     """Adam on smooth-L1(prediction, ground-truth disparity) over fresh synthetic pairs (pair i of step s is
     ``stereo_pair(h, w, seed=seed + s * batch + i)``).  The model must map ImageNet-normalised RGB pairs to positive
     disparity [B,H,W] (Fast-ACVNet+).  Batch norms stay in eval mode (their affine parameters train).  Returns the
@@ -60,3 +61,25 @@ def train_synthetic(model: torch.nn.Module, steps: int = 300, h: int = 128, w: i
     for p in model.parameters():
         p.requires_grad_(False)
     return losses
+
+
+def fp16_storage_agreement(model: torch.nn.Module, left: torch.Tensor, right: torch.Tensor,
+                           keep_fp32=("hourglass.conv1_up", "hourglass_att.conv1_up")) -> float:
+    """Fraction of pixels within 1 px between the fp32 oracle and the same oracle with every conv / batch-norm output
+    rounded to fp16 (the engine's storage; the two selection-logit heads stay fp32 as in the engine).  A
+    well-conditioned network is ~1.0; a random-init one ~0.45; fp16 overflow shows up as ~0."""
+    import torch.nn as nn
+    rounded = (nn.Conv2d, nn.Conv3d, nn.ConvTranspose2d, nn.ConvTranspose3d, nn.BatchNorm2d, nn.BatchNorm3d)
+
+    def hook(mod, inp, out):
+        return out.half().float()
+    with torch.no_grad():
+        ref = model(left, right)
+        hs = [mod.register_forward_hook(hook) for n, mod in model.named_modules()
+              if isinstance(mod, rounded) and not n.startswith(keep_fp32)]
+        try:
+            out = model(left, right)
+        finally:
+            for h in hs:
+                h.remove()
+    return float(((out - ref).abs() <= 1.0).float().mean())

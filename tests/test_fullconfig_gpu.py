@@ -114,13 +114,17 @@ def test_fastacvnet_end_to_end(tmp_path, monkeypatch):
     (test_fastacvnet_random_weights_precision below keeps that study).  Trained, the same fp16-storage oracle agrees
     on 99.98 % (utils/condition.py), so what is left to measure is the engine's arithmetic."""
     from stereoalgorithms_amd.models import fast_acvnet as FA
-    from stereoalgorithms_amd.utils.condition import imagenet_input, train_synthetic
+    from stereoalgorithms_amd.utils.condition import fp16_storage_agreement, imagenet_input, train_synthetic
     m = FA.build("fastacvnet-plus", seed=0)
     losses = train_synthetic(m, steps=300, device="cuda")
     print(f"conditioning: smooth-L1 {losses[0]:.3f} -> {losses[-1]:.3f}")
     assert losses[-1] < 0.25 * losses[0]
-    eng, plan = _engine(tmp_path, monkeypatch, m.cpu(), "fastacvnet-plus", 1)
     left, right = _pairs(1)
+    # precondition: the network itself tolerates fp16 activation storage (else no fp16 engine could match it)
+    agree = fp16_storage_agreement(m, imagenet_input(left), imagenet_input(right))
+    print(f"fp16-storage oracle vs fp32 oracle: <1px {agree:.5f}")
+    assert agree >= 0.99, agree
+    eng, plan = _engine(tmp_path, monkeypatch, m.cpu(), "fastacvnet-plus", 1)
     disp = eng.run(left, right).clone()
     disp2 = eng.run(left, right)
     torch.cuda.synchronize()

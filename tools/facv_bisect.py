@@ -16,6 +16,7 @@ def main():
     p.add_argument("--height", type=int, default=96)
     p.add_argument("--width", type=int, default=128)
     p.add_argument("--batch", type=int, default=1)
+    p.add_argument("--conditioned", action="store_true", help="weights after utils.condition.train_synthetic (300 steps)")
     a = p.parse_args()
     tapdir = tempfile.mkdtemp(prefix="taps")
     os.environ["SA_TAP_DIR"] = tapdir
@@ -29,7 +30,13 @@ def main():
     from stereoalgorithms_amd.utils.weights import save_model
 
     B, H, W = a.batch, a.height, a.width
-    m = FA.sharpen(FA.build("fastacvnet-plus", seed=0))
+    if a.conditioned:
+        from stereoalgorithms_amd.utils.condition import train_synthetic
+        m = FA.build("fastacvnet-plus", seed=0)
+        train_synthetic(m, steps=300, device="cuda")
+        m = m.cpu()
+    else:
+        m = FA.sharpen(FA.build("fastacvnet-plus", seed=0))
     path = save_model(m, os.path.join(tapdir, "w.safetensors"), "fastacvnet-plus")
     l, r = batch_pairs(B, H, W, seed=5)
     left, right = torch.from_numpy(l).cuda(), torch.from_numpy(r).cuda()
