@@ -119,7 +119,10 @@ struct Level {
     mask = make_tensor(a, B, h, w, 144);
     qx = make_tensor(a, B, h, w, 128);
     flow = (float*)a.alloc((size_t)B * h * w * 2 * 4);
+    bar = (unsigned*)a.alloc(4 * sizeof(unsigned));
+    HIP_CHECK(hipMemset(bar, 0, 4 * sizeof(unsigned)));
   }
+  unsigned* bar = nullptr;  // grid-barrier words of this level's one-launch GRU halves (sa_gru_level)
 };
 
 class CreStereo : public StereoEngine {
@@ -153,6 +156,10 @@ class CreStereo : public StereoEngine {
   bool agcl_first_ = !(std::getenv("SA_CRE_AGCL_FIRST") && std::getenv("SA_CRE_AGCL_FIRST")[0] == '0');
   int gru_split_mode_ = std::getenv("SA_CRE_GRU_SPLIT") ? std::atoi(std::getenv("SA_CRE_GRU_SPLIT")) : -1;
   bool gru_split_ = false;
+  // SA_CRE_FUSED_LEVEL (bit i = level i): each SepConvGRU half (z/r/q-x conv, grid barrier, q conv) in ONE launch
+  // (sa_gru_level) at batch <= 2 with the GRU split -- the coarse levels' four small convs per update are
+  // latency-bound on one queue (profiles/timeline_r5_cre10.txt: igemm<64,64> 65 launches, 954 us)
+  int fused_level_mask_ = std::getenv("SA_CRE_FUSED_LEVEL") ? std::atoi(std::getenv("SA_CRE_FUSED_LEVEL")) : 0;
   Level lv_[3];  // 0: 1/4, 1: 1/8, 2: 1/16
   void* fh2_w16_ = nullptr;
   // iter-mode AGCL fused with convc1 (sa_agcl_conv1x1): [256][64] fp16 weights (k >= 36 zero) + fp32 bias;
@@ -418,7 +425,6 @@ void CreStereo::update(hipStream_t s, Level& L, const Tensor& f1, const Tensor& 
     za.h_stride = L.net.stride;
     za.rh = L.rh.ptr;
     za.rh_stride = L.rh.stride;
-    zrq_[d].launch(s, za);
     SaConvArgs qa = qh_[d].args({L.rh}, L.net);
     qa.epi = SA_EPI_GRU_Q;
     qa.res = L.qx.ptr;
@@ -427,6 +433,23 @@ void CreStereo::update(hipStream_t s, Level& L, const Tensor& f1, const Tensor& 
     qa.aux_stride = L.z.stride;
     qa.hbuf = L.net.ptr;
     qa.h_stride = L.net.stride;
+    const int li = (int)(&L - lv_);
+    if (((fused_level_mask_ >> li) & 1) && B <= 2 && za.ws && qa.ws) {
+      static const int grid = std::getenv("SA_GRU_LEVEL_GRID") ? std::atoi(std::getenv("SA_GRU_LEVEL_GRID")) : 64;
+      const int rc = sa_gru_level(&za, &qa, L.bar, grid, s);
+      if (rc == 0) {
+        SA_LAUNCH_CHECK(s);
+        if (const SplitKWorkspace* sk = current_splitk()) {
+          long fl = 0, tiles = 0;
+          sa_conv2d_last_split(&fl, &tiles);
+          sk->max_floats = std::max<int64_t>(sk->max_floats, fl);
+          sk->max_counters = std::max<int32_t>(sk->max_counters, (int32_t)tiles);
+        }
+        continue;
+      }
+      SA_LOGW("fused SepConvGRU half not eligible (rc %d): two launches", rc);
+    }
+    zrq_[d].launch(s, za);
     qh_[d].launch(s, qa);
   }
   for (int d = 0; d < 2 && !gru_split_; ++d) {

@@ -14,7 +14,7 @@ run() {  # name model iter-marker [batch]
   rm -rf /tmp/tl_$name
   timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d /tmp/tl_$name -o run -- \
     python3 tools/run_engine.py --model $model --batch $batch --frames 4 > gpurun_out/tl/${TAG}_${name}_prof.log 2>&1 || return 1
-  python3 tools/timeline.py /tmp/tl_$name --iter-marker "$marker" --chain 40 > gpurun_out/tl/${TAG}_${name}.txt 2>&1 || return 1
+  python3 tools/timeline.py /tmp/tl_$name --iter-marker "$marker" --chain 40 --kernel-stats 40 > gpurun_out/tl/${TAG}_${name}.txt 2>&1 || return 1
   cp $(find /tmp/tl_$name -name "*kernel_trace.csv" | head -1) gpurun_out/tl/${TAG}_${name}_kernels.csv
 }
 if [ -n "$ONLY" ]; then

@@ -6,6 +6,7 @@ dispatches, plus derived MFMA busy fraction when SQ_VALU_MFMA_BUSY_CYCLES and SQ
 """
 import argparse
 import csv
+import re
 import statistics
 import sys
 from collections import defaultdict
@@ -14,7 +15,7 @@ from collections import defaultdict
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("csv")
-    ap.add_argument("--match", default="")
+    ap.add_argument("--match", default="", help="regex on the kernel name")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.csv)))
     if not rows:
@@ -25,7 +26,7 @@ def main():
     disp = defaultdict(lambda: defaultdict(float))  # (kernel, grid, dispatch) -> counter -> summed value
     for r in rows:
         k = r[kcol]
-        if a.match and a.match not in k:
+        if a.match and not re.search(a.match, k):
             continue
         g = r.get("Grid_Size") or r.get("Grid-Size") or ""
         d = r.get("Dispatch_Id") or r.get("Dispatch-Id") or ""

@@ -88,6 +88,9 @@ def main():
     ap.add_argument("--frame", type=int, default=-2, help="which frame (python index over complete frames)")
     ap.add_argument("--chain", type=int, default=60, help="critical-chain links to print (from the end)")
     ap.add_argument("--list", type=int, default=0, help="print the first N kernels of the frame in start order")
+    ap.add_argument("--kernel-stats", type=int, default=0,
+                    help="per-kernel dispatch counts and device time of THIS frame replay only (top N), so no tuning "
+                         "pass or eager launch is averaged into 'per frame'")
     a = ap.parse_args()
     rows = load(a.trace)
     fs = frames(rows, a.frame_marker, 200_000)
@@ -104,6 +107,18 @@ def main():
     print(f"frame {a.frame}: {len(fr)} kernels, span {span / 1e3:.1f} us, busy {busy / 1e3:.1f} us "
           f"({100 * busy / span:.1f} %), idle {(span - busy) / 1e3:.1f} us in {len(gaps)} gaps "
           f"(>5us: {sum(1 for g in gaps if g > 5000)}, sum {sum(g for g in gaps if g > 5000) / 1e3:.1f} us)")
+    if a.kernel_stats:
+        agg = {}
+        for s_, e_, n, w, q in fr:
+            k = short(n)
+            c, t = agg.get(k, (0, 0))
+            agg[k] = (c + 1, t + (e_ - s_))
+        tot = sum(t for _, t in agg.values())
+        print(f"\nper-kernel device time in this frame replay ({len(fr)} dispatches, {tot / 1e3:.1f} us summed over "
+              f"queues; concurrent kernels overlap, so the sum exceeds the span)")
+        print(f"  {'kernel':62s} {'n':>4s} {'us':>9s} {'avg us':>8s} {'%':>6s}")
+        for k, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:a.kernel_stats]:
+            print(f"  {k:62s} {c:4d} {t / 1e3:9.1f} {t / c / 1e3:8.2f} {100 * t / tot:6.2f}")
     if a.list:
         for s, e, n, w, q in fr[:a.list]:
             print(f"  +{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f} us  wg {w:6d}  q{q}  {n}")
