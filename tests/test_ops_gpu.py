@@ -884,7 +884,7 @@ def test_raft_motion_head_vs_torch():
     assert torch.allclose(fc[..., 0].float(), flow, atol=1e-2) and fc[..., 1].abs().max().item() == 0
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 @pytest.mark.parametrize("b,h,w", [(2, 7, 44), (1, 24, 32), (1, 13, 37), (2, 20, 64)])
 def test_raft_motion_encoder_vs_torch(b, h, w, variant):
     """The whole motion encoder in one kernel == lookup -> convc1/convf1 -> convc2/convf2 -> conv (fp32 torch on

@@ -25,6 +25,7 @@ MODES = [
     ("cnet-first", {"SA_RAFT_CNET_FIRST": "1"}),
     # the two-workgroups-per-CU motion encoder (v2): same MFMAs in the same k order as the default v1
     ("motion-encoder-v2", {"SA_RAFT_MENC": "2"}),
+    ("motion-encoder-v1-conflict-free", {"SA_RAFT_MENC": "3"}),
     # conv1's tap projections + their stencil as its own launch (the default at batch > 2) and inside the next
     # motion encoder: same arithmetic as each other, other summation order than conv1 stored + the tail kernel
     ("fh-projection", {"SA_RAFT_FH_PROJ": "1"}),
@@ -44,6 +45,7 @@ RT_MODES = [
     ("pipeline", {}),
     ("cnet-second", {"SA_RAFT_CNET_FIRST": "0"}),
     ("motion-encoder-v2", {"SA_RAFT_MENC": "2"}),
+    ("motion-encoder-v1-conflict-free", {"SA_RAFT_MENC": "3"}),
     ("fh-fused-stencil", {"SA_RAFT_FH_FUSE": "1"}),
 ]
 
