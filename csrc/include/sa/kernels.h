@@ -100,6 +100,11 @@ typedef struct {
   // SA_EPI_TAPPROJ: the projection weights fp16 [taps][Cout] and their count
   const void* tapw;
   int32_t taps;
+  // input instance norm folded into the conv (tile_cfg 23 only; other tactics return -5): src[0] is a conv's RAW
+  // output and in_stats its slotted statistics ([in_slots][N][Cin][2]); the conv reads relu(IN(src[0])) (eps in_eps)
+  const sa_stat_t* in_stats;
+  int32_t in_slots;
+  float in_eps;
 } SaConvArgs;
 
 int sa_conv2d(const SaConvArgs* a, hipStream_t stream);
@@ -127,10 +132,12 @@ int sa_conv7x7_stem(const void* x, int xs, int creal, const void* w, int kpad, i
 // Direct 3x3 / stride 1 / pad 1 conv, 64 -> 64 channels (8-wave persistent workgroups over 2x64-pixel tiles,
 // channel-split weights stationary in registers, DMA ring, register epilogue with buffer stores): bias / act,
 // optional slotted IN statistics or residual y = act2(act(acc + bias) + res) (not both); tile_cfg = 23.
+// in_stats (no residual): x is a conv's raw output with those slotted statistics and the conv reads relu(IN(x)).
 // -5 when the output span exceeds 32-bit buffer offsets.
 int sa_conv3x3_c64_direct2(const void* x, int xs, const void* w, int kpad, const float* bias, void* out, int os,
                            int N, int H, int W, int act, float alpha, sa_stat_t* stats, int slots, const void* res,
-                           int rs, int act2, int max_blocks, hipStream_t stream);
+                           int rs, int act2, const sa_stat_t* in_stats, int in_slots, float in_eps, int max_blocks,
+                           hipStream_t stream);
 // Direct 3x3 / pad 1 conv to 96 channels: 96 -> 96 at stride 1 or 64 -> 96 at stride 2 (12-wave persistent
 // tiles, weights stationary in registers, DMA ring); act none / relu / leaky, optional slotted IN statistics or
 // residual (not both); tile_cfg = 24.  -5 for other shapes or an output span past 32-bit buffer offsets.
@@ -160,7 +167,7 @@ int sa_flow_head_tail_oc(const void* y, int ys, int C, const void* w16, int oc, 
                          int H, int W, hipStream_t stream);
 
 // ---- normalisation / elementwise ------------------------------------------------------------
-// Instance-norm apply (biased var, eps): y = act(norm(x)); if res: y = act2(resnorm(res) + y)
+// Instance-norm apply (biased var, eps): y = act(norm(x)); if res: y = act2(res_act(resnorm(res)) + y)
 typedef struct {
   const void* x; int32_t x_stride;
   const sa_stat_t* stats;      // [N][C][2] fixed-point sums of x (stat_slots copies of it, summed here)
@@ -171,6 +178,7 @@ typedef struct {
   int32_t act, act2;
   float eps, alpha;
   int32_t stat_slots;          // copies of [N][C][2] the conv epilogues accumulated into (0 / 1: one, reduced)
+  int32_t res_act;             // activation of the normalised residual (res_stats only)
 } SaNormArgs;
 int sa_instnorm_apply(const SaNormArgs* a, hipStream_t stream);
 // stats[0][i] = sum_r stats[r][i], stats[r>0][i] = 0 for i < count (idempotent)

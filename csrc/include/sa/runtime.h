@@ -261,7 +261,7 @@ class ConvLayer {
   SaConvArgs args(const std::vector<Tensor>& srcs, const Tensor& out) const;
   void run(hipStream_t s, const std::vector<Tensor>& srcs, const Tensor& out, int act = SA_ACT_NONE,
            const Tensor* res = nullptr, int act2 = SA_ACT_NONE, sa_stat_t* stats = nullptr,
-           float alpha = 0.01f) const;
+           float alpha = 0.01f, const sa_stat_t* in_stats = nullptr) const;  // in_stats: SaConvArgs.in_stats
   void launch(hipStream_t s, SaConvArgs& a) const;
 
  private:

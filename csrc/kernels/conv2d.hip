@@ -2557,7 +2557,9 @@ extern "C" int sa_gru_level(const SaConvArgs* za, const SaConvArgs* qa, unsigned
 
 extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
   if (a->Kpad % 32 != 0 || a->Cin % 8 != 0 || a->nsrc < 1 || a->nsrc > 4) return -2;
-  const int cfg = pick_cfg(a);
+  // the folded input norm exists in the direct 64-channel kernel only
+  if (a->in_stats && a->tile_cfg >= 0 && a->tile_cfg != 23) return -5;
+  const int cfg = a->in_stats ? 23 : pick_cfg(a);
   if (a->epi == SA_EPI_TAPPROJ) {
     // partial sums per 128-channel n-tile: the tile configs with BN = 128 only
     const bool bn128 = cfg == 0 || cfg == 4 || cfg == 7 || cfg == 11 || cfg == 15 || cfg == 19 || (cfg >= 26 && cfg <= 33);
@@ -2585,7 +2587,7 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
       note_split(1, 0, 0);
       return sa_conv3x3_c64_direct2(a->src[0].ptr, a->src[0].stride, a->weight, a->Kpad, a->bias, a->out,
                                     a->out_stride, a->N, a->H, a->W, a->act, a->alpha, a->stats, a->stats_slots,
-                                    a->res, a->res_stride, a->act2, 0, stream);
+                                    a->res, a->res_stride, a->act2, a->in_stats, a->in_slots, a->in_eps, 0, stream);
     }
     case 24: {
       // direct 3x3 -> 96 (conv_direct96.hip): one 96-channel source at stride 1 or a 64-channel one at stride 2,

@@ -35,6 +35,10 @@ constexpr int IN_PIECES = IR * IC * 8;        // 16-B pieces per input tile (211
 constexpr int IN_INSTR = (IN_PIECES + 63) / 64;  // wave-instructions per tile (33)
 
 __device__ __attribute__((aligned(16))) const unsigned char g_zero16d[64] = {0};
+// padding source of the folded input norm (NIN): -65504 in fp16, which relu(IN(.)) maps to +0 for any statistics,
+// i.e. the zero padding of the normalised input without a per-piece bounds test in the transform
+__device__ __attribute__((aligned(16))) const unsigned short g_negmax16d[8] = {0xFBFF, 0xFBFF, 0xFBFF, 0xFBFF,
+                                                                              0xFBFF, 0xFBFF, 0xFBFF, 0xFBFF};
 
 // workgroup barrier that orders LDS only: __syncthreads() would also wait vmcnt(0), i.e. for the
 // in-flight input DMA of the next tiles and for this tile's global stores to be acknowledged
@@ -79,15 +83,17 @@ constexpr int V2_PIECES = IN_INSTR;                                    // 33 DMA
 constexpr int V2_PER_WAVE = (V2_PIECES + V2_WAVES - 1) / V2_WAVES;     // 5 (waves 1..7: one dummy)
 // LDS layout: NB ring buffers | 1 KB sink for the dummy pieces | 64 fp32 biases | (STATS) per-lane running
 // IN sums [512 lanes][sum 8 | sumsq 8] -- in LDS, not VGPRs: 16 more live registers next to the 144 of the
-// stationary weights made the compiler drop the fragment prefetch (a lgkmcnt(0) after every ds_read)
-template <bool STATS>
+// stationary weights made the compiler drop the fragment prefetch (a lgkmcnt(0) after every ds_read) |
+// (NIN) the folded input norm's mean / rstd, [2 image slots][mean 64 | rstd 64] fp32
+template <bool STATS, bool NIN = false>
 struct V2Lds {
   static constexpr int NB = STATS ? 3 : 4;  // ring depth (3 leaves room for the statistics)
   static constexpr int DUMMY = NB * IN_BYTES;
   static constexpr int BIAS = DUMMY + 1024;
   static constexpr int ST = BIAS + 256;
   static constexpr int RED = ST + (STATS ? 512 * 64 : 0);  // flush: [8 waves][4 kq][16] wave totals
-  static constexpr int SMEM = RED + (STATS ? 8 * 4 * 16 * 4 : 0);
+  static constexpr int NRM = RED + (STATS ? 8 * 4 * 16 * 4 : 0);
+  static constexpr int SMEM = NRM + (NIN ? 2 * 128 * 4 : 0);
 };
 
 // sum over the 16 lanes of a DPP row (every lane gets the row total)
@@ -129,11 +135,24 @@ struct DirectArgs2 {
   const f16* res;  // optional residual (RES): y = act2(act(acc + bias) + res)
   int rs;
   int act2;
+  // NIN: x is a conv's raw output with these slotted statistics ([in_slots][N][64][2]); the conv reads relu(IN(x))
+  const sa_stat_t* in_stats;
+  int in_slots;
+  float in_eps;
+  double in_inv;  // 1 / (H W SA_STAT_SCALE), from the host: a kernel argument (SGPRs), not a hoisted VGPR pair
 };
 
-template <int ACT, bool STATS, bool RES>
+// NIN (input instance norm folded in): the instance-norm residual blocks' conv2 reads conv1's
+// RAW output and normalises it in LDS instead of a separate relu(IN(.)) pass over the full-resolution tensor (one
+// HBM read + write of it).  Each wave transforms the 16-B pieces it DMA'd itself -- landed per its own vmcnt, no
+// extra barrier -- for tile k+1 at the end of tile k (after the epilogue: the fragment and accumulator registers
+// are free there, and the DMA of tile k+2 stays in flight); the loop-top barrier of tile k+1 publishes it.  The
+// arithmetic is instnorm_apply's ((x - mean) * rstd, relu, round to fp16), so the conv sees bitwise the same input.
+// Round 2 measured a transform phase of the round-2 kernel between two extra barriers as neutral
+// (profiles/fused_input_norm_r02.txt).
+template <int ACT, bool STATS, bool RES, bool NIN = false>
 __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const DirectArgs2 p) {
-  using L = V2Lds<STATS>;
+  using L = V2Lds<STATS, NIN>;
   constexpr int NB = L::NB;
   __shared__ __attribute__((aligned(16))) char smem[L::SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -142,7 +161,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const Direc
   const int tiles_x = (p.W + TC - 1) / TC, tiles_y = (p.H + TR - 1) / TR;
   const int tiles_img = tiles_x * tiles_y;
   const int ntiles = p.N * tiles_img;
-  const void* zero = g_zero16d;
+  const void* zero = NIN ? (const void*)g_negmax16d : (const void*)g_zero16d;
 
   auto issue_tile = [&](int t, int buf) {
     const int n = t / tiles_img, r = t - n * tiles_img;
@@ -245,13 +264,78 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const Direc
   for (int k = 0; k < NB - 1; ++k)
     if (k < kb) issue_tile(t0 + k, k);
 
+  // NIN: per-image mean / rstd into LDS slot (n & 1) (the arithmetic of elementwise.hip norm_lds: integer sums over
+  // the slots, then double), block-uniform call
+  float* nrm = reinterpret_cast<float*>(smem + L::NRM);
+  int nrm_img = -1;
+  auto nrm_load = [&](int n) {
+    if constexpr (NIN) {
+      if (tid < 64) {
+        const double inv = p.in_inv;
+        const long slot = (long)p.N * 64 * 2;
+        const sa_stat_t* sp = p.in_stats + ((long)n * 64 + tid) * 2;
+        long long s0 = 0, s1 = 0;
+        for (int r = 0; r < p.in_slots; ++r) {
+          s0 += sp[r * slot];
+          s1 += sp[r * slot + 1];
+        }
+        const double m = (double)s0 * inv;
+        const double var = (double)s1 * inv - m * m;
+        nrm[(n & 1) * 128 + tid] = (float)m;
+        nrm[(n & 1) * 128 + 64 + tid] = rsqrtf((float)(var > 0.0 ? var : 0.0) + p.in_eps);
+      }
+      lds_barrier();
+      nrm_img = n;
+    }
+  };
+  // NIN: this wave's own (landed) pieces of tile t0 + kk -> relu(IN(.)) in place
+  auto fold_tile = [&](int kk) {
+    if constexpr (NIN) {
+      const int n1 = (t0 + kk) / tiles_img;
+      if (n1 != nrm_img) nrm_load(n1);
+      char* ib = smem + (kk % NB) * IN_BYTES;
+      const float* d = nrm + (n1 & 1) * 128;
+      // laundered lane index and a rolled loop: the tile-invariant piece decomposition is not hoisted into
+      // long-lived VGPRs next to the stationary weights (the STATS variant spilled 36 of them)
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+#pragma unroll 1
+      for (int i = 0; i < V2_PER_WAVE; ++i) {
+        const int ins = i * V2_WAVES + wave;
+        if (ins < V2_PIECES) {
+          const int g = ins * 64 + ln;
+          const int q = (g & 7) ^ v2_swz(g >> 3);
+          half8 h = *reinterpret_cast<const half8*>(ib + g * 16);
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf) {  // 4 channels at a time: 8 parameter VGPRs live, not 16
+            const floatx4 m = *reinterpret_cast<const floatx4*>(d + q * 8 + hf * 4);
+            const floatx4 r = *reinterpret_cast<const floatx4*>(d + 64 + q * 8 + hf * 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float v = ((float)h[hf * 4 + e] - m[e]) * r[e];
+              h[hf * 4 + e] = (f16)(v > 0.f ? v : 0.f);
+            }
+          }
+          *reinterpret_cast<half8*>(ib + g * 16) = h;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // complete before the loop-top barrier publishes the tile
+    }
+  };
+  constexpr int kOpsPerTile = RES ? 4 : 2;  // buffer stores (+ residual buffer loads), range-checked, never skipped
+  if constexpr (NIN) {
+    if (kb > 0) {
+      wait_vmcnt((kb - 1 < NB - 2 ? kb - 1 : NB - 2) * V2_PER_WAVE);  // tile 0's pieces (later tiles in flight)
+      fold_tile(0);
+    }
+  }
+
   for (int k = 0; k < kb; ++k) {
     const int t = t0 + k;
     const int cur = k % NB;
     // ops this wave issued after tile t's DMA: the ring pieces of tiles k+1, k+2 and the stores of the
     // (at most 3) tiles computed since
     const int ahead = (kb - 1 - k) < NB - 2 ? (kb - 1 - k) : NB - 2;
-    constexpr int kOpsPerTile = RES ? 4 : 2;  // buffer stores (+ residual buffer loads), range-checked, never skipped
     wait_vmcnt(ahead * V2_PER_WAVE + (k < NB - 1 ? k : NB - 1) * kOpsPerTile);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -280,7 +364,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const Direc
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const int fr = frow, kql = kq;
+    int fr = frow, kql = kq;
+    if constexpr (NIN) {
+      // laundered per tile: the fragment addresses are recomputed here instead of living across the whole tile
+      // loop (with the fold's temporaries they spilled, and a scratch reload inside the MFMA loop waits vmcnt(0))
+      asm volatile("" : "+v"(fr), "+v"(kql));
+    }
     auto load = [&](int ks, half8* bf) {
       const int tap = ks >> 1, kh = tap / 3, kw = tap - kh * 3;
       const int q = (ks & 1) * 4 + kql;
@@ -355,23 +444,32 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const Direc
       st_lane[2] += floatx4{tsq[0], tsq[1], tsq[2], tsq[3]};
       st_lane[3] += floatx4{tsq[4], tsq[5], tsq[6], tsq[7]};
     }
+    if constexpr (NIN) {
+      if (k + 1 < kb) {
+        // ops this wave issued after tile k+1's DMA: tile k+2's (.. k+NB-2's) pieces and the stores of the tiles
+        // computed since (this one included)
+        const int a2 = (kb - 2 - k) < NB - 2 ? (kb - 2 - k) : NB - 2;
+        wait_vmcnt(a2 * V2_PER_WAVE + (k + 1 < NB - 1 ? k + 1 : NB - 1) * kOpsPerTile);
+        fold_tile(k + 1);
+      }
+    }
   }
   if constexpr (STATS) {
     if (stat_img >= 0) flush_stats();
   }
 }
 
-template <bool STATS, bool RES>
+template <bool STATS, bool RES, bool NIN = false>
 void launch_direct2(const DirectArgs2& a, int act, unsigned g, hipStream_t s) {
   switch (act) {
     case SA_ACT_RELU:
-      hipLaunchKernelGGL((conv3x3_c64_direct2_kernel<SA_ACT_RELU, STATS, RES>), dim3(g), dim3(512), 0, s, a);
+      hipLaunchKernelGGL((conv3x3_c64_direct2_kernel<SA_ACT_RELU, STATS, RES, NIN>), dim3(g), dim3(512), 0, s, a);
       break;
     case SA_ACT_LEAKY:
-      hipLaunchKernelGGL((conv3x3_c64_direct2_kernel<SA_ACT_LEAKY, STATS, RES>), dim3(g), dim3(512), 0, s, a);
+      hipLaunchKernelGGL((conv3x3_c64_direct2_kernel<SA_ACT_LEAKY, STATS, RES, NIN>), dim3(g), dim3(512), 0, s, a);
       break;
     default:
-      hipLaunchKernelGGL((conv3x3_c64_direct2_kernel<SA_ACT_NONE, STATS, RES>), dim3(g), dim3(512), 0, s, a);
+      hipLaunchKernelGGL((conv3x3_c64_direct2_kernel<SA_ACT_NONE, STATS, RES, NIN>), dim3(g), dim3(512), 0, s, a);
       break;
   }
 }
@@ -380,21 +478,27 @@ void launch_direct2(const DirectArgs2& a, int act, unsigned g, hipStream_t s) {
 
 extern "C" int sa_conv3x3_c64_direct2(const void* x, int xs, const void* w, int kpad, const float* bias, void* out,
                                       int os, int N, int H, int W, int act, float alpha, sa_stat_t* stats, int slots,
-                                      const void* res, int rs, int act2, int max_blocks, hipStream_t stream) {
+                                      const void* res, int rs, int act2, const sa_stat_t* in_stats, int in_slots,
+                                      float in_eps, int max_blocks, hipStream_t stream) {
   if (kpad < KTOT || xs < 64 || os < 64 || xs % 8 || os % 8 ||
       (act != SA_ACT_NONE && act != SA_ACT_RELU && act != SA_ACT_LEAKY))
     return -2;
   if (res && (stats || rs < 64 || rs % 8 || (act2 != SA_ACT_NONE && act2 != SA_ACT_RELU))) return -5;
+  if (in_stats && res) return -5;  // the folded input norm is the instance-norm blocks' conv2: no residual
   const size_t span = (((size_t)N * H - 1) * W + (W - 1)) * (size_t)os * 2 + 128;  // last pixel's 64 channels
   const size_t rspan = res ? (((size_t)N * H - 1) * W + (W - 1)) * (size_t)rs * 2 + 128 : 0;
   if (span >= 0xFFFFFF00ull || rspan >= 0xFFFFFF00ull) return -5;  // 32-bit buffer offsets
   DirectArgs2 a{(const f16*)x, xs, (const f16*)w, kpad, bias, (f16*)out, os, (unsigned)span, (unsigned)rspan, N, H, W,
-                alpha, stats, slots, (const f16*)res, rs, act2};
+                alpha, stats, slots, (const f16*)res, rs, act2, in_stats, in_slots > 1 ? in_slots : 1, in_eps,
+                1.0 / ((double)H * W * SA_STAT_SCALE)};
   const long ntiles = (long)N * ((H + TR - 1) / TR) * ((W + TC - 1) / TC);
   long g = max_blocks > 0 ? max_blocks : 256;
   if (g > ntiles) g = ntiles;
   if (g < 1) return 0;
-  if (stats) launch_direct2<true, false>(a, act, (unsigned)g, stream);
+  if (in_stats) {
+    if (stats) launch_direct2<true, false, true>(a, act, (unsigned)g, stream);
+    else launch_direct2<false, false, true>(a, act, (unsigned)g, stream);
+  } else if (stats) launch_direct2<true, false>(a, act, (unsigned)g, stream);
   else if (res) launch_direct2<false, true>(a, act, (unsigned)g, stream);
   else launch_direct2<false, false>(a, act, (unsigned)g, stream);
   return (int)hipGetLastError();

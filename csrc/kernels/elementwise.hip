@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void instnorm_apply_kernel(const SaNormArgs a,
       if (rb) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float r = rs ? ((float)hr[u][j] - rmean[j]) * rrstd[j] : (float)hr[u][j];
+          const float r = rs ? act_apply(((float)hr[u][j] - rmean[j]) * rrstd[j], a.res_act, a.alpha) : (float)hr[u][j];
           v[j] = act_apply(v[j] + r, a.act2, a.alpha);
         }
       }

@@ -10,7 +10,7 @@ Norm parse_norm(const std::string& s) {
 }
 
 void instnorm(hipStream_t s, const Tensor& x, const sa_stat_t* stats, const Tensor& out, int act,
-              const Tensor* res, const sa_stat_t* res_stats, int act2) {
+              const Tensor* res, const sa_stat_t* res_stats, int act2, int res_act) {
   // the apply kernel folds the conv epilogues' kStatSlots statistic copies itself (per block, into LDS)
   SaNormArgs a{};
   a.stat_slots = kStatSlots;
@@ -27,6 +27,7 @@ void instnorm(hipStream_t s, const Tensor& x, const sa_stat_t* stats, const Tens
   a.C = x.c;
   a.act = act;
   a.act2 = act2;
+  a.res_act = res_act;
   a.eps = 1e-5f;
   a.alpha = 0.01f;
   const int rc = sa_instnorm_apply(&a, s);
@@ -34,9 +35,16 @@ void instnorm(hipStream_t s, const Tensor& x, const sa_stat_t* stats, const Tens
   SA_LAUNCH_CHECK(s);
 }
 
-// The instance-norm blocks materialise relu(IN(conv1)) before conv2.  Normalising conv1's raw output inside
-// conv2's LDS staging instead was measured neutral in round 2 (the in-LDS transform is a serial phase between
-// two barriers that eats the saved HBM pass; profiles/fused_input_norm_r02.txt) and has been removed.
+// The instance-norm blocks of the 64-channel full-resolution layer materialised relu(IN(conv1)) before conv2 (and
+// relu(IN(stem)) before layer1).  With SA_FOLD_IN the direct conv (conv_direct.hip, NIN) reads
+// the raw tensor and normalises its own DMA'd pieces in LDS one tile ahead, and the residual apply normalises the raw
+// block input itself: 3 of the 5 full-resolution apply passes of a RAFT / CREStereo feature trunk are gone.  Round
+// 2's version (a serial in-LDS phase between two extra barriers of the round-2 kernel) measured neutral
+// (profiles/fused_input_norm_r02.txt).
+bool fold_in_enabled() {  // read per engine build: an in-process A/B knob (tools/ab_engine.py)
+  const char* e = std::getenv("SA_FOLD_IN");
+  return !(e && e[0] == '0');
+}
 
 void ResBlock::build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std::string& p,
                      int in_planes, int planes, int stride, Norm nrm, int N, int H, int W, ActPlan* plan,
@@ -66,6 +74,10 @@ void ResBlock::build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std
                bn ? std::vector<std::string>{p + ".norm3"} : std::vector<std::string>{});
   }
   const int Ho = c1.out_h(H), Wo = c1.out_w(W);
+  // the direct kernel's shape (sa_conv2d tile_cfg 23): 64 -> 64, 3x3, stride 1, 32-bit buffer offsets
+  fold = norm == Norm::Instance && !has_down && planes == 64 && fold_in_enabled() &&
+         (size_t)N * Ho * Wo * 64 * 2 < 0xFFFFFF00ull;
+  SA_REQUIRE(!x_raw || fold, "ResBlock: a raw (un-normalised) input needs the folded instance norm");
   if (norm == Norm::Instance) {
     st1 = sp.take(N, planes);
     st2 = sp.take(N, planes);
@@ -73,7 +85,11 @@ void ResBlock::build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std
   }
   if (plan) {
     // lifetimes in run() order (see below); x is the block input (tracked only if the plan owns it)
-    if (norm == Norm::Instance) {
+    if (norm == Norm::Instance && fold) {
+      plan->use(x), plan->def(&y1, N, Ho, Wo, planes), plan->next();                   // c1(x) -> y1
+      plan->use(&y1), plan->def(&y2, N, Ho, Wo, planes), plan->next();                 // c2(relu(IN(y1))) -> y2
+      plan->use(&y2), plan->use(x), plan->def(&out, N, Ho, Wo, planes), plan->next();
+    } else if (norm == Norm::Instance) {
       plan->use(x), plan->def(&y1, N, Ho, Wo, planes), plan->next();                   // c1(x) -> y1
       plan->use(&y1), plan->def(&a1, N, Ho, Wo, planes), plan->next();                 // IN -> a1
       plan->use(&a1), plan->def(&y2, N, Ho, Wo, planes), plan->next();                 // c2(a1) -> y2
@@ -90,14 +106,19 @@ void ResBlock::build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std
     y1 = make_tensor(a, N, Ho, Wo, planes);
     y2 = make_tensor(a, N, Ho, Wo, planes);
   }
-  a1 = make_tensor(a, N, Ho, Wo, planes);
+  if (!fold) a1 = make_tensor(a, N, Ho, Wo, planes);
   if (has_down) yd = make_tensor(a, N, Ho, Wo, planes);
   out = make_tensor(a, N, Ho, Wo, planes);
 }
 
 
-void ResBlock::run(hipStream_t s, const StatsPool& sp, const Tensor& x) const {
-  if (norm == Norm::Instance) {
+void ResBlock::run(hipStream_t s, const StatsPool& sp, const Tensor& x, const sa_stat_t* x_stats) const {
+  SA_REQUIRE(x_raw == (x_stats != nullptr), "ResBlock: raw input without its statistics (or the reverse)");
+  if (norm == Norm::Instance && fold) {
+    c1.run(s, {x}, y1, SA_ACT_NONE, nullptr, SA_ACT_NONE, sp.resolve(st1), 0.01f, x_stats);
+    c2.run(s, {y1}, y2, SA_ACT_NONE, nullptr, SA_ACT_NONE, sp.resolve(st2), 0.01f, sp.resolve(st1));
+    instnorm(s, y2, sp.resolve(st2), out, SA_ACT_RELU, &x, x_stats, SA_ACT_RELU, x_stats ? SA_ACT_RELU : SA_ACT_NONE);
+  } else if (norm == Norm::Instance) {
     c1.run(s, {x}, y1, SA_ACT_NONE, nullptr, SA_ACT_NONE, sp.resolve(st1));
     instnorm(s, y1, sp.resolve(st1), a1, SA_ACT_RELU);
     c2.run(s, {a1}, y2, SA_ACT_NONE, nullptr, SA_ACT_NONE, sp.resolve(st2));
@@ -131,7 +152,13 @@ void Trunk::build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std::s
   // the trunk's activations go through a liveness plan: at most ~3 full-resolution tensors are alive
   // at once (batch 8 RAFT-Stereo sceneflow: several GB less than one buffer per tensor)
   ActPlan plan;
-  if (norm == Norm::Instance) {
+  // stem fold: layer1.0 is a 64 -> 64 stride-1 block whose conv1 and residual normalise c1y themselves
+  stem_fold = norm == Norm::Instance && fold_in_enabled() && strides[0] == 1 &&
+              (size_t)N * h * w * 64 * 2 < 0xFFFFFF00ull;
+  if (norm == Norm::Instance && stem_fold) {
+    c1st = sp.take(N, 64);
+    plan.def(&c1y, N, h, w, 64), plan.next();                      // conv1(img) -> c1y (raw)
+  } else if (norm == Norm::Instance) {
     c1st = sp.take(N, 64);
     plan.def(&c1y, N, h, w, 64), plan.next();                      // conv1(img) -> c1y
     plan.use(&c1y), plan.def(&c1a, N, h, w, 64), plan.next();      // IN -> c1a
@@ -141,10 +168,11 @@ void Trunk::build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std::s
   const int dims[3] = {64, 96, 128};
   int inp = 64;
   layers.resize(6);  // sized up front: the plan holds pointers into the blocks
-  const Tensor* x = &c1a;
+  const Tensor* x = stem_fold ? &c1y : &c1a;
   for (int l = 0; l < 3; ++l)
     for (int b = 0; b < 2; ++b) {
       ResBlock& rb = layers[l * 2 + b];
+      rb.x_raw = stem_fold && l == 0 && b == 0;
       rb.build(a, src, sp, p + ".layer" + std::to_string(l + 1) + "." + std::to_string(b), inp, dims[l],
                b == 0 ? strides[l] : 1, norm, N, h, w, &plan, x);
       x = &rb.out;
@@ -160,10 +188,14 @@ void Trunk::run_step(hipStream_t s, const StatsPool& sp, const Tensor& img, int 
   if (k == 0) {
     if (norm == Norm::Instance) {
       conv1.run(s, {img}, c1y, SA_ACT_NONE, nullptr, SA_ACT_NONE, sp.resolve(c1st));
-      instnorm(s, c1y, sp.resolve(c1st), c1a, SA_ACT_RELU);
+      if (!stem_fold) instnorm(s, c1y, sp.resolve(c1st), c1a, SA_ACT_RELU);
     } else {
       conv1.run(s, {img}, c1a, SA_ACT_RELU);
     }
+    return;
+  }
+  if (k == 1 && stem_fold) {
+    layers[0].run(s, sp, c1y, sp.resolve(c1st));
     return;
   }
   layers[k - 1].run(s, sp, k == 1 ? c1a : layers[k - 2].out);

@@ -45,6 +45,10 @@ struct ResBlock {
   ConvLayer c1, c2, down;
   bool has_down = false;
   Norm norm = Norm::None;
+  // instance norm folded into the direct 64-channel convs (fold_in_enabled(), 64 -> 64 stride 1 blocks): conv2 reads
+  // conv1's raw output y1 (no a1 pass); with x_raw (set before build) the block input x is itself a raw conv output
+  // whose statistics run() receives -- conv1 and the residual apply normalise it on the fly
+  bool fold = false, x_raw = false;
   Tensor y1, a1, y2, yd, out;
   sa_stat_t *st1 = nullptr, *st2 = nullptr, *std_ = nullptr;  // StatsPool handles
   // plan != nullptr: the block's activations are declared in `plan` (lifetimes in run() order, x =
@@ -52,8 +56,11 @@ struct ResBlock {
   void build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std::string& prefix, int in_planes,
              int planes, int stride, Norm norm, int N, int H, int W, ActPlan* plan = nullptr,
              const Tensor* x = nullptr);
-  void run(hipStream_t s, const StatsPool& sp, const Tensor& x) const;
+  void run(hipStream_t s, const StatsPool& sp, const Tensor& x, const sa_stat_t* x_stats = nullptr) const;
 };
+
+// SA_FOLD_IN (default on): fold the instance-norm applies that feed a direct 64-channel conv into that conv
+bool fold_in_enabled();
 
 // BasicEncoder / MultiBasicEncoder trunk shared by RAFT-Stereo and CREStereo (upstream
 // core/extractor.py): conv1 7x7 (stride s1) + norm + ReLU, then layer1..3 of two residual
@@ -63,6 +70,7 @@ struct Trunk {
   Norm norm = Norm::None;
   Tensor c1y, c1a;
   sa_stat_t* c1st = nullptr;
+  bool stem_fold = false;  // relu(IN(conv1)) never materialised: layer1.0 reads c1y raw (ResBlock::x_raw)
   std::vector<ResBlock> layers;
   void build(DeviceArena& a, WeightSource& src, StatsPool& sp, const std::string& prefix, Norm norm, int N, int H,
              int W, int conv1_stride, const int strides[3]);
@@ -75,6 +83,7 @@ struct Trunk {
 
 // norm apply helper
 void instnorm(hipStream_t s, const Tensor& x, const sa_stat_t* stats, const Tensor& out, int act,
-              const Tensor* res = nullptr, const sa_stat_t* res_stats = nullptr, int act2 = SA_ACT_NONE);
+              const Tensor* res = nullptr, const sa_stat_t* res_stats = nullptr, int act2 = SA_ACT_NONE,
+              int res_act = SA_ACT_NONE);
 
 }  // namespace sa

@@ -538,8 +538,13 @@ void ConvLayer::launch(hipStream_t s, SaConvArgs& a) const {
 }
 
 void ConvLayer::run(hipStream_t s, const std::vector<Tensor>& srcs, const Tensor& out, int act,
-                    const Tensor* res, int act2, sa_stat_t* stats, float alpha) const {
+                    const Tensor* res, int act2, sa_stat_t* stats, float alpha, const sa_stat_t* in_stats) const {
   SaConvArgs a = args(srcs, out);
+  if (in_stats) {
+    a.in_stats = in_stats;
+    a.in_slots = kStatSlots;
+    a.in_eps = 1e-5f;
+  }
   SA_REQUIRE(out.c >= (up_ ? cout_real_ : cout_) || stats == nullptr, "conv output view too narrow");
   a.act = act;
   a.alpha = alpha;
@@ -708,6 +713,7 @@ std::string plan_key(const SaConvArgs& a) {
                 a.Kpad, a.epi, (int)(a.stats != nullptr), a.up, (int)(a.gate != nullptr), (int)(a.res != nullptr),
                 (int)(a.ws != nullptr && a.counters != nullptr));
   std::string k(buf);
+  if (a.in_stats) k += "|i";  // folded input norm (direct kernel only)
   if (side_branch()) k += "|b";  // side-branch conv (ScopedSideBranch): tuned for co-residency
   return k;
 }

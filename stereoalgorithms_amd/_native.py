@@ -84,6 +84,7 @@ class SaConvArgs(C.Structure):
         ("up", C.c_int32), ("cout_real", C.c_int32), ("gate", C.c_void_p), ("gate_stride", C.c_int32),
         ("stats_slots", C.c_int32), ("cin_real", C.c_int32),
         ("tapw", C.c_void_p), ("taps", C.c_int32),
+        ("in_stats", C.c_void_p), ("in_slots", C.c_int32), ("in_eps", C.c_float),
     ]
 
 
@@ -97,7 +98,7 @@ class SaNormArgs(C.Structure):
         ("N", C.c_int32), ("HW", C.c_int32), ("C", C.c_int32),
         ("act", C.c_int32), ("act2", C.c_int32),
         ("eps", C.c_float), ("alpha", C.c_float),
-        ("stat_slots", C.c_int32),
+        ("stat_slots", C.c_int32), ("res_act", C.c_int32),
     ]
 
 

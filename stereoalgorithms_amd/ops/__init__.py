@@ -143,11 +143,13 @@ def pack_conv_weight(w: torch.Tensor, segs: Sequence[tuple[int, int]] | None = N
 def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1, act="none",
            act2="none", res=None, out=None, epi="store", scale=1.0, alpha=0.01, stats=None,
            ctx=None, aux=None, hbuf=None, rh=None, tile_cfg=-1, splitk=1, workspace=None, up=0, cout_real=0,
-           gate=None, stats_slots=1, cin_real=0, tapw=None, taps=0, launch=True):
+           gate=None, stats_slots=1, cin_real=0, tapw=None, taps=0, launch=True, in_stats=None, in_slots=1,
+           in_eps=1e-5):
     """NHWC fp16 implicit-GEMM conv.  ``splitk``: 1 = off, 0 = auto, >1 = forced; needs
     ``workspace`` = (fp32 slab tensor, int32 counter tensor zero-initialised).  ``up`` = 2: transposed
     conv, the 4 parity classes (cout = 4 * cout_real) are scattered to a 2x output.  ``gate``: fp16
-    NHWC multiplier applied after the activation."""
+    NHWC multiplier applied after the activation.  ``in_stats`` (int64 [in_slots][N][Cin][2], the direct
+    64-channel kernel only): ``xs`` is a conv's raw output and the conv reads relu(IN(xs)) instead."""
     if isinstance(xs, torch.Tensor):
         xs = [xs]
     n, h, w, _ = xs[0].shape
@@ -207,6 +209,9 @@ def conv2d(xs, wpacked, kpad, cout, kh, kw, bias=None, stride=1, pad=None, dil=1
         a.stats_slots = stats_slots
     if tapw is not None:  # epi "tapproj": fp16 [taps][cout] projection weights; out fp32 [n,h,w,(cout//128)*taps]
         a.tapw, a.taps = tapw.data_ptr(), taps
+    if in_stats is not None:
+        assert in_stats.dtype == torch.int64
+        a.in_stats, a.in_slots, a.in_eps = in_stats.data_ptr(), in_slots, in_eps
     a.tile_cfg = tile_cfg
     a.splitk = splitk
     if workspace is not None:
@@ -235,8 +240,10 @@ def tapproj_stencil(P, taps, oc, bias, flow):
     return flow
 
 
-def instnorm_apply(x, stats, act="none", res=None, res_stats=None, act2="none", eps=1e-5, out=None, slots=1):
-    """slots > 1: stats (and res_stats) hold that many [N][C][2] copies, summed by the kernel."""
+def instnorm_apply(x, stats, act="none", res=None, res_stats=None, act2="none", eps=1e-5, out=None, slots=1,
+                   res_act="none"):
+    """slots > 1: stats (and res_stats) hold that many [N][C][2] copies, summed by the kernel.  ``res_act``: the
+    activation of the normalised residual (with ``res_stats``)."""
     n, h, w, c = x.shape
     out = torch.empty_like(x) if out is None else out
     a = N.SaNormArgs()
@@ -251,6 +258,7 @@ def instnorm_apply(x, stats, act="none", res=None, res_stats=None, act2="none", 
     a.act, a.act2 = N.ACT[act], N.ACT[act2]
     a.eps, a.alpha = eps, 0.01
     a.stat_slots = slots
+    a.res_act = N.ACT[res_act]
     N.check(N.dev().sa_instnorm_apply(C.byref(a), _stream()), "sa_instnorm_apply")
     return out
 

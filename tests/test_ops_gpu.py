@@ -485,6 +485,67 @@ def test_conv3x3_c64_direct2_residual(n, hw, act2):
     assert rel_err(nchw(out), ref) < 2e-3
 
 
+@pytest.mark.parametrize("n,hw,stats,act", [(2, (17, 70), True, "none"), (1, (48, 128), False, "relu"),
+                                            (3, (5, 9), True, "none"), (2, (33, 190), True, "leaky"),
+                                            (300, (2, 64), True, "none"), (4, (64, 640), True, "none")])
+def test_conv3x3_c64_direct2_folded_input_norm(n, hw, stats, act):
+    """Direct conv v2 (tile_cfg 23) with the input instance norm folded in (SaConvArgs.in_stats): the conv reads a
+    raw conv output and normalises its DMA'd pieces in LDS one tile ahead (-65504 padding -> relu(IN) = 0) --
+    BITWISE the conv of instnorm_apply's relu(IN(x)) (same arithmetic), output statistics included; many images per
+    workgroup (the per-image mean / rstd slots), tails in both dims.  Other tactics refuse in_stats."""
+    O = ops()
+    torch.manual_seed(35)
+    raw = (torch.randn(n, *hw, 64, device=DEV) * 3 + torch.randn(1, 1, 1, 64, device=DEV) * 5).half()
+    st_in = torch.zeros(16, n, 64, 2, dtype=torch.int64, device=DEV)
+    for r in range(16):  # spread like the conv epilogues' slotted atomics
+        part = raw.float()[:, r::16]
+        st_in[r, ..., 0] = torch.round(part.sum((1, 2)).double() * 2 ** 24).long()
+        st_in[r, ..., 1] = torch.round((part * part).sum((1, 2)).double() * 2 ** 24).long()
+    w = torch.randn(64, 64, 3, 3, device=DEV) / 24
+    b = torch.randn(64, device=DEV) * 0.1
+    wp, kpad, _ = O.pack_conv_weight(w)
+    a1 = O.instnorm_apply(raw, st_in, act="relu", slots=16)
+    kw_ref, kw_fold = {}, {}
+    if stats:
+        st_ref = torch.zeros(16, n, 64, 2, dtype=torch.int64, device=DEV)
+        st_fold = torch.zeros_like(st_ref)
+        kw_ref, kw_fold = dict(stats=st_ref, stats_slots=16), dict(stats=st_fold, stats_slots=16)
+    ref = O.conv2d(a1, wp, kpad, 64, 3, 3, bias=b.contiguous(), act=act, alpha=0.1, tile_cfg=23, **kw_ref)
+    out = O.conv2d(raw, wp, kpad, 64, 3, 3, bias=b.contiguous(), act=act, alpha=0.1, tile_cfg=23,
+                   in_stats=st_in, in_slots=16, **kw_fold)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    if stats:
+        assert torch.equal(st_fold, st_ref)
+    # and against fp32 torch: relu(instance_norm(raw)) -> conv
+    xn = F.relu(F.instance_norm(raw.float().permute(0, 3, 1, 2), eps=1e-5)).half().float()
+    r32 = F.conv2d(xn, w.half().float(), b, padding=1)
+    r32 = {"relu": F.relu, "none": lambda t: t, "leaky": lambda t: F.leaky_relu(t, 0.1)}[act](r32)
+    assert rel_err(nchw(out), r32) < 3e-3
+    with pytest.raises(RuntimeError):
+        O.conv2d(raw, wp, kpad, 64, 3, 3, bias=b.contiguous(), tile_cfg=1, in_stats=st_in, in_slots=16)
+
+
+def test_instnorm_apply_residual_activation():
+    """instnorm_apply's res_act: y = act2(res_act(IN(res)) + act(IN(x))) -- the folded stem's layer1.0 residual."""
+    O = ops()
+    torch.manual_seed(36)
+    n, hw, c = 2, (13, 40), 64
+    x = (torch.randn(n, *hw, c, device=DEV) * 2).half()
+    r = (torch.randn(n, *hw, c, device=DEV) + 0.5).half()
+
+    def stats(t):
+        st = torch.zeros(1, n, c, 2, dtype=torch.int64, device=DEV)
+        st[0, ..., 0] = torch.round(t.float().sum((1, 2)).double() * 2 ** 24).long()
+        st[0, ..., 1] = torch.round((t.float() ** 2).sum((1, 2)).double() * 2 ** 24).long()
+        return st
+    out = O.instnorm_apply(x, stats(x), act="relu", res=r, res_stats=stats(r), act2="relu", res_act="relu")
+    torch.cuda.synchronize()
+    inn = lambda t: F.instance_norm(t.float().permute(0, 3, 1, 2), eps=1e-5)
+    ref = F.relu(F.relu(inn(r)) + F.relu(inn(x)))
+    assert rel_err(nchw(out), ref) < 2e-3
+
+
 def test_conv2d_padded_channels_and_output_slice():
     O = ops()
     torch.manual_seed(2)

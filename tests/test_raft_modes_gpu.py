@@ -32,11 +32,15 @@ MODES = [
     ("fh-projection-fused-stencil", {"SA_RAFT_FH_PROJ": "1", "SA_RAFT_FH_FUSE": "1"}),
     # the fused coarse GRU level (z/r + grid barrier + q in one launch): other tiles, other summation order
     ("fused-gru-level", {"SA_RAFT_FUSED_LEVEL": "4"}),
+    # the encoders' instance-norm applies materialised again (the default folds three of them into the direct
+    # convs with instnorm_apply's arithmetic, bitwise the same conv; but the unfolded conv2 may be tuned to another
+    # tactic, i.e. another summation order)
+    ("unfolded-instance-norm", {"SA_FOLD_IN": "0"}),
 ]
 TOL = {"unfused-motion-encoder": 1e-2, "fh-projection": 5e-2, "fh-projection-fused-stencil": 5e-2,
-       "fused-gru-level": 5e-2}
+       "fused-gru-level": 5e-2, "unfolded-instance-norm": 2e-2}
 KNOBS = ("SA_RAFT_PARALLEL", "SA_RAFT_PIPELINE", "SA_RAFT_FUSE_MENC", "SA_RAFT_M2_MAIN", "SA_RAFT_CNET_FIRST",
-         "SA_RAFT_MENC", "SA_RAFT_FH_FUSE", "SA_RAFT_FH_PROJ", "SA_RAFT_FUSED_LEVEL")
+         "SA_RAFT_MENC", "SA_RAFT_FH_FUSE", "SA_RAFT_FH_PROJ", "SA_RAFT_FUSED_LEVEL", "SA_FOLD_IN")
 
 
 RT_MODES = [
@@ -47,6 +51,7 @@ RT_MODES = [
     ("motion-encoder-v2", {"SA_RAFT_MENC": "2"}),
     ("motion-encoder-v1-conflict-free", {"SA_RAFT_MENC": "3"}),
     ("fh-fused-stencil", {"SA_RAFT_FH_FUSE": "1"}),
+    ("unfolded-instance-norm", {"SA_FOLD_IN": "0"}),
 ]
 
 
