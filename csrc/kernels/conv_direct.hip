@@ -288,33 +288,33 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const Direc
       nrm_img = n;
     }
   };
-  // NIN: this wave's own (landed) pieces of tile t0 + kk -> relu(IN(.)) in place
+  // NIN: this wave's own (landed) pieces of tile t0 + kk -> relu(IN(.)) in place; the image's mean / rstd must be in
+  // its LDS slot already (nrm_load has a barrier: called by all waves at the same point)
   auto fold_tile = [&](int kk) {
     if constexpr (NIN) {
       const int n1 = (t0 + kk) / tiles_img;
-      if (n1 != nrm_img) nrm_load(n1);
       char* ib = smem + (kk % NB) * IN_BYTES;
-      const float* d = nrm + (n1 & 1) * 128;
       // laundered lane index and a rolled loop: the tile-invariant piece decomposition is not hoisted into
       // long-lived VGPRs next to the stationary weights (the STATS variant spilled 36 of them)
       int ln = lane;
       asm volatile("" : "+v"(ln));
+      // a lane's channel chunk is the same in all its pieces: piece g = (i * 8 + wave) * 64 + ln holds chunk
+      // (g & 7) ^ v2_swz(g >> 3) = (ln & 7) ^ (4 (wave & 1) + (ln >> 4)) for every i, so its 8 means / rstds
+      // are read once per tile
+      const int q = (ln & 7) ^ (4 * (wave & 1) + (ln >> 4));
+      const float* d = nrm + (n1 & 1) * 128 + q * 8;
+      const floatx4 m0 = *reinterpret_cast<const floatx4*>(d), m1 = *reinterpret_cast<const floatx4*>(d + 4);
+      const floatx4 r0 = *reinterpret_cast<const floatx4*>(d + 64), r1 = *reinterpret_cast<const floatx4*>(d + 68);
 #pragma unroll 1
       for (int i = 0; i < V2_PER_WAVE; ++i) {
         const int ins = i * V2_WAVES + wave;
         if (ins < V2_PIECES) {
           const int g = ins * 64 + ln;
-          const int q = (g & 7) ^ v2_swz(g >> 3);
           half8 h = *reinterpret_cast<const half8*>(ib + g * 16);
 #pragma unroll
-          for (int hf = 0; hf < 2; ++hf) {  // 4 channels at a time: 8 parameter VGPRs live, not 16
-            const floatx4 m = *reinterpret_cast<const floatx4*>(d + q * 8 + hf * 4);
-            const floatx4 r = *reinterpret_cast<const floatx4*>(d + 64 + q * 8 + hf * 4);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float v = ((float)h[hf * 4 + e] - m[e]) * r[e];
-              h[hf * 4 + e] = (f16)(v > 0.f ? v : 0.f);
-            }
+          for (int e = 0; e < 8; ++e) {
+            const float v = ((float)h[e] - (e < 4 ? m0[e & 3] : m1[e & 3])) * (e < 4 ? r0[e & 3] : r1[e & 3]);
+            h[e] = (f16)(v > 0.f ? v : 0.f);
           }
           *reinterpret_cast<half8*>(ib + g * 16) = h;
         }
@@ -325,6 +325,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const Direc
   constexpr int kOpsPerTile = RES ? 4 : 2;  // buffer stores (+ residual buffer loads), range-checked, never skipped
   if constexpr (NIN) {
     if (kb > 0) {
+      nrm_load(t0 / tiles_img);
       wait_vmcnt((kb - 1 < NB - 2 ? kb - 1 : NB - 2) * V2_PER_WAVE);  // tile 0's pieces (later tiles in flight)
       fold_tile(0);
     }
@@ -358,6 +359,20 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const Direc
     }
     // every wave is past tile k-1: its buffer takes tile k+NB-1
     if (k + NB - 1 < kb) issue_tile(t + NB - 1, (k + NB - 1) % NB);
+    if constexpr (NIN) {
+      // tile k+1's pieces are normalised by the waves of channel half 1 HERE, before their MFMA loop, and by those
+      // of half 0 after their epilogue: the two waves sharing a SIMD (w, w + 4) fold while the other computes
+      if (k + 1 < kb) {
+        const int n1 = (t + 1) / tiles_img;
+        if (n1 != nrm_img) nrm_load(n1);  // block-uniform (every wave, same k)
+        if (hc == 1) {
+          // ops issued after tile k+1's DMA: tile k+2's (.. k+NB-2's) pieces and the stores of tiles since
+          const int a2 = (kb - 2 - k) < NB - 2 ? (kb - 2 - k) : NB - 2;
+          wait_vmcnt(a2 * V2_PER_WAVE + (k < NB - 2 ? k : NB - 2) * kOpsPerTile);
+          fold_tile(k + 1);
+        }
+      }
+    }
     const char* ib = smem + cur * IN_BYTES;
     floatx4 acc[2][2];
 #pragma unroll
@@ -445,7 +460,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const Direc
       st_lane[3] += floatx4{tsq[4], tsq[5], tsq[6], tsq[7]};
     }
     if constexpr (NIN) {
-      if (k + 1 < kb) {
+      if (k + 1 < kb && hc == 0) {
         // ops this wave issued after tile k+1's DMA: tile k+2's (.. k+NB-2's) pieces and the stores of the tiles
         // computed since (this one included)
         const int a2 = (kb - 2 - k) < NB - 2 ? (kb - 2 - k) : NB - 2;
