@@ -226,7 +226,10 @@ __global__ __launch_bounds__(256) void topk_kernel(const T* __restrict__ att, in
   const int n = (int)(p / ((long)H * W));
   const long hw = p - (long)n * H * W;
   const bool valid = lane < D;
-  const float v = valid ? (float)att[(((long)n * D + lane) * H * W + hw) * as] : -3.0e38f;
+  // clamped to +-3e38 (NaN -> -3e38): with an inf or NaN logit, exp(v - mx) was NaN, a NaN lane ranked 0 beside K
+  // others and the K+1-th selection was written past this pixel's K slots (past the buffer at the last pixel)
+  const float v = valid ? fminf(fmaxf((float)att[(((long)n * D + lane) * H * W + hw) * as], -3.0e38f), 3.0e38f)
+                        : -3.0e38f;
   float mx = v;
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
   const float e = valid ? __expf(v - mx) : 0.f;
@@ -239,8 +242,8 @@ __global__ __launch_bounds__(256) void topk_kernel(const T* __restrict__ att, in
   }
   const bool sel = valid && rank < K;
   const unsigned long long m = __ballot(sel);
-  if (sel) {
-    const int k = __popcll(m & ((1ull << lane) - 1ull));
+  const int k = __popcll(m & ((1ull << lane) - 1ull));
+  if (sel && k < K) {
     prob[p * K + k] = e / sum;
     disp[p * K + k] = (float)lane;
   }
@@ -345,11 +348,12 @@ __global__ void topk_regress_kernel(const T* __restrict__ cost, int cs, const fl
     float best[4];
     int bi[4];
     for (int t = 0; t < top; ++t) {
-      best[t] = -1e30f;
+      best[t] = -3.4e38f;
       bi[t] = -1;
     }
     for (int k = 0; k < K; ++k) {
-      const float v = (float)cost[(((long)n * K + k) * H * W + hw) * cs];
+      // clamped (NaN -> -3e38) so every plane ranks: a NaN cost left bi = -1, read as disp[p * K - 1]
+      const float v = fminf(fmaxf((float)cost[(((long)n * K + k) * H * W + hw) * cs], -3.0e38f), 3.0e38f);
       for (int t = 0; t < top; ++t)
         if (v > best[t]) {
           for (int u = top - 1; u > t; --u) {
@@ -363,6 +367,7 @@ __global__ void topk_regress_kernel(const T* __restrict__ cost, int cs, const fl
     }
     float den = 0.f, num = 0.f;
     for (int t = 0; t < top; ++t) {
+      if (bi[t] < 0) continue;  // K < top
       const float e = __expf(best[t] - best[0]);
       den += e;
       num += e * disp[p * K + bi[t]];

@@ -173,6 +173,45 @@ def test_topk_concat_regress_spx():
     assert rel_err(up, ref) < 1e-4
 
 
+def test_topk_nonfinite_logits_stay_in_bounds():
+    """inf / NaN attention logits or costs (an fp16 overflow upstream) select exactly K planes per pixel and never
+    write past the pixel's K slots (round 6: a NaN lane ranked 0 beside K others and the K+1-th selection was written
+    into the next pixel's slots -- past the buffer at the last pixel); top-k regression on NaN costs reads no
+    disparity before the buffer and stays finite where any plane is."""
+    from stereoalgorithms_amd import _native as N
+    import ctypes as C
+    torch.manual_seed(8)
+    n, d, h, w, K = 1, 48, 4, 8, 24
+    att = torch.randn(n, d, h, w, device=DEV)
+    att[0, 5, 0, 0] = float("inf")
+    att[0, :, 0, 1] = float("nan")
+    att[0, 7:20, 1, 2] = float("nan")
+    att[0, :, h - 1, w - 1] = float("inf")  # the last pixel
+    a32 = att.unsqueeze(-1).permute(0, 1, 2, 3, 4).contiguous()  # [n, d, h, w, 1]
+    P = n * h * w
+    guard = 64
+    prob = torch.full((P * K + guard,), -7.0, device=DEV)
+    disp = torch.full((P * K + guard,), -7.0, device=DEV)
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    N.check(N.dev().sa_topk_disparity(a32.data_ptr(), 1, 1, n, d, h, w, K, prob.data_ptr(), disp.data_ptr(), stream),
+            "sa_topk_disparity")
+    torch.cuda.synchronize()
+    assert (prob[P * K:] == -7.0).all() and (disp[P * K:] == -7.0).all()
+    dk = disp[:P * K].view(P, K)
+    assert ((dk >= 0) & (dk < d)).all()  # every slot written with a plane index
+    assert all(len(set(r.tolist())) == K for r in dk)  # K distinct planes
+    assert dk[0].tolist().count(5.0) == 1  # the +inf plane is selected
+    cost = torch.randn(n, K, h, w, 1, device=DEV)
+    cost[0, :, 0, 3] = float("nan")
+    out = torch.empty(P, device=DEV)
+    N.check(N.dev().sa_topk_regress(cost.data_ptr(), 1, 1, disp.data_ptr(), n, K, h, w, 2, out.data_ptr(), stream),
+            "sa_topk_regress")
+    torch.cuda.synchronize()
+    fin = torch.ones(P, dtype=torch.bool, device=DEV)
+    fin[3] = False
+    assert torch.isfinite(out[fin]).all()
+
+
 def test_topk_fp32_logits_near_ties():
     """fp32 selection logits (what the engine's attention / cost heads now write): logits that differ by less than
     fp16 resolution must keep their fp32 order -- rounded to fp16 they tie and the lower-index rule picks small
