@@ -206,7 +206,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_direct2_kernel(const Direc
   const int c0 = hc * 32 + kq * 8;
   // instance-norm statistics: per-lane running sums of the lane's 8 channels over its pixels, across tiles
   // of one image; row-reduced with DPP and flushed to the slotted fixed-point atomics when the image changes
-  floatx4* st_lane = reinterpret_cast<floatx4*>(smem + L::ST) + tid * 4;  // [sum 0-3, sum 4-7, sq 0-3, sq 4-7]
+  // [sum 0-3 | sum 4-7 | sq 0-3 | sq 4-7][512 lanes]: a wave's 16-B accesses are contiguous (conflict-free); the
+  // lane-major [512][4] layout put lanes 4 apart on the same banks (4-way on every ds_read / ds_write_b128):
+  // fr8 with statistics 552.7 -> 545.6 us, l1b8 139.9 -> 138.7 us (conv_bench, profiles/round6_notes.md)
+  struct StLane {
+    floatx4* b;
+    __device__ floatx4& operator[](int v) const { return b[v * 512]; }
+  } st_lane{reinterpret_cast<floatx4*>(smem + L::ST) + tid};
   if constexpr (STATS) {
 #pragma unroll
     for (int v = 0; v < 4; ++v) st_lane[v] = floatx4{0.f, 0.f, 0.f, 0.f};

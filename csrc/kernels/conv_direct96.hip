@@ -50,7 +50,7 @@ struct Geo {
   static constexpr int NB = S == 1 ? 4 : 3;                           // ring depth
   static constexpr int DUMMY = NB * BUF;
   static constexpr int BIAS = DUMMY + 1024;
-  static constexpr int ST = BIAS + C * 4;                             // per-lane IN sums [768][sum 4 | sumsq 4]
+  static constexpr int ST = BIAS + C * 4;                             // per-lane IN sums [sum 4 | sumsq 4][768]
   static constexpr int RED = ST + NW * 64 * 32;                       // flush: [12 waves][4 kq][8]
   static constexpr int SMEM = RED + NW * 4 * 8 * 4;
   static_assert(SMEM <= 163840, "LDS budget");
@@ -158,7 +158,12 @@ __global__ __launch_bounds__(768, 1) void conv3x3_c96_direct_kernel(const D96Arg
   float* bias_lds = reinterpret_cast<float*>(smem + BIAS);
   if (tid < C) bias_lds[tid] = p.bias ? p.bias[tid] : 0.f;
 
-  floatx4* st_lane = reinterpret_cast<floatx4*>(smem + ST) + tid * 2;  // [sum 0-3, sq 0-3]
+  // [sum 0-3 | sq 0-3][768 lanes]: contiguous 16-B accesses per wave (the lane-major [768][2] layout put lanes 8
+  // apart on the same banks: 2-way on every statistics ds_read / ds_write_b128)
+  struct StLane {
+    floatx4* b;
+    __device__ floatx4& operator[](int v) const { return b[v * 768]; }
+  } st_lane{reinterpret_cast<floatx4*>(smem + ST) + tid};
   if constexpr (STATS) st_lane[0] = st_lane[1] = floatx4{0.f, 0.f, 0.f, 0.f};
   int stat_img = -1;
   auto flush_stats = [&]() {
