@@ -16,6 +16,11 @@ int sa_engine_set_q(void* engine, const float* q16);
 int sa_engine_set_rectify_maps(void* engine, const float* map_left, const float* map_right);
 int sa_engine_run_device(void* engine, const void* left, const void* right, float* disp,
                          float* cloud, int rectify, void* stream, void* rect_left, void* rect_right);
+// Host buffers in / out.  A caller buffer passed for the same role (left, right, disp, cloud) on two consecutive
+// frames is mapped into the GPU (hipHostRegister) and read / written by the frame graph over PCIe; it stays mapped
+// until a different buffer is passed for that role or the engine is destroyed, so it must not be freed (or
+// reallocated at the same address) before then.  Transient buffers: use sa_engine_host_buffers' staging instead,
+// or SA_HOST_REGISTER=0 (copies through the pinned staging).
 int sa_engine_run_host(void* engine, void* left, void* right, float* disp, float* cloud,
                        int rectify);
 long long sa_engine_device_bytes(void* engine);

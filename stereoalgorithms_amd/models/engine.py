@@ -216,20 +216,45 @@ class NativeStereoEngine:
                  out: np.ndarray | None = None, cloud_out: np.ndarray | None = None):
         """The reference's timed region: host BGR in, host disparity (+cloud) out.  ``out`` / ``cloud_out``: caller
         arrays to write (the reference's caller-allocated point cloud, RAFTStereo/test/main.cpp:20), e.g. the
-        engine's own pinned buffers from host_buffers(); fresh arrays otherwise."""
+        engine's own pinned buffers from host_buffers(); fresh arrays otherwise.
+
+        Caller arrays passed on two consecutive frames are mapped into the GPU and stay mapped until another array is
+        passed for that role or the engine is closed (sa_engine_run_host): keep them alive that long.  Arrays this
+        wrapper would create per call -- fresh outputs, contiguous / uint8 copies of the inputs -- never reach the
+        engine: they go through its pinned staging (a freed temporary re-allocated at the same address would
+        otherwise hit a stale mapping)."""
         b, h, w = self.batch, self.height, self.width
-        left = np.ascontiguousarray(left, dtype=np.uint8).reshape(b, h, w, 3)
-        right = np.ascontiguousarray(right, dtype=np.uint8).reshape(b, h, w, 3)
-        disp = out if out is not None else np.empty((b, h, w), np.float32)
+        hb = None
+        ins = []
+        for name, img in (("left", left), ("right", right)):
+            a = np.asarray(img)
+            if a.dtype == np.uint8 and a.flags["C_CONTIGUOUS"] and a.size == b * h * w * 3:
+                ins.append(a.reshape(b, h, w, 3))
+            else:  # a temporary would be made: stage it in the pinned buffer instead
+                hb = hb if hb is not None else self.host_buffers()
+                hb[name][...] = np.asarray(a, dtype=np.uint8).reshape(b, h, w, 3)
+                ins.append(hb[name])
+        left, right = ins
+        fresh_out = out is None or (cloud and cloud_out is None)
+        if fresh_out:
+            hb = hb if hb is not None else self.host_buffers()
+        disp = out if out is not None else hb["disp"]
         assert disp.shape == (b, h, w) and disp.dtype == np.float32 and disp.flags["C_CONTIGUOUS"]
         pc = None
         if cloud:
-            pc = cloud_out if cloud_out is not None else np.empty((b, h, w, 6), np.float32)
+            pc = cloud_out if cloud_out is not None else hb["cloud"]
             assert pc.shape == (b, h, w, 6) and pc.dtype == np.float32 and pc.flags["C_CONTIGUOUS"]
         N.check(self._lib.sa_engine_run_host(self._live, left.ctypes.data_as(C.c_void_p), right.ctypes.data_as(C.c_void_p),
                                              disp.ctypes.data_as(C.c_void_p),
                                              pc.ctypes.data_as(C.c_void_p) if pc is not None else None,
                                              int(rectify)), "engine run_host")
+        if out is None:
+            disp = disp.copy()
+        if cloud and cloud_out is None:
+            pc = pc.copy()
+        if hb is not None:  # inputs staged in the pinned buffers are overwritten by the next call
+            left = left.copy() if left is hb["left"] else left
+            right = right.copy() if right is hb["right"] else right
         return (disp, pc, left, right) if cloud else (disp, left, right)
 
     def low_res_flow(self) -> int:
