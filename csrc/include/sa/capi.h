@@ -25,7 +25,8 @@ int sa_engine_run_host(void* engine, void* left, void* right, float* disp, float
                        int rectify);
 long long sa_engine_device_bytes(void* engine);
 // run_host's pinned staging (pass these pointers back to run_host to skip the host-side copies) and the timing
-// split of the last run_host (ms: total, input copies, enqueue, wait + output copies[, H2D, graph, D2H])
+// split of the last run_host (ms: total, input copies, enqueue, wait + output copies[, H2D, graph, D2H]; H2D is -1
+// when the frame graph read the images itself over PCIe -- zero-copy inputs -- and 'graph' includes that read)
 void sa_engine_host_buffers(void* engine, void** left, void** right, float** disp, float** cloud);
 int sa_engine_host_times(void* engine, float* out, int max);
 const float* sa_engine_aux_output(void* engine, int* n);

@@ -670,6 +670,9 @@ void StereoEngine::run_host(uint8_t* left, uint8_t* right, float* disp, float* c
   host_times_[3] = ms(t2, t3);  // wait for the device + pinned -> caller output copies
   if (host_ev_[0]) {  // SA_HOST_TIMES=1: device-side split of the same frame
     HIP_CHECK(hipEventElapsedTime(&host_times_[4], host_ev_[0], host_ev_[1]));  // H2D
+    // zero-copy inputs: the frame graph's first node reads the images over PCIe, so nothing lies between the first
+    // two events -- the H2D is inside 'graph' (reporting ~0 ms here misread against round-4 records)
+    if (host_in) host_times_[4] = -1.f;
     HIP_CHECK(hipEventElapsedTime(&host_times_[5], host_ev_[1], host_ev_[2]));  // frame graph
     HIP_CHECK(hipEventElapsedTime(&host_times_[6], host_ev_[2], host_ev_[3]));  // D2H
   }

@@ -206,7 +206,8 @@ class NativeStereoEngine:
                 "cloud": view(ptrs[3], (b, h, w, 6), C.c_float, np.float32)}
 
     def host_times(self) -> dict:
-        """Timing split of the last run_host in ms (device-side entries need SA_HOST_TIMES=1 at creation)."""
+        """Timing split of the last run_host in ms (device-side entries need SA_HOST_TIMES=1 at creation; h2d is -1
+        when the frame graph read the inputs itself over PCIe, zero-copy inputs, and graph includes that read)."""
         t = (C.c_float * 8)()
         n = self._lib.sa_engine_host_times(self._live, t, 8)
         keys = ("total", "input_copies", "enqueue", "wait_and_output_copies", "h2d", "graph", "d2h")
