@@ -108,6 +108,10 @@ typedef struct {
 } SaConvArgs;
 
 int sa_conv2d(const SaConvArgs* a, hipStream_t stream);
+// pointwise 1x1 / stride 1 conv for narrow GEMMs (tile_cfg 35): Cin <= 256 (multiple of 8), Cout <= 192, NHWC fp16
+// over M pixels; y = act(acc * scale + bias) [; y = act2(y + res)] -> fp16
+int sa_conv_pw(const void* x, int xs, int Cin, const void* w, int Kpad, const float* bias, void* out, int os, long M,
+               int Cout, int act, float alpha, float scale, const void* res, int rs, int act2, hipStream_t stream);
 // direct 3x3x3 / stride 1 / pad 1 conv over NDHWC fp16 volumes with Cin in {8, 16, 32}, Cout <= 32 (tile_cfg 34):
 // y = act(acc * scale + bias) [* gate[n][h][w][c]] -> fp16
 int sa_conv3d_small(const void* x, int xs, int Cin, const void* w, int Kpad, const float* bias, void* out, int os,

@@ -2619,6 +2619,19 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
                              a->out_stride, a->N, a->Di, a->H, a->W, a->Cout, a->act, a->alpha, a->scale, a->gate,
                              a->gate_stride, stream);
     }
+    case 35: {
+      // pointwise 1x1 stride-1 conv for narrow GEMMs (conv_pw.hip): one source of <= 256 channels, <= 192 outputs,
+      // store epilogue with optional residual
+      const bool ok = a->nsrc == 1 && a->src[0].channels == a->Cin && a->Cin <= 256 && a->Cout <= 192 &&
+                      a->KH == 1 && a->KW == 1 && a->KD <= 0 && a->sh == 1 && a->sw == 1 && a->ph == 0 &&
+                      a->pw == 0 && a->dh == 1 && a->dw == 1 && a->up == 0 && !a->gate && !a->stats &&
+                      a->epi == SA_EPI_STORE && a->Ho == a->H && a->Wo == a->W;
+      if (!ok) return -5;
+      note_split(1, 0, 0);
+      return sa_conv_pw(a->src[0].ptr, a->src[0].stride, a->Cin, a->weight, a->Kpad, a->bias, a->out, a->out_stride,
+                        (long)a->N * a->H * a->W, a->Cout, a->act, a->alpha, a->scale, a->res, a->res_stride,
+                        a->act2, stream);
+    }
     case 25: {
       // strided 1x1 conv (conv_point.hip): 64 -> 96 / 96 -> 128, weights in registers, no LDS
       const bool ok = a->nsrc == 1 && a->src[0].channels == a->Cin && a->KH == 1 && a->KW == 1 && a->ph == 0 &&

@@ -526,6 +526,41 @@ def test_conv3x3_c64_direct2_folded_input_norm(n, hw, stats, act):
         O.conv2d(raw, wp, kpad, 64, 3, 3, bias=b.contiguous(), tile_cfg=1, in_stats=st_in, in_slots=16)
 
 
+@pytest.mark.parametrize("n,hw,cin,cout,act,res", [(2, (60, 80), 16, 96, "relu6", False),
+                                                    (2, (30, 40), 24, 144, "relu6", False),
+                                                    (1, (30, 40), 144, 24, "none", True),
+                                                    (3, (7, 9), 8, 20, "leaky", False),
+                                                    (1, (15, 20), 256, 192, "relu", True),
+                                                    (2, (5, 13), 32, 192, "none", False)])
+def test_conv_pointwise_narrow(n, hw, cin, cout, act, res):
+    """Pointwise 1x1 conv (tile_cfg 35: one wave per 16 pixels x all <= 192 columns, transposed MFMA product):
+    odd pixel counts (partial last tile), K and N not multiples of 32 / 16, residual from a channel slice of a wider
+    tensor, output into a channel slice."""
+    O = ops()
+    torch.manual_seed(51)
+    x = torch.randn(n, cin, *hw, device=DEV)
+    w = torch.randn(cout, cin, 1, 1, device=DEV) / math.sqrt(cin)
+    b = torch.randn(cout, device=DEV) * 0.1
+    ref = F.conv2d(x.half().float(), w.half().float(), b)
+    acts = {"relu": F.relu, "none": lambda t: t, "leaky": lambda t: F.leaky_relu(t, 0.1),
+            "relu6": lambda t: t.clamp(0, 6)}
+    ref = acts[act](ref)
+    wp, kpad, _ = O.pack_conv_weight(w)
+    kw = {}
+    if res:
+        big = torch.randn(n, *hw, cout + 8, device=DEV).half()
+        r = big[..., 8:]
+        kw = dict(res=r, act2="none")
+        ref = ref + nchw(r)
+    outbuf = torch.zeros(n, *hw, cout + 4, device=DEV, dtype=torch.float16)
+    out = outbuf[..., 4:]
+    O.conv2d(nhwc(x).half(), wp, kpad, cout, 1, 1, bias=b.contiguous(), act=act, alpha=0.1, tile_cfg=35, out=out,
+             pad=0, **kw)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(out), ref) < 2e-3
+    assert (outbuf[..., :4] == 0).all()
+
+
 def test_instnorm_apply_residual_activation():
     """instnorm_apply's res_act: y = act2(res_act(IN(res)) + act(IN(x))) -- the folded stem's layer1.0 residual."""
     O = ops()
