@@ -561,6 +561,42 @@ def test_conv_pointwise_narrow(n, hw, cin, cout, act, res):
     assert (outbuf[..., :4] == 0).all()
 
 
+@pytest.mark.parametrize("n,hw,cins,cout,act,res", [(2, (60, 80), (32,), 32, "leaky", False),
+                                                     (2, (30, 40), (24, 24), 48, "relu", False),
+                                                     (1, (17, 70), (8,), 20, "none", False),
+                                                     (1, (20, 50), (64,), 64, "relu", True),
+                                                     (2, (9, 33), (48,), 36, "none", False),
+                                                     (1, (24, 40), (32, 32), 64, "leaky", False),
+                                                     (3, (5, 7), (16,), 16, "relu", True)])
+def test_conv2d_small_direct(n, hw, cins, cout, act, res):
+    """Direct 3x3 conv for small channel counts (tile_cfg 36: 8 x 32 blocks, the 10 x 34 patch in LDS once for all 9
+    taps, transposed MFMA): one or two channel-concatenated sources, tails in both dims, Cout not a multiple of 16,
+    residual from a channel slice, output into a channel slice."""
+    O = ops()
+    torch.manual_seed(53)
+    cin = sum(cins)
+    xs = [torch.randn(n, c, *hw, device=DEV) for c in cins]
+    x = torch.cat(xs, 1)
+    w = torch.randn(cout, cin, 3, 3, device=DEV) / math.sqrt(cin * 9)
+    b = torch.randn(cout, device=DEV) * 0.1
+    ref = F.conv2d(x.half().float(), w.half().float(), b, padding=1)
+    ref = {"relu": F.relu, "none": lambda t: t, "leaky": lambda t: F.leaky_relu(t, 0.1)}[act](ref)
+    wp, kpad, _ = O.pack_conv_weight(w)
+    kw = {}
+    if res:
+        big = torch.randn(n, *hw, cout + 8, device=DEV).half()
+        r = big[..., 8:]
+        kw = dict(res=r, act2="none")
+        ref = ref + nchw(r)
+    outbuf = torch.zeros(n, *hw, cout + 4, device=DEV, dtype=torch.float16)
+    out = outbuf[..., 4:]
+    O.conv2d([nhwc(t).half() for t in xs], wp, kpad, cout, 3, 3, bias=b.contiguous(), act=act, alpha=0.1,
+             tile_cfg=36, out=out, **kw)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(out), ref) < 2e-3
+    assert (outbuf[..., :4] == 0).all()
+
+
 def test_instnorm_apply_residual_activation():
     """instnorm_apply's res_act: y = act2(res_act(IN(res)) + act(IN(x))) -- the folded stem's layer1.0 residual."""
     O = ops()

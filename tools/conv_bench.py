@@ -48,6 +48,12 @@ SHAPES = {
     # same GEMM as zr8 / q8 but 1x1 over K = 3456 channels: no im2col re-reads (isolates the gather's
     # cache traffic from the main loop)
     "zr8g": (8, 120, 160, 3456, 256, 1, 1),
+    # Fast-ACVNet+ small-channel 3x3 convs (tactic 36 candidates) and its 1x1 expand (tactic 35)
+    "fa32": (2, 240, 320, 32, 32, 3, 1),
+    "fa48": (2, 120, 160, 48, 48, 3, 1),
+    "fa64": (1, 240, 320, 64, 64, 3, 1),
+    "fa16": (2, 120, 160, 32, 16, 3, 1),
+    "faex": (2, 240, 320, 16, 96, 1, 1),
     "q8g": (8, 120, 160, 3456, 128, 1, 1),
 }
 
