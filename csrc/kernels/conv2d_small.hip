@@ -1,5 +1,5 @@
 // Direct 3x3 / stride 1 convolution for small channel counts (tactic 36): Cin in {8, 16, 32, 48, 64} from one or two
-// channel-concatenated sources, Cout <= 64.
+// channel-concatenated sources, Cout <= 64, dilation 1, 2 or 4 ("same" padding), fp16 or fp32 output.
 //
 // Fast-ACVNet+'s feature upsampling / refinement convs (32 -> 32 at 240 x 320, 48 -> 48 and [24|24] -> 48 at
 // 120 x 160, the spx branch's [32|32] -> 64 at full resolution) and HITNet's feature extractor run 3x3 convs whose
@@ -7,10 +7,11 @@
 // input pixel 9 times (e.g. 2 x 240 x 320, 32 -> 32: 39 us at 73 TFLOP/s for 20 MB that HBM moves in 4 us,
 // profiles/round6_notes.md).  The 3-D twin of this kernel is conv3d_small.hip (tactic 34).
 //
-// One workgroup (4 waves) owns an 8 x 32 output block = 16 row fragments of 16 pixels.  Its 10 x 34 input patch x Cin
-// channels (<= 43.5 KB) is loaded into LDS ONCE and every one of the 9 taps reads its fragments there at a shifted
-// pixel offset.  K runs in the packed weights' (kh, kw, ci) order, 32 per v_mfma_f32_16x16x32_f16: a lane's 8
-// k-values are one 8-channel chunk of one tap of one pixel, one 16-B LDS read.  The product is transposed (weights
+// One workgroup (4 waves) owns an 8 x 32 output block = 16 row fragments of 16 pixels.  Its (8 + 2d) x (32 + 2d) input
+// patch x Cin channels (<= 80 KB at dilation 4) is loaded into LDS ONCE and every one of the 9 taps reads its fragments
+// there at a shifted pixel offset (HITNet's tile-update residual blocks are dilated 1 / 2 / 4).  K runs in the packed
+// weights' (kh, kw, ci) order, 32 per v_mfma_f32_16x16x32_f16: a lane's 8 k-values are one 8-channel chunk of one tap
+// of one pixel, one 16-B LDS read.  The product is transposed (weights
 // are the A operand, from L1 one k-step ahead), so a lane ends with 4 consecutive output channels of one pixel: one
 // 8-B store per fragment and column tile.  Power-of-two chunk counts XOR-swizzle the chunk by the pixel index so the
 // 16 lanes of a fragment read hit distinct 16-B bank groups.
@@ -28,9 +29,7 @@ typedef f16 half8 __attribute__((ext_vector_type(8)));
 typedef f16 half4 __attribute__((ext_vector_type(4)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-constexpr int HT = 8, WT = 32;             // output block
-constexpr int PH = HT + 2, PW = WT + 2;    // input patch 10 x 34
-constexpr int PPIX = PH * PW;              // 340
+constexpr int HT = 8, WT = 32;  // output block; input patch (HT + 2 dil) x (WT + 2 dil)
 
 struct C2Args {
   const f16* x0;  // source 0: c0 channels at pixel stride xs0
@@ -47,6 +46,8 @@ struct C2Args {
   float alpha, scale;
   const f16* res;
   int rs, act2;
+  int dil;      // dilation = padding (1, 2, 4)
+  int out_f32;  // fp32 output (SA_EPI_STORE_F32)
 };
 
 __device__ __forceinline__ float act_apply(float v, int act, float alpha) {
@@ -78,7 +79,8 @@ __device__ __forceinline__ int pslot(int pix, int chunk) {
 template <int NCH, int NCT>
 __global__ __launch_bounds__(256) void conv2d_small_kernel(const C2Args p) {
   constexpr int CIN = 8 * NCH;
-  __shared__ __attribute__((aligned(16))) char patch[PPIX * NCH * 16];
+  extern __shared__ __attribute__((aligned(16))) char patch[];  // [PH * PW pixels][NCH chunks] (pslot)
+  const int d = p.dil, PH = HT + 2 * d, PW = WT + 2 * d, PPIX = PH * PW;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r16 = lane & 15, g = lane >> 4;
@@ -91,27 +93,30 @@ __global__ __launch_bounds__(256) void conv2d_small_kernel(const C2Args p) {
   const int x0 = bx * WT, y0 = by * HT;
   const int nch0 = p.c0 >> 3;
 
-  // ---- input patch -> LDS (zero padding outside the image): every load of the thread issued before any store ----
-  constexpr int NLD = (PPIX * NCH + 255) / 256;
-  half8 pv[NLD];
+  // ---- input patch -> LDS (zero padding outside the image), 8 loads of a thread in flight before their stores ----
+  constexpr int LB = 8;
+  const int npiece = PPIX * NCH;
+  for (int k0 = 0; k0 < npiece; k0 += 256 * LB) {
+    half8 pv[LB];
 #pragma unroll
-  for (int k = 0; k < NLD; ++k) {
-    const int i = tid + 256 * k;
-    const int pix = i / NCH, c = i - pix * NCH;
-    const int py = pix / PW, px = pix - py * PW;
-    const int y = y0 - 1 + py, x = x0 - 1 + px;
+    for (int k = 0; k < LB; ++k) {
+      const int i = k0 + tid + 256 * k;
+      const int pix = i / NCH, c = i - pix * NCH;
+      const int py = pix / PW, px = pix - py * PW;
+      const int y = y0 - d + py, x = x0 - d + px;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) pv[k][j] = (f16)0.f;
-    if (i < PPIX * NCH && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W) {
-      const long q = ((long)n * p.H + y) * p.W + x;
-      pv[k] = c < nch0 ? *reinterpret_cast<const half8*>(p.x0 + q * p.xs0 + 8 * c)
-                       : *reinterpret_cast<const half8*>(p.x1 + q * p.xs1 + 8 * (c - nch0));
+      for (int j = 0; j < 8; ++j) pv[k][j] = (f16)0.f;
+      if (i < npiece && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W) {
+        const long q = ((long)n * p.H + y) * p.W + x;
+        pv[k] = c < nch0 ? *reinterpret_cast<const half8*>(p.x0 + q * p.xs0 + 8 * c)
+                         : *reinterpret_cast<const half8*>(p.x1 + q * p.xs1 + 8 * (c - nch0));
+      }
     }
-  }
 #pragma unroll
-  for (int k = 0; k < NLD; ++k) {
-    const int i = tid + 256 * k;
-    if (i < PPIX * NCH) *reinterpret_cast<half8*>(patch + pslot<NCH>(i / NCH, i % NCH)) = pv[k];
+    for (int k = 0; k < LB; ++k) {
+      const int i = k0 + tid + 256 * k;
+      if (i < npiece) *reinterpret_cast<half8*>(patch + pslot<NCH>(i / NCH, i % NCH)) = pv[k];
+    }
   }
   __syncthreads();
 
@@ -143,7 +148,7 @@ __global__ __launch_bounds__(256) void conv2d_small_kernel(const C2Args p) {
     const int u = 4 * ks + g;  // this lane's chunk of the (tap, chunk) sequence
     const int tap = u / NCH, c = u - tap * NCH;
     const bool live = tap < 9;
-    const int toff = (tap / 3) * PW + tap % 3;
+    const int toff = ((tap / 3) * PW + tap % 3) * d;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       half8 a;
@@ -181,14 +186,24 @@ __global__ __launch_bounds__(256) void conv2d_small_kernel(const C2Args p) {
         v[r] = act_apply(acc[i][j][r] * p.scale + (p.bias && cc < p.Cout ? p.bias[cc] : 0.f), p.act, p.alpha);
         if (p.res && cc < p.Cout) v[r] = act_apply(v[r] + (float)(full ? r4[r] : p.res[pix * p.rs + cc]), p.act2, p.alpha);
       }
-      f16* op = p.out + pix * p.os + co;
-      if (full) {
-        half4 h;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) h[r] = (f16)v[r];
-        *reinterpret_cast<half4*>(op) = h;
+      if (p.out_f32) {
+        float* op = reinterpret_cast<float*>(p.out) + pix * p.os + co;
+        typedef float floatx2 __attribute__((ext_vector_type(2)));
+        if (full) {  // two 8-B stores: fp32 rows of an even (not necessarily 4-aligned) width, e.g. HITNet's 34
+          reinterpret_cast<floatx2*>(op)[0] = floatx2{v[0], v[1]};
+          reinterpret_cast<floatx2*>(op)[1] = floatx2{v[2], v[3]};
+        } else
+          for (int r = 0; co + r < p.Cout; ++r) op[r] = v[r];
       } else {
-        for (int r = 0; co + r < p.Cout; ++r) op[r] = (f16)v[r];
+        f16* op = p.out + pix * p.os + co;
+        if (full) {
+          half4 h;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) h[r] = (f16)v[r];
+          *reinterpret_cast<half4*>(op) = h;
+        } else {
+          for (int r = 0; co + r < p.Cout; ++r) op[r] = (f16)v[r];
+        }
       }
     }
   }
@@ -196,11 +211,12 @@ __global__ __launch_bounds__(256) void conv2d_small_kernel(const C2Args p) {
 
 template <int NCH>
 int launch_nct(const C2Args& a, dim3 grid, hipStream_t s) {
+  const unsigned lds = (unsigned)((HT + 2 * a.dil) * (WT + 2 * a.dil) * NCH * 16);
   switch ((a.Cout + 15) / 16) {
-    case 1: hipLaunchKernelGGL((conv2d_small_kernel<NCH, 1>), grid, dim3(256), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((conv2d_small_kernel<NCH, 2>), grid, dim3(256), 0, s, a); break;
-    case 3: hipLaunchKernelGGL((conv2d_small_kernel<NCH, 3>), grid, dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL((conv2d_small_kernel<NCH, 4>), grid, dim3(256), 0, s, a); break;
+    case 1: hipLaunchKernelGGL((conv2d_small_kernel<NCH, 1>), grid, dim3(256), lds, s, a); break;
+    case 2: hipLaunchKernelGGL((conv2d_small_kernel<NCH, 2>), grid, dim3(256), lds, s, a); break;
+    case 3: hipLaunchKernelGGL((conv2d_small_kernel<NCH, 3>), grid, dim3(256), lds, s, a); break;
+    default: hipLaunchKernelGGL((conv2d_small_kernel<NCH, 4>), grid, dim3(256), lds, s, a); break;
   }
   return (int)hipGetLastError();
 }
@@ -209,17 +225,20 @@ int launch_nct(const C2Args& a, dim3 grid, hipStream_t s) {
 
 extern "C" int sa_conv2d_small(const void* x0, int xs0, int c0, const void* x1, int xs1, int Cin, const void* w,
                                int Kpad, const float* bias, void* out, int os, int N, int H, int W, int Cout, int act,
-                               float alpha, float scale, const void* res, int rs, int act2, hipStream_t stream) {
+                               float alpha, float scale, const void* res, int rs, int act2, int dil, int out_f32,
+                               hipStream_t stream) {
+  if (!(dil == 1 || dil == 2 || dil == 4) || (out_f32 && (res || os % 2))) return -2;
   if (!(Cin == 8 || Cin == 16 || Cin == 32 || Cin == 48 || Cin == 64) || Cout < 1 || Cout > 64 || Kpad % 32 ||
       Kpad < 9 * Cin)
     return -2;
   if (c0 < 8 || c0 % 8 || c0 > Cin || (c0 < Cin && !x1)) return -2;
-  if (xs0 % 8 || ((uintptr_t)x0 & 15) || (x1 && (xs1 % 8 || ((uintptr_t)x1 & 15))) || os % 4 || ((uintptr_t)out & 7) ||
+  if (xs0 % 8 || ((uintptr_t)x0 & 15) || (x1 && (xs1 % 8 || ((uintptr_t)x1 & 15))) || (!out_f32 && os % 4) ||
+      ((uintptr_t)out & 7) ||
       ((uintptr_t)w & 15) || (res && (rs % 4 || ((uintptr_t)res & 7))))
     return -2;
   if (N < 1 || H < 1 || W < 1) return -2;
   C2Args a{(const f16*)x0, xs0, c0, (const f16*)x1, xs1, (const f16*)w, Kpad, bias, (f16*)out, os, N, H, W, Cout,
-           act, alpha, scale, (const f16*)res, rs, act2};
+           act, alpha, scale, (const f16*)res, rs, act2, dil, out_f32};
   const long blocks = (long)N * ((H + HT - 1) / HT) * ((W + WT - 1) / WT);
   if (blocks > 0x7fffffffL) return -2;
   const dim3 grid((unsigned)blocks);

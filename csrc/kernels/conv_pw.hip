@@ -1,4 +1,6 @@
-// Pointwise (1x1, stride 1) convolution for narrow GEMMs (tactic 35): Cin <= 256, Cout <= 192.
+// Pointwise (1x1, stride 1) convolution for narrow GEMMs (tactic 35): Cin <= 256 from one or two channel-concatenated
+// sources, Cout <= 192; also the k = 2 / s = 2 transposed conv as a 1x1 conv with the parity scatter (HITNet's
+// upsampling).
 //
 // Fast-ACVNet+'s MobileNetV2 feature extractor expands 16 -> 96, 24 -> 144, 32 -> 192 channels and projects back
 // 144 -> 24, 192 -> 32 with 1x1 convs (/root/reference/README_en.md:293-295 times the whole network at 12 ms on an
@@ -28,7 +30,10 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 struct PwArgs {
   const f16* x;
   int xs;       // input pixel stride (elements)
-  int Cin;      // real input channels (multiple of 8)
+  int c0;       // channels of x (the rest, Cin - c0, come from x1)
+  const f16* x1;
+  int xs1;
+  int Cin;      // input channels (multiple of 8)
   const f16* w;  // packed [Cout_pad][Kpad]
   int Kpad;
   const float* bias;
@@ -41,6 +46,9 @@ struct PwArgs {
   const f16* res;
   int rs;
   int act2;
+  int H, W;       // the M pixels are N x H x W (up: output H, W doubled)
+  int cout_real;  // up == 2: Cout = 4 parity classes of cout_real channels, scattered to the 2x output (ConvTranspose
+                  // k = 2, s = 2 as a 1x1 conv; class pi -> row parity pi >> 1, column parity pi & 1)
 };
 
 __device__ __forceinline__ float act_apply(float v, int act, float alpha) {
@@ -76,8 +84,10 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(const PwArgs p) {
   for (int kt = 0; kt < nk; ++kt) {
     const int c = kt * 32 + g * 8;  // this lane's 8 k-values: channels c .. c + 7 of pixel px
     half8 b;
-    if (pv && c < p.Cin) {
+    if (pv && c < p.c0) {
       b = *reinterpret_cast<const half8*>(xrow + c);
+    } else if (pv && c < p.Cin) {
+      b = *reinterpret_cast<const half8*>(p.x1 + px * p.xs1 + (c - p.c0));
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) b[e] = (f16)0.f;
@@ -91,6 +101,23 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(const PwArgs p) {
   }
   // lane (r16, g) holds output channels 16 j + 4 g .. + 3 of pixel px0 + r16
   if (!pv) return;
+  if (p.cout_real > 0) {  // transposed 1x1: channel cj -> parity class cj / cout_real of the 2x output
+    const long hw = (long)p.H * p.W;
+    const long nimg = px / hw, r = px - nimg * hw;
+    const int oh = (int)(r / p.W), ow = (int)(r - (long)oh * p.W);
+#pragma unroll
+    for (int j = 0; j < NN; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int cj = 16 * j + 4 * g + i;
+        if (cj >= p.Cout) continue;
+        const int pi = cj / p.cout_real, c = cj - pi * p.cout_real;
+        const long opix = (nimg * 2 * p.H + 2 * oh + ((pi >> 1) & 1)) * 2 * p.W + 2 * ow + (pi & 1);
+        const float v = act_apply(acc[j][i] * p.scale + (p.bias ? p.bias[cj] : 0.f), p.act, p.alpha);
+        p.out[opix * p.os + c] = (f16)v;
+      }
+    return;
+  }
   f16* orow = p.out + px * p.os;
   const f16* rrow = p.res ? p.res + px * p.rs : nullptr;
 #pragma unroll
@@ -126,16 +153,19 @@ void launch_pw(const PwArgs& a, hipStream_t s) {
 
 }  // namespace
 
-extern "C" int sa_conv_pw(const void* x, int xs, int Cin, const void* w, int Kpad, const float* bias, void* out,
-                          int os, long M, int Cout, int act, float alpha, float scale, const void* res, int rs,
-                          int act2, hipStream_t stream) {
+extern "C" int sa_conv_pw(const void* x, int xs, int c0, const void* x1, int xs1, int Cin, const void* w, int Kpad,
+                          const float* bias, void* out, int os, int N, int H, int W, int Cout, int act, float alpha,
+                          float scale, const void* res, int rs, int act2, int cout_real, hipStream_t stream) {
+  const long M = (long)N * H * W;
   if (Cin < 8 || Cin % 8 || Cin > 256 || Kpad < (Cin + 31) / 32 * 32 || Kpad % 32 || Cout < 1 || Cout > 192) return -2;
-  if (xs % 8 || os % 4 || (res && rs % 4) || ((uintptr_t)x & 15) || ((uintptr_t)out & 7) || ((uintptr_t)w & 15) ||
-      (res && ((uintptr_t)res & 7)) || M < 1)
+  if (c0 < 8 || c0 % 8 || c0 > Cin || (c0 < Cin && (!x1 || xs1 % 8 || ((uintptr_t)x1 & 15)))) return -2;
+  if (cout_real > 0 && (res || Cout != 4 * cout_real)) return -2;
+  if (xs % 8 || (cout_real == 0 && os % 4) || (res && rs % 4) || ((uintptr_t)x & 15) ||
+      (cout_real == 0 && ((uintptr_t)out & 7)) || ((uintptr_t)w & 15) || (res && ((uintptr_t)res & 7)) || M < 1)
     return -2;
   if ((M + 63) / 64 > 0x7fffffffL) return -2;
-  PwArgs a{(const f16*)x, xs, Cin, (const f16*)w, Kpad, bias, (f16*)out, os, M, Cout, act, alpha, scale,
-           (const f16*)res, rs, act2};
+  PwArgs a{(const f16*)x, xs, c0, (const f16*)x1, xs1, Cin, (const f16*)w, Kpad, bias, (f16*)out, os, M, Cout, act,
+           alpha, scale, (const f16*)res, rs, act2, H, W, cout_real};
   switch ((Cout + 15) / 16) {
     case 1: launch_pw<1>(a, stream); break;
     case 2: launch_pw<2>(a, stream); break;

@@ -561,17 +561,44 @@ def test_conv_pointwise_narrow(n, hw, cin, cout, act, res):
     assert (outbuf[..., :4] == 0).all()
 
 
-@pytest.mark.parametrize("n,hw,cins,cout,act,res", [(2, (60, 80), (32,), 32, "leaky", False),
-                                                     (2, (30, 40), (24, 24), 48, "relu", False),
-                                                     (1, (17, 70), (8,), 20, "none", False),
-                                                     (1, (20, 50), (64,), 64, "relu", True),
-                                                     (2, (9, 33), (48,), 36, "none", False),
-                                                     (1, (24, 40), (32, 32), 64, "leaky", False),
-                                                     (3, (5, 7), (16,), 16, "relu", True)])
-def test_conv2d_small_direct(n, hw, cins, cout, act, res):
-    """Direct 3x3 conv for small channel counts (tile_cfg 36: 8 x 32 blocks, the 10 x 34 patch in LDS once for all 9
-    taps, transposed MFMA): one or two channel-concatenated sources, tails in both dims, Cout not a multiple of 16,
-    residual from a channel slice, output into a channel slice."""
+@pytest.mark.parametrize("n,hw,cin,cout", [(2, (30, 40), 16, 16), (1, (15, 21), 32, 12), (1, (7, 9), 24, 48)])
+def test_conv_pointwise_transposed_k2s2(n, hw, cin, cout):
+    """ConvTranspose2d(k=2, s=2) as tactic 35's 1x1 conv over 4 parity classes scattered to the 2x output (HITNet's
+    upsampling) == F.conv_transpose2d in fp32 on the same fp16 operands; two channel-concatenated sources too."""
+    O = ops()
+    torch.manual_seed(55)
+    x = torch.randn(n, cin, *hw, device=DEV)
+    wt = torch.randn(cin, cout, 2, 2, device=DEV) / math.sqrt(cin)
+    b = torch.randn(cout, device=DEV) * 0.1
+    ref = F.leaky_relu(F.conv_transpose2d(x.half().float(), wt.half().float(), b, stride=2), 0.1)
+    w1 = torch.zeros(4 * cout, cin, 1, 1, device=DEV)
+    for p in range(4):
+        w1[p * cout:(p + 1) * cout, :, 0, 0] = wt[:, :, p >> 1, p & 1].t()
+    wp, kpad, _ = O.pack_conv_weight(w1)
+    out = torch.full((n, 2 * hw[0], 2 * hw[1], cout), 7.0, device=DEV, dtype=torch.float16)
+    xh = nhwc(x).half()
+    srcs = [xh] if cin % 16 else [xh[..., :cin // 2].contiguous(), xh[..., cin // 2:].contiguous()]
+    O.conv2d(srcs, wp, kpad, 4 * cout, 1, 1, bias=b.repeat(4).contiguous(), act="leaky", alpha=0.1, tile_cfg=35,
+             out=out, pad=0, up=2, cout_real=cout)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(out), ref) < 2e-3
+
+
+@pytest.mark.parametrize("n,hw,cins,cout,act,res,dil,f32", [(2, (60, 80), (32,), 32, "leaky", False, 1, False),
+                                                             (2, (30, 40), (24, 24), 48, "relu", False, 1, False),
+                                                             (1, (17, 70), (8,), 20, "none", False, 1, False),
+                                                             (1, (20, 50), (64,), 64, "relu", True, 1, False),
+                                                             (2, (9, 33), (48,), 36, "none", False, 1, False),
+                                                             (1, (24, 40), (32, 32), 64, "leaky", False, 1, False),
+                                                             (3, (5, 7), (16,), 16, "relu", True, 1, False),
+                                                             (1, (30, 40), (32,), 32, "leaky", True, 2, False),
+                                                             (2, (19, 45), (64,), 32, "none", False, 4, False),
+                                                             (1, (33, 70), (32,), 34, "none", False, 1, True),
+                                                             (1, (15, 20), (16,), 17, "leaky", False, 2, True)])
+def test_conv2d_small_direct(n, hw, cins, cout, act, res, dil, f32):
+    """Direct 3x3 conv for small channel counts (tile_cfg 36: 8 x 32 blocks, the (8 + 2d) x (32 + 2d) patch in LDS once
+    for all 9 taps, transposed MFMA): one or two channel-concatenated sources, dilation 1 / 2 / 4, tails in both dims,
+    Cout not a multiple of 16, residual from a channel slice, fp16 output into a channel slice or fp32 output."""
     O = ops()
     torch.manual_seed(53)
     cin = sum(cins)
@@ -579,7 +606,7 @@ def test_conv2d_small_direct(n, hw, cins, cout, act, res):
     x = torch.cat(xs, 1)
     w = torch.randn(cout, cin, 3, 3, device=DEV) / math.sqrt(cin * 9)
     b = torch.randn(cout, device=DEV) * 0.1
-    ref = F.conv2d(x.half().float(), w.half().float(), b, padding=1)
+    ref = F.conv2d(x.half().float(), w.half().float(), b, padding=dil, dilation=dil)
     ref = {"relu": F.relu, "none": lambda t: t, "leaky": lambda t: F.leaky_relu(t, 0.1)}[act](ref)
     wp, kpad, _ = O.pack_conv_weight(w)
     kw = {}
@@ -588,13 +615,18 @@ def test_conv2d_small_direct(n, hw, cins, cout, act, res):
         r = big[..., 8:]
         kw = dict(res=r, act2="none")
         ref = ref + nchw(r)
-    outbuf = torch.zeros(n, *hw, cout + 4, device=DEV, dtype=torch.float16)
-    out = outbuf[..., 4:]
+    if f32:  # an even row width that is not a multiple of 4 (HITNet's 34-wide fp32 tiles)
+        outbuf = torch.zeros(n, *hw, cout + cout % 2 + 2, device=DEV, dtype=torch.float32)
+        out = outbuf[..., 2:2 + cout]
+        kw["epi"] = "store_f32"
+    else:
+        outbuf = torch.zeros(n, *hw, cout + 4, device=DEV, dtype=torch.float16)
+        out = outbuf[..., 4:]
     O.conv2d([nhwc(t).half() for t in xs], wp, kpad, cout, 3, 3, bias=b.contiguous(), act=act, alpha=0.1,
-             tile_cfg=36, out=out, **kw)
+             tile_cfg=36, out=out, dil=dil, **kw)
     torch.cuda.synchronize()
     assert rel_err(nchw(out), ref) < 2e-3
-    assert (outbuf[..., :4] == 0).all()
+    assert (outbuf[..., :2] == 0).all()
 
 
 def test_instnorm_apply_residual_activation():
