@@ -2611,29 +2611,32 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
       const bool ok = a->KD == 3 && a->KH == 3 && a->KW == 3 && sd == 1 && a->sh == 1 && a->sw == 1 && a->pd == 1 &&
                       a->ph == 1 && a->pw == 1 && a->dh == 1 && a->dw == 1 && a->nsrc == 1 &&
                       a->src[0].channels == a->Cin && (a->Cin == 8 || a->Cin == 16 || a->Cin == 32) &&
-                      a->Cout <= 32 && a->up == 0 && !a->res && !a->stats && a->epi == SA_EPI_STORE &&
-                      a->Do == a->Di && a->Ho == a->H && a->Wo == a->W;
+                      a->Cout <= 32 && (a->up == 0 || (a->up == 3 && !a->gate)) && !a->res && !a->stats &&
+                      (a->epi == SA_EPI_STORE || a->epi == SA_EPI_STORE_F32) && a->Do == a->Di && a->Ho == a->H &&
+                      a->Wo == a->W;
       if (!ok) return -5;
       note_split(1, 0, 0);
       return sa_conv3d_small(a->src[0].ptr, a->src[0].stride, a->Cin, a->weight, a->Kpad, a->bias, a->out,
                              a->out_stride, a->N, a->Di, a->H, a->W, a->Cout, a->act, a->alpha, a->scale, a->gate,
-                             a->gate_stride, stream);
+                             a->gate_stride, a->epi == SA_EPI_STORE_F32, a->up == 3 ? a->cout_real : 0, stream);
     }
     case 36: {
       // direct 3x3 / stride 1 conv for small channel counts (conv2d_small.hip): one or two sources, Cin 8-64, Cout <= 64,
       // dilation 1 / 2 / 4, fp16 store epilogue with optional residual or fp32 store
       const bool ok = (a->nsrc == 1 || a->nsrc == 2) && a->Cout <= 64 && a->KH == 3 && a->KW == 3 && a->KD <= 0 &&
                       a->sh == 1 && a->sw == 1 && a->dh == a->dw && (a->dh == 1 || a->dh == 2 || a->dh == 4) &&
-                      a->ph == a->dh && a->pw == a->dw && a->up == 0 && !a->gate && !a->stats &&
-                      (a->epi == SA_EPI_STORE || (a->epi == SA_EPI_STORE_F32 && !a->res)) && a->Ho == a->H &&
-                      a->Wo == a->W && a->src[0].channels + (a->nsrc == 2 ? a->src[1].channels : 0) == a->Cin &&
-                      (a->Cin == 8 || a->Cin == 16 || a->Cin == 32 || a->Cin == 48 || a->Cin == 64);
+                      a->ph == a->dh && a->pw == a->dw && (a->up == 0 || (a->up == 2 && !a->res)) && !a->gate &&
+                      !a->stats && (a->epi == SA_EPI_STORE || (a->epi == SA_EPI_STORE_F32 && !a->res)) &&
+                      a->Ho == a->H && a->Wo == a->W &&
+                      a->src[0].channels + (a->nsrc == 2 ? a->src[1].channels : 0) == a->Cin &&
+                      (a->Cin == 8 || a->Cin == 16 || a->Cin == 32 || a->Cin == 48 || a->Cin == 64 || a->Cin == 96);
       if (!ok) return -5;
       note_split(1, 0, 0);
       return sa_conv2d_small(a->src[0].ptr, a->src[0].stride, a->src[0].channels, a->nsrc == 2 ? a->src[1].ptr : nullptr,
                              a->nsrc == 2 ? a->src[1].stride : 0, a->Cin, a->weight, a->Kpad, a->bias, a->out,
                              a->out_stride, a->N, a->H, a->W, a->Cout, a->act, a->alpha, a->scale, a->res,
-                             a->res_stride, a->act2, a->dh, a->epi == SA_EPI_STORE_F32, stream);
+                             a->res_stride, a->act2, a->dh, a->epi == SA_EPI_STORE_F32,
+                             a->up == 2 ? a->cout_real : 0, stream);
     }
     case 35: {
       // pointwise 1x1 stride-1 conv for narrow GEMMs (conv_pw.hip): one or two sources of <= 256 channels, <= 192

@@ -1,5 +1,6 @@
-// Direct 3x3 / stride 1 convolution for small channel counts (tactic 36): Cin in {8, 16, 32, 48, 64} from one or two
-// channel-concatenated sources, Cout <= 64, dilation 1, 2 or 4 ("same" padding), fp16 or fp32 output.
+// Direct 3x3 / stride 1 convolution for small channel counts (tactic 36): Cin in {8, 16, 32, 48, 64, 96} from one or two
+// channel-concatenated sources, Cout <= 64, dilation 1, 2 or 4 ("same" padding), fp16 or fp32 output, optionally the
+// parity scatter of a k4 / s2 transposed conv.
 //
 // Fast-ACVNet+'s feature upsampling / refinement convs (32 -> 32 at 240 x 320, 48 -> 48 and [24|24] -> 48 at
 // 120 x 160, the spx branch's [32|32] -> 64 at full resolution) and HITNet's feature extractor run 3x3 convs whose
@@ -46,8 +47,11 @@ struct C2Args {
   float alpha, scale;
   const f16* res;
   int rs, act2;
-  int dil;      // dilation = padding (1, 2, 4)
-  int out_f32;  // fp32 output (SA_EPI_STORE_F32)
+  int dil;        // dilation = padding (1, 2, 4)
+  int out_f32;    // fp32 output (SA_EPI_STORE_F32)
+  int cout_real;  // > 0: Cout = 4 parity classes of cout_real channels scattered to the 2x output (a k4 / s2 / p1
+                  // transposed conv as a 3x3 conv, ops.deconv_as_conv_weight): class pi -> row parity pi >> 1,
+                  // column parity pi & 1
 };
 
 __device__ __forceinline__ float act_apply(float v, int act, float alpha) {
@@ -75,7 +79,7 @@ __device__ __forceinline__ int pslot(int pix, int chunk) {
   }
 }
 
-// NCH = Cin / 8 (1, 2, 4, 6, 8); NCT = 16-column output tiles (1..4)
+// NCH = Cin / 8 (1, 2, 4, 6, 8, 12); NCT = 16-column output tiles (1..4)
 template <int NCH, int NCT>
 __global__ __launch_bounds__(256) void conv2d_small_kernel(const C2Args p) {
   constexpr int CIN = 8 * NCH;
@@ -186,7 +190,17 @@ __global__ __launch_bounds__(256) void conv2d_small_kernel(const C2Args p) {
         v[r] = act_apply(acc[i][j][r] * p.scale + (p.bias && cc < p.Cout ? p.bias[cc] : 0.f), p.act, p.alpha);
         if (p.res && cc < p.Cout) v[r] = act_apply(v[r] + (float)(full ? r4[r] : p.res[pix * p.rs + cc]), p.act2, p.alpha);
       }
-      if (p.out_f32) {
+      if (p.cout_real > 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int cj = co + r;
+          if (cj >= p.Cout) break;
+          const int pi = cj / p.cout_real, c = cj - pi * p.cout_real;
+          const long opix = ((long)n * 2 * p.H + 2 * y + ((pi >> 1) & 1)) * 2 * p.W + 2 * x + (pi & 1);
+          if (p.out_f32) reinterpret_cast<float*>(p.out)[opix * p.os + c] = v[r];
+          else p.out[opix * p.os + c] = (f16)v[r];
+        }
+      } else if (p.out_f32) {
         float* op = reinterpret_cast<float*>(p.out) + pix * p.os + co;
         typedef float floatx2 __attribute__((ext_vector_type(2)));
         if (full) {  // two 8-B stores: fp32 rows of an even (not necessarily 4-aligned) width, e.g. HITNet's 34
@@ -226,19 +240,21 @@ int launch_nct(const C2Args& a, dim3 grid, hipStream_t s) {
 extern "C" int sa_conv2d_small(const void* x0, int xs0, int c0, const void* x1, int xs1, int Cin, const void* w,
                                int Kpad, const float* bias, void* out, int os, int N, int H, int W, int Cout, int act,
                                float alpha, float scale, const void* res, int rs, int act2, int dil, int out_f32,
-                               hipStream_t stream) {
-  if (!(dil == 1 || dil == 2 || dil == 4) || (out_f32 && (res || os % 2))) return -2;
-  if (!(Cin == 8 || Cin == 16 || Cin == 32 || Cin == 48 || Cin == 64) || Cout < 1 || Cout > 64 || Kpad % 32 ||
+                               int cout_real, hipStream_t stream) {
+  if (!(dil == 1 || dil == 2 || dil == 4) || (out_f32 && !cout_real && (res || os % 2))) return -2;
+  if (cout_real > 0 && (res || Cout != 4 * cout_real)) return -2;
+  if (!(Cin == 8 || Cin == 16 || Cin == 32 || Cin == 48 || Cin == 64 || Cin == 96) || Cout < 1 || Cout > 64 ||
+      Kpad % 32 ||
       Kpad < 9 * Cin)
     return -2;
   if (c0 < 8 || c0 % 8 || c0 > Cin || (c0 < Cin && !x1)) return -2;
-  if (xs0 % 8 || ((uintptr_t)x0 & 15) || (x1 && (xs1 % 8 || ((uintptr_t)x1 & 15))) || (!out_f32 && os % 4) ||
-      ((uintptr_t)out & 7) ||
+  if (xs0 % 8 || ((uintptr_t)x0 & 15) || (x1 && (xs1 % 8 || ((uintptr_t)x1 & 15))) ||
+      (!out_f32 && !cout_real && os % 4) || (!cout_real && ((uintptr_t)out & 7)) ||
       ((uintptr_t)w & 15) || (res && (rs % 4 || ((uintptr_t)res & 7))))
     return -2;
   if (N < 1 || H < 1 || W < 1) return -2;
   C2Args a{(const f16*)x0, xs0, c0, (const f16*)x1, xs1, (const f16*)w, Kpad, bias, (f16*)out, os, N, H, W, Cout,
-           act, alpha, scale, (const f16*)res, rs, act2, dil, out_f32};
+           act, alpha, scale, (const f16*)res, rs, act2, dil, out_f32, cout_real};
   const long blocks = (long)N * ((H + HT - 1) / HT) * ((W + WT - 1) / WT);
   if (blocks > 0x7fffffffL) return -2;
   const dim3 grid((unsigned)blocks);
@@ -247,6 +263,7 @@ extern "C" int sa_conv2d_small(const void* x0, int xs0, int c0, const void* x1, 
     case 2: return launch_nct<2>(a, grid, stream);
     case 4: return launch_nct<4>(a, grid, stream);
     case 6: return launch_nct<6>(a, grid, stream);
-    default: return launch_nct<8>(a, grid, stream);
+    case 8: return launch_nct<8>(a, grid, stream);
+    default: return launch_nct<12>(a, grid, stream);
   }
 }

@@ -46,6 +46,9 @@ struct Conv3dArgs {
   float alpha, scale;
   const f16* gate;  // [N][H][W][gs] (broadcast over depth) or null
   int gs;
+  int out_f32;    // fp32 output (SA_EPI_STORE_F32)
+  int cout_real;  // > 0: Cout = 8 parity classes of cout_real channels scattered to the 2x output volume (a k4 / s2
+                  // transposed conv3d as a 3x3x3 conv): class pi -> depth parity pi >> 2, row (pi >> 1) & 1, column pi & 1
 };
 
 __device__ __forceinline__ float act_apply(float v, int act, float alpha) {
@@ -175,6 +178,24 @@ __global__ __launch_bounds__(256) void conv3d_small_kernel(const Conv3dArgs p) {
         v[r] = act_apply(v[r], p.act, p.alpha);
         if (p.gate && cc < p.Cout) v[r] *= (float)p.gate[(((long)n * p.H + y) * p.W + x) * p.gs + cc];
       }
+      if (p.cout_real > 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int cj = co + r;
+          if (cj >= p.Cout) break;
+          const int pi = cj / p.cout_real, c = cj - pi * p.cout_real;
+          const long ovox = ((((long)n * 2 * p.D + 2 * z + (pi >> 2)) * 2 * p.H + 2 * y + ((pi >> 1) & 1)) * 2 * p.W +
+                             2 * x + (pi & 1));
+          if (p.out_f32) reinterpret_cast<float*>(p.out)[ovox * p.os + c] = v[r];
+          else p.out[ovox * p.os + c] = (f16)v[r];
+        }
+        continue;
+      }
+      if (p.out_f32) {
+        float* op = reinterpret_cast<float*>(p.out) + vox * p.os + co;
+        for (int r = 0; r < 4 && co + r < p.Cout; ++r) op[r] = v[r];
+        continue;
+      }
       f16* op = p.out + vox * p.os + co;
       if (co + 4 <= p.Cout) {
         half4 h;
@@ -192,12 +213,16 @@ __global__ __launch_bounds__(256) void conv3d_small_kernel(const Conv3dArgs p) {
 
 extern "C" int sa_conv3d_small(const void* x, int xs, int Cin, const void* w, int Kpad, const float* bias, void* out,
                                int os, int N, int D, int H, int W, int Cout, int act, float alpha, float scale,
-                               const void* gate, int gs, hipStream_t stream) {
+                               const void* gate, int gs, int out_f32, int cout_real, hipStream_t stream) {
   if (!(Cin == 8 || Cin == 16 || Cin == 32) || Cout < 1 || Cout > 32 || Kpad % 32 || Kpad < 27 * Cin) return -2;
-  if (xs % 8 || os % 4 || ((uintptr_t)x & 15) || ((uintptr_t)out & 7) || ((uintptr_t)w & 15)) return -2;
+  if (cout_real > 0 && (gate || Cout != 8 * cout_real)) return -2;
+  const bool scatter_or_f32 = cout_real > 0 || out_f32;  // element stores
+  if (xs % 8 || (!scatter_or_f32 && os % 4) || ((uintptr_t)x & 15) || (!scatter_or_f32 && ((uintptr_t)out & 7)) ||
+      ((uintptr_t)w & 15))
+    return -2;
   if (N < 1 || D < 1 || H < 1 || W < 1) return -2;
   Conv3dArgs a{(const f16*)x, xs, (const f16*)w, Kpad, bias, (f16*)out, os, N, D, H, W, Cout, act, alpha, scale,
-               (const f16*)gate, gs};
+               (const f16*)gate, gs, out_f32, cout_real};
   const long blocks = (long)N * ((D + DT - 1) / DT) * ((H + HT - 1) / HT) * ((W + WT - 1) / WT);
   if (blocks > 0x7fffffffL) return -2;
   const dim3 grid((unsigned)blocks), blk(256);

@@ -766,7 +766,7 @@ constexpr Tactic kTactics[] = {
     {33, true, false, 0, 0, 384, 128, "3x3 halo patch 12x32, 32-channel chunks, ping-pong wave groups"},
     {34, false, false, 0, 0, 0, 0, "direct 3x3x3, 8-32 channels, 2x4x32 voxel blocks"},
     {35, false, false, 0, 192, 0, 0, "pointwise 1x1, <= 256 -> <= 192 channels, one wave per 16 pixels x all columns"},
-    {36, false, false, 0, 64, 0, 0, "direct 3x3 (dilation 1 / 2 / 4), 8-64 -> <= 64 channels, 8x32 pixel blocks"},
+    {36, false, false, 0, 64, 0, 0, "direct 3x3 (dilation 1 / 2 / 4, k4s2 deconv scatter), 8-96 -> <= 64 channels, 8x32 blocks"},
 };
 
 bool known_tactic(int cfg) {

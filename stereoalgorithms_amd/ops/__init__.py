@@ -550,7 +550,7 @@ def deconv_as_conv_weight(wt: torch.Tensor) -> torch.Tensor:
 
 
 def conv3d(x, wpacked, kpad, cout, k=3, stride=1, pad=None, bias=None, act="none", alpha=0.01, gate=None,
-           up=0, cout_real=0, out=None, tile_cfg=-1):
+           up=0, cout_real=0, out=None, tile_cfg=-1, epi="store"):
     """NDHWC fp16 volume [N, D, H, W, C] conv (implicit GEMM over (kd, kh, kw, ci)).  ``gate``: fp16
     [N, H, W, >=cout] multiplied after the activation (broadcast over depth).  ``up`` = 3 scatters the
     8 parity classes of a transposed conv (cout = 8 * cout_real)."""
@@ -570,12 +570,12 @@ def conv3d(x, wpacked, kpad, cout, k=3, stride=1, pad=None, bias=None, act="none
     oc = cout_real if up else cout
     if out is None:
         shape = (n, 2 * a.Do, 2 * a.Ho, 2 * a.Wo, oc) if up else (n, a.Do, a.Ho, a.Wo, oc)
-        out = torch.zeros(shape, dtype=torch.float16, device=x.device)
+        out = torch.zeros(shape, dtype=torch.float32 if epi == "store_f32" else torch.float16, device=x.device)
     a.weight = wpacked.data_ptr()
     a.bias = bias.data_ptr() if bias is not None else None
     a.Cout, a.Kpad = cout, kpad
     a.out, a.out_stride = out.data_ptr(), out.shape[-1]
-    a.epi, a.act, a.alpha, a.scale = N.EPI["store"], N.ACT[act], alpha, 1.0
+    a.epi, a.act, a.alpha, a.scale = N.EPI[epi], N.ACT[act], alpha, 1.0
     a.tile_cfg, a.splitk = tile_cfg, 1
     a.up, a.cout_real = up, cout_real
     if gate is not None:

@@ -84,11 +84,14 @@ def test_conv3d_small_direct(cin_real, cin, cout, gated):
     assert rel_err(out.permute(0, 4, 1, 2, 3), ref) < 3e-3
 
 
-@pytest.mark.parametrize("is3d", [False, True])
-def test_transposed_conv_parity_scatter(is3d):
+@pytest.mark.parametrize("is3d,cfg,f32,cout", [(False, -1, False, 8), (True, -1, False, 8), (False, 36, False, 8),
+                                               (False, 36, True, 9), (True, 34, False, 4), (True, 34, True, 1)])
+def test_transposed_conv_parity_scatter(is3d, cfg, f32, cout):
+    """k4 / s2 / p1 transposed convs as 3x3(x3) convs over 2^d parity classes scattered to the 2x output: the
+    launcher's tile (cfg -1), the direct small-channel kernels (tactic 36 2-D, 34 3-D) with fp16 and fp32 output."""
     O = ops()
     torch.manual_seed(2)
-    n, cin, cout = 2, 16, 8
+    n, cin = 2, 16
     if is3d:
         x = torch.randn(n, cin, 6, 5, 7, device=DEV).half().float()
         wt = torch.randn(cin, cout, 4, 4, 4, device=DEV) * 0.1
@@ -97,7 +100,8 @@ def test_transposed_conv_parity_scatter(is3d):
         # equivalence of the re-packed weight, checked in fp32 first
         eq = F.conv3d(x, weq, None, 1, 1)
         wp, kpad, _ = O.pack_conv3d_weight(weq)
-        out = O.conv3d(ndhwc(x).half(), wp, kpad, 8 * cout, 3, 1, up=3, cout_real=cout)
+        out = O.conv3d(ndhwc(x).half(), wp, kpad, 8 * cout, 3, 1, up=3, cout_real=cout, tile_cfg=cfg,
+                       epi="store_f32" if f32 else "store")
         got = out.permute(0, 4, 1, 2, 3)
     else:
         x = torch.randn(n, cin, 9, 11, device=DEV).half().float()
@@ -106,8 +110,10 @@ def test_transposed_conv_parity_scatter(is3d):
         weq = O.deconv_as_conv_weight(wt)
         eq = F.conv2d(x, weq, None, 1, 1)
         wp, kpad, _ = O.pack_conv_weight(weq)
-        out = O.conv2d(nhwc(x).half(), wp, kpad, 4 * cout, 3, 3, up=2, cout_real=cout)
+        out = O.conv2d(nhwc(x).half(), wp, kpad, 4 * cout, 3, 3, up=2, cout_real=cout, tile_cfg=cfg,
+                       epi="store_f32" if f32 else "store")
         got = out.permute(0, 3, 1, 2)
+    assert got.dtype == (torch.float32 if f32 else torch.float16)
     # parity-class identity: conv output channel p*cout + o equals deconv output at parity p
     for p in range(8 if is3d else 4):
         pb, pa, pc = p & 1, (p >> 1) & 1, p >> 2

@@ -594,7 +594,9 @@ def test_conv_pointwise_transposed_k2s2(n, hw, cin, cout):
                                                              (1, (30, 40), (32,), 32, "leaky", True, 2, False),
                                                              (2, (19, 45), (64,), 32, "none", False, 4, False),
                                                              (1, (33, 70), (32,), 34, "none", False, 1, True),
-                                                             (1, (15, 20), (16,), 17, "leaky", False, 2, True)])
+                                                             (1, (15, 20), (16,), 17, "leaky", False, 2, True),
+                                                             (1, (12, 40), (48, 48), 32, "relu", False, 1, False),
+                                                             (2, (9, 20), (96,), 64, "none", True, 2, False)])
 def test_conv2d_small_direct(n, hw, cins, cout, act, res, dil, f32):
     """Direct 3x3 conv for small channel counts (tile_cfg 36: 8 x 32 blocks, the (8 + 2d) x (32 + 2d) patch in LDS once
     for all 9 taps, transposed MFMA): one or two channel-concatenated sources, dilation 1 / 2 / 4, tails in both dims,
