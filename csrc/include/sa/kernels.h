@@ -108,13 +108,13 @@ typedef struct {
 } SaConvArgs;
 
 int sa_conv2d(const SaConvArgs* a, hipStream_t stream);
-// direct 3x3 / stride 1 conv for small channel counts (tile_cfg 36): Cin in {8, 16, 32, 48, 64, 96} from one source or
+// direct 3x3 / stride 1 or 2 conv for small channel counts (tile_cfg 36; stride 2: dilation 1, no scatter): Cin in {8, 16, 32, 48, 64, 96} from one source or
 // two channel-concatenated ones (x0: c0 channels, x1: Cin - c0), Cout <= 64, dilation = padding in {1, 2, 4};
 // y = act(acc * scale + bias) [; y = act2(y + res)] -> fp16, or fp32 with out_f32 (no residual); cout_real > 0: the
 // 4 parity classes of a k4 / s2 transposed conv scattered to the 2x output (no residual)
 int sa_conv2d_small(const void* x0, int xs0, int c0, const void* x1, int xs1, int Cin, const void* w, int Kpad,
                     const float* bias, void* out, int os, int N, int H, int W, int Cout, int act, float alpha,
-                    float scale, const void* res, int rs, int act2, int dil, int out_f32, int cout_real,
+                    float scale, const void* res, int rs, int act2, int dil, int out_f32, int cout_real, int stride,
                     hipStream_t stream);
 // pointwise 1x1 / stride 1 conv for narrow GEMMs (tile_cfg 35): Cin <= 256 (multiple of 8) from x (c0 channels) and
 // x1 (the rest), Cout <= 192, NHWC fp16 over N x H x W pixels; y = act(acc * scale + bias) [; y = act2(y + res)] ->
@@ -122,12 +122,13 @@ int sa_conv2d_small(const void* x0, int xs0, int c0, const void* x1, int xs1, in
 int sa_conv_pw(const void* x, int xs, int c0, const void* x1, int xs1, int Cin, const void* w, int Kpad,
                const float* bias, void* out, int os, int N, int H, int W, int Cout, int act, float alpha, float scale,
                const void* res, int rs, int act2, int cout_real, hipStream_t stream);
-// direct 3x3x3 / stride 1 / pad 1 conv over NDHWC fp16 volumes with Cin in {8, 16, 32}, Cout <= 32 (tile_cfg 34):
+// direct 3x3x3 / pad 1 conv over NDHWC fp16 volumes with Cin in {8, 16, 32}, Cout <= 32 (tile_cfg 34), stride 1 (or 2
+// for Cin <= 16):
 // y = act(acc * scale + bias) [* gate[n][h][w][c]] -> fp16 (fp32 with out_f32); cout_real > 0: the 8 parity classes
 // of a k4 / s2 transposed conv3d scattered to the 2x output volume (no gate)
 int sa_conv3d_small(const void* x, int xs, int Cin, const void* w, int Kpad, const float* bias, void* out, int os,
                     int N, int D, int H, int W, int Cout, int act, float alpha, float scale, const void* gate, int gs,
-                    int out_f32, int cout_real, hipStream_t stream);
+                    int out_f32, int cout_real, int stride, hipStream_t stream);
 // One ConvGRU level in one launch: the z/r conv `za` (SA_EPI_GRU_ZR or SA_EPI_GRU_ZRQ), a grid-wide barrier, the q
 // conv `qa` (SA_EPI_GRU_Q), on `grid` <= 128 co-resident workgroups (64x64 deep-ring tiles, split-K slices over the
 // workspace both args carry).  `bar`: 4 zero-initialised uints owned by this level (arrivals, generation, timeout

@@ -2608,26 +2608,28 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
       // direct 3x3x3 conv for small channel counts (conv3d_small.hip): one 8 / 16 / 32-channel source, <= 32 outputs,
       // stride 1, pad 1, store epilogue with optional gate
       const int sd = a->sd > 0 ? a->sd : 1;
-      const bool ok = a->KD == 3 && a->KH == 3 && a->KW == 3 && sd == 1 && a->sh == 1 && a->sw == 1 && a->pd == 1 &&
+      const bool ok = a->KD == 3 && a->KH == 3 && a->KW == 3 && sd == a->sh && a->sh == a->sw &&
+                      (sd == 1 || (sd == 2 && a->Cin <= 16 && a->up == 0)) && a->pd == 1 &&
                       a->ph == 1 && a->pw == 1 && a->dh == 1 && a->dw == 1 && a->nsrc == 1 &&
                       a->src[0].channels == a->Cin && (a->Cin == 8 || a->Cin == 16 || a->Cin == 32) &&
                       a->Cout <= 32 && (a->up == 0 || (a->up == 3 && !a->gate)) && !a->res && !a->stats &&
-                      (a->epi == SA_EPI_STORE || a->epi == SA_EPI_STORE_F32) && a->Do == a->Di && a->Ho == a->H &&
-                      a->Wo == a->W;
+                      (a->epi == SA_EPI_STORE || a->epi == SA_EPI_STORE_F32) && a->Do == (a->Di - 1) / sd + 1 &&
+                      a->Ho == (a->H - 1) / sd + 1 && a->Wo == (a->W - 1) / sd + 1;
       if (!ok) return -5;
       note_split(1, 0, 0);
       return sa_conv3d_small(a->src[0].ptr, a->src[0].stride, a->Cin, a->weight, a->Kpad, a->bias, a->out,
                              a->out_stride, a->N, a->Di, a->H, a->W, a->Cout, a->act, a->alpha, a->scale, a->gate,
-                             a->gate_stride, a->epi == SA_EPI_STORE_F32, a->up == 3 ? a->cout_real : 0, stream);
+                             a->gate_stride, a->epi == SA_EPI_STORE_F32, a->up == 3 ? a->cout_real : 0, sd, stream);
     }
     case 36: {
       // direct 3x3 / stride 1 conv for small channel counts (conv2d_small.hip): one or two sources, Cin 8-64, Cout <= 64,
       // dilation 1 / 2 / 4, fp16 store epilogue with optional residual or fp32 store
       const bool ok = (a->nsrc == 1 || a->nsrc == 2) && a->Cout <= 64 && a->KH == 3 && a->KW == 3 && a->KD <= 0 &&
-                      a->sh == 1 && a->sw == 1 && a->dh == a->dw && (a->dh == 1 || a->dh == 2 || a->dh == 4) &&
+                      a->sh == a->sw && (a->sh == 1 || (a->sh == 2 && a->dh == 1 && a->up == 0 && a->Cin <= 32)) &&
+                      a->dh == a->dw && (a->dh == 1 || a->dh == 2 || a->dh == 4) &&
                       a->ph == a->dh && a->pw == a->dw && (a->up == 0 || (a->up == 2 && !a->res)) && !a->gate &&
                       !a->stats && (a->epi == SA_EPI_STORE || (a->epi == SA_EPI_STORE_F32 && !a->res)) &&
-                      a->Ho == a->H && a->Wo == a->W &&
+                      a->Ho == (a->H - 1) / a->sh + 1 && a->Wo == (a->W - 1) / a->sw + 1 &&
                       a->src[0].channels + (a->nsrc == 2 ? a->src[1].channels : 0) == a->Cin &&
                       (a->Cin == 8 || a->Cin == 16 || a->Cin == 32 || a->Cin == 48 || a->Cin == 64 || a->Cin == 96);
       if (!ok) return -5;
@@ -2636,7 +2638,7 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
                              a->nsrc == 2 ? a->src[1].stride : 0, a->Cin, a->weight, a->Kpad, a->bias, a->out,
                              a->out_stride, a->N, a->H, a->W, a->Cout, a->act, a->alpha, a->scale, a->res,
                              a->res_stride, a->act2, a->dh, a->epi == SA_EPI_STORE_F32,
-                             a->up == 2 ? a->cout_real : 0, stream);
+                             a->up == 2 ? a->cout_real : 0, a->sh, stream);
     }
     case 35: {
       // pointwise 1x1 stride-1 conv for narrow GEMMs (conv_pw.hip): one or two sources of <= 256 channels, <= 192

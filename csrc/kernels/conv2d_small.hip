@@ -1,4 +1,4 @@
-// Direct 3x3 / stride 1 convolution for small channel counts (tactic 36): Cin in {8, 16, 32, 48, 64, 96} from one or two
+// Direct 3x3 / stride 1 or 2 convolution for small channel counts (tactic 36): Cin in {8, 16, 32, 48, 64, 96} from one or two
 // channel-concatenated sources, Cout <= 64, dilation 1, 2 or 4 ("same" padding), fp16 or fp32 output, optionally the
 // parity scatter of a k4 / s2 transposed conv.
 //
@@ -49,6 +49,8 @@ struct C2Args {
   int rs, act2;
   int dil;        // dilation = padding (1, 2, 4)
   int out_f32;    // fp32 output (SA_EPI_STORE_F32)
+  int stride;     // 1 or 2 (input H x W -> output Ho x Wo)
+  int Ho, Wo;
   int cout_real;  // > 0: Cout = 4 parity classes of cout_real channels scattered to the 2x output (a k4 / s2 / p1
                   // transposed conv as a 3x3 conv, ops.deconv_as_conv_weight): class pi -> row parity pi >> 1,
                   // column parity pi & 1
@@ -84,11 +86,12 @@ template <int NCH, int NCT>
 __global__ __launch_bounds__(256) void conv2d_small_kernel(const C2Args p) {
   constexpr int CIN = 8 * NCH;
   extern __shared__ __attribute__((aligned(16))) char patch[];  // [PH * PW pixels][NCH chunks] (pslot)
-  const int d = p.dil, PH = HT + 2 * d, PW = WT + 2 * d, PPIX = PH * PW;
+  const int d = p.dil, st = p.stride;
+  const int PH = (HT - 1) * st + 1 + 2 * d, PW = (WT - 1) * st + 1 + 2 * d, PPIX = PH * PW;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r16 = lane & 15, g = lane >> 4;
-  const int tw = (p.W + WT - 1) / WT, th = (p.H + HT - 1) / HT;
+  const int tw = (p.Wo + WT - 1) / WT, th = (p.Ho + HT - 1) / HT;
   int b = blockIdx.x;
   const int bx = b % tw;
   b /= tw;
@@ -107,7 +110,7 @@ __global__ __launch_bounds__(256) void conv2d_small_kernel(const C2Args p) {
       const int i = k0 + tid + 256 * k;
       const int pix = i / NCH, c = i - pix * NCH;
       const int py = pix / PW, px = pix - py * PW;
-      const int y = y0 - d + py, x = x0 - d + px;
+      const int y = y0 * st - d + py, x = x0 * st - d + px;
 #pragma unroll
       for (int j = 0; j < 8; ++j) pv[k][j] = (f16)0.f;
       if (i < npiece && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W) {
@@ -129,7 +132,7 @@ __global__ __launch_bounds__(256) void conv2d_small_kernel(const C2Args p) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int f = 4 * wave + i;
-    fbase[i] = (f / 2) * PW + (f % 2) * 16 + r16;
+    fbase[i] = ((f / 2) * PW + (f % 2) * 16 + r16) * st;
   }
   floatx4 acc[4][NCT];
 #pragma unroll
@@ -174,8 +177,8 @@ __global__ __launch_bounds__(256) void conv2d_small_kernel(const C2Args p) {
   for (int i = 0; i < 4; ++i) {
     const int f = 4 * wave + i;
     const int y = y0 + f / 2, x = x0 + (f % 2) * 16 + r16;
-    if (y >= p.H || x >= p.W) continue;
-    const long pix = ((long)n * p.H + y) * p.W + x;
+    if (y >= p.Ho || x >= p.Wo) continue;
+    const long pix = ((long)n * p.Ho + y) * p.Wo + x;
 #pragma unroll
     for (int j = 0; j < NCT; ++j) {
       const int co = 16 * j + 4 * g;
@@ -196,7 +199,7 @@ __global__ __launch_bounds__(256) void conv2d_small_kernel(const C2Args p) {
           const int cj = co + r;
           if (cj >= p.Cout) break;
           const int pi = cj / p.cout_real, c = cj - pi * p.cout_real;
-          const long opix = ((long)n * 2 * p.H + 2 * y + ((pi >> 1) & 1)) * 2 * p.W + 2 * x + (pi & 1);
+          const long opix = ((long)n * 2 * p.Ho + 2 * y + ((pi >> 1) & 1)) * 2 * p.Wo + 2 * x + (pi & 1);
           if (p.out_f32) reinterpret_cast<float*>(p.out)[opix * p.os + c] = v[r];
           else p.out[opix * p.os + c] = (f16)v[r];
         }
@@ -225,7 +228,8 @@ __global__ __launch_bounds__(256) void conv2d_small_kernel(const C2Args p) {
 
 template <int NCH>
 int launch_nct(const C2Args& a, dim3 grid, hipStream_t s) {
-  const unsigned lds = (unsigned)((HT + 2 * a.dil) * (WT + 2 * a.dil) * NCH * 16);
+  const unsigned lds = (unsigned)(((HT - 1) * a.stride + 1 + 2 * a.dil) * ((WT - 1) * a.stride + 1 + 2 * a.dil) * NCH * 16);
+  if (lds > 102400) return -2;  // stride 2 with many channels: the 17 x 65 patch
   switch ((a.Cout + 15) / 16) {
     case 1: hipLaunchKernelGGL((conv2d_small_kernel<NCH, 1>), grid, dim3(256), lds, s, a); break;
     case 2: hipLaunchKernelGGL((conv2d_small_kernel<NCH, 2>), grid, dim3(256), lds, s, a); break;
@@ -240,7 +244,8 @@ int launch_nct(const C2Args& a, dim3 grid, hipStream_t s) {
 extern "C" int sa_conv2d_small(const void* x0, int xs0, int c0, const void* x1, int xs1, int Cin, const void* w,
                                int Kpad, const float* bias, void* out, int os, int N, int H, int W, int Cout, int act,
                                float alpha, float scale, const void* res, int rs, int act2, int dil, int out_f32,
-                               int cout_real, hipStream_t stream) {
+                               int cout_real, int stride, hipStream_t stream) {
+  if (!(stride == 1 || (stride == 2 && dil == 1 && !cout_real))) return -2;
   if (!(dil == 1 || dil == 2 || dil == 4) || (out_f32 && !cout_real && (res || os % 2))) return -2;
   if (cout_real > 0 && (res || Cout != 4 * cout_real)) return -2;
   if (!(Cin == 8 || Cin == 16 || Cin == 32 || Cin == 48 || Cin == 64 || Cin == 96) || Cout < 1 || Cout > 64 ||
@@ -254,8 +259,9 @@ extern "C" int sa_conv2d_small(const void* x0, int xs0, int c0, const void* x1, 
     return -2;
   if (N < 1 || H < 1 || W < 1) return -2;
   C2Args a{(const f16*)x0, xs0, c0, (const f16*)x1, xs1, (const f16*)w, Kpad, bias, (f16*)out, os, N, H, W, Cout,
-           act, alpha, scale, (const f16*)res, rs, act2, dil, out_f32, cout_real};
-  const long blocks = (long)N * ((H + HT - 1) / HT) * ((W + WT - 1) / WT);
+           act, alpha, scale, (const f16*)res, rs, act2, dil, out_f32, stride, (H - 1) / stride + 1,
+           (W - 1) / stride + 1, cout_real};
+  const long blocks = (long)N * ((a.Ho + HT - 1) / HT) * ((a.Wo + WT - 1) / WT);
   if (blocks > 0x7fffffffL) return -2;
   const dim3 grid((unsigned)blocks);
   switch (Cin / 8) {

@@ -1,4 +1,5 @@
-// Direct 3x3x3 convolution for the small-channel cost volumes of Fast-ACVNet+ (tactic 34).
+// Direct 3x3x3 convolution for the small-channel cost volumes of Fast-ACVNet+ (tactic 34): stride
+// 1, or 2 for 8 / 16 input channels (the hourglasses' downsampling convs).
 //
 // Fast-ACVNet+'s correlation stem (1 real -> 8 channels over [48, 120, 160]) and concatenation stem (32 -> 16 over
 // [24, 120, 160]) and the hourglasses' stride-1 convs (8-32 channels) ran as implicit GEMMs on 256 x 16 register
@@ -29,9 +30,13 @@ typedef f16 half8 __attribute__((ext_vector_type(8)));
 typedef f16 half4 __attribute__((ext_vector_type(4)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-constexpr int DT = 2, HT = 4, WT = 32;                   // output block
-constexpr int PD = DT + 2, PH = HT + 2, PW = WT + 2;     // input patch 4 x 6 x 34
-constexpr int PVOX = PD * PH * PW;                       // 816
+constexpr int DT = 2, HT = 4, WT = 32;  // output block
+// input patch of a stride-ST block: 4 x 6 x 34 (ST 1), 5 x 9 x 65 (ST 2)
+template <int ST>
+struct Patch {
+  static constexpr int PD = (DT - 1) * ST + 3, PH = (HT - 1) * ST + 3, PW = (WT - 1) * ST + 3;
+  static constexpr int PVOX = PD * PH * PW;
+};
 
 struct Conv3dArgs {
   const f16* x;
@@ -41,7 +46,8 @@ struct Conv3dArgs {
   const float* bias;
   f16* out;
   int os;
-  int N, D, H, W, Cout;
+  int N, D, H, W, Cout;  // input dims
+  int Do, Ho, Wo;        // output dims (stride 1: the input's)
   int act;
   float alpha, scale;
   const f16* gate;  // [N][H][W][gs] (broadcast over depth) or null
@@ -72,15 +78,16 @@ __device__ __forceinline__ int pslot(int vox, int chunk) {
   return (vox * NCH + (chunk ^ ((vox >> SH) & (NCH - 1)))) << 4;
 }
 
-// NCH = Cin / 8 (1, 2, 4); NCT = output column tiles of 16 (1 or 2)
-template <int NCH, int NCT>
+// NCH = Cin / 8 (1, 2, 4); NCT = output column tiles of 16 (1 or 2); ST = stride (1, or 2 for NCH <= 2)
+template <int NCH, int NCT, int ST = 1>
 __global__ __launch_bounds__(256) void conv3d_small_kernel(const Conv3dArgs p) {
   constexpr int CIN = 8 * NCH;
+  constexpr int PH = Patch<ST>::PH, PW = Patch<ST>::PW, PVOX = Patch<ST>::PVOX;
   __shared__ __attribute__((aligned(16))) char patch[PVOX * NCH * 16];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r16 = lane & 15, g = lane >> 4;
-  const int tw = (p.W + WT - 1) / WT, th = (p.H + HT - 1) / HT, td = (p.D + DT - 1) / DT;
+  const int tw = (p.Wo + WT - 1) / WT, th = (p.Ho + HT - 1) / HT, td = (p.Do + DT - 1) / DT;
   int b = blockIdx.x;
   const int bx = b % tw;
   b /= tw;
@@ -90,25 +97,31 @@ __global__ __launch_bounds__(256) void conv3d_small_kernel(const Conv3dArgs p) {
   const int n = b / td;
   const int x0 = bx * WT, y0 = by * HT, z0 = bz * DT;
 
-  // ---- input patch -> LDS (zero padding outside the volume): every load of the thread issued before any store ----
+  // ---- input patch -> LDS (zero padding outside the volume): a thread's loads issued in batches of up to 13 before
+  // their stores ----
   constexpr int NLD = (PVOX * NCH + 255) / 256;
-  half8 pv[NLD];
+  constexpr int LB = NLD < 13 ? NLD : 13;
 #pragma unroll
-  for (int k = 0; k < NLD; ++k) {
-    const int i = tid + 256 * k;
-    const int vox = i / NCH, c = i - vox * NCH;
-    const int pz = vox / (PH * PW), rem = vox - pz * (PH * PW);
-    const int py = rem / PW, px = rem - py * PW;
-    const int z = z0 - 1 + pz, y = y0 - 1 + py, x = x0 - 1 + px;
+  for (int k0 = 0; k0 < NLD; k0 += LB) {
+    half8 pv[LB];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) pv[k][j] = (f16)0.f;
-    if (i < PVOX * NCH && (unsigned)z < (unsigned)p.D && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W)
-      pv[k] = *reinterpret_cast<const half8*>(p.x + ((((long)n * p.D + z) * p.H + y) * p.W + x) * p.xs + 8 * c);
-  }
+    for (int k = 0; k < LB; ++k) {
+      const int i = tid + 256 * (k0 + k);
+      const int vox = i / NCH, c = i - vox * NCH;
+      const int pz = vox / (PH * PW), rem = vox - pz * (PH * PW);
+      const int py = rem / PW, px = rem - py * PW;
+      const int z = z0 * ST - 1 + pz, y = y0 * ST - 1 + py, x = x0 * ST - 1 + px;
 #pragma unroll
-  for (int k = 0; k < NLD; ++k) {
-    const int i = tid + 256 * k;
-    if (i < PVOX * NCH) *reinterpret_cast<half8*>(patch + pslot<NCH>(i / NCH, i % NCH)) = pv[k];
+      for (int j = 0; j < 8; ++j) pv[k][j] = (f16)0.f;
+      if (k0 + k < NLD && i < PVOX * NCH && (unsigned)z < (unsigned)p.D && (unsigned)y < (unsigned)p.H &&
+          (unsigned)x < (unsigned)p.W)
+        pv[k] = *reinterpret_cast<const half8*>(p.x + ((((long)n * p.D + z) * p.H + y) * p.W + x) * p.xs + 8 * c);
+    }
+#pragma unroll
+    for (int k = 0; k < LB; ++k) {
+      const int i = tid + 256 * (k0 + k);
+      if (k0 + k < NLD && i < PVOX * NCH) *reinterpret_cast<half8*>(patch + pslot<NCH>(i / NCH, i % NCH)) = pv[k];
+    }
   }
   __syncthreads();
 
@@ -117,7 +130,7 @@ __global__ __launch_bounds__(256) void conv3d_small_kernel(const Conv3dArgs p) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int f = 4 * wave + i;
-    fbase[i] = ((f / 8) * PH + (f / 2) % 4) * PW + (f % 2) * 16 + r16;
+    fbase[i] = (((f / 8) * PH + (f / 2) % 4) * PW + (f % 2) * 16 + r16) * ST;
   }
   floatx4 acc[4][NCT];
 #pragma unroll
@@ -164,8 +177,8 @@ __global__ __launch_bounds__(256) void conv3d_small_kernel(const Conv3dArgs p) {
   for (int i = 0; i < 4; ++i) {
     const int f = 4 * wave + i;
     const int z = z0 + f / 8, y = y0 + (f / 2) % 4, x = x0 + (f % 2) * 16 + r16;
-    if (z >= p.D || y >= p.H || x >= p.W) continue;
-    const long vox = (((long)n * p.D + z) * p.H + y) * p.W + x;
+    if (z >= p.Do || y >= p.Ho || x >= p.Wo) continue;
+    const long vox = (((long)n * p.Do + z) * p.Ho + y) * p.Wo + x;
 #pragma unroll
     for (int j = 0; j < NCT; ++j) {
       const int co = 16 * j + 4 * g;
@@ -176,7 +189,7 @@ __global__ __launch_bounds__(256) void conv3d_small_kernel(const Conv3dArgs p) {
         const int cc = co + r;
         v[r] = acc[i][j][r] * p.scale + (p.bias && cc < p.Cout ? p.bias[cc] : 0.f);
         v[r] = act_apply(v[r], p.act, p.alpha);
-        if (p.gate && cc < p.Cout) v[r] *= (float)p.gate[(((long)n * p.H + y) * p.W + x) * p.gs + cc];
+        if (p.gate && cc < p.Cout) v[r] *= (float)p.gate[(((long)n * p.Ho + y) * p.Wo + x) * p.gs + cc];
       }
       if (p.cout_real > 0) {
 #pragma unroll
@@ -184,7 +197,7 @@ __global__ __launch_bounds__(256) void conv3d_small_kernel(const Conv3dArgs p) {
           const int cj = co + r;
           if (cj >= p.Cout) break;
           const int pi = cj / p.cout_real, c = cj - pi * p.cout_real;
-          const long ovox = ((((long)n * 2 * p.D + 2 * z + (pi >> 2)) * 2 * p.H + 2 * y + ((pi >> 1) & 1)) * 2 * p.W +
+          const long ovox = ((((long)n * 2 * p.Do + 2 * z + (pi >> 2)) * 2 * p.Ho + 2 * y + ((pi >> 1) & 1)) * 2 * p.Wo +
                              2 * x + (pi & 1));
           if (p.out_f32) reinterpret_cast<float*>(p.out)[ovox * p.os + c] = v[r];
           else p.out[ovox * p.os + c] = (f16)v[r];
@@ -213,21 +226,31 @@ __global__ __launch_bounds__(256) void conv3d_small_kernel(const Conv3dArgs p) {
 
 extern "C" int sa_conv3d_small(const void* x, int xs, int Cin, const void* w, int Kpad, const float* bias, void* out,
                                int os, int N, int D, int H, int W, int Cout, int act, float alpha, float scale,
-                               const void* gate, int gs, int out_f32, int cout_real, hipStream_t stream) {
+                               const void* gate, int gs, int out_f32, int cout_real, int stride, hipStream_t stream) {
   if (!(Cin == 8 || Cin == 16 || Cin == 32) || Cout < 1 || Cout > 32 || Kpad % 32 || Kpad < 27 * Cin) return -2;
+  if (!(stride == 1 || (stride == 2 && Cin <= 16 && !cout_real))) return -2;  // stride 2: the 5 x 9 x 65 patch
   if (cout_real > 0 && (gate || Cout != 8 * cout_real)) return -2;
   const bool scatter_or_f32 = cout_real > 0 || out_f32;  // element stores
   if (xs % 8 || (!scatter_or_f32 && os % 4) || ((uintptr_t)x & 15) || (!scatter_or_f32 && ((uintptr_t)out & 7)) ||
       ((uintptr_t)w & 15))
     return -2;
   if (N < 1 || D < 1 || H < 1 || W < 1) return -2;
-  Conv3dArgs a{(const f16*)x, xs, (const f16*)w, Kpad, bias, (f16*)out, os, N, D, H, W, Cout, act, alpha, scale,
-               (const f16*)gate, gs, out_f32, cout_real};
-  const long blocks = (long)N * ((D + DT - 1) / DT) * ((H + HT - 1) / HT) * ((W + WT - 1) / WT);
+  const int Do = (D - 1) / stride + 1, Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  Conv3dArgs a{(const f16*)x, xs, (const f16*)w, Kpad, bias, (f16*)out, os, N, D, H, W, Cout, Do, Ho, Wo, act, alpha,
+               scale, (const f16*)gate, gs, out_f32, cout_real};
+  const long blocks = (long)N * ((Do + DT - 1) / DT) * ((Ho + HT - 1) / HT) * ((Wo + WT - 1) / WT);
   if (blocks > 0x7fffffffL) return -2;
   const dim3 grid((unsigned)blocks), blk(256);
   const bool two = Cout > 16;
-  if (Cin == 8) {
+  if (stride == 2) {
+    if (Cin == 8) {
+      if (two) hipLaunchKernelGGL((conv3d_small_kernel<1, 2, 2>), grid, blk, 0, stream, a);
+      else hipLaunchKernelGGL((conv3d_small_kernel<1, 1, 2>), grid, blk, 0, stream, a);
+    } else {
+      if (two) hipLaunchKernelGGL((conv3d_small_kernel<2, 2, 2>), grid, blk, 0, stream, a);
+      else hipLaunchKernelGGL((conv3d_small_kernel<2, 1, 2>), grid, blk, 0, stream, a);
+    }
+  } else if (Cin == 8) {
     if (two) hipLaunchKernelGGL((conv3d_small_kernel<1, 2>), grid, blk, 0, stream, a);
     else hipLaunchKernelGGL((conv3d_small_kernel<1, 1>), grid, blk, 0, stream, a);
   } else if (Cin == 16) {

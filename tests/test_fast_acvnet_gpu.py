@@ -84,6 +84,28 @@ def test_conv3d_small_direct(cin_real, cin, cout, gated):
     assert rel_err(out.permute(0, 4, 1, 2, 3), ref) < 3e-3
 
 
+@pytest.mark.parametrize("cin,cout,gated", [(8, 16, False), (16, 32, True), (16, 12, False)])
+def test_conv3d_small_stride2(cin, cout, gated):
+    """Tactic 34 at stride 2 (the hourglasses' downsampling convs; 5 x 9 x 65 input patch per 2 x 4 x 32 output block)
+    == F.conv3d(stride 2) + bias + leaky ReLU (+ gate at the output resolution), odd volume sizes."""
+    O = ops()
+    torch.manual_seed(4)
+    n, d, h, w = 1, 9, 13, 70
+    x = torch.randn(n, cin, d, h, w, device=DEV).half().float()
+    wt = torch.randn(cout, cin, 3, 3, 3, device=DEV) / (cin * 27) ** 0.5
+    b = torch.randn(cout, device=DEV) * 0.1
+    ref = F.leaky_relu(F.conv3d(x, wt, b, 2, 1), 0.01)
+    ho, wo = ref.shape[3:]
+    gate = torch.rand(n, cout, ho, wo, device=DEV).half().float() if gated else None
+    if gated:
+        ref = ref * gate.unsqueeze(2)
+    wp, kpad, _ = O.pack_conv3d_weight(wt)
+    out = O.conv3d(ndhwc(x).half(), wp, kpad, cout, 3, 2, bias=b.float(), act="leaky", tile_cfg=34,
+                   gate=nhwc(gate).half() if gated else None)
+    torch.cuda.synchronize()
+    assert rel_err(out.permute(0, 4, 1, 2, 3), ref) < 3e-3
+
+
 @pytest.mark.parametrize("is3d,cfg,f32,cout", [(False, -1, False, 8), (True, -1, False, 8), (False, 36, False, 8),
                                                (False, 36, True, 9), (True, 34, False, 4), (True, 34, True, 1)])
 def test_transposed_conv_parity_scatter(is3d, cfg, f32, cout):

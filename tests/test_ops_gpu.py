@@ -631,6 +631,29 @@ def test_conv2d_small_direct(n, hw, cins, cout, act, res, dil, f32):
     assert (outbuf[..., :2] == 0).all()
 
 
+@pytest.mark.parametrize("n,hw,cin,cout,res", [(2, (48, 64), 8, 32, False), (1, (33, 71), 32, 48, True),
+                                                (1, (20, 40), 16, 64, False), (2, (9, 17), 32, 20, False)])
+def test_conv2d_small_direct_stride2(n, hw, cin, cout, res):
+    """Tactic 36 at stride 2 (the 17 x 65 input patch in LDS, Cin <= 32): odd input sizes, residual."""
+    O = ops()
+    torch.manual_seed(57)
+    x = torch.randn(n, cin, *hw, device=DEV)
+    w = torch.randn(cout, cin, 3, 3, device=DEV) / math.sqrt(cin * 9)
+    b = torch.randn(cout, device=DEV) * 0.1
+    ref = F.relu(F.conv2d(x.half().float(), w.half().float(), b, stride=2, padding=1))
+    ho, wo = ref.shape[2:]
+    kw = {}
+    if res:
+        r = torch.randn(n, ho, wo, cout, device=DEV).half()
+        kw = dict(res=r, act2="none")
+        ref = ref + nchw(r)
+    wp, kpad, _ = O.pack_conv_weight(w)
+    out = O.conv2d(nhwc(x).half(), wp, kpad, cout, 3, 3, bias=b.contiguous(), act="relu", stride=2, tile_cfg=36, **kw)
+    torch.cuda.synchronize()
+    assert out.shape[1:3] == (ho, wo)
+    assert rel_err(nchw(out), ref) < 2e-3
+
+
 def test_instnorm_apply_residual_activation():
     """instnorm_apply's res_act: y = act2(res_act(IN(res)) + act(IN(x))) -- the folded stem's layer1.0 residual."""
     O = ops()
