@@ -117,7 +117,7 @@ int sa_conv2d_small(const void* x0, int xs0, int c0, const void* x1, int xs1, in
                     float scale, const void* res, int rs, int act2, int dil, int out_f32, int cout_real, int stride,
                     hipStream_t stream);
 // pointwise 1x1 / stride 1 conv for narrow GEMMs (tile_cfg 35): Cin <= 256 (multiple of 8) from x (c0 channels) and
-// x1 (the rest), Cout <= 192, NHWC fp16 over N x H x W pixels; y = act(acc * scale + bias) [; y = act2(y + res)] ->
+// x1 (the rest), Cout <= 256, NHWC fp16 over N x H x W pixels; y = act(acc * scale + bias) [; y = act2(y + res)] ->
 // fp16; cout_real > 0: Cout = 4 parity classes scattered to the 2x output (transposed k = 2, s = 2), no residual
 int sa_conv_pw(const void* x, int xs, int c0, const void* x1, int xs1, int Cin, const void* w, int Kpad,
                const float* bias, void* out, int os, int N, int H, int W, int Cout, int act, float alpha, float scale,

@@ -2641,11 +2641,11 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
                              a->up == 2 ? a->cout_real : 0, a->sh, stream);
     }
     case 35: {
-      // pointwise 1x1 stride-1 conv for narrow GEMMs (conv_pw.hip): one or two sources of <= 256 channels, <= 192
+      // pointwise 1x1 stride-1 conv for narrow GEMMs (conv_pw.hip): one or two sources of <= 256 channels, <= 256
       // outputs, store epilogue with optional residual, or the transposed k = 2 / s = 2 parity scatter
       const bool ok = (a->nsrc == 1 || a->nsrc == 2) &&
                       a->src[0].channels + (a->nsrc == 2 ? a->src[1].channels : 0) == a->Cin && a->Cin <= 256 &&
-                      a->Cout <= 192 && a->KH == 1 && a->KW == 1 && a->KD <= 0 && a->sh == 1 && a->sw == 1 &&
+                      a->Cout <= 256 && a->KH == 1 && a->KW == 1 && a->KD <= 0 && a->sh == 1 && a->sw == 1 &&
                       a->ph == 0 && a->pw == 0 && a->dh == 1 && a->dw == 1 && (a->up == 0 || (a->up == 2 && !a->res)) &&
                       !a->gate && !a->stats && a->epi == SA_EPI_STORE && a->Ho == a->H && a->Wo == a->W;
       if (!ok) return -5;

@@ -1,5 +1,5 @@
 // Pointwise (1x1, stride 1) convolution for narrow GEMMs (tactic 35): Cin <= 256 from one or two channel-concatenated
-// sources, Cout <= 192; also the k = 2 / s = 2 transposed conv as a 1x1 conv with the parity scatter (HITNet's
+// sources, Cout <= 256; also the k = 2 / s = 2 transposed conv as a 1x1 conv with the parity scatter (HITNet's
 // upsampling).
 //
 // Fast-ACVNet+'s MobileNetV2 feature extractor expands 16 -> 96, 24 -> 144, 32 -> 192 channels and projects back
@@ -7,7 +7,7 @@
 // RTX 3090).  As implicit GEMMs those are K = 16-32 or N = 24-32 problems on 128-wide tiles: the expand at 1/2
 // resolution (153600 pixels, 16 -> 96) took 47 us for 34 MB of traffic that HBM moves in 7 (profiles/round6_notes.md).
 //
-// Here one wave owns 16 pixels and ALL Cout columns: the product is transposed (C^T = W X^T), so the weights are the
+// Here one wave owns 16 pixels and ALL (<= 256) Cout columns: the product is transposed (C^T = W X^T), so the weights are the
 // MFMA A operand, the pixels' 8-channel chunks the B operand (one 16-B load per lane per k-step straight from the
 // NHWC input), and a lane ends with 4 consecutive output channels of one pixel per 16-column tile: one 8-B store
 // each, the 4 lane groups of a pixel writing 64 contiguous bytes.  Weight fragments come from global memory (<= 96 KB,
@@ -157,7 +157,7 @@ extern "C" int sa_conv_pw(const void* x, int xs, int c0, const void* x1, int xs1
                           const float* bias, void* out, int os, int N, int H, int W, int Cout, int act, float alpha,
                           float scale, const void* res, int rs, int act2, int cout_real, hipStream_t stream) {
   const long M = (long)N * H * W;
-  if (Cin < 8 || Cin % 8 || Cin > 256 || Kpad < (Cin + 31) / 32 * 32 || Kpad % 32 || Cout < 1 || Cout > 192) return -2;
+  if (Cin < 8 || Cin % 8 || Cin > 256 || Kpad < (Cin + 31) / 32 * 32 || Kpad % 32 || Cout < 1 || Cout > 256) return -2;
   if (c0 < 8 || c0 % 8 || c0 > Cin || (c0 < Cin && (!x1 || xs1 % 8 || ((uintptr_t)x1 & 15)))) return -2;
   if (cout_real > 0 && (res || Cout != 4 * cout_real)) return -2;
   if (xs % 8 || (cout_real == 0 && os % 4) || (res && rs % 4) || ((uintptr_t)x & 15) ||
@@ -178,7 +178,11 @@ extern "C" int sa_conv_pw(const void* x, int xs, int c0, const void* x1, int xs1
     case 9: launch_pw<9>(a, stream); break;
     case 10: launch_pw<10>(a, stream); break;
     case 11: launch_pw<11>(a, stream); break;
-    default: launch_pw<12>(a, stream); break;
+    case 12: launch_pw<12>(a, stream); break;
+    case 13: launch_pw<13>(a, stream); break;
+    case 14: launch_pw<14>(a, stream); break;
+    case 15: launch_pw<15>(a, stream); break;
+    default: launch_pw<16>(a, stream); break;
   }
   return (int)hipGetLastError();
 }

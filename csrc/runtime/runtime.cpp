@@ -765,7 +765,7 @@ constexpr Tactic kTactics[] = {
     {32, true, false, 0, 0, 512, 128, "3x3 halo patch 16x32, 32-channel chunks, ping-pong wave groups"},
     {33, true, false, 0, 0, 384, 128, "3x3 halo patch 12x32, 32-channel chunks, ping-pong wave groups"},
     {34, false, false, 0, 0, 0, 0, "direct 3x3x3, 8-32 channels, 2x4x32 voxel blocks"},
-    {35, false, false, 0, 192, 0, 0, "pointwise 1x1, <= 256 -> <= 192 channels, one wave per 16 pixels x all columns"},
+    {35, false, false, 0, 256, 0, 0, "pointwise 1x1, <= 256 -> <= 256 channels, one wave per 16 pixels x all columns"},
     {36, false, false, 0, 64, 0, 0, "direct 3x3 (dilation 1 / 2 / 4, k4s2 deconv scatter), 8-96 -> <= 64 channels, 8x32 blocks"},
 };
 

@@ -531,7 +531,9 @@ def test_conv3x3_c64_direct2_folded_input_norm(n, hw, stats, act):
                                                     (1, (30, 40), 144, 24, "none", True),
                                                     (3, (7, 9), 8, 20, "leaky", False),
                                                     (1, (15, 20), 256, 192, "relu", True),
-                                                    (2, (5, 13), 32, 192, "none", False)])
+                                                    (2, (5, 13), 32, 192, "none", False),
+                                                    (1, (30, 40), 128, 256, "relu", False),
+                                                    (1, (9, 11), 96, 232, "none", True)])
 def test_conv_pointwise_narrow(n, hw, cin, cout, act, res):
     """Pointwise 1x1 conv (tile_cfg 35: one wave per 16 pixels x all <= 192 columns, transposed MFMA product):
     odd pixel counts (partial last tile), K and N not multiples of 32 / 16, residual from a channel slice of a wider
