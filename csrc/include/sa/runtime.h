@@ -163,6 +163,18 @@ struct ScopedSideBranch {
 };
 bool side_branch();
 
+// Convs enqueued while a ScopedWgSplit(true) is alive may be tuned to the workgroup split-K tactics (37 / 38: fp32
+// partial tiles of S K-slices + a reduce / epilogue launch).  Faster alone on small-M / deep-K grids (coarse GRU
+// shapes 10-25 %), but they fill the chip for two launches: on schedules whose branches share the GPU (RAFT's
+// pipelined levels) the frame got slower (RAFT-SF b1 8.22 -> 8.59 ms, realtime 1.87 -> 1.95), on CREStereo's
+// serial chain faster (iter10 5.72 -> 5.64).  Opt-in per model; the plan key carries the mark.
+struct ScopedWgSplit {
+  bool prev;
+  explicit ScopedWgSplit(bool on);
+  ~ScopedWgSplit();
+};
+bool wg_split_allowed();
+
 // ------------------------------------------------------------------ conv tactic selection
 // The MI355X analogue of TensorRT's tactic selection at engine build (common/ONNX2TRT.cpp:111):
 // during the engine's eager tuning pass every distinct conv shape is timed over the tile / split-K

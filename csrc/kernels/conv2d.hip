@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
 
+#include <cstdint>
 #include <cstdlib>
 #include <type_traits>
 
@@ -266,11 +267,19 @@ __device__ __forceinline__ void wait_stages(int s) {
 // skI k-steps): contributor c is block b = slab_base + c, and since only a block's first and last segments
 // can be partial tiles its slab is 2b (the segment starts the block's range) or 2b + 1, so 2G slabs cover
 // any tile count.  Called once per block (grid tiling / split-K) or once per segment of a stream-K block.
-template <int BM, int BN, int WM, int WN, int MODE>
+//
+// EXT (split-K over workgroups without a cross-workgroup handshake, tactics 37 / 38): EXT = 1 runs the K range and
+// stores the fp32 partial tile into slice z of the row-major [S][M][LD] workspace p.ws (LD = Cout rounded up to 64),
+// no epilogue; EXT = 2 replaces the main loop by the sum of the p.splitk slices of its own (smaller) tile in fixed
+// order and runs the normal epilogue.  The two are separate launches on one stream, so the kernel boundary orders
+// the partials: no agent-scope release / acquire fences (~3.5 us each per workgroup, the cost that made the
+// last-arriver split slower than no split on the small coarse-level GRU grids).
+template <int BM, int BN, int WM, int WN, int MODE, int EXT = 0>
 __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const int bx, const int by, const int kt0,
                                           const int nk, const int S, const int z, const int slab_base,
                                           const int ctr, const int skG, const long skI) {
   using C = ConvCfg<BM, BN, WM, WN, MODE>;
+  static_assert(EXT == 0 || (!C::BANDED && !C::HALO), "workgroup split-K: plain tiles only");
 
   // opaque per call: in the stream-K segment loop nothing lane-dependent is hoisted out of the loop (it would
   // stay live across the main loop)
@@ -312,7 +321,35 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc32[i][j][r] = 0.f;
   }
-  if constexpr (MODE == kFastK64) {
+  if constexpr (EXT == 2) {
+    // ---------------- split-K reduction: sum the S partial slices (fixed order) into the accumulators ----------------
+    // slice layout [S][LD][Mp] (column-major: a lane's 4 accumulator rows are one 16-B load); all S x FM x FN loads
+    // are issued before the sums
+    const int LD = (p.Cout + 63) & ~63, Mp = (M + 3) & ~3;
+    const int Sx = p.splitk;
+    floatx4 part[8][C::FM][C::FN];
+#pragma unroll
+    for (int sl = 0; sl < 8; ++sl)
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) {
+          const int m = m0 + wm * C::TM + i * 16 + (lane >> 4) * 4;
+          const int n = n0 + wn * C::TN + j * 16 + (lane & 15);
+          part[sl][i][j] = (sl < Sx && m < M && n < LD)
+                               ? *reinterpret_cast<const floatx4*>(p.ws + ((size_t)sl * LD + n) * Mp + m)
+                               : floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) {
+        floatx4 v = part[0][i][j];
+#pragma unroll
+        for (int sl = 1; sl < 8; ++sl) v += part[sl][i][j];
+        acc[i][j] = v;
+      }
+  } else if constexpr (MODE == kFastK64) {
     // ---------------- uniform-k im2col, register staged, BK = 64 ----------------
     constexpr int RPT = C::A_PT;  // A rows per thread: (tid >> 3) + 32 i
     const int cth = tid & 7;
@@ -1623,6 +1660,24 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
 
   }  // register-staged path
 
+  if constexpr (EXT == 1) {
+    // workgroup split-K: this K slice's partial tile -> workspace slice z, column-major [LD][Mp] (Mp = M rounded up to
+    // 4): one 16-B store per accumulator (rows < Mp, columns < LD)
+    const int LD = (p.Cout + 63) & ~63, Mp = (M + 3) & ~3;
+    float* dst = p.ws + (size_t)z * LD * Mp;
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) {
+        const int m = m0 + wm * C::TM + i * 16 + (lane >> 4) * 4;
+        const int n = n0 + wn * C::TN + j * 16 + (lane & 15);
+        // non-temporal: the partials bypass this XCD's L2 (the reduce launch reads them from other XCDs, and the
+        // end-of-kernel write-back of ~10 MB of dirty L2 lines is not on the chain)
+        if (m < M && n < LD) __builtin_nontemporal_store(acc[i][j], reinterpret_cast<floatx4*>(dst + (size_t)n * Mp + m));
+      }
+    return;
+  }
+
   // ---------------- split-K: partial slabs + last-arriver reduction ----------------
   // Protocol of cdna_hip_programming.md "Projection GEMM at M = 256" item 2 (agent-scope release
   // by every slice, acquire by the last arriver), valid for any placement of slices over XCDs.
@@ -2287,6 +2342,59 @@ int launch_glds3(const SaConvArgs* a, hipStream_t stream, bool forced) {
   return (int)hipGetLastError();
 }
 
+// Workgroup split-K (tactics 37 / 38): the small-M, deep-K convs of the coarse GRU levels at batch 1 (M = 1200 /
+// 4800 pixels, K = 2304 / 3456) give 38-228 tiles of a 256-CU chip, each walking 36-54 k-steps at the DMA gather
+// rate of ONE CU.  Here S workgroups share a tile's K range and store fp32 partials (conv_tile EXT = 1), and a second
+// launch sums them per 32 x 64 tile and runs the conv's epilogue (EXT = 2; GRU gates, statistics, residual, ...).
+template <int BM, int BN, int WM, int WN, int MODE>
+__global__ __launch_bounds__(64 * WM * WN) void conv_splitx_kernel(const SaConvArgs p) {
+  using C = ConvCfg<BM, BN, WM, WN, MODE>;
+  __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
+  const int nk_all = p.Kpad / C::BK;
+  const int S = gridDim.z, z = blockIdx.z;
+  const int kt0 = (int)((long)z * nk_all / S);
+  const int nk = (int)((long)(z + 1) * nk_all / S) - kt0;
+  conv_tile<BM, BN, WM, WN, MODE, 1>(p, smem, blockIdx.x, blockIdx.y, kt0, nk, S, z, 0, 0, 0, 0);
+}
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void conv_splitx_reduce_kernel(const SaConvArgs p) {
+  using C = ConvCfg<BM, BN, WM, WN, kFastK64>;
+  static_assert(4 * C::NW * BN * 4 <= C::C_BYTES, "the epilogue's statistics reduction fits the C tile");
+  __shared__ __attribute__((aligned(16))) char smem[C::C_BYTES];
+  conv_tile<BM, BN, WM, WN, kFastK64, 2>(p, smem, blockIdx.x, blockIdx.y, 0, 0, 1, 0, 0, 0, 0, 0);
+}
+
+// Returns 1 when the shape does not qualify (not the uniform-k gather, a grid that needs no split, workspace short).
+template <int BM, int BN, int WM, int WN, int MODE>
+int launch_splitx(const SaConvArgs* a, hipStream_t stream) {
+  if (!glds3_eligible(a) || a->splitk < 0 || a->epi == SA_EPI_TAPPROJ) return 1;
+  const long M = (long)a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
+  const int LD = (a->Cout + 63) & ~63;
+  const long gx = (M + BM - 1) / BM, gy = (a->Cout + BN - 1) / BN;
+  const long tiles = gx * gy;
+  const int nk = a->Kpad / 64;
+  const int cus = device_cus();
+  // at most one workgroup per CU (one round), >= 3 k-steps per slice, <= 8 slices (the reduction unrolls 8)
+  int S = (int)(cus / tiles);
+  if (S > 8) S = 8;
+  if (S > nk / 3) S = nk / 3;
+  const long Mp = (M + 3) & ~3L;
+  if (S < 2 || M >= (1L << 31) || (long)S * Mp * LD >= (1L << 31)) return 1;
+  if (!a->ws || (long)S * Mp * LD > a->ws_floats || ((uintptr_t)a->ws & 15)) return 1;
+  using CP = ConvCfg<BM, BN, WM, WN, MODE>;
+  hipLaunchKernelGGL((conv_splitx_kernel<BM, BN, WM, WN, MODE>), dim3((unsigned)gx, (unsigned)gy, S), dim3(CP::NT), 0,
+                     stream, *a);
+  SaConvArgs b = *a;
+  b.splitk = S;
+  using CR = ConvCfg<32, 64, 2, 2, kFastK64>;
+  hipLaunchKernelGGL((conv_splitx_reduce_kernel<32, 64, 2, 2>), dim3((unsigned)((M + 31) / 32), (unsigned)(LD / 64)),
+                     dim3(CR::NT), 0, stream, b);
+  g_split_floats = (long)S * Mp * LD;
+  g_split_tiles = 0;
+  return (int)hipGetLastError();
+}
+
 // kHalo launcher (8 waves, 1 block per CU, never split): 3x3 / stride 1 / pad 1 / dilation 1 2-D convs whose
 // sources are multiples of 64 channels, K unpadded.  Returns 1 when the shape does not qualify.
 template <int MODE>
@@ -2438,6 +2546,8 @@ extern "C" int sa_conv2d_tile_lds(int cfg) {
     case 31: return ConvCfg<384, 128, 4, 2, kHaloW12>::SMEM;
     case 32: return ConvCfg<512, 128, 4, 2, kHaloQ>::SMEM;
     case 33: return ConvCfg<384, 128, 4, 2, kHaloQ12>::SMEM;
+    case 37: return ConvCfg<128, 128, 2, 4, kGldsDeep>::SMEM;
+    case 38: return ConvCfg<64, 64, 2, 2, kGldsDeep>::SMEM;
     default: return -1;
   }
 }
@@ -2697,6 +2807,13 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
                   : cfg == 15 ? launch_glds3<128, 128, 2, 4, kGldsDeep>(a, stream, true)
                   : cfg == 16 ? launch_glds3<64, 64, 2, 2, kGldsDeep>(a, stream, true)
                               : launch_glds3<256, 64, 4, 2, kGldsDeep>(a, stream, true);
+      return r == 1 ? -5 : r;
+    }
+    case 37: case 38: {
+      // workgroup split-K + reduce / epilogue launch: 128x128 (37) / 64x64 (38) deep DMA ring partial tiles (a slice
+      // is only a few k-steps: the whole of it in flight)
+      const int r = cfg == 37 ? launch_splitx<128, 128, 2, 4, kGldsDeep>(a, stream)
+                              : launch_splitx<64, 64, 2, 2, kGldsDeep>(a, stream);
       return r == 1 ? -5 : r;
     }
     case 10: case 11: {

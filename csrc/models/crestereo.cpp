@@ -492,6 +492,11 @@ void CreStereo::update(hipStream_t s, Level& L, const Tensor& f1, const Tensor& 
 
 void CreStereo::forward(hipStream_t s) {
   const int B = this->B();
+  // the workgroup split-K tactics are candidates here (one serial chain; SA_CRE_WG_SPLIT=0 turns them off): same-process
+  // A/B with fresh tuning, iter10 5.715 -> 5.642 ms, iter2 2.106 -> 2.095 (profiles/round6_notes.md)
+  // (read per forward, i.e. per tuning pass / capture: an in-process A/B knob)
+  const bool wg_split = !(std::getenv("SA_CRE_WG_SPLIT") && std::getenv("SA_CRE_WG_SPLIT")[0] == '0');
+  ScopedWgSplit wgs(wg_split);
   sp_.zero(s);
   check(sa_preprocess(in_left_, B, H(), W(), SA_PRE_SIGNED, img_.ptr, 8, 0, 8, s), "preprocess");
   check(sa_preprocess(in_right_, B, H(), W(), SA_PRE_SIGNED, img_.slice_n(B, B).ptr, 8, 0, 8, s), "preprocess");

@@ -576,6 +576,10 @@ static thread_local bool g_side_branch = false;
 ScopedSideBranch::ScopedSideBranch(bool on) : prev(g_side_branch) { g_side_branch = prev || on; }
 ScopedSideBranch::~ScopedSideBranch() { g_side_branch = prev; }
 bool side_branch() { return g_side_branch; }
+static thread_local bool g_wg_split = false;
+ScopedWgSplit::ScopedWgSplit(bool on) : prev(g_wg_split) { g_wg_split = on; }
+ScopedWgSplit::~ScopedWgSplit() { g_wg_split = prev; }
+bool wg_split_allowed() { return g_wg_split; }
 
 static thread_local const SplitKWorkspace* g_splitk = nullptr;
 const SplitKWorkspace* current_splitk() { return g_splitk; }
@@ -715,6 +719,7 @@ std::string plan_key(const SaConvArgs& a) {
   std::string k(buf);
   if (a.in_stats) k += "|i";  // folded input norm (direct kernel only)
   if (side_branch()) k += "|b";  // side-branch conv (ScopedSideBranch): tuned for co-residency
+  if (wg_split_allowed()) k += "|x";  // the workgroup split-K tactics are candidates (ScopedWgSplit)
   return k;
 }
 
@@ -767,6 +772,8 @@ constexpr Tactic kTactics[] = {
     {34, false, false, 0, 0, 0, 0, "direct 3x3x3, 8-32 channels, 2x4x32 voxel blocks"},
     {35, false, false, 0, 256, 0, 0, "pointwise 1x1, <= 256 -> <= 256 channels, one wave per 16 pixels x all columns"},
     {36, false, false, 0, 64, 0, 0, "direct 3x3 (dilation 1 / 2 / 4, k4s2 deconv scatter), 8-96 -> <= 64 channels, 8x32 blocks"},
+    {37, false, false, 0, 0, 0, 0, "workgroup split-K, 128x128 deep DMA ring partials + reduce / epilogue launch"},
+    {38, false, false, 0, 0, 0, 0, "workgroup split-K, 64x64 deep DMA ring partials + reduce / epilogue launch"},
 };
 
 bool known_tactic(int cfg) {
@@ -789,6 +796,7 @@ bool tactic_applies(const Tactic& t, const SaConvArgs& a, long M) {
   // SA_TUNE_MIN_TILES: the grid size below which the wide tiles are not timed (default 256 = one per CU)
   const char* mt = std::getenv("SA_TUNE_MIN_TILES");  // read per shape (tuning is rare): in-process A/B knob
   const long min_tiles = mt ? std::atol(mt) : 256L;
+  if ((t.cfg == 37 || t.cfg == 38) && !wg_split_allowed()) return false;  // opt-in (ScopedWgSplit)
   if (a.Cout <= t.min_cout || (t.max_cout > 0 && a.Cout > t.max_cout)) return false;
   if (t.tile_m > 0 && ((M + t.tile_m - 1) / t.tile_m) * ((a.Cout + t.tile_n - 1) / t.tile_n) < min_tiles) return false;
   return true;

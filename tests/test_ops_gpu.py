@@ -726,7 +726,7 @@ def test_conv2d_gru_epilogues():
     assert rel_err(nchw(net_h), ref) < 3e-3
 
 
-@pytest.mark.parametrize("cfg,splitk", [(-1, 1), (5, 1), (4, 1), (16, 2), (7, 3)])
+@pytest.mark.parametrize("cfg,splitk", [(-1, 1), (5, 1), (4, 1), (16, 2), (7, 3), (37, 1), (38, 1)])
 def test_conv2d_gru_zrq_split(cfg, splitk):
     """ConvGRU with q's x-input half hoisted into the z/r conv (SA_EPI_GRU_ZRQ, Cout = 3 hd, q's h-input weights
     zeroed there) and the q conv over r*h alone adding it back (SA_EPI_GRU_Q + res), against the fp32 GRU."""
@@ -755,13 +755,48 @@ def test_conv2d_gru_zrq_split(cfg, splitk):
     zb = torch.empty(n, h, w, hd, device=DEV, dtype=torch.float16)
     rhb = torch.empty_like(zb)
     qx = torch.empty_like(zb)
-    ws = O.splitk_workspace(1 << 22, 4096) if splitk != 1 else None
+    wsplit = cfg in (37, 38)  # workgroup split-K: partials in the workspace, reduce + gate epilogue launch
+    ws = O.splitk_workspace(1 << 22, 4096) if splitk != 1 or wsplit else None
     O.conv2d([net_h, xh], wzrq, kpad, 3 * hd, 3, 3, bias=torch.cat([bz, br, bq]).contiguous(), out=qx,
              epi="gru_zrq", ctx=ctx, aux=zb, hbuf=net_h, rh=rhb, tile_cfg=cfg, splitk=splitk, workspace=ws)
-    O.conv2d([rhb], wqh, kph, hd, 3, 3, out=net_h, epi="gru_q", res=qx, aux=zb, hbuf=net_h, tile_cfg=cfg)
+    O.conv2d([rhb], wqh, kph, hd, 3, 3, out=net_h, epi="gru_q", res=qx, aux=zb, hbuf=net_h, tile_cfg=cfg,
+             workspace=ws if wsplit else None)
     torch.cuda.synchronize()
     assert rel_err(nchw(zb), z) < 3e-3
     assert rel_err(nchw(net_h), ref) < 4e-3
+
+
+@pytest.mark.parametrize("cfg", [37, 38])
+@pytest.mark.parametrize("srcs,cout,hw,n,res", [
+    ((128, 128), 256, (30, 40), 1, False),  # coarse GRU level shape, two sources
+    ((64,), 96, (15, 20), 2, True),        # Cout not a multiple of 64 (workspace rows padded to 128), residual
+    ((128, 64, 64), 384, (13, 21), 1, False),  # three sources, rows not a multiple of any tile
+])
+def test_conv2d_workgroup_splitk(srcs, cout, hw, n, res, cfg):
+    """Workgroup split-K (tactics 37 / 38): S workgroups store fp32 partial tiles of one output tile's K slices, a
+    second launch sums them in fixed order and runs the epilogue (bias, activation, residual) == F.conv2d; two runs
+    give identical bits."""
+    O = ops()
+    torch.manual_seed(37)
+    xs = [torch.randn(n, c, *hw, device=DEV) for c in srcs]
+    cin = sum(srcs)
+    w = torch.randn(cout, cin, 3, 3, device=DEV) / math.sqrt(cin * 9)
+    b = torch.randn(cout, device=DEV) * 0.1
+    r = torch.randn(n, cout, *hw, device=DEV) if res else None
+    xcat = torch.cat(xs, 1).half().float()
+    ref = F.relu(F.conv2d(xcat, w.half().float(), b, padding=1))
+    if res:
+        ref = ref + r.half().float()
+    wp, kpad, _ = O.pack_conv_weight(w)
+    ws = O.splitk_workspace(1 << 22, 16)
+    outs = []
+    for _ in range(2):
+        out = O.conv2d([nhwc(t).half() for t in xs], wp, kpad, cout, 3, 3, bias=b.contiguous(), act="relu",
+                       res=nhwc(r).half() if res else None, tile_cfg=cfg, workspace=ws)
+        torch.cuda.synchronize()
+        outs.append(out.clone())
+    assert rel_err(nchw(outs[0]), ref) < 3e-3
+    assert torch.equal(outs[0], outs[1])
 
 
 @pytest.mark.parametrize("n,h,w,xs,grid", [(1, 30, 40, (256,), 128), (2, 60, 80, (128, 128), 64),

@@ -119,7 +119,7 @@ def main():
         combos = [(cfg, sp) for cfg in map(int, a.cfgs.split(","))
                   for sp in (map(int, a.splits.split(",")) if a.splits else [sk])]
         for cfg, sk in combos:
-            kw = dict(bias=b, out=out, splitk=sk, workspace=ws if sk != 1 else None, tile_cfg=cfg, **extra)
+            kw = dict(bias=b, out=out, splitk=sk, workspace=ws if sk != 1 or cfg in (37, 38) else None, tile_cfg=cfg, **extra)
             if a.stats:
                 kw["stats"] = torch.zeros(16, n, cout, 2, dtype=torch.int64, device="cuda")
                 kw["stats_slots"] = a.stats

@@ -17,8 +17,16 @@ run() {  # name model iter-marker [batch]
   python3 tools/timeline.py /tmp/tl_$name --iter-marker "$marker" --chain 40 --kernel-stats 40 > gpurun_out/tl/${TAG}_${name}.txt 2>&1 || return 1
   cp $(find /tmp/tl_$name -name "*kernel_trace.csv" | head -1) gpurun_out/tl/${TAG}_${name}_kernels.csv
 }
-if [ -n "$ONLY" ]; then
-  run $ONLY && echo done
+if [ -n "$ONLY" ]; then  # one preset by its short name
+  case $ONLY in
+    sf) run sf raftstereo-sceneflow motion_encoder ;;
+    sf8) run sf8 raftstereo-sceneflow motion_encoder 8 ;;
+    rt) run rt raftstereo-realtime motion_encoder ;;
+    cre10) run cre10 crestereo-iter10 "" ;;
+    hit) run hit hitnet-d400 "" ;;
+    facv) run facv fastacvnet-plus "" ;;
+    *) echo "ONLY=$ONLY: sf sf8 rt cre10 hit facv"; exit 2 ;;
+  esac && echo done
   exit $?
 fi
 run sf raftstereo-sceneflow motion_encoder && \
