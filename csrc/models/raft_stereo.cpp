@@ -403,6 +403,10 @@ void RaftStereo::gru(hipStream_t s, int i, const std::vector<Tensor>& x) const {
   // level i, bit 3 the flow head (default 15; 6 = round 4's coarse levels only; 4 / 0: b1 8.51 / 8.62 ms).
   const int side_mask = std::getenv("SA_RAFT_SIDE_MASK") ? std::atoi(std::getenv("SA_RAFT_SIDE_MASK")) : 15;
   ScopedSideBranch sb(((side_mask >> i) & 1) && B() <= 2 && rc_.n_gru == 3 && !rc_.slow_fast);
+  // SA_RAFT_WG_SPLIT (bit i = level i, default 0): the workgroup split-K tactics (37 / 38) become candidates for the
+  // level's GRU convs.  All levels on: b1 SF 8.22 -> 8.59 ms, realtime 1.87 -> 1.95 (profiles/round6_notes.md)
+  const int wgs_mask = std::getenv("SA_RAFT_WG_SPLIT") ? std::atoi(std::getenv("SA_RAFT_WG_SPLIT")) : 0;
+  ScopedWgSplit wgs((wgs_mask >> i) & 1);
   std::vector<Tensor> srcs = {net_[i]};
   srcs.insert(srcs.end(), x.begin(), x.end());
   if (gru_split_) {
