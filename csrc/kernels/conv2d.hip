@@ -111,6 +111,10 @@ enum : int {
                   // phase, so per step the pipe idles through the barrier, the DMA issue and the LDS drain of both
                   // (ablation: the MFMA-free kernel took 75 % of the full kernel's time)
   kHaloQ12 = 16,  // kHaloQ with 12 x 32 output patches
+  kRegAll = 17,   // register-staged gather (any source widths), but the global loads of the WHOLE K range (<= 8 64-deep
+                  // steps) are issued up front into registers; the 2-buffer LDS stage then only pays a store + barrier
+                  // per step, not a load latency.  For the tiny-K / tiny-grid convs of the latency presets (HITNet's
+                  // 32-channel tile updates, K = 320), whose 2-stage pipeline waited on one load per k-step
 };
 __host__ __device__ constexpr bool is_glds(int mode) { return mode == kGlds3 || mode == kGldsDeep; }
 __host__ __device__ constexpr bool is_halop(int mode) { return mode == kHaloP || mode == kHaloP16; }
@@ -1614,6 +1618,53 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
   const int frow = lane & 15;
   const int foff = frow * 64 + (((lane >> 4) ^ (((frow >> 3) & 1) * 3)) << 4);
 
+  if constexpr (MODE == kRegAll) {
+    // the loads of every k-step issued up front (registers), then per step: store to LDS buffer kt & 1, barrier,
+    // MFMAs.  Buffer kt & 1 was last read by the MFMAs of step kt - 2, which every wave finished before the barrier
+    // of step kt - 1.
+    static_assert(C::BK == 64, "kRegAll: 64-deep steps");
+    constexpr int NS = 8;
+    half8 xa[NS][C::A_PT], xb[NS][C::B_PT];
+#pragma unroll
+    for (int st = 0; st < NS; ++st) {
+      if (st < nk) {
+        load_tile(st);
+#pragma unroll
+        for (int i = 0; i < C::A_PT; ++i) xa[st][i] = ra[i];
+#pragma unroll
+        for (int i = 0; i < C::B_PT; ++i) xb[st][i] = rb[i];
+      }
+    }
+#pragma unroll
+    for (int kt = 0; kt < NS; ++kt) {
+      if (kt >= nk) break;
+#pragma unroll
+      for (int i = 0; i < C::A_PT; ++i) ra[i] = xa[kt][i];
+#pragma unroll
+      for (int i = 0; i < C::B_PT; ++i) rb[i] = xb[kt][i];
+      store_tile(kt & 1);
+      __syncthreads();
+      const char* sa = smem + (kt & 1) * (C::A_BYTES + C::B_BYTES);
+      const char* sb = sa + C::A_BYTES;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        half8 af[C::FM], bf[C::FN];
+        const int lc = (lane >> 4) + 4 * kk;
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+          af[i] = *reinterpret_cast<const half8*>(sa + swz64(wm * C::TM + i * 16 + frow, lc));
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j)
+          bf[j] = *reinterpret_cast<const half8*>(sb + swz64(wn * C::TN + j * 16 + frow, lc));
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int j = 0; j < C::FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // the epilogue's C tile aliases the stage buffers
+  } else {
   load_tile(0);
   store_tile(0);
   __syncthreads();
@@ -1657,6 +1708,7 @@ __device__ __forceinline__ void conv_tile(const SaConvArgs& p, char* smem, const
     if (kt + 1 < nk) store_tile(cur ^ 1);
     __syncthreads();
   }
+  }  // two-stage pipeline
 
   }  // register-staged path
 
@@ -2291,6 +2343,19 @@ int launch_cfg(const SaConvArgs* a, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+// kRegAll launcher (tactic 39): any gather, the whole K (<= NSTAGE 64-deep steps) loaded up front, never split.
+// Returns 1 when the shape does not qualify.
+template <int BM, int BN, int WM, int WN>
+int launch_regall(const SaConvArgs* a, hipStream_t stream) {
+  if (a->Kpad % 64 != 0 || a->Kpad / 64 > 8 || a->splitk < 0 || a->splitk > 1) return 1;
+  const long M = (long)a->N * (a->Do > 0 ? a->Do : 1) * a->Ho * a->Wo;
+  const long gx = (M + BM - 1) / BM, gy = (a->Cout + BN - 1) / BN;
+  if (gx >= (1L << 31) || gy > 65535) return 1;
+  note_split(1, 0, 0);
+  launch_kernel<BM, BN, WM, WN, kRegAll>(dim3((unsigned)gx, (unsigned)gy, 1), a, stream);
+  return (int)hipGetLastError();
+}
+
 // kGlds3 launcher (8 waves, 1 block per CU): only for the uniform-k fast gather (every source a
 // multiple of 64 channels, K unpadded, <= 64 taps).  Returns 1 when the shape does not qualify.
 bool glds3_eligible(const SaConvArgs* a);
@@ -2547,6 +2612,7 @@ extern "C" int sa_conv2d_tile_lds(int cfg) {
     case 32: return ConvCfg<512, 128, 4, 2, kHaloQ>::SMEM;
     case 33: return ConvCfg<384, 128, 4, 2, kHaloQ12>::SMEM;
     case 37: return ConvCfg<128, 128, 2, 4, kGldsDeep>::SMEM;
+    case 39: return ConvCfg<64, 64, 2, 2, kRegAll>::SMEM;
     case 38: return ConvCfg<64, 64, 2, 2, kGldsDeep>::SMEM;
     default: return -1;
   }
@@ -2807,6 +2873,11 @@ extern "C" int sa_conv2d(const SaConvArgs* a, hipStream_t stream) {
                   : cfg == 15 ? launch_glds3<128, 128, 2, 4, kGldsDeep>(a, stream, true)
                   : cfg == 16 ? launch_glds3<64, 64, 2, 2, kGldsDeep>(a, stream, true)
                               : launch_glds3<256, 64, 4, 2, kGldsDeep>(a, stream, true);
+      return r == 1 ? -5 : r;
+    }
+    case 39: {
+      // 64x64 register-staged tile with the whole K (<= 512) in flight at once
+      const int r = launch_regall<64, 64, 2, 2>(a, stream);
       return r == 1 ? -5 : r;
     }
     case 37: case 38: {

@@ -774,6 +774,9 @@ constexpr Tactic kTactics[] = {
     {36, false, false, 0, 64, 0, 0, "direct 3x3 (dilation 1 / 2 / 4, k4s2 deconv scatter), 8-96 -> <= 64 channels, 8x32 blocks"},
     {37, false, false, 0, 0, 0, 0, "workgroup split-K, 128x128 deep DMA ring partials + reduce / epilogue launch"},
     {38, false, false, 0, 0, 0, 0, "workgroup split-K, 64x64 deep DMA ring partials + reduce / epilogue launch"},
+    // (tile_cfg 39, the 64x64 register-staged tile with the whole K's loads issued up front, is not timed: faster alone
+    // on the tiny-K convs, but in the frames HITNet d400 1.117 -> 1.135, Fast-ACVNet+ 1.523 -> 1.538, HITNet XL
+    // 1.968 -> 1.954, RAFT realtime 1.863 -> 1.844 ms with it a candidate: profiles/round6_notes.md)
 };
 
 bool known_tactic(int cfg) {

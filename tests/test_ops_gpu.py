@@ -766,6 +766,39 @@ def test_conv2d_gru_zrq_split(cfg, splitk):
     assert rel_err(nchw(net_h), ref) < 4e-3
 
 
+@pytest.mark.parametrize("srcs,cout,k,stride,dil,hw,n,res", [
+    ((32,), 32, 3, 1, 1, (60, 80), 1, False),      # HITNet tile-update conv (K = 288 -> Kpad 320)
+    ((24, 8), 64, 3, 1, 2, (30, 40), 2, True),     # two sources, dilation 2, residual
+    ((16,), 24, 2, 2, 1, (120, 160), 2, False),    # k2 / s2 downsampling, Cout not a multiple of 16
+    ((64, 64), 48, 3, 1, 1, (15, 20), 1, False),   # K = 1152 -> 18 steps: rejected (whole K > 8 steps)
+])
+def test_conv2d_whole_k_tile(srcs, cout, k, stride, dil, hw, n, res):
+    """Tactic 39: the 64x64 register-staged tile with every k-step's loads issued up front (K <= 512) == F.conv2d
+    (bias, relu, optional residual); a K beyond 8 steps is rejected (-5), not run."""
+    O = ops()
+    torch.manual_seed(39)
+    xs = [torch.randn(n, c, *hw, device=DEV) for c in srcs]
+    cin = sum(srcs)
+    w = torch.randn(cout, cin, k, k, device=DEV) / math.sqrt(cin * k * k)
+    b = torch.randn(cout, device=DEV) * 0.1
+    pad = (k // 2) * dil if k % 2 else 0
+    xcat = torch.cat(xs, 1).half().float()
+    ref = F.relu(F.conv2d(xcat, w.half().float(), b, stride=stride, padding=pad, dilation=dil))
+    r = torch.randn_like(ref) if res else None
+    if res:
+        ref = ref + r.half().float()
+    wp, kpad, _ = O.pack_conv_weight(w)
+    args = dict(bias=b.contiguous(), stride=stride, pad=pad, dil=dil, act="relu",
+                res=nhwc(r).half() if res else None, tile_cfg=39)
+    if kpad > 512:
+        with pytest.raises(RuntimeError):
+            O.conv2d([nhwc(t).half() for t in xs], wp, kpad, cout, k, k, **args)
+        return
+    out = O.conv2d([nhwc(t).half() for t in xs], wp, kpad, cout, k, k, **args)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(out), ref) < 3e-3
+
+
 @pytest.mark.parametrize("cfg", [37, 38])
 @pytest.mark.parametrize("srcs,cout,hw,n,res", [
     ((128, 128), 256, (30, 40), 1, False),  # coarse GRU level shape, two sources
